@@ -1,0 +1,65 @@
+// Host-side internals of libvr_hip.so (not part of the public ABI).
+#pragma once
+#include <cstdint>
+#include <string>
+#include <vector>
+
+#ifndef __HIPCC__
+#ifndef __host__
+#define __host__
+#endif
+#ifndef __device__
+#define __device__
+#endif
+#endif
+
+#include "../../../include/vr_hip.h"
+#include "../vr_internal.h"
+
+namespace vr {
+
+// Error channel: every C entry point funnels failures through fail(), which records a
+// thread-local message for vr_last_error() and returns the status.
+vr_status fail(vr_status st, const std::string& msg);
+void clear_error();
+
+// Precomputed per-Gaussian quantities (gaussian.h:52-55), in scene order.
+struct GaussianPre {
+    float mean[3];
+    float density;
+    float inv_cov[6];  // 00 01 02 11 12 22
+    float norm;
+    float albedo;
+    float cov[6];      // input covariance (for bounds)
+};
+
+// Host scene.
+struct HostScene {
+    int32_t type = VR_VOLUME_GAUSSIANS;
+    std::vector<vr_gaussian> gaussians;
+    std::vector<GaussianPre> pre;
+    std::vector<vr_sphere> spheres;
+    std::vector<vr_light> lights;
+    float env[3] = {0.53f, 0.81f, 0.92f};  // scene.h:29
+};
+
+GaussianPre precompute_gaussian(const vr_gaussian& g);
+void gaussian_bounds(const GaussianPre& g, float bmin[3], float bmax[3]);
+void sphere_bounds(const vr_sphere& s, float bmin[3], float bmax[3]);
+
+// BVH over primitive boxes. Output: child-pair nodes + primitive order (leaf-contiguous).
+struct BVHBuild {
+    std::vector<BVHNode> nodes;
+    std::vector<uint32_t> order;  // order[j] = scene index of the j-th primitive in leaf order
+    int max_depth = 0;
+};
+BVHBuild build_bvh(const std::vector<float>& boxes /* 6 per prim: min xyz, max xyz */);
+
+// Iterated float step sequence t_0 = 0, t_{k+1} = t_k + step (test_integrators.h:184,289).
+std::vector<float> step_table(float step, float t_max);
+
+}  // namespace vr
+
+struct vr_scene {
+    vr::HostScene s;
+};

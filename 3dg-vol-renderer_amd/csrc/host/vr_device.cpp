@@ -1,0 +1,389 @@
+// Device context: scene upload (BVH build + HBM layout), step tables, launch and statistics.
+// Host C++ over the HIP runtime; the kernels live in kernels/vr_kernels.hip.
+#include <hip/hip_runtime_api.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <map>
+#include <mutex>
+
+#include "vr_common.h"
+
+namespace vr {
+hipError_t launch_render(const RenderArgs& A, hipStream_t stream, int volume_type, int integrator);
+hipError_t launch_unshuffle(const float* slabs, uint32_t nslabs, uint32_t tiles_per_slab, uint32_t tiles_x, uint32_t W,
+                            uint32_t H, float* img, hipStream_t stream);
+}  // namespace vr
+
+using namespace vr;
+
+struct vr_ctx {
+    int device = 0;
+    hipStream_t stream = nullptr;  // used by the synchronous vr_render
+    // scene
+    bool has_scene = false;
+    int32_t type = VR_VOLUME_GAUSSIANS;
+    int32_t num_prims = 0;
+    GaussianRecord* d_gauss = nullptr;
+    BVHNode* d_nodes = nullptr;
+    SphereRecord* d_spheres = nullptr;
+    std::vector<LightRecord> lights;
+    float env[3] = {0, 0, 0};
+    float bmin[3] = {0, 0, 0}, bmax[3] = {0, 0, 0};
+    int bvh_depth = 0;
+    size_t num_nodes = 0;
+    // step tables keyed by step size
+    struct Table {
+        float* d = nullptr;
+        int n = 0;
+        float tmax = 0;
+    };
+    std::map<uint32_t, Table> tables;
+    // workspaces
+    uint32_t* d_queue = nullptr;
+    uint32_t queue_cap = 0;
+    uint32_t* d_counters = nullptr;  // [0] errors
+    uint32_t* h_counters = nullptr;  // pinned: [0] queue count, [1] errors
+    float* d_frame = nullptr;
+    size_t frame_cap = 0;
+    hipEvent_t ev_start = nullptr, ev_stop = nullptr;
+    bool stats_pending = false;
+    int64_t last_pixels = 0;
+};
+
+namespace {
+
+vr_status hip_fail(hipError_t e, const char* what) {
+    return fail(VR_ERR_HIP, std::string(what) + ": " + hipGetErrorString(e));
+}
+#define HIP_TRY(expr, what)                          \
+    do {                                             \
+        hipError_t e_ = (expr);                      \
+        if (e_ != hipSuccess) return hip_fail(e_, what); \
+    } while (0)
+
+void free_scene(vr_ctx* c) {
+    if (c->d_gauss) (void)hipFree(c->d_gauss);
+    if (c->d_nodes) (void)hipFree(c->d_nodes);
+    if (c->d_spheres) (void)hipFree(c->d_spheres);
+    c->d_gauss = nullptr;
+    c->d_nodes = nullptr;
+    c->d_spheres = nullptr;
+    c->has_scene = false;
+}
+
+// Farthest distance any ray can travel before leaving the scene box: the rays of both camera
+// models start on the 2x2 sensor square position +- right +- up (camera.h:50,69).
+float scene_tmax(const vr_ctx* c, const vr_camera* cam) {
+    float best = 0.0f;
+    for (int su = -1; su <= 1; su += 2)
+        for (int sv = -1; sv <= 1; sv += 2) {
+            float o[3];
+            for (int k = 0; k < 3; ++k) o[k] = cam->position[k] + su * cam->right[k] + sv * cam->up[k];
+            for (int cx = 0; cx < 2; ++cx)
+                for (int cy = 0; cy < 2; ++cy)
+                    for (int cz = 0; cz < 2; ++cz) {
+                        float p[3] = {cx ? c->bmax[0] : c->bmin[0], cy ? c->bmax[1] : c->bmin[1], cz ? c->bmax[2] : c->bmin[2]};
+                        double d = 0;
+                        for (int k = 0; k < 3; ++k) d += (double)(p[k] - o[k]) * (p[k] - o[k]);
+                        best = std::max(best, (float)std::sqrt(d));
+                    }
+        }
+    return best * 1.01f + 1.0f;
+}
+
+vr_status get_table(vr_ctx* c, float step, float tmax, const float** d, int* n) {
+    if (!(step > 0.0f) || !std::isfinite(step)) return fail(VR_ERR_INVALID, "step_size must be a positive finite float");
+    uint32_t key;
+    std::memcpy(&key, &step, 4);
+    auto it = c->tables.find(key);
+    if (it == c->tables.end() || it->second.tmax < tmax) {
+        float want = it == c->tables.end() ? tmax : std::max(tmax, 2.0f * it->second.tmax);
+        std::vector<float> t = step_table(step, want);
+        if (t.back() <= tmax) return fail(VR_ERR_OVERFLOW, "step_size too small for the scene extent (float step sequence stalls)");
+        vr_ctx::Table tb;
+        tb.n = (int)t.size();
+        tb.tmax = want;
+        HIP_TRY(hipMalloc(&tb.d, t.size() * sizeof(float)), "hipMalloc(step table)");
+        HIP_TRY(hipMemcpy(tb.d, t.data(), t.size() * sizeof(float), hipMemcpyHostToDevice), "hipMemcpy(step table)");
+        if (it != c->tables.end()) (void)hipFree(it->second.d);
+        c->tables[key] = tb;
+        it = c->tables.find(key);
+    }
+    *d = it->second.d;
+    *n = it->second.n;
+    return VR_OK;
+}
+
+vr_status ensure_queue(vr_ctx* c, uint64_t pixels) {
+    if (pixels + 1 > (uint64_t)c->queue_cap + 1 || !c->d_queue) {
+        if (c->d_queue) (void)hipFree(c->d_queue);
+        c->d_queue = nullptr;
+        uint64_t cap = std::max<uint64_t>(pixels, 4096);
+        if (cap > 0xffffffffull) return fail(VR_ERR_INVALID, "frame too large");
+        HIP_TRY(hipMalloc(&c->d_queue, (cap + 1) * sizeof(uint32_t)), "hipMalloc(queue)");
+        c->queue_cap = (uint32_t)cap;
+    }
+    return VR_OK;
+}
+
+vr_status fill_args(vr_ctx* c, const vr_camera* cam, const vr_render_params* p, uint32_t W, uint32_t H, RenderArgs& A) {
+    if (!c->has_scene) return fail(VR_ERR_NOSCENE, "no scene uploaded (call vr_upload_scene first)");
+    if (!cam || !p) return fail(VR_ERR_INVALID, "NULL camera or params");
+    if (W == 0 || H == 0 || W > 65535 || H > 65535) return fail(VR_ERR_INVALID, "width/height must be in [1, 65535]");
+    if (cam->type != VR_CAMERA_PINHOLE && cam->type != VR_CAMERA_ORTHOGRAPHIC) return fail(VR_ERR_INVALID, "unknown camera type");
+    if (p->flags != 0) return fail(VR_ERR_INVALID, "vr_render_params.flags must be 0");
+    if (p->integrator == VR_RAYMARCH_GAUSSIANS && c->type != VR_VOLUME_GAUSSIANS)
+        return fail(VR_ERR_INVALID, "RayMarchingGaussians needs a Gaussian scene");
+    if (p->integrator == VR_RAYMARCH_SPHERES && c->type != VR_VOLUME_SPHERES)
+        return fail(VR_ERR_INVALID, "RayMarchingSpheres needs a sphere scene");
+    if (p->integrator != VR_RAYMARCH_GAUSSIANS && p->integrator != VR_RAYMARCH_SPHERES && p->integrator != VR_TEST_HITMASK)
+        return fail(VR_ERR_UNSUPPORTED, "integrator has no device implementation");
+    if (p->integrator != VR_TEST_HITMASK && p->env_samples < 0) return fail(VR_ERR_INVALID, "env_samples must be >= 0");
+    if (!(p->t_eps >= 0.0f) || p->t_eps >= 1.0f) return fail(VR_ERR_INVALID, "t_eps must be in [0, 1)");
+    std::memset(&A, 0, sizeof(A));
+    A.cam_type = cam->type;
+    for (int k = 0; k < 3; ++k) {
+        A.cam_pos[k] = cam->position[k];
+        A.cam_view[k] = cam->view_dir[k];
+        A.cam_right[k] = cam->right[k];
+        A.cam_up[k] = cam->up[k];
+        A.cam_pinhole[k] = cam->pinhole[k];
+    }
+    A.width = W;
+    A.height = H;
+    A.tiles_x = (W + kTile - 1) / kTile;
+    A.gauss = c->d_gauss;
+    A.nodes = c->d_nodes;
+    A.spheres = c->d_spheres;
+    A.num_prims = c->num_prims;
+    A.num_lights = (int32_t)c->lights.size();
+    for (size_t l = 0; l < c->lights.size(); ++l) A.lights[l] = c->lights[l];
+    for (int k = 0; k < 3; ++k) A.env[k] = c->env[k];
+    A.step_size = p->step_size;
+    A.env_samples = p->env_samples;
+    A.t_eps = p->t_eps;
+    if (p->integrator != VR_TEST_HITMASK) {
+        const float* d;
+        int n;
+        vr_status st = get_table(c, p->step_size, scene_tmax(c, cam), &d, &n);
+        if (st != VR_OK) return st;
+        A.tsteps = d;
+        A.num_tsteps = n;
+    }
+    A.counters = c->d_counters;
+    return VR_OK;
+}
+
+vr_status launch(vr_ctx* c, RenderArgs& A, const vr_render_params* p, hipStream_t s) {
+    vr_status st = ensure_queue(c, (uint64_t)A.num_tiles * 256u);
+    if (st != VR_OK) return st;
+    A.queue = c->d_queue;
+    A.queue_cap = c->queue_cap;
+    if (c->stats_pending) {  // previous stats copy must land before we reuse the pinned buffer
+        HIP_TRY(hipEventSynchronize(c->ev_stop), "hipEventSynchronize");
+        c->stats_pending = false;
+    }
+    HIP_TRY(hipMemsetAsync(c->d_queue, 0, sizeof(uint32_t), s), "hipMemsetAsync(queue)");
+    HIP_TRY(hipMemsetAsync(c->d_counters, 0, 4 * sizeof(uint32_t), s), "hipMemsetAsync(counters)");
+    HIP_TRY(hipEventRecord(c->ev_start, s), "hipEventRecord");
+    HIP_TRY(launch_render(A, s, c->type, p->integrator), "kernel launch");
+    HIP_TRY(hipEventRecord(c->ev_stop, s), "hipEventRecord");
+    HIP_TRY(hipMemcpyAsync(&c->h_counters[0], c->d_queue, sizeof(uint32_t), hipMemcpyDeviceToHost, s), "hipMemcpyAsync(stats)");
+    HIP_TRY(hipMemcpyAsync(&c->h_counters[1], c->d_counters, sizeof(uint32_t), hipMemcpyDeviceToHost, s), "hipMemcpyAsync(stats)");
+    c->stats_pending = true;
+    c->last_pixels = (int64_t)A.num_tiles * 256;
+    return VR_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+vr_status vr_init(int device, vr_ctx** out) {
+    if (!out) return fail(VR_ERR_INVALID, "vr_init: out is NULL");
+    int n = 0;
+    hipError_t e = hipGetDeviceCount(&n);
+    if (e != hipSuccess || n == 0) return fail(VR_ERR_HIP, "vr_init: no HIP device available");
+    if (device < 0 || device >= n) return fail(VR_ERR_INVALID, "vr_init: device index out of range");
+    HIP_TRY(hipSetDevice(device), "hipSetDevice");
+    vr_ctx* c = new vr_ctx();
+    c->device = device;
+    if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
+        hipMalloc(&c->d_counters, 4 * sizeof(uint32_t)) != hipSuccess ||
+        hipHostMalloc(&c->h_counters, 4 * sizeof(uint32_t), hipHostMallocDefault) != hipSuccess ||
+        hipEventCreate(&c->ev_start) != hipSuccess || hipEventCreate(&c->ev_stop) != hipSuccess) {
+        vr_destroy(c);
+        return fail(VR_ERR_HIP, "vr_init: failed to create stream/workspace");
+    }
+    std::memset(c->h_counters, 0, 4 * sizeof(uint32_t));
+    *out = c;
+    return VR_OK;
+}
+
+void vr_destroy(vr_ctx* c) {
+    if (!c) return;
+    (void)hipSetDevice(c->device);
+    (void)hipDeviceSynchronize();
+    free_scene(c);
+    for (auto& kv : c->tables) (void)hipFree(kv.second.d);
+    if (c->d_queue) (void)hipFree(c->d_queue);
+    if (c->d_counters) (void)hipFree(c->d_counters);
+    if (c->h_counters) (void)hipHostFree(c->h_counters);
+    if (c->d_frame) (void)hipFree(c->d_frame);
+    if (c->ev_start) (void)hipEventDestroy(c->ev_start);
+    if (c->ev_stop) (void)hipEventDestroy(c->ev_stop);
+    if (c->stream) (void)hipStreamDestroy(c->stream);
+    delete c;
+}
+
+vr_status vr_upload_scene(vr_ctx* c, const vr_scene* sc) {
+    if (!c || !sc) return fail(VR_ERR_INVALID, "vr_upload_scene: NULL argument");
+    const HostScene& s = sc->s;
+    if (s.lights.size() > (size_t)kMaxLights) return fail(VR_ERR_UNSUPPORTED, "more than 16 lights");
+    HIP_TRY(hipSetDevice(c->device), "hipSetDevice");
+    HIP_TRY(hipDeviceSynchronize(), "hipDeviceSynchronize");
+    free_scene(c);
+    c->type = s.type;
+    c->lights.clear();
+    for (const vr_light& l : s.lights)
+        c->lights.push_back(LightRecord{l.position[0], l.position[1], l.position[2], l.intensity[0], l.intensity[1], l.intensity[2]});
+    std::memcpy(c->env, s.env, sizeof(c->env));
+    for (int k = 0; k < 3; ++k) {
+        c->bmin[k] = INFINITY;
+        c->bmax[k] = -INFINITY;
+    }
+    if (s.type == VR_VOLUME_GAUSSIANS) {
+        const size_t N = s.pre.size();
+        if (N >= (1u << 27)) return fail(VR_ERR_UNSUPPORTED, "more than 2^27 Gaussians");
+        std::vector<float> boxes(6 * N);
+        for (size_t i = 0; i < N; ++i) {
+            gaussian_bounds(s.pre[i], &boxes[6 * i], &boxes[6 * i + 3]);
+            for (int k = 0; k < 3; ++k) {
+                c->bmin[k] = std::min(c->bmin[k], boxes[6 * i + k]);
+                c->bmax[k] = std::max(c->bmax[k], boxes[6 * i + 3 + k]);
+            }
+        }
+        BVHBuild b = build_bvh(boxes);
+        if (b.max_depth > kMaxDepth + 1) return fail(VR_ERR_OVERFLOW, "BVH deeper than the traversal stack");
+        std::vector<GaussianRecord> rec(std::max<size_t>(N, 1));
+        for (size_t j = 0; j < N; ++j) {
+            const GaussianPre& p = s.pre[b.order[j]];
+            rec[j] = GaussianRecord{p.mean[0], p.mean[1], p.mean[2], p.density, p.inv_cov[0], p.inv_cov[1],
+                                    p.inv_cov[2], p.inv_cov[3], p.inv_cov[4], p.inv_cov[5], p.norm, p.albedo};
+        }
+        HIP_TRY(hipMalloc(&c->d_gauss, rec.size() * sizeof(GaussianRecord)), "hipMalloc(records)");
+        HIP_TRY(hipMemcpy(c->d_gauss, rec.data(), rec.size() * sizeof(GaussianRecord), hipMemcpyHostToDevice), "hipMemcpy(records)");
+        HIP_TRY(hipMalloc(&c->d_nodes, b.nodes.size() * sizeof(BVHNode)), "hipMalloc(nodes)");
+        HIP_TRY(hipMemcpy(c->d_nodes, b.nodes.data(), b.nodes.size() * sizeof(BVHNode), hipMemcpyHostToDevice), "hipMemcpy(nodes)");
+        c->num_prims = (int32_t)N;
+        c->bvh_depth = b.max_depth;
+        c->num_nodes = b.nodes.size();
+    } else {
+        const size_t N = s.spheres.size();
+        if (N > 16) return fail(VR_ERR_UNSUPPORTED, "the device sphere path supports at most 16 spheres");
+        std::vector<SphereRecord> rec(std::max<size_t>(N, 1));
+        for (size_t i = 0; i < N; ++i) {
+            const vr_sphere& sp = s.spheres[i];
+            rec[i] = SphereRecord{sp.center[0], sp.center[1], sp.center[2], sp.radius, sp.sigma_a, sp.sigma_s, 0, 0};
+            float lo[3], hi[3];
+            sphere_bounds(sp, lo, hi);
+            for (int k = 0; k < 3; ++k) {
+                c->bmin[k] = std::min(c->bmin[k], lo[k]);
+                c->bmax[k] = std::max(c->bmax[k], hi[k]);
+            }
+        }
+        HIP_TRY(hipMalloc(&c->d_spheres, rec.size() * sizeof(SphereRecord)), "hipMalloc(spheres)");
+        HIP_TRY(hipMemcpy(c->d_spheres, rec.data(), rec.size() * sizeof(SphereRecord), hipMemcpyHostToDevice), "hipMemcpy(spheres)");
+        c->num_prims = (int32_t)N;
+    }
+    if (c->num_prims == 0)
+        for (int k = 0; k < 3; ++k) c->bmin[k] = c->bmax[k] = 0.0f;
+    c->has_scene = true;
+    return VR_OK;
+}
+
+uint32_t vr_num_tiles(uint32_t W, uint32_t H) { return ((W + kTile - 1) / kTile) * ((H + kTile - 1) / kTile); }
+
+vr_status vr_render(vr_ctx* c, const vr_camera* cam, const vr_render_params* p, uint32_t W, uint32_t H, float* rgb) {
+    if (!c || !rgb) return fail(VR_ERR_INVALID, "vr_render: NULL argument");
+    HIP_TRY(hipSetDevice(c->device), "hipSetDevice");
+    RenderArgs A;
+    vr_status st = fill_args(c, cam, p, W, H, A);
+    if (st != VR_OK) return st;
+    size_t bytes = (size_t)W * H * 3 * sizeof(float);
+    if (bytes > c->frame_cap) {
+        if (c->d_frame) (void)hipFree(c->d_frame);
+        c->d_frame = nullptr;
+        HIP_TRY(hipMalloc(&c->d_frame, bytes), "hipMalloc(frame)");
+        c->frame_cap = bytes;
+    }
+    A.first_tile = 0;
+    A.tile_stride = 1;
+    A.num_tiles = vr_num_tiles(W, H);
+    A.packed = 0;
+    A.out = c->d_frame;
+    st = launch(c, A, p, c->stream);
+    if (st != VR_OK) return st;
+    HIP_TRY(hipMemcpyAsync(rgb, c->d_frame, bytes, hipMemcpyDeviceToHost, c->stream), "hipMemcpyAsync(frame)");
+    HIP_TRY(hipStreamSynchronize(c->stream), "render");
+    c->stats_pending = false;
+    if (c->h_counters[1] != 0)
+        return fail(VR_ERR_OVERFLOW, std::to_string(c->h_counters[1]) + " pixels exceeded the active-set capacity (NaN)");
+    return VR_OK;
+}
+
+vr_status vr_render_tiles_device(vr_ctx* c, const vr_camera* cam, const vr_render_params* p, uint32_t W, uint32_t H,
+                                 uint32_t first_tile, uint32_t tile_stride, uint32_t num_tiles, int32_t packed,
+                                 float* d_out, void* stream) {
+    if (!c || !d_out) return fail(VR_ERR_INVALID, "vr_render_tiles_device: NULL argument");
+    HIP_TRY(hipSetDevice(c->device), "hipSetDevice");
+    RenderArgs A;
+    vr_status st = fill_args(c, cam, p, W, H, A);
+    if (st != VR_OK) return st;
+    uint32_t total = vr_num_tiles(W, H);
+    if (tile_stride == 0) return fail(VR_ERR_INVALID, "tile_stride must be >= 1");
+    if (num_tiles == 0) return VR_OK;
+    if ((uint64_t)first_tile + (uint64_t)(num_tiles - 1) * tile_stride >= total)
+        return fail(VR_ERR_INVALID, "tile range exceeds the frame");
+    if (num_tiles >= (1u << 24)) return fail(VR_ERR_INVALID, "too many tiles in one call");
+    A.first_tile = first_tile;
+    A.tile_stride = tile_stride;
+    A.num_tiles = num_tiles;
+    A.packed = packed ? 1 : 0;
+    A.out = d_out;
+    return launch(c, A, p, (hipStream_t)stream);
+}
+
+vr_status vr_unshuffle_tiles_device(vr_ctx* c, const float* d_slabs, uint32_t nslabs, uint32_t tiles_per_slab, uint32_t W,
+                                    uint32_t H, float* d_image, void* stream) {
+    if (!c || !d_slabs || !d_image || nslabs == 0) return fail(VR_ERR_INVALID, "vr_unshuffle_tiles_device: bad argument");
+    HIP_TRY(hipSetDevice(c->device), "hipSetDevice");
+    HIP_TRY(launch_unshuffle(d_slabs, nslabs, tiles_per_slab, (W + kTile - 1) / kTile, W, H, d_image, (hipStream_t)stream),
+            "unshuffle launch");
+    return VR_OK;
+}
+
+vr_status vr_synchronize(vr_ctx* c) {
+    if (!c) return fail(VR_ERR_INVALID, "vr_synchronize: NULL ctx");
+    HIP_TRY(hipSetDevice(c->device), "hipSetDevice");
+    HIP_TRY(hipDeviceSynchronize(), "hipDeviceSynchronize");
+    return VR_OK;
+}
+
+vr_status vr_get_stats(vr_ctx* c, vr_render_stats* o) {
+    if (!c || !o) return fail(VR_ERR_INVALID, "vr_get_stats: NULL argument");
+    HIP_TRY(hipSetDevice(c->device), "hipSetDevice");
+    HIP_TRY(hipEventSynchronize(c->ev_stop), "hipEventSynchronize");
+    c->stats_pending = false;
+    float ms = 0.0f;
+    HIP_TRY(hipEventElapsedTime(&ms, c->ev_start, c->ev_stop), "hipEventElapsedTime");
+    o->kernel_ms = ms;
+    o->pixels = c->last_pixels;
+    o->fallback_pixels = c->h_counters[0];
+    o->error_pixels = c->h_counters[1];
+    return VR_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,276 @@
+// Device-side building blocks of the ray-march kernels (gfx950, wave64).
+//
+// Floating point: the whole library is compiled with -ffp-contract=off and HIP's default
+// correctly rounded f32 division and square root, and every geometric expression below keeps
+// the reference's (Eigen 3.4) evaluation order. Ray origins/directions, ellipsoid entry/exit
+// distances t0/t1 and the march positions are therefore bit-identical to the CPU restatement,
+// which is what makes the discrete decisions (which Gaussian is active at which step, which
+// secondary event is the first one past a light) agree exactly. exp/erf come from the device
+// math library and differ from glibc by a few ulp; those only feed continuous quantities.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../vr_internal.h"
+
+namespace vr {
+namespace dev {
+
+struct Ray {
+    float ox, oy, oz, dx, dy, dz;
+};
+
+__device__ __forceinline__ float dot3(float a0, float a1, float a2, float b0, float b1, float b2) {
+    return a0 * b0 + (a1 * b1 + a2 * b2);
+}
+
+// Eigen normalized(): v / sqrt(squaredNorm) when squaredNorm > 0.
+__device__ __forceinline__ void normalize3(float& x, float& y, float& z) {
+    float s = dot3(x, y, z, x, y, z);
+    if (s > 0.0f) {
+        float r = sqrtf(s);
+        x = __fdiv_rn(x, r);
+        y = __fdiv_rn(y, r);
+        z = __fdiv_rn(z, r);
+    }
+}
+
+__device__ __forceinline__ Ray make_ray(float ox, float oy, float oz, float dx, float dy, float dz) {
+    normalize3(dx, dy, dz);  // ray.h:11-12
+    return Ray{ox, oy, oz, dx, dy, dz};
+}
+
+// camera.h:45-53 (pinhole) / :64-73 (orthographic); u,v = (x + 0.5f) / W, (y + 0.5f) / H.
+__device__ __forceinline__ Ray primary_ray(const RenderArgs& A, int x, int y) {
+    float uvx = __fdiv_rn((float)x + 0.5f, (float)A.width);
+    float uvy = __fdiv_rn((float)y + 0.5f, (float)A.height);
+    float u, v;
+    if (A.cam_type == 0) {
+        u = 1.0f - uvx * 2.0f;
+        v = uvy * 2.0f - 1.0f;
+    } else {
+        u = uvx * 2.0f - 1.0f;
+        v = 1.0f - uvy * 2.0f;
+    }
+    float o0 = (A.cam_pos[0] + u * A.cam_right[0]) + v * A.cam_up[0];
+    float o1 = (A.cam_pos[1] + u * A.cam_right[1]) + v * A.cam_up[1];
+    float o2 = (A.cam_pos[2] + u * A.cam_right[2]) + v * A.cam_up[2];
+    float d0, d1, d2;
+    if (A.cam_type == 0) {
+        d0 = A.cam_pinhole[0] - o0;
+        d1 = A.cam_pinhole[1] - o1;
+        d2 = A.cam_pinhole[2] - o2;
+    } else {
+        d0 = A.cam_view[0];
+        d1 = A.cam_view[1];
+        d2 = A.cam_view[2];
+    }
+    normalize3(d0, d1, d2);  // sample_ray's .normalized()
+    return make_ray(o0, o1, o2, d0, d1, d2);
+}
+
+// ---- Gaussian record access (3 x 16-B loads) ----
+struct GRec {
+    float mx, my, mz, density, m00, m01, m02, m11, m12, m22, norm, albedo;
+};
+__device__ __forceinline__ GRec load_rec(const GaussianRecord* __restrict__ g, int i) {
+    const float4* p = reinterpret_cast<const float4*>(g + i);
+    float4 a = p[0], b = p[1], c = p[2];
+    return GRec{a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w, c.x, c.y, c.z, c.w};
+}
+
+// Quadratic coefficients shared by intersect_direct and optical_depth (gaussian.h:126-136,
+// 208-218): A = d.Md, B = 2 p.Md, Cq = p.Mp with p = o - mean.
+struct Quad {
+    float A, B, Cq;
+};
+__device__ __forceinline__ Quad quad(const GRec& g, const Ray& r) {
+    float px = r.ox - g.mx, py = r.oy - g.my, pz = r.oz - g.mz;
+    // inv_cov * d, rows (M00 M01 M02), (M10 M11 M12), (M20 M21 M22); M symmetric
+    float mdx = g.m00 * r.dx + (g.m01 * r.dy + g.m02 * r.dz);
+    float mdy = g.m01 * r.dx + (g.m11 * r.dy + g.m12 * r.dz);
+    float mdz = g.m02 * r.dx + (g.m12 * r.dy + g.m22 * r.dz);
+    float mpx = g.m00 * px + (g.m01 * py + g.m02 * pz);
+    float mpy = g.m01 * px + (g.m11 * py + g.m12 * pz);
+    float mpz = g.m02 * px + (g.m12 * py + g.m22 * pz);
+    Quad q;
+    q.A = dot3(r.dx, r.dy, r.dz, mdx, mdy, mdz);
+    q.B = 2.0f * dot3(px, py, pz, mdx, mdy, mdz);
+    q.Cq = dot3(px, py, pz, mpx, mpy, mpz);
+    return q;
+}
+
+// Gaussian::intersect_direct (gaussian.h:126-164), R = 3.
+__device__ __forceinline__ bool intersect(const Quad& q, float& t_enter, float& t_exit) {
+    float C = q.Cq - 9.0f;
+    float disc = q.B * q.B - 4.0f * q.A * C;
+    if (disc < 0.0f) return false;
+    float sqrtD = sqrtf(disc);
+    float twoA = 2.0f * q.A;
+    float t0 = __fdiv_rn(-q.B - sqrtD, twoA);
+    float t1 = __fdiv_rn(-q.B + sqrtD, twoA);
+    if (t0 > t1) {
+        float tmp = t0;
+        t0 = t1;
+        t1 = tmp;
+    }
+    if (t1 < 0.0f) return false;
+    t_enter = (t0 >= 0.0f) ? t0 : 0.0f;
+    t_exit = t1;
+    return true;
+}
+
+// Gaussian::optical_depth (gaussian.h:208-231) for the same ray. The reference evaluates
+// sqrt(pi / (2A)) in double; f32 here (relative difference ~1 ulp).
+__device__ __forceinline__ float optical_depth(const GRec& g, const Quad& q, float t0, float t1) {
+    float twoA = 2.0f * q.A;
+    float pref = (g.density * g.norm) * sqrtf(__fdiv_rn(3.14159265358979323846f, twoA));
+    float den = 2.0f * sqrtf(twoA);
+    float F1 = erff(__fdiv_rn(q.B + twoA * t1, den));
+    float F0 = erff(__fdiv_rn(q.B + twoA * t0, den));
+    float e = expf(-0.5f * (q.Cq - __fdiv_rn(q.B * q.B, 4.0f * q.A)));
+    return pref * e * (F1 - F0);
+}
+
+// Gaussian::mu_t = density * evaluate(x) (gaussian.h:111-117), exponent -0.5 d^T M d with
+// Eigen's lazy-product order.
+__device__ __forceinline__ float mu_t(const GRec& g, float x, float y, float z) {
+    float d0 = x - g.mx, d1 = y - g.my, d2 = z - g.mz;
+    float l0 = -0.5f * d0, l1 = -0.5f * d1, l2 = -0.5f * d2;
+    float w0 = l0 * g.m00 + (l1 * g.m01 + l2 * g.m02);
+    float w1 = l0 * g.m01 + (l1 * g.m11 + l2 * g.m12);
+    float w2 = l0 * g.m02 + (l1 * g.m12 + l2 * g.m22);
+    float ex = w0 * d0 + (w1 * d1 + w2 * d2);
+    return g.density * (g.norm * expf(ex));
+}
+
+// ---- rng.h:13-57 ----
+__device__ __forceinline__ uint64_t splitmix64(uint64_t x) {
+    x += 0x9e3779b97f4a7c15ULL;
+    x = (x ^ (x >> 30)) * 0xbf58476d1ce4e5b9ULL;
+    x = (x ^ (x >> 27)) * 0x94d049bb133111ebULL;
+    return x ^ (x >> 31);
+}
+struct PCG32 {
+    uint64_t state, inc;
+    __device__ __forceinline__ PCG32(uint64_t seed_state, uint64_t seed_seq) {
+        state = 0;
+        inc = (seed_seq << 1) | 1;
+        next_u32();
+        state += seed_state;
+        next_u32();
+    }
+    __device__ __forceinline__ uint32_t next_u32() {
+        uint64_t old = state;
+        state = old * 6364136223846793005ULL + inc;
+        uint32_t shifted = (uint32_t)(((old >> 18u) ^ old) >> 27u);
+        uint32_t rot = (uint32_t)(old >> 59u);
+        return (shifted >> rot) | (shifted << ((-rot + 1u) & 31));
+    }
+    __device__ __forceinline__ float uniform() { return (float)(next_u32() >> 8) * (1.0f / 16777216.0f); }
+};
+__device__ __forceinline__ uint64_t derive_path_seed(int x, int y, int si) {
+    uint64_t seed = ((uint64_t)(uint32_t)si << 32) | ((uint64_t)(uint32_t)y << 16) | (uint64_t)(uint32_t)x;
+    return splitmix64(seed);
+}
+
+// Deterministic environment direction (replaces the non-reproducible
+// sample_uniform_direction_old, integrator.h:13-28; same distribution). Identical float
+// operations to oracle/vr_oracle.cpp env_dir.
+__device__ __forceinline__ void env_dir(float xi1, float xi2, float& x, float& y, float& z) {
+    z = 1.0f - 2.0f * xi2;
+    float s2 = (1.0f - z) * (1.0f + z);
+    float s = sqrtf(s2 > 0.0f ? s2 : 0.0f);
+    float t = xi1 * 4.0f;
+    float q = floorf(t + 0.5f);
+    float f = t - q;
+    float a = f * 1.57079632679489662f;
+    float a2 = a * a;
+    float sp = a * (1.0f + a2 * (-1.66666672e-1f + a2 * (8.33333377e-3f + a2 * (-1.98412701e-4f + a2 * 2.75573188e-6f))));
+    float cp = 1.0f + a2 * (-0.5f + a2 * (4.16666679e-2f + a2 * (-1.38888892e-3f + a2 * (2.48015876e-5f + a2 * -2.75573188e-7f))));
+    int qi = ((int)q) & 3;
+    float ct, st;
+    if (qi == 0) { ct = cp; st = sp; }
+    else if (qi == 1) { ct = -sp; st = cp; }
+    else if (qi == 2) { ct = -cp; st = -sp; }
+    else { ct = sp; st = -cp; }
+    x = s * ct;
+    y = s * st;
+}
+
+// Slab test against a child box; returns [tmin, tmax] (NaN-robust: fminf/fmaxf drop NaNs).
+__device__ __forceinline__ void slab(const float* b, const Ray& r, float ix, float iy, float iz, float& tmin, float& tmax) {
+    float tx1 = (b[0] - r.ox) * ix, tx2 = (b[3] - r.ox) * ix;
+    float ty1 = (b[1] - r.oy) * iy, ty2 = (b[4] - r.oy) * iy;
+    float tz1 = (b[2] - r.oz) * iz, tz2 = (b[5] - r.oz) * iz;
+    tmin = fmaxf(fmaxf(fminf(tx1, tx2), fminf(ty1, ty2)), fminf(tz1, tz2));
+    tmax = fminf(fminf(fmaxf(tx1, tx2), fmaxf(ty1, ty2)), fmaxf(tz1, tz2));
+}
+
+// Generic stack traversal of the child-pair BVH. `prune(tmin, tmax)` says whether a child box
+// whose ray interval is [tmin, tmax] (already known to satisfy tmax >= max(tmin, 0)) must be
+// visited; `leaf(first, count)` handles a leaf's primitive range. The stack lives in LDS with a
+// per-thread stride (bank-conflict-free: lane i uses word i of every row).
+template <class Prune, class Leaf>
+__device__ __forceinline__ void traverse(const BVHNode* __restrict__ nodes, const Ray& r, int* stack, int stride,
+                                         Prune prune, Leaf leaf) {
+    const float ix = __frcp_rn(r.dx), iy = __frcp_rn(r.dy), iz = __frcp_rn(r.dz);
+    int sp = 0;
+    int node = 0;
+    for (;;) {
+        const float4* np = reinterpret_cast<const float4*>(nodes + node);
+        float4 n0 = np[0], n1 = np[1], n2 = np[2];
+        int4 nc = reinterpret_cast<const int4*>(nodes + node)[3];
+        float bl[6] = {n0.x, n0.y, n0.z, n0.w, n1.x, n1.y};
+        float br[6] = {n1.z, n1.w, n2.x, n2.y, n2.z, n2.w};
+        float lmin, lmax, rmin, rmax;
+        slab(bl, r, ix, iy, iz, lmin, lmax);
+        slab(br, r, ix, iy, iz, rmin, rmax);
+        bool hl = nc.x != 0 && lmax >= fmaxf(lmin, 0.0f) && prune(lmin, lmax);
+        bool hr = nc.y != 0 && rmax >= fmaxf(rmin, 0.0f) && prune(rmin, rmax);
+        if (hl && ref_is_leaf(nc.x)) {
+            leaf(leaf_first(nc.x), leaf_count(nc.x));
+            hl = false;
+        }
+        if (hr && ref_is_leaf(nc.y)) {
+            leaf(leaf_first(nc.y), leaf_count(nc.y));
+            hr = false;
+        }
+        if (hl && hr) {
+            int nearer = nc.x, farther = nc.y;
+            if (rmin < lmin) {
+                nearer = nc.y;
+                farther = nc.x;
+            }
+            stack[sp * stride] = farther;
+            ++sp;
+            node = nearer;
+        } else if (hl) {
+            node = nc.x;
+        } else if (hr) {
+            node = nc.y;
+        } else {
+            if (sp == 0) break;
+            --sp;
+            node = stack[sp * stride];
+        }
+    }
+}
+
+// First index k with t_k >= a in the iterated step table (returns n if beyond the table).
+__device__ __forceinline__ int kfirst(const float* __restrict__ ts, int n, float step, float a) {
+    int k = (int)(a / step);
+    if (k < 0) k = 0;
+    if (k > n - 1) k = n - 1;
+    while (k > 0 && ts[k - 1] >= a) --k;
+    while (k < n && ts[k] < a) ++k;
+    return k;
+}
+
+}  // namespace dev
+}  // namespace vr
+
+// NOTE on rounding: HIP's __fsqrt_rn maps to __ocml_native_sqrt_f32 (approximate) unless
+// OCML_BASIC_ROUNDED_OPERATIONS is defined; plain sqrtf / '/' are correctly rounded under hipcc's
+// default -fhip-fp32-correctly-rounded-divide-sqrt, which is what the bit-exactness relies on
+// (verified against the CPU oracle by tests/test_gpu_parity.py::test_device_geometry_bit_exact).

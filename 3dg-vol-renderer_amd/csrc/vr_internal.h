@@ -1,0 +1,90 @@
+// Internal layouts shared by the host side (scene prep, BVH build, launch) and the HIP kernels.
+// Everything here is plain data: it is the HBM image of a scene.
+#pragma once
+#include <stdint.h>
+
+namespace vr {
+
+// ------------------------------------------------------------------------------------------
+// Gaussian record: 48 B = 3 x float4 (three 16-B loads, one 64-B sector pair when aligned).
+//   r0 = { mean.x, mean.y, mean.z, density }
+//   r1 = { M00, M01, M02, M11 }         M = Sigma^-1 (exactly symmetric, see vr_scene.cpp)
+//   r2 = { M12, M22, norm, albedo }     norm = (2pi)^-1.5 det^-0.5   (gaussian.h:52-55)
+// Stored in BVH leaf order (contiguous per leaf).
+// ------------------------------------------------------------------------------------------
+struct GaussianRecord {
+    float mx, my, mz, density;
+    float m00, m01, m02, m11;
+    float m12, m22, norm, albedo;
+};
+static_assert(sizeof(GaussianRecord) == 48, "record must be 48 B");
+
+// ------------------------------------------------------------------------------------------
+// BVH node, child-pair layout, 64 B: one node fetch tests both children.
+//   f[0..5]  = left  child box (min xyz, max xyz)
+//   f[6..11] = right child box
+//   c[0], c[1] = child refs: >= 0 internal node index; < 0 leaf:
+//                 leaf = 0x80000000 | (first << 4) | (count - 1), count <= 16, first < 2^27
+//   c[2], c[3] = unused (0)
+// Node 0 is the root pair. An empty child has an inverted box (+inf, -inf) and ref 0 (never hit).
+// ------------------------------------------------------------------------------------------
+struct BVHNode {
+    float f[12];
+    int32_t c[4];
+};
+static_assert(sizeof(BVHNode) == 64, "node must be 64 B");
+
+constexpr int kLeafMax = 4;          // primitives per leaf
+constexpr int kMaxDepth = 30;        // builder guarantees node depth <= kMaxDepth
+constexpr int kStackSize = 32;       // traversal stack entries (>= kMaxDepth + 1)
+constexpr int kTile = 16;            // pixel tile edge (one 256-thread workgroup per tile)
+
+__host__ __device__ inline bool ref_is_leaf(int32_t r) { return r < 0; }
+__host__ __device__ inline uint32_t leaf_first(int32_t r) { return ((uint32_t)r & 0x7fffffffu) >> 4; }
+__host__ __device__ inline uint32_t leaf_count(int32_t r) { return ((uint32_t)r & 15u) + 1u; }
+__host__ __device__ inline int32_t make_leaf(uint32_t first, uint32_t count) {
+    return (int32_t)(0x80000000u | (first << 4) | (count - 1u));
+}
+
+struct SphereRecord {  // 32 B
+    float cx, cy, cz, radius;
+    float sigma_a, sigma_s, pad0, pad1;
+};
+
+struct LightRecord {
+    float px, py, pz, ix, iy, iz;
+};
+
+constexpr int kMaxLights = 16;
+constexpr int kMaxSpheres = 64;
+
+// Kernel launch parameters (passed by value).
+struct RenderArgs {
+    // camera
+    int32_t cam_type;
+    float cam_pos[3], cam_view[3], cam_right[3], cam_up[3], cam_pinhole[3];
+    // frame / tiles
+    uint32_t width, height, tiles_x, first_tile, tile_stride, num_tiles;
+    int32_t packed;
+    float* out;
+    // scene
+    const GaussianRecord* gauss;
+    const BVHNode* nodes;
+    const SphereRecord* spheres;
+    int32_t num_prims;
+    int32_t num_lights;
+    LightRecord lights[kMaxLights];
+    float env[3];
+    // march
+    float step_size;
+    int32_t env_samples;
+    float t_eps;
+    const float* tsteps;  // iterated float step sequence t_k (test_integrators.h:184,289)
+    int32_t num_tsteps;
+    // fallback queue (active-set overflow) and error counters
+    uint32_t* queue;       // [0] = count, [1..] = packed pixel ids (tile_local << 8 | lane)
+    uint32_t queue_cap;
+    uint32_t* counters;    // [0] = error pixels
+};
+
+}  // namespace vr

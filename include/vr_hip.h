@@ -1,0 +1,193 @@
+/*
+ * vr_hip.h — C ABI of the MI355X-native forward volume renderer (libvr_hip.so).
+ *
+ * This is the drop-in boundary for the reference's forward render call
+ *     Integrator::render(const Scene&, Image&)            (include/integrator.h:49-57)
+ * of wantonsushi/3DG-vol-renderer. Plain C: opaque handles, plain structs, pointers and sizes,
+ * integer status codes, no exceptions and no C++/torch types across the boundary. The header-only
+ * C++ mirror of the reference API (3dg-vol-renderer_amd/include/vr/: Scene, Camera, Image,
+ * Integrator, HipRayMarchingGaussians ...) and the Python ctypes mirror (vr_amd) both sit on top
+ * of exactly these entry points. INTEGRATION.md shows the bindings.
+ *
+ * Every entry point returns VR_OK (0) on success; on failure it returns a non-zero vr_status and
+ * vr_last_error() (thread-local) describes why. The C++ wrappers turn a non-zero status into
+ * std::runtime_error, which is the reference's error convention (scene.h:47,79; image.h:26,30).
+ */
+#ifndef VR_HIP_H_
+#define VR_HIP_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define VR_ABI_VERSION 1
+
+typedef enum vr_status {
+    VR_OK = 0,
+    VR_ERR_INVALID = 1,     /* bad argument / inconsistent request */
+    VR_ERR_IO = 2,          /* cannot open / read / write a file */
+    VR_ERR_PARSE = 3,       /* malformed scene / XML / PPM */
+    VR_ERR_HIP = 4,         /* HIP runtime error (includes "no GPU") */
+    VR_ERR_NOSCENE = 5,     /* render before vr_upload_scene */
+    VR_ERR_OVERFLOW = 6,    /* a per-ray capacity (active set, stack, step table) was exceeded */
+    VR_ERR_UNSUPPORTED = 7  /* valid request the device path does not implement */
+} vr_status;
+
+/* scene.h:18-22 Scene::VolumeType */
+typedef enum vr_volume_type { VR_VOLUME_GAUSSIANS = 0, VR_VOLUME_SPHERES = 1 } vr_volume_type;
+
+/* camera.h:31 Pinhole_Camera, camera.h:58 Orthographic_Camera */
+typedef enum vr_camera_type { VR_CAMERA_PINHOLE = 0, VR_CAMERA_ORTHOGRAPHIC = 1 } vr_camera_type;
+
+/* Integrators with a device implementation. */
+typedef enum vr_integrator {
+    VR_RAYMARCH_GAUSSIANS = 0, /* RayMarchingGaussians  test_integrators.h:143-297 */
+    VR_RAYMARCH_SPHERES = 1,   /* RayMarchingSpheres    test_integrators.h:11-136  */
+    VR_TEST_HITMASK = 2        /* TestIntegrator        integrator.h:65-94         */
+} vr_integrator;
+
+/* Light (scene.h:12-15). */
+typedef struct vr_light {
+    float position[3];
+    float intensity[3];
+} vr_light;
+
+/* One 'g' record of a scene file / arguments of Gaussian(mean, cov, density, albedo, emission)
+ * (scene.h:91-113, gaussian.h:75-92). cov = {xx, xy, xz, yy, yz, zz}. Emission is carried for API
+ * parity but is never read by any reference integrator. */
+typedef struct vr_gaussian {
+    float mean[3];
+    float cov[6];
+    float density;
+    float albedo;
+    float emission[3];
+} vr_gaussian;
+
+/* Sphere(center, radius, sigma_a, sigma_s) (smm.h:17-27). */
+typedef struct vr_sphere {
+    float center[3];
+    float radius;
+    float sigma_a;
+    float sigma_s;
+} vr_sphere;
+
+/* Camera state after the reference constructors ran (camera.h:15-22, 38-43, 60-62). */
+typedef struct vr_camera {
+    int32_t type;        /* vr_camera_type */
+    float position[3];
+    float view_dir[3];   /* normalised member Camera::view_dir */
+    float right[3];
+    float up[3];
+    float pinhole[3];    /* pinhole cameras only */
+    float fov;
+    float focal_length;  /* 1 / tan(fov / 2) */
+} vr_camera;
+
+/* Render parameters = the integrator constructor arguments (test_integrators.h:17,149-153). */
+typedef struct vr_render_params {
+    int32_t integrator;   /* vr_integrator */
+    float step_size;      /* ray-march step (reference default 0.01) */
+    int32_t env_samples;  /* environment directions per scattering step (20 Gaussians, 5 spheres) */
+    float t_eps;          /* stop a ray once T <= t_eps; 0 = exact (stop only when T == 0) */
+    uint32_t flags;       /* reserved, must be 0 */
+} vr_render_params;
+
+typedef struct vr_scene_info {
+    int32_t volume_type;  /* vr_volume_type */
+    int64_t num_primitives;
+    int64_t num_lights;
+    float env_color[3];
+    float bounds_min[3];  /* union of the primitives' 3-sigma / sphere boxes */
+    float bounds_max[3];
+} vr_scene_info;
+
+/* Statistics of the last vr_render / vr_render_tiles_device call on a context. */
+typedef struct vr_render_stats {
+    double kernel_ms;         /* device time of the render kernels (HIP events) */
+    int64_t pixels;           /* pixels rendered */
+    int64_t fallback_pixels;  /* pixels re-run on the large-capacity path (active-set overflow) */
+    int64_t error_pixels;     /* pixels that exceeded every capacity (output NaN) */
+} vr_render_stats;
+
+typedef struct vr_scene vr_scene; /* host-side scene: primitives, lights, env colour */
+typedef struct vr_ctx vr_ctx;     /* device context: one GPU, uploaded scene, workspaces */
+
+/* ---------------- library ---------------- */
+const char* vr_version(void);
+/* Thread-local description of the last failure of any vr_* call on this thread. */
+const char* vr_last_error(void);
+
+/* ---------------- host scene (scene.h) ---------------- */
+vr_status vr_scene_create(int32_t volume_type, vr_scene** out);
+/* Scene::load_GMM (scene.h:72-120), incl. its skip-unknown-token and emission-peek behaviour. */
+vr_status vr_scene_load_gmm(const char* path, vr_scene** out);
+/* Scene::load_SMM (scene.h:38-68). */
+vr_status vr_scene_load_smm(const char* path, vr_scene** out);
+/* Mitsuba-3 subset used by tests/env_one_sphere_test_ortho.xml (no reference equivalent; the
+ * reference rendered that XML in Mitsuba). Fills the scene, camera, film size and parameters.
+ * Any output pointer may be NULL. */
+vr_status vr_scene_load_xml(const char* path, vr_scene** out, vr_camera* camera, uint32_t* width,
+                            uint32_t* height, vr_render_params* params);
+vr_status vr_scene_add_gaussians(vr_scene* s, const vr_gaussian* g, size_t n);
+vr_status vr_scene_add_spheres(vr_scene* s, const vr_sphere* sp, size_t n);
+vr_status vr_scene_add_lights(vr_scene* s, const vr_light* l, size_t n);
+vr_status vr_scene_set_env_color(vr_scene* s, const float rgb[3]);
+vr_status vr_scene_get_info(const vr_scene* s, vr_scene_info* out);
+/* Gaussian precompute (gaussian.h:52-55): 12 floats per Gaussian, in scene order:
+ * mean[3], density, inv_cov{00,01,02,11,12,22}, norm, albedo. */
+vr_status vr_scene_get_records(const vr_scene* s, float* out, size_t n);
+vr_status vr_scene_get_lights(const vr_scene* s, vr_light* out, size_t n);
+vr_status vr_scene_get_gaussians(const vr_scene* s, vr_gaussian* out, size_t n);
+vr_status vr_scene_get_spheres(const vr_scene* s, vr_sphere* out, size_t n);
+void vr_scene_destroy(vr_scene* s);
+
+/* ---------------- camera (camera.h) ---------------- */
+vr_status vr_camera_pinhole(const float position[3], const float view_dir[3], float fov, vr_camera* out);
+vr_status vr_camera_orthographic(const float position[3], const float forward[3], vr_camera* out);
+/* Camera::sample_ray (camera.h:45-53, 64-73) followed by Ray's normalisation (ray.h:11-12). */
+vr_status vr_camera_sample_ray(const vr_camera* c, double u, double v, float origin[3], float direction[3]);
+
+/* ---------------- image (image.h) ---------------- */
+/* Image::make_PPM (image.h:62-84): 8-bit P6 with clamp(v*255) truncation. rgb is 3*W*H floats. */
+vr_status vr_image_write_ppm(const char* path, const float* rgb, uint32_t width, uint32_t height);
+/* Image(const std::string&) (image.h:24-45): P6 reader; rgb must hold 3*W*H floats. Pass rgb=NULL
+ * to query width/height only. */
+vr_status vr_image_read_ppm(const char* path, float* rgb, uint32_t* width, uint32_t* height);
+
+/* ---------------- device ---------------- */
+vr_status vr_init(int device, vr_ctx** out);
+void vr_destroy(vr_ctx* ctx);
+/* Prepare (BVH build) and upload the scene; replaces any previous one. Host copies are not kept. */
+vr_status vr_upload_scene(vr_ctx* ctx, const vr_scene* s);
+/* Integrator::render(scene, image): full W x H frame into rgb_host (3*W*H floats, row-major,
+ * idx = 3*(y*W + x) as image.h:13-17). Synchronous. */
+vr_status vr_render(vr_ctx* ctx, const vr_camera* cam, const vr_render_params* p, uint32_t width,
+                    uint32_t height, float* rgb_host);
+/* Multi-GPU building block (asynchronous on `stream`, a hipStream_t or NULL for the default).
+ * The frame is cut into 16x16 tiles numbered row-major; this call renders tiles
+ * first_tile, first_tile + tile_stride, ... (num_tiles of them). If `packed` is non-zero the
+ * output is a slab of num_tiles * 256 pixels (tile-major, row-major inside a tile, 3 floats per
+ * pixel; pixels outside the frame are written as 0); otherwise `d_out` is the full W x H frame and
+ * only those tiles' pixels are written. d_out is device memory. */
+vr_status vr_render_tiles_device(vr_ctx* ctx, const vr_camera* cam, const vr_render_params* p,
+                                 uint32_t width, uint32_t height, uint32_t first_tile,
+                                 uint32_t tile_stride, uint32_t num_tiles, int32_t packed,
+                                 float* d_out, void* stream);
+/* Scatter `nslabs` packed slabs (slab r = tiles r, r+nslabs, ...; each tiles_per_slab * 256 px)
+ * into the row-major W x H frame d_image. Asynchronous on `stream`. */
+vr_status vr_unshuffle_tiles_device(vr_ctx* ctx, const float* d_slabs, uint32_t nslabs,
+                                    uint32_t tiles_per_slab, uint32_t width, uint32_t height,
+                                    float* d_image, void* stream);
+/* Number of 16x16 tiles of a W x H frame. */
+uint32_t vr_num_tiles(uint32_t width, uint32_t height);
+vr_status vr_synchronize(vr_ctx* ctx);
+vr_status vr_get_stats(vr_ctx* ctx, vr_render_stats* out);
+
+#ifdef __cplusplus
+} /* extern "C" */
+#endif
+
+#endif /* VR_HIP_H_ */

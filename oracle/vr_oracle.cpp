@@ -1,0 +1,968 @@
+// =================================================================================================
+//  vr_oracle.cpp — TEST INFRASTRUCTURE ONLY.
+//
+//  A line-faithful CPU restatement of wantonsushi/3DG-vol-renderer's forward ray-march path, used
+//  ONLY as the checker by tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg. It is
+//  never linked into, loaded by, or called from the product (libvr_hip.so / vr_amd). The product
+//  path fails loudly when its HIP extension is missing; it never falls back to this file.
+//
+//  Parity status:
+//    * The reference cannot be built here (Eigen 3.4.0 / gif-h are empty submodules, no network).
+//      This file restates the algorithm from the reference sources, citing file:line, and
+//      restates the Eigen 3.4.0 operations it relies on (evaluation order of 3-term reductions,
+//      3x3 inverse/determinant) from Eigen's published algorithm. Bits at the Eigen boundary are
+//      therefore "parity unpinned"; the restatement is pinned against the reference's own golden
+//      renders (tests/golden/renders/*.ppm, produced by the reference) statistically and by the
+//      exact miss-mask known-answer test (tests/test_oracle_golden.py).
+//    * Documented deviation: the reference samples environment directions from a thread-local
+//      std::mt19937 seeded by std::random_device (integrator.h:13-28) and is therefore not
+//      reproducible. Here env directions come from the reference's own PCG32 (rng.h:20-57) keyed
+//      by (pixel x, pixel y, march-step index) and a trig-free mapping of the same uniform-sphere
+//      distribution (env_dir below). The GPU path implements the identical sampler so that GPU and
+//      oracle agree per pixel.
+//
+//  Build: oracle/Makefile  (g++ -O3 -ffp-contract=off -fopenmp, shared library, C ABI for ctypes).
+// =================================================================================================
+#include <algorithm>
+#include <cmath>
+#include <cstdint>
+#include <cstdio>
+#include <cstring>
+#include <fstream>
+#include <limits>
+#include <numbers>
+#include <sstream>
+#include <stdexcept>
+#include <string>
+#include <vector>
+#include <omp.h>
+
+namespace orc {
+
+// ---------------------------------------------------------------------------------------------
+// Minimal fixed-size float vector/matrix with Eigen 3.4 evaluation order.
+//   dot / squaredNorm / sum of 3 terms: Eigen redux_novec_unroller splits 3 as 1 + 2, i.e.
+//   e0 + (e1 + e2). Matrix3f * Vector3f (lazy coeff product) rows use the same reduction.
+//   normalized(): v / sqrt(squaredNorm()) when squaredNorm() > 0 (Eigen Dot.h).
+// ---------------------------------------------------------------------------------------------
+struct V3 {
+    float x, y, z;
+    float operator[](int i) const { return i == 0 ? x : (i == 1 ? y : z); }
+    float& operator[](int i) { return i == 0 ? x : (i == 1 ? y : z); }
+};
+static inline V3 operator+(V3 a, V3 b) { return {a.x + b.x, a.y + b.y, a.z + b.z}; }
+static inline V3 operator-(V3 a, V3 b) { return {a.x - b.x, a.y - b.y, a.z - b.z}; }
+static inline V3 operator*(float s, V3 a) { return {s * a.x, s * a.y, s * a.z}; }
+static inline V3 operator/(V3 a, float s) { return {a.x / s, a.y / s, a.z / s}; }
+static inline float dot(V3 a, V3 b) { return a.x * b.x + (a.y * b.y + a.z * b.z); }
+static inline float sqnorm(V3 a) { return dot(a, a); }
+static inline float norm(V3 a) { return std::sqrt(sqnorm(a)); }
+static inline V3 normalized(V3 a) {
+    float z = sqnorm(a);
+    if (z > 0.0f) return a / std::sqrt(z);
+    return a;
+}
+static inline V3 cross(V3 l, V3 r) {  // Eigen OrthoMethods.h cross()
+    return {l.y * r.z - l.z * r.y, l.z * r.x - l.x * r.z, l.x * r.y - l.y * r.x};
+}
+struct M3 {  // row-major
+    float m[3][3];
+    float operator()(int i, int j) const { return m[i][j]; }
+};
+static inline V3 mul(const M3& M, V3 v) {
+    return {M.m[0][0] * v.x + (M.m[0][1] * v.y + M.m[0][2] * v.z),
+            M.m[1][0] * v.x + (M.m[1][1] * v.y + M.m[1][2] * v.z),
+            M.m[2][0] * v.x + (M.m[2][1] * v.y + M.m[2][2] * v.z)};
+}
+// Eigen InverseImpl.h cofactor_3x3<M,i,j>
+static inline float cofactor(const M3& m, int i, int j) {
+    int i1 = (i + 1) % 3, i2 = (i + 2) % 3, j1 = (j + 1) % 3, j2 = (j + 2) % 3;
+    return m(i1, j1) * m(i2, j2) - m(i1, j2) * m(i2, j1);
+}
+// Eigen InverseImpl.h compute_inverse<..., 3>::run + compute_inverse_size3_helper
+static inline M3 inverse3(const M3& m) {
+    float c00 = cofactor(m, 0, 0), c10 = cofactor(m, 1, 0), c20 = cofactor(m, 2, 0);
+    float det = c00 * m(0, 0) + (c10 * m(1, 0) + c20 * m(2, 0));
+    float invdet = 1.0f / det;
+    M3 r;
+    float c01 = cofactor(m, 0, 1) * invdet;
+    float c11 = cofactor(m, 1, 1) * invdet;
+    float c02 = cofactor(m, 0, 2) * invdet;
+    r.m[1][2] = cofactor(m, 2, 1) * invdet;
+    r.m[2][1] = cofactor(m, 1, 2) * invdet;
+    r.m[2][2] = cofactor(m, 2, 2) * invdet;
+    r.m[1][0] = c01;
+    r.m[1][1] = c11;
+    r.m[2][0] = c02;
+    r.m[0][0] = c00 * invdet;
+    r.m[0][1] = c10 * invdet;
+    r.m[0][2] = c20 * invdet;
+    return r;
+}
+// Eigen Determinant.h determinant_impl<Derived,3> / bruteforce_det3_helper
+static inline float det3_helper(const M3& m, int a, int b, int c) {
+    return m(0, a) * (m(1, b) * m(2, c) - m(1, c) * m(2, b));
+}
+static inline float determinant3(const M3& m) {
+    return det3_helper(m, 0, 1, 2) - det3_helper(m, 1, 0, 2) + det3_helper(m, 2, 0, 1);
+}
+
+// ---------------------------------------------------------------------------------------------
+// rng.h:13-57 — splitmix64, non-standard PCG32 (rotation (-rot+1u)&31 at rng.h:43), path seed.
+// ---------------------------------------------------------------------------------------------
+static inline uint64_t splitmix64(uint64_t x) {
+    x += 0x9e3779b97f4a7c15ULL;
+    x = (x ^ (x >> 30)) * 0xbf58476d1ce4e5b9ULL;
+    x = (x ^ (x >> 27)) * 0x94d049bb133111ebULL;
+    return x ^ (x >> 31);
+}
+struct PCG32 {
+    uint64_t state, inc;
+    PCG32(uint64_t seed_state, uint64_t seed_seq) {
+        state = 0;
+        inc = (seed_seq << 1) | 1;
+        next_u32();
+        state += seed_state;
+        next_u32();
+    }
+    uint32_t next_u32() {
+        uint64_t old = state;
+        state = old * 6364136223846793005ULL + inc;
+        uint32_t shifted = (uint32_t)(((old >> 18u) ^ old) >> 27u);
+        uint32_t rot = (uint32_t)(old >> 59u);
+        return (shifted >> rot) | (shifted << ((-rot + 1u) & 31));
+    }
+    float uniform() { return (next_u32() >> 8) * (1.0f / 16777216.0f); }
+};
+static inline uint64_t derive_path_seed(int x, int y, int sample_index) {
+    uint64_t seed = (uint64_t(sample_index) << 32) | (uint64_t(y) << 16) | (uint64_t(x));
+    return splitmix64(seed);
+}
+
+// Deterministic replacement for sample_uniform_direction_old (integrator.h:13-28): same
+// distribution (theta = 2 pi xi1, cos(phi) = 1 - 2 xi2), evaluated trig-free for phi and with a
+// fixed polynomial for theta so that the GPU implementation is bit-identical.
+static inline void sincos_2pi(float u, float* c, float* s) {
+    float t = u * 4.0f;
+    float q = std::floor(t + 0.5f);
+    float f = t - q;                          // [-0.5, 0.5]
+    float a = f * 1.57079632679489662f;       // [-pi/4, pi/4]
+    float a2 = a * a;
+    float sp = a * (1.0f + a2 * (-1.66666672e-1f + a2 * (8.33333377e-3f + a2 * (-1.98412701e-4f + a2 * 2.75573188e-6f))));
+    float cp = 1.0f + a2 * (-0.5f + a2 * (4.16666679e-2f + a2 * (-1.38888892e-3f + a2 * (2.48015876e-5f + a2 * -2.75573188e-7f))));
+    int qi = ((int)q) & 3;
+    if (qi == 0) { *c = cp; *s = sp; }
+    else if (qi == 1) { *c = -sp; *s = cp; }
+    else if (qi == 2) { *c = -cp; *s = -sp; }
+    else { *c = sp; *s = -cp; }
+}
+static inline V3 env_dir(float xi1, float xi2) {
+    float z = 1.0f - 2.0f * xi2;
+    float s2 = (1.0f - z) * (1.0f + z);
+    float s = std::sqrt(s2 > 0.0f ? s2 : 0.0f);
+    float ct, st;
+    sincos_2pi(xi1, &ct, &st);
+    return {s * ct, s * st, z};
+}
+
+// ---------------------------------------------------------------------------------------------
+// ray.h:7-16 — direction normalised in the constructor.
+// ---------------------------------------------------------------------------------------------
+struct Ray {
+    V3 origin, direction;
+    Ray() {}
+    Ray(V3 o, V3 d) : origin(o), direction(normalized(d)) {}
+};
+
+// ---------------------------------------------------------------------------------------------
+// camera.h:7-74. NB the base ctor body uses the *parameter* view_dir (unnormalised) for right/up
+// (camera.h:20-21); Pinhole uses the parameter for the pinhole point (camera.h:42).
+// ---------------------------------------------------------------------------------------------
+struct Camera {
+    int type = 0;  // 0 pinhole, 1 orthographic
+    V3 position, view_dir, right, up, pinhole;
+    float focal_length = 0.0f;
+    void base(V3 pos, V3 vd) {
+        position = pos;
+        view_dir = normalized(vd);
+        const V3 world_up{0.0f, 1.0f, 0.0f};
+        right = normalized(cross(vd, world_up));
+        up = normalized(cross(right, vd));
+    }
+    static Camera make_pinhole(V3 pos, V3 vd, float fov) {
+        Camera c;
+        c.base(pos, vd);
+        c.type = 0;
+        c.focal_length = 1.0f / std::tan(0.5f * fov);
+        c.pinhole = pos + c.focal_length * vd;
+        return c;
+    }
+    static Camera make_ortho(V3 pos, V3 fwd) {
+        Camera c;
+        c.base(pos, fwd);
+        c.type = 1;
+        return c;
+    }
+    Ray sample_ray(double uvx, double uvy) const {
+        if (type == 0) {  // camera.h:45-53
+            float u = 1.0f - static_cast<float>(uvx) * 2.0f;
+            float v = static_cast<float>(uvy) * 2.0f - 1.0f;
+            V3 o = position + u * right + v * up;
+            V3 d = pinhole - o;
+            return Ray(o, normalized(d));
+        } else {  // camera.h:64-73
+            float u = static_cast<float>(uvx) * 2.0f - 1.0f;
+            float v = 1.0f - static_cast<float>(uvy) * 2.0f;
+            V3 o = position + u * right + v * up;
+            V3 d = view_dir;
+            return Ray(o, normalized(d));
+        }
+    }
+};
+
+// ---------------------------------------------------------------------------------------------
+// gaussian.h:28-321 — only the members used by the forward integrators.
+// ---------------------------------------------------------------------------------------------
+static constexpr float R = 3.0f;  // gaussian.h:36
+struct Gaussian {
+    V3 mean;
+    M3 cov;
+    float density, albedo;
+    M3 inv_cov;
+    float norm;
+    V3 bmin, bmax;  // conservative AABB (see BuildBVH note)
+
+    Gaussian(V3 mean_, const M3& cov_, float density_, float albedo_)
+        : mean(mean_), cov(cov_), density(density_), albedo(albedo_) {
+        // gaussian.h:52-55
+        inv_cov = inverse3(cov);
+        float det_cov = determinant3(cov);
+        norm = std::pow(2.0f * std::numbers::pi, -1.5f) * std::pow(det_cov, -0.5f);
+        // AABB: tight 3-sigma box of the ellipsoid, +-R*sqrt(Sigma_kk), padded. The reference
+        // derives a looser box from the eigen-decomposition (gaussian.h:304-319); both are
+        // conservative, so the BVH event SET (what the integrators consume) is identical.
+        for (int k = 0; k < 3; ++k) {
+            float h = R * std::sqrt(std::max(cov(k, k), 0.0f));
+            h = h * 1.05f + 1e-6f;
+            bmin[k] = mean[k] - h;
+            bmax[k] = mean[k] + h;
+        }
+    }
+    // gaussian.h:111-117
+    float evaluate(V3 x) const {
+        V3 d = x - mean;
+        // (-0.5f * d^T) * inv_cov * d, coefficient-wise lazy products (1+2 reductions)
+        V3 l{-0.5f * d.x, -0.5f * d.y, -0.5f * d.z};
+        V3 w{l.x * inv_cov(0, 0) + (l.y * inv_cov(1, 0) + l.z * inv_cov(2, 0)),
+             l.x * inv_cov(0, 1) + (l.y * inv_cov(1, 1) + l.z * inv_cov(2, 1)),
+             l.x * inv_cov(0, 2) + (l.y * inv_cov(1, 2) + l.z * inv_cov(2, 2))};
+        float exponent = w.x * d.x + (w.y * d.y + w.z * d.z);
+        return norm * std::exp(exponent);
+    }
+    float mu_t(V3 x) const { return density * evaluate(x); }
+    // gaussian.h:126-164
+    bool intersect_direct(const Ray& ray, float& t_enter, float& t_exit) const {
+        V3 p = ray.origin - mean;
+        V3 Md = mul(inv_cov, ray.direction);
+        V3 Mp = mul(inv_cov, p);
+        float A = dot(ray.direction, Md);
+        float B = 2.0f * dot(p, Md);
+        float C = dot(p, Mp) - (R * R);
+        float discriminant = B * B - 4.0f * A * C;
+        if (discriminant < 0.0f) return false;
+        float sqrtD = std::sqrt(discriminant);
+        float t0 = (-B - sqrtD) / (2.0f * A);
+        float t1 = (-B + sqrtD) / (2.0f * A);
+        if (t0 > t1) std::swap(t0, t1);
+        if (t1 < 0.0f) return false;
+        t_enter = (t0 >= 0.0f) ? t0 : 0.0f;
+        t_exit = t1;
+        return true;
+    }
+    // gaussian.h:208-231
+    float optical_depth(const Ray& ray, float t0, float t1) const {
+        V3 p = ray.origin - mean;
+        V3 Md = mul(inv_cov, ray.direction);
+        V3 Mp = mul(inv_cov, p);
+        float A = dot(ray.direction, Md);
+        float B = 2.0f * dot(p, Md);
+        float C = dot(p, Mp);
+        float pref = density * norm * std::sqrt(std::numbers::pi / (2.0f * A));
+        auto F = [&](float t) {
+            float arg = (B + 2.0f * A * t) / (2.0f * std::sqrt(2.0f * A));
+            return std::erf(arg);
+        };
+        return pref * std::exp(-0.5f * (C - B * B / (4.0f * A))) * (F(t1) - F(t0));
+    }
+};
+
+// smm.h:7-15
+struct PrimitiveHitEvent {
+    float t;
+    bool entering;
+    size_t index;
+    bool operator<(const PrimitiveHitEvent& o) const { return t < o.t; }
+};
+
+// ---------------------------------------------------------------------------------------------
+// gmm.h:35-578 — mixture + midpoint-split BVH (leaf <= 4; SAH compiled out, gmm.h:162).
+// ---------------------------------------------------------------------------------------------
+struct GMM {
+    struct Node {
+        V3 bmin{INFINITY, INFINITY, INFINITY}, bmax{-INFINITY, -INFINITY, -INFINITY};
+        uint32_t leftFirst = 0, count = 0;
+        bool isLeaf() const { return count > 0; }
+    };
+    std::vector<Gaussian> gaussians;
+    std::vector<uint32_t> indices;
+    std::vector<Node> nodes;
+
+    static float IntersectAABB(const Ray& ray, V3 bmin, V3 bmax) {  // gmm.h:48-63
+        V3 rD{1.0f / ray.direction.x, 1.0f / ray.direction.y, 1.0f / ray.direction.z};
+        float tx1 = (bmin.x - ray.origin.x) * rD.x;
+        float tx2 = (bmax.x - ray.origin.x) * rD.x;
+        float tmin = std::min(tx1, tx2), tmax = std::max(tx1, tx2);
+        float ty1 = (bmin.y - ray.origin.y) * rD.y;
+        float ty2 = (bmax.y - ray.origin.y) * rD.y;
+        tmin = std::max(tmin, std::min(ty1, ty2));
+        tmax = std::min(tmax, std::max(ty1, ty2));
+        float tz1 = (bmin.z - ray.origin.z) * rD.z;
+        float tz2 = (bmax.z - ray.origin.z) * rD.z;
+        tmin = std::max(tmin, std::min(tz1, tz2));
+        tmax = std::min(tmax, std::max(tz1, tz2));
+        if (tmax >= tmin && tmin < std::numeric_limits<float>::infinity() && tmax > 0.0f) return tmin;
+        return std::numeric_limits<float>::infinity();
+    }
+    void UpdateNodeBounds(uint32_t ni) {
+        Node& n = nodes[ni];
+        n.bmin = {INFINITY, INFINITY, INFINITY};
+        n.bmax = {-INFINITY, -INFINITY, -INFINITY};
+        for (uint32_t i = 0; i < n.count; ++i) {
+            const Gaussian& g = gaussians[indices[n.leftFirst + i]];
+            for (int k = 0; k < 3; ++k) {
+                n.bmin[k] = std::min(n.bmin[k], g.bmin[k]);
+                n.bmax[k] = std::max(n.bmax[k], g.bmax[k]);
+            }
+        }
+    }
+    void BuildBVH() {  // gmm.h:231-260
+        uint32_t N = (uint32_t)gaussians.size();
+        indices.resize(N);
+        for (uint32_t i = 0; i < N; ++i) indices[i] = i;
+        nodes.clear();
+        nodes.reserve(std::max<size_t>(1, 2 * N));
+        nodes.emplace_back();
+        nodes[0].leftFirst = 0;
+        nodes[0].count = N;
+        UpdateNodeBounds(0);
+        // iterative version of SubdivideNode (gmm.h:318-446, midpoint branch) — same splits
+        std::vector<uint32_t> todo{0};
+        while (!todo.empty()) {
+            uint32_t ni = todo.back();
+            todo.pop_back();
+            Node node = nodes[ni];
+            if (node.count <= 4) continue;
+            V3 e = node.bmax - node.bmin;
+            int axis = (e.y > e.x) ? 1 : 0;
+            if (e.z > e[axis]) axis = 2;
+            float splitPos = 0.5f * (node.bmin[axis] + node.bmax[axis]);
+            int64_t i = node.leftFirst;
+            int64_t j = i + node.count - 1;
+            while (i <= j) {
+                if (gaussians[indices[i]].mean[axis] < splitPos) ++i;
+                else { std::swap(indices[i], indices[j]); --j; }
+            }
+            uint32_t leftCount = (uint32_t)(i - node.leftFirst);
+            if (leftCount == 0 || leftCount == node.count) continue;
+            uint32_t l = (uint32_t)nodes.size();
+            nodes.emplace_back();
+            uint32_t r = (uint32_t)nodes.size();
+            nodes.emplace_back();
+            nodes[l].leftFirst = node.leftFirst;
+            nodes[l].count = leftCount;
+            nodes[r].leftFirst = node.leftFirst + leftCount;
+            nodes[r].count = node.count - leftCount;
+            nodes[ni].leftFirst = l;
+            nodes[ni].count = 0;
+            UpdateNodeBounds(l);
+            UpdateNodeBounds(r);
+            todo.push_back(r);
+            todo.push_back(l);
+        }
+    }
+    // gmm.h:457-515
+    void intersect_events(const Ray& ray, std::vector<PrimitiveHitEvent>& out) const {
+        out.clear();
+        if (gaussians.empty() || nodes.empty()) return;
+        std::vector<int> stack;
+        stack.reserve(64);
+        stack.push_back(0);
+        const float inf = std::numeric_limits<float>::infinity();
+        while (!stack.empty()) {
+            int ni = stack.back();
+            stack.pop_back();
+            const Node& node = nodes[ni];
+            float tmin = IntersectAABB(ray, node.bmin, node.bmax);
+            if (tmin == inf) continue;
+            if (node.isLeaf()) {
+                for (int ii = 0; ii < (int)node.count; ++ii) {
+                    uint32_t gidx = indices[node.leftFirst + ii];
+                    float t0, t1;
+                    if (gaussians[gidx].intersect_direct(ray, t0, t1)) {
+                        if (t0 >= 0.0f) out.push_back({t0, true, gidx});
+                        if (t1 >= 0.0f) out.push_back({t1, false, gidx});
+                    }
+                }
+            } else {
+                int li = (int)node.leftFirst, ri = li + 1;
+                float dl = IntersectAABB(ray, nodes[li].bmin, nodes[li].bmax);
+                float dr = IntersectAABB(ray, nodes[ri].bmin, nodes[ri].bmax);
+                if (dl > dr) {
+                    if (dl != inf) stack.push_back(li);
+                    if (dr != inf) stack.push_back(ri);
+                } else {
+                    if (dr != inf) stack.push_back(ri);
+                    if (dl != inf) stack.push_back(li);
+                }
+            }
+        }
+        if (!out.empty())
+            std::sort(out.begin(), out.end(), [](const PrimitiveHitEvent& a, const PrimitiveHitEvent& b) { return a.t < b.t; });
+    }
+    // gmm.h:98-126
+    void evaluate_sigma(const std::vector<bool>& active, V3 pos, float& sigma_a, float& sigma_s) const {
+        float sum_mu_t = 0.0f, sum_mu_t_alb = 0.0f;
+        for (size_t i = 0; i < gaussians.size(); ++i) {
+            if (!active[i]) continue;
+            float mu_t_i = gaussians[i].mu_t(pos);
+            sum_mu_t += mu_t_i;
+            sum_mu_t_alb += mu_t_i * gaussians[i].albedo;
+        }
+        if (sum_mu_t <= 0.0f) { sigma_s = sigma_a = 0.0f; return; }
+        float a_mix = sum_mu_t_alb / sum_mu_t;
+        sigma_s = a_mix * sum_mu_t;
+        sigma_a = (1.0f - a_mix) * sum_mu_t;
+    }
+    // gmm.h:146-157
+    float transmittance_over_segment(const Ray& ray, float t0, float t1, const std::vector<size_t>& act) const {
+        float s = 0.0f;
+        for (size_t i : act) s += gaussians[i].optical_depth(ray, t0, t1);
+        return std::exp(-s);
+    }
+};
+
+// smm.h:17-103
+struct Sphere {
+    V3 center;
+    float radius, sigma_a, sigma_s;
+    bool intersect(const Ray& ray, float& t_enter, float& t_exit) const {  // smm.h:29-39
+        V3 L = center - ray.origin;
+        float tca = dot(L, ray.direction);
+        float d2 = sqnorm(L) - tca * tca;
+        float r2 = radius * radius;
+        if (d2 > r2) return false;
+        float thc = std::sqrt(r2 - d2);
+        t_enter = tca - thc;
+        t_exit = tca + thc;
+        return t_exit >= 0.0f;
+    }
+};
+struct SMM {
+    std::vector<Sphere> spheres;
+    void intersect_events(const Ray& ray, std::vector<PrimitiveHitEvent>& out) const {  // smm.h:54-63
+        for (size_t i = 0; i < spheres.size(); ++i) {
+            float a, b;
+            if (spheres[i].intersect(ray, a, b)) {
+                if (a >= 0.0f) out.push_back({a, true, i});
+                if (b >= 0.0f) out.push_back({b, false, i});
+            }
+        }
+        std::sort(out.begin(), out.end());
+    }
+    void evaluate_sigma(const std::vector<bool>& active, float& sa, float& ss) const {  // :66-76
+        sa = 0.0f; ss = 0.0f;
+        for (size_t i = 0; i < spheres.size(); ++i)
+            if (active[i]) { sa += spheres[i].sigma_a; ss += spheres[i].sigma_s; }
+    }
+    float transmittance_from_events(const Ray&, const std::vector<PrimitiveHitEvent>& events, float tmax) const {  // :79-103
+        float T = 1.0f;
+        std::vector<bool> active(spheres.size(), false);
+        float t_prev = 0.0f;
+        for (const auto& e : events) {
+            if (e.t > tmax) break;
+            float dt = e.t - t_prev;
+            float sigma_t = 0.0f;
+            for (size_t i = 0; i < spheres.size(); ++i)
+                if (active[i]) sigma_t += spheres[i].sigma_a + spheres[i].sigma_s;
+            T *= std::exp(-sigma_t * dt);
+            active[e.index] = e.entering;
+            t_prev = e.t;
+        }
+        return T;
+    }
+};
+
+struct Light { V3 position, intensity; };
+
+struct Scene {
+    int volume_type = 0;  // 0 gaussians, 1 spheres
+    GMM gmm;
+    SMM smm;
+    std::vector<Light> lights;
+    V3 env_color{0.53f, 0.81f, 0.92f};  // scene.h:29
+    size_t num() const { return volume_type == 0 ? gmm.gaussians.size() : smm.spheres.size(); }
+};
+
+// scene.h:38-68 (CRLF-tolerant through operator>>, any other tag skipped)
+static Scene load_SMM(const std::string& fn) {
+    Scene s;
+    s.volume_type = 1;
+    std::ifstream file(fn);
+    if (!file) throw std::runtime_error("Failed to open scene file: " + fn);
+    std::string tag;
+    while (file >> tag) {
+        if (tag == "l") {
+            float x, y, z, r, g, b;
+            file >> x >> y >> z >> r >> g >> b;
+            s.lights.push_back({{x, y, z}, {r, g, b}});
+        } else if (tag == "s") {
+            float x, y, z, rad, sa, ss;
+            file >> x >> y >> z >> rad >> sa >> ss;
+            s.smm.spheres.push_back({{x, y, z}, rad, sa, ss});
+        }
+    }
+    return s;
+}
+// scene.h:72-120 — including the emission peek quirk (scene.h:99-106).
+static Scene load_GMM(const std::string& fn) {
+    Scene s;
+    s.volume_type = 0;
+    std::ifstream file(fn);
+    if (!file) throw std::runtime_error("Failed to open scene file: " + fn);
+    std::string tag;
+    while (file >> tag) {
+        if (tag == "l") {
+            float x, y, z, r, g, b;
+            file >> x >> y >> z >> r >> g >> b;
+            s.lights.push_back({{x, y, z}, {r, g, b}});
+        } else if (tag == "g") {
+            float mx, my, mz, cxx, cxy, cxz, cyy, cyz, czz, density, albedo;
+            file >> mx >> my >> mz >> cxx >> cxy >> cxz >> cyy >> cyz >> czz >> density >> albedo;
+            int next = file.peek();
+            if (next != '\n' && next != EOF) {
+                float er, eg, eb;
+                if (file >> er >> eg >> eb) { (void)er; }
+            }
+            M3 cov{{{cxx, cxy, cxz}, {cxy, cyy, cyz}, {cxz, cyz, czz}}};
+            s.gmm.gaussians.emplace_back(V3{mx, my, mz}, cov, density, albedo);
+        }
+    }
+    s.gmm.BuildBVH();
+    return s;
+}
+
+// =============================================================================================
+// Integrators
+// =============================================================================================
+static const float kInv4Pi = (float)(1.0f / (4.0f * std::numbers::pi));  // Vector3f * double → float
+static const float k4Pi = (float)(4.0f * std::numbers::pi);
+
+// test_integrators.h:160-296 — RayMarchingGaussians per pixel.
+static V3 rm_gaussians_pixel(const Scene& scene, const Camera& cam, int x, int y, int W, int H,
+                             float step_size, int env_samples) {
+    const GMM& gmm = scene.gmm;
+    float u = (x + 0.5f) / W, v = (y + 0.5f) / H;
+    Ray ray = cam.sample_ray(u, v);
+    std::vector<PrimitiveHitEvent> events;
+    gmm.intersect_events(ray, events);
+    if (events.empty()) return scene.env_color;
+    float t_end = events.back().t;
+    std::vector<bool> active(gmm.gaussians.size(), false);
+    size_t evt_i = 0;
+    float t = 0.0f, T = 1.0f;
+    V3 L{0, 0, 0};
+    int k = 0;  // step counter (keys the deterministic env RNG)
+    while (t < t_end) {
+        while (evt_i < events.size() && events[evt_i].t <= t) {
+            active[events[evt_i].index] = events[evt_i].entering;
+            ++evt_i;
+        }
+        V3 pos = ray.origin + t * ray.direction;
+        float sigma_a, sigma_s;
+        gmm.evaluate_sigma(active, pos, sigma_a, sigma_s);
+        if (sigma_s > 0.0f) {
+            V3 Li{0, 0, 0};
+            for (const auto& light : scene.lights) {
+                V3 wi = normalized(light.position - pos);
+                float dist = norm(light.position - pos);
+                Ray shadow_ray(pos, wi);
+                std::vector<PrimitiveHitEvent> shadow_ev;
+                gmm.intersect_events(shadow_ray, shadow_ev);
+                for (size_t i = 0; i < active.size(); ++i)
+                    if (active[i]) shadow_ev.insert(shadow_ev.begin(), {0.0f, true, i});
+                std::vector<size_t> active_idxs;
+                std::vector<bool> mask = active;
+                float t_prev = 0;
+                size_t se_i = 0;
+                float Tr = 1.0f;
+                while (t_prev < dist) {
+                    float t_next = (se_i < shadow_ev.size() ? shadow_ev[se_i].t : dist);
+                    active_idxs.clear();
+                    for (size_t i = 0; i < mask.size(); ++i)
+                        if (mask[i]) active_idxs.push_back(i);
+                    Tr *= gmm.transmittance_over_segment(shadow_ray, t_prev, t_next, active_idxs);
+                    if (se_i < shadow_ev.size()) {
+                        mask[shadow_ev[se_i].index] = shadow_ev[se_i].entering;
+                        ++se_i;
+                    }
+                    t_prev = t_next;
+                }
+                float d2 = dist * dist;
+                Li = Li + V3{(Tr * light.intensity.x) / d2, (Tr * light.intensity.y) / d2, (Tr * light.intensity.z) / d2};
+            }
+            V3 Le{0, 0, 0};
+            PCG32 rng(derive_path_seed(x, y, k), 1);
+            for (int si = 0; si < env_samples; ++si) {
+                float xi1 = rng.uniform();
+                float xi2 = rng.uniform();
+                V3 wi = env_dir(xi1, xi2);
+                Ray env_ray(pos, wi);
+                std::vector<PrimitiveHitEvent> env_ev;
+                gmm.intersect_events(env_ray, env_ev);
+                for (size_t i = 0; i < active.size(); ++i)
+                    if (active[i]) env_ev.insert(env_ev.begin(), {0.0f, true, i});
+                std::vector<size_t> active_idxs;
+                std::vector<bool> mask = active;
+                float t_prev = 0, Tr_env = 1.0f;
+                size_t ei = 0;
+                while (ei < env_ev.size()) {
+                    float t_next = env_ev[ei].t;
+                    active_idxs.clear();
+                    for (size_t i = 0; i < mask.size(); ++i)
+                        if (mask[i]) active_idxs.push_back(i);
+                    Tr_env *= gmm.transmittance_over_segment(env_ray, t_prev, t_next, active_idxs);
+                    mask[env_ev[ei].index] = env_ev[ei].entering;
+                    t_prev = t_next;
+                    ++ei;
+                }
+                Le = Le + Tr_env * scene.env_color;
+            }
+            float fs = float(env_samples);
+            Le = V3{(Le.x / fs) * k4Pi, (Le.y / fs) * k4Pi, (Le.z / fs) * k4Pi};
+            float Ts = T * sigma_s;
+            V3 S = Li + Le;
+            L = L + V3{((Ts * S.x) * step_size) * kInv4Pi, ((Ts * S.y) * step_size) * kInv4Pi, ((Ts * S.z) * step_size) * kInv4Pi};
+        }
+        std::vector<size_t> active_idxs;
+        for (size_t i = 0; i < active.size(); ++i)
+            if (active[i]) active_idxs.push_back(i);
+        float segmentTr = gmm.transmittance_over_segment(ray, t, t + step_size, active_idxs);
+        T *= segmentTr;
+        t += step_size;
+        ++k;
+    }
+    L = L + T * scene.env_color;
+    return L;
+}
+
+// test_integrators.h:23-135 — RayMarchingSpheres per pixel.
+static V3 rm_spheres_pixel(const Scene& scene, const Camera& cam, int i, int j, int W, int H,
+                           float step_size, int env_samples) {
+    const SMM& smm = scene.smm;
+    float u = (i + 0.5f) / W;
+    float v = (j + 0.5f) / H;
+    Ray ray = cam.sample_ray(u, v);
+    V3 radiance{0, 0, 0};
+    std::vector<PrimitiveHitEvent> events;
+    smm.intersect_events(ray, events);
+    if (events.empty()) return scene.env_color;
+    std::vector<bool> active(smm.spheres.size(), false);
+    size_t current_event = 0;
+    float t = 0.0f, T = 1.0f;
+    float t_end = events.back().t;
+    int k = 0;
+    while (t < t_end) {
+        while (current_event < events.size() && events[current_event].t <= t) {
+            active[events[current_event].index] = events[current_event].entering;
+            current_event++;
+        }
+        V3 pos = ray.origin + t * ray.direction;
+        float sigma_a, sigma_s;
+        smm.evaluate_sigma(active, sigma_a, sigma_s);
+        if (sigma_s > 0.0f) {
+            V3 Li{0, 0, 0};
+            for (const auto& light : scene.lights) {
+                V3 wi = normalized(light.position - pos);
+                float dist = norm(light.position - pos);
+                Ray shadow_ray(pos, wi);
+                std::vector<PrimitiveHitEvent> shadow_events;
+                smm.intersect_events(shadow_ray, shadow_events);
+                for (size_t ii = 0; ii < active.size(); ++ii)
+                    if (active[ii]) shadow_events.insert(shadow_events.begin(), {0.0f, true, ii});
+                float Tr = smm.transmittance_from_events(shadow_ray, shadow_events, dist);
+                float d2 = dist * dist;
+                Li = Li + V3{(Tr * light.intensity.x) / d2, (Tr * light.intensity.y) / d2, (Tr * light.intensity.z) / d2};
+            }
+            V3 Le_env{0, 0, 0};
+            PCG32 rng(derive_path_seed(i, j, k), 1);
+            for (int s = 0; s < env_samples; ++s) {
+                float xi1 = rng.uniform();
+                float xi2 = rng.uniform();
+                V3 wi = env_dir(xi1, xi2);
+                Ray shadow(pos, wi);
+                std::vector<PrimitiveHitEvent> shadow_ev;
+                smm.intersect_events(shadow, shadow_ev);
+                for (size_t ii = 0; ii < active.size(); ++ii)
+                    if (active[ii]) shadow_ev.insert(shadow_ev.begin(), {0.0f, true, ii});
+                float Tr_env = smm.transmittance_from_events(shadow, shadow_ev, std::numeric_limits<float>::infinity());
+                Le_env = Le_env + Tr_env * scene.env_color;
+            }
+            float fs = float(env_samples);
+            Le_env = V3{Le_env.x / fs, Le_env.y / fs, Le_env.z / fs};
+            Le_env = V3{Le_env.x * k4Pi, Le_env.y * k4Pi, Le_env.z * k4Pi};
+            float Ts = T * sigma_s;
+            V3 S = Li + Le_env;
+            radiance = radiance + V3{((Ts * S.x) * step_size) * kInv4Pi, ((Ts * S.y) * step_size) * kInv4Pi, ((Ts * S.z) * step_size) * kInv4Pi};
+        }
+        T *= std::exp(-step_size * (sigma_a + sigma_s));
+        t += step_size;
+        ++k;
+    }
+    radiance = radiance + T * scene.env_color;
+    return radiance;
+}
+
+}  // namespace orc
+
+// =============================================================================================
+// C ABI for ctypes (tests / bench cpu_baseline only)
+// =============================================================================================
+using namespace orc;
+static thread_local std::string g_err;
+
+extern "C" {
+
+const char* orc_last_error() { return g_err.c_str(); }
+
+void* orc_load_gmm(const char* path) {
+    try { return new Scene(load_GMM(path)); } catch (const std::exception& e) { g_err = e.what(); return nullptr; }
+}
+void* orc_load_smm(const char* path) {
+    try { return new Scene(load_SMM(path)); } catch (const std::exception& e) { g_err = e.what(); return nullptr; }
+}
+// n Gaussians: mean[3n], cov6[6n] (xx xy xz yy yz zz), density[n], albedo[n]; lights pos[3nl], int[3nl]
+void* orc_scene_from_gaussians(int64_t n, const float* mean, const float* cov6, const float* density,
+                               const float* albedo, int64_t nl, const float* lpos, const float* lint) {
+    Scene* s = new Scene();
+    s->volume_type = 0;
+    s->gmm.gaussians.reserve(n);
+    for (int64_t i = 0; i < n; ++i) {
+        const float* c = cov6 + 6 * i;
+        M3 cov{{{c[0], c[1], c[2]}, {c[1], c[3], c[4]}, {c[2], c[4], c[5]}}};
+        s->gmm.gaussians.emplace_back(V3{mean[3 * i], mean[3 * i + 1], mean[3 * i + 2]}, cov, density[i], albedo[i]);
+    }
+    for (int64_t i = 0; i < nl; ++i)
+        s->lights.push_back({{lpos[3 * i], lpos[3 * i + 1], lpos[3 * i + 2]}, {lint[3 * i], lint[3 * i + 1], lint[3 * i + 2]}});
+    s->gmm.BuildBVH();
+    return s;
+}
+void orc_scene_free(void* s) { delete (Scene*)s; }
+void orc_scene_set_env(void* s, float r, float g, float b) { ((Scene*)s)->env_color = {r, g, b}; }
+int64_t orc_scene_num(void* s) { return (int64_t)((Scene*)s)->num(); }
+int64_t orc_scene_num_lights(void* s) { return (int64_t)((Scene*)s)->lights.size(); }
+int orc_scene_type(void* s) { return ((Scene*)s)->volume_type; }
+// per Gaussian 12 floats: mean3, density, inv_cov(00 01 02 11 12 22), norm, albedo
+void orc_scene_records(void* sp, float* out) {
+    Scene* s = (Scene*)sp;
+    for (size_t i = 0; i < s->gmm.gaussians.size(); ++i) {
+        const Gaussian& g = s->gmm.gaussians[i];
+        float* o = out + 12 * i;
+        o[0] = g.mean.x; o[1] = g.mean.y; o[2] = g.mean.z; o[3] = g.density;
+        o[4] = g.inv_cov(0, 0); o[5] = g.inv_cov(0, 1); o[6] = g.inv_cov(0, 2);
+        o[7] = g.inv_cov(1, 1); o[8] = g.inv_cov(1, 2); o[9] = g.inv_cov(2, 2);
+        o[10] = g.norm; o[11] = g.albedo;
+    }
+}
+// camera: type 0 pinhole (pos, view_dir, fov), 1 ortho (pos, forward). out[17]:
+// type, position3, view_dir3, right3, up3, pinhole3, focal
+void orc_camera(int type, const float* pos, const float* vd, float fov, float* out) {
+    Camera c = type == 0 ? Camera::make_pinhole({pos[0], pos[1], pos[2]}, {vd[0], vd[1], vd[2]}, fov)
+                         : Camera::make_ortho({pos[0], pos[1], pos[2]}, {vd[0], vd[1], vd[2]});
+    float v[17] = {(float)c.type, c.position.x, c.position.y, c.position.z, c.view_dir.x, c.view_dir.y, c.view_dir.z,
+                   c.right.x, c.right.y, c.right.z, c.up.x, c.up.y, c.up.z, c.pinhole.x, c.pinhole.y, c.pinhole.z, c.focal_length};
+    std::memcpy(out, v, sizeof(v));
+}
+// primary ray for pixel (x,y): out[6] origin, direction
+void orc_primary_ray(int type, const float* pos, const float* vd, float fov, int x, int y, int W, int H, float* out) {
+    Camera c = type == 0 ? Camera::make_pinhole({pos[0], pos[1], pos[2]}, {vd[0], vd[1], vd[2]}, fov)
+                         : Camera::make_ortho({pos[0], pos[1], pos[2]}, {vd[0], vd[1], vd[2]});
+    float u = (x + 0.5f) / W, v = (y + 0.5f) / H;
+    Ray r = c.sample_ray(u, v);
+    out[0] = r.origin.x; out[1] = r.origin.y; out[2] = r.origin.z;
+    out[3] = r.direction.x; out[4] = r.direction.y; out[5] = r.direction.z;
+}
+// Gaussian i vs a ray: out[4] = hit, t_enter, t_exit, optical_depth(t_enter, t_exit)
+void orc_gaussian_probe(void* sp, int64_t i, const float* o, const float* d, float* out) {
+    Scene* s = (Scene*)sp;
+    Ray r{{o[0], o[1], o[2]}, {d[0], d[1], d[2]}};
+    const Gaussian& g = s->gmm.gaussians[i];
+    float a = 0, b = 0;
+    bool hit = g.intersect_direct(r, a, b);
+    out[0] = hit ? 1.0f : 0.0f; out[1] = a; out[2] = b;
+    out[3] = hit ? g.optical_depth(r, a, b) : 0.0f;
+}
+
+// DEBUG: for pixel (x,y) of RayMarchingGaussians, compare every secondary-ray transmittance of the
+// faithful segment loop with the telescoped per-Gaussian-interval model used by the device code.
+// out[0] = max |Tr_ref - Tr_model| (light rays), out[1] = same (env rays), out[2] = #rays checked,
+// out[3..6] = (step k, ray kind 0/1, Tr_ref, Tr_model) of the worst ray.
+void orc_debug_secondary(void* sp, const float* pos, const float* vd, float fov, int x, int y, int W, int H,
+                         float step_size, int env_samples, float* out) {
+    Scene& s = *(Scene*)sp;
+    const GMM& gmm = s.gmm;
+    Camera c = Camera::make_pinhole({pos[0], pos[1], pos[2]}, {vd[0], vd[1], vd[2]}, fov);
+    float u = (x + 0.5f) / W, v = (y + 0.5f) / H;
+    Ray ray = c.sample_ray(u, v);
+    std::vector<PrimitiveHitEvent> events;
+    gmm.intersect_events(ray, events);
+    for (int i = 0; i < 7; ++i) out[i] = 0;
+    if (events.empty()) return;
+    float t_end = events.back().t;
+    std::vector<bool> active(gmm.gaussians.size(), false);
+    size_t evt_i = 0;
+    float t = 0.0f;
+    int k = 0;
+    auto model = [&](const Ray& r, bool is_light, float dist) {
+        // telescoped model
+        std::vector<PrimitiveHitEvent> ev;
+        gmm.intersect_events(r, ev);
+        std::vector<float> lo(gmm.gaussians.size(), NAN), hi(gmm.gaussians.size(), NAN);
+        std::vector<bool> hit(gmm.gaussians.size(), false);
+        for (size_t i = 0; i < gmm.gaussians.size(); ++i) {
+            float a, b;
+            if (gmm.gaussians[i].intersect_direct(r, a, b)) { hit[i] = true; lo[i] = a; hi[i] = b; }
+        }
+        float tstop;
+        if (is_light) {
+            tstop = INFINITY;
+            for (auto& e : ev) if (e.t >= dist) tstop = std::min(tstop, e.t);
+            if (tstop == INFINITY) tstop = dist;
+        } else {
+            tstop = 0.0f;
+            for (auto& e : ev) tstop = std::max(tstop, e.t);
+        }
+        double tau = 0;
+        for (size_t i = 0; i < gmm.gaussians.size(); ++i) {
+            float l, h;
+            if (active[i]) { l = 0.0f; h = hit[i] ? hi[i] : tstop; }
+            else if (hit[i]) { l = lo[i]; h = hi[i]; }
+            else continue;
+            h = std::min(h, tstop);
+            if (l < h) tau += gmm.gaussians[i].optical_depth(r, l, h);
+        }
+        return (float)std::exp(-tau);
+    };
+    int nrays = 0;
+    while (t < t_end) {
+        while (evt_i < events.size() && events[evt_i].t <= t) {
+            active[events[evt_i].index] = events[evt_i].entering;
+            ++evt_i;
+        }
+        V3 p = ray.origin + t * ray.direction;
+        float sa, ss;
+        gmm.evaluate_sigma(active, p, sa, ss);
+        if (ss > 0.0f) {
+            for (const auto& light : s.lights) {
+                V3 wi = normalized(light.position - p);
+                float dist = norm(light.position - p);
+                Ray sr(p, wi);
+                std::vector<PrimitiveHitEvent> sev;
+                gmm.intersect_events(sr, sev);
+                for (size_t i = 0; i < active.size(); ++i) if (active[i]) sev.insert(sev.begin(), {0.0f, true, i});
+                std::vector<size_t> ai;
+                std::vector<bool> mask = active;
+                float tp = 0, Tr = 1.0f;
+                size_t se = 0;
+                while (tp < dist) {
+                    float tn = se < sev.size() ? sev[se].t : dist;
+                    ai.clear();
+                    for (size_t i = 0; i < mask.size(); ++i) if (mask[i]) ai.push_back(i);
+                    Tr *= gmm.transmittance_over_segment(sr, tp, tn, ai);
+                    if (se < sev.size()) { mask[sev[se].index] = sev[se].entering; ++se; }
+                    tp = tn;
+                }
+                float Tm = model(sr, true, dist);
+                float d = std::fabs(Tr - Tm);
+                ++nrays;
+                if (d > out[0]) out[0] = d;
+                if (d >= out[0] && d > 0 && d >= out[1]) { out[3] = k; out[4] = 0; out[5] = Tr; out[6] = Tm; }
+            }
+            PCG32 rng(derive_path_seed(x, y, k), 1);
+            for (int si = 0; si < env_samples; ++si) {
+                float xi1 = rng.uniform(), xi2 = rng.uniform();
+                Ray er(p, env_dir(xi1, xi2));
+                std::vector<PrimitiveHitEvent> eev;
+                gmm.intersect_events(er, eev);
+                for (size_t i = 0; i < active.size(); ++i) if (active[i]) eev.insert(eev.begin(), {0.0f, true, i});
+                std::vector<size_t> ai;
+                std::vector<bool> mask = active;
+                float tp = 0, Tr = 1.0f;
+                for (size_t ei = 0; ei < eev.size(); ++ei) {
+                    float tn = eev[ei].t;
+                    ai.clear();
+                    for (size_t i = 0; i < mask.size(); ++i) if (mask[i]) ai.push_back(i);
+                    Tr *= gmm.transmittance_over_segment(er, tp, tn, ai);
+                    mask[eev[ei].index] = eev[ei].entering;
+                    tp = tn;
+                }
+                float Tm = model(er, false, 0.0f);
+                float d = std::fabs(Tr - Tm);
+                ++nrays;
+                if (d > out[1]) { out[1] = d; if (d >= out[0]) { out[3] = k; out[4] = 1; out[5] = Tr; out[6] = Tm; } }
+            }
+        }
+        t += step_size;
+        ++k;
+    }
+    out[2] = nrays;
+}
+
+uint64_t orc_derive_path_seed(int x, int y, int si) { return derive_path_seed(x, y, si); }
+void orc_pcg32(uint64_t seed, uint64_t seq, int n, uint32_t* out) {
+    PCG32 r(seed, seq);
+    for (int i = 0; i < n; ++i) out[i] = r.next_u32();
+}
+void orc_env_dir(float xi1, float xi2, float* out) {
+    V3 d = env_dir(xi1, xi2);
+    out[0] = d.x; out[1] = d.y; out[2] = d.z;
+}
+
+// integrator: 0 RayMarchingGaussians, 1 RayMarchingSpheres.
+// If pix != nullptr, render only the npix pixels pix[2k]=x, pix[2k+1]=y into out[3*npix];
+// otherwise the whole W*H frame into out[3*W*H] (row-major, image.h:13-17).
+int orc_render(void* sp, int cam_type, const float* pos, const float* vd, float fov, int integrator,
+               float step_size, int env_samples, int W, int H, const int* pix, int64_t npix, float* out,
+               int nthreads) {
+    try {
+        Scene* s = (Scene*)sp;
+        Camera c = cam_type == 0 ? Camera::make_pinhole({pos[0], pos[1], pos[2]}, {vd[0], vd[1], vd[2]}, fov)
+                                 : Camera::make_ortho({pos[0], pos[1], pos[2]}, {vd[0], vd[1], vd[2]});
+        if ((integrator == 0) != (s->volume_type == 0)) { g_err = "integrator/scene type mismatch"; return 1; }
+        int64_t total = pix ? npix : (int64_t)W * H;
+        if (nthreads > 0) omp_set_num_threads(nthreads);
+#pragma omp parallel for schedule(dynamic, 1)
+        for (int64_t q = 0; q < total; ++q) {
+            int x = pix ? pix[2 * q] : (int)(q % W);
+            int y = pix ? pix[2 * q + 1] : (int)(q / W);
+            V3 L = integrator == 0 ? rm_gaussians_pixel(*s, c, x, y, W, H, step_size, env_samples)
+                                   : rm_spheres_pixel(*s, c, x, y, W, H, step_size, env_samples);
+            out[3 * q] = L.x; out[3 * q + 1] = L.y; out[3 * q + 2] = L.z;
+        }
+        return 0;
+    } catch (const std::exception& e) {
+        g_err = e.what();
+        return 2;
+    }
+}
+
+}  // extern "C"

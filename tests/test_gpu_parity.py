@@ -1,0 +1,288 @@
+"""GPU parity: libvr_hip.so (through the C ABI) vs the CPU restatement (oracle/).
+
+Bar (BASELINE.md / SURVEY.md §8(c)): per-pixel L-infinity < 1e-4 between the device path and the
+oracle on the same scene, camera and deterministic environment-sampling RNG. Both sides compute
+ray origins/directions, ellipsoid entry/exit distances and march positions bit-identically (no FMA
+contraction, correctly rounded div/sqrt, reference evaluation order); they differ only through
+libm-vs-device exp/erf ulps and summation order, which the tolerance covers.
+"""
+import numpy as np
+import pytest
+
+import pyoracle as O
+import vr_amd as vr
+from helpers import CAM_POS, FOV, main_view_dir, scene_path
+
+pytestmark = pytest.mark.gpu
+
+TOL = 1e-4
+
+
+def _linf(a, b):
+    a = np.asarray(a, np.float64)
+    b = np.asarray(b, np.float64)
+    both_nan = np.isnan(a) & np.isnan(b)
+    d = np.abs(a - b)
+    d[both_nan] = 0.0
+    return float(np.nanmax(d)) if d.size else 0.0, int(np.sum(np.isnan(a) != np.isnan(b)))
+
+
+def _pixels(W, H, n, seed=0):
+    rng = np.random.default_rng(seed)
+    idx = rng.choice(W * H, size=min(n, W * H), replace=False)
+    return np.stack([idx % W, idx // W], axis=1).astype(np.int32)
+
+
+def _render_gpu_gmm(path, W, H, env_samples=20, env=None, cam=None, step=0.01):
+    scene = vr.Scene.load_GMM(path)
+    if env is not None:
+        scene.env_color = env
+    camera = cam or vr.Pinhole_Camera(CAM_POS, main_view_dir(), FOV)
+    img = vr.Image(W, H)
+    integ = vr.RayMarchingGaussians(camera, step_size=step, env_samples=env_samples)
+    integ.render(scene, img)
+    return img.pixels, integ.last_stats
+
+
+def _oracle_gmm(path, W, H, env_samples=20, env=None, pixels=None, cam_type=O.PINHOLE, pos=CAM_POS, vd=None,
+                fov=FOV, step=0.01):
+    s = O.OracleScene.load_gmm(path)
+    if env is not None:
+        s.set_env(env)
+    vd = main_view_dir() if vd is None else vd
+    return O.render(s, cam_type, pos, vd, fov, W, H, O.RAYMARCH_GAUSSIANS, step, env_samples, pixels=pixels)
+
+
+@pytest.mark.parametrize("name,W,H,npix", [
+    ("1_gaussian.txt", 96, 96, None),
+    ("1_gaussian_rotated.txt", 96, 96, None),
+    ("2_gaussian.txt", 96, 96, None),
+    ("2g_altered.txt", 64, 64, None),
+    ("many_gaussians.txt", 128, 128, None),
+    ("god_ray.txt", 64, 64, None),
+    ("middle_light.txt", 64, 64, None),
+    ("50_random.txt", 256, 256, 1024),
+    ("250_random.txt", 256, 256, 256),
+    ("1000_random.txt", 512, 512, 48),
+])
+def test_raymarch_gaussians_matches_oracle(name, W, H, npix):
+    path = scene_path(name)
+    gpu, stats = _render_gpu_gmm(path, W, H)
+    assert stats["error_pixels"] == 0
+    if npix is None:
+        ref = _oracle_gmm(path, W, H)
+        got = gpu
+    else:
+        pix = _pixels(W, H, npix)
+        ref = _oracle_gmm(path, W, H, pixels=pix)
+        got = gpu[pix[:, 1], pix[:, 0]]
+    err, nan_mismatch = _linf(got, ref)
+    assert nan_mismatch == 0
+    assert err < TOL, f"{name}: L-inf {err:.3e}"
+
+
+def test_ortho_xml_sphere_c1_matches_oracle():
+    """Config 1: tests/env_one_sphere_test_ortho.xml at 256x256 (RayMarchingSpheres, 5 env samples)."""
+    scene, camera, (W0, H0), kw = vr.Scene.load_XML(scene_path("env_one_sphere_test_ortho.xml"))
+    assert (W0, H0) == (512, 512) and kw["env_samples"] == 5
+    W = H = 256
+    img = vr.Image(W, H)
+    vr.RayMarchingSpheres(camera, **kw).render(scene, img)
+    s = O.OracleScene.load_smm(scene_path("sph_1_spheres.txt"))
+    ref = O.render(s, O.ORTHO, np.array([0, 1, 6], np.float32), np.array([0, 0, -1], np.float32), 0.0, W, H,
+                   O.RAYMARCH_SPHERES, 0.01, 5)
+    err, nm = _linf(img.pixels, ref)
+    assert nm == 0 and err < TOL, f"L-inf {err:.3e}"
+
+
+@pytest.mark.parametrize("name", ["sph_2_spheres.txt", "sph_3_spheres.txt", "sph_2_lights.txt"])
+def test_raymarch_spheres_pinhole_matches_oracle(name):
+    W = H = 96
+    scene = vr.Scene.load_SMM(scene_path(name))
+    img = vr.Image(W, H)
+    vr.RayMarchingSpheres(vr.Pinhole_Camera(CAM_POS, main_view_dir(), FOV)).render(scene, img)
+    ref = O.render(O.OracleScene.load_smm(scene_path(name)), O.PINHOLE, CAM_POS, main_view_dir(), FOV, W, H,
+                   O.RAYMARCH_SPHERES, 0.01, 5)
+    err, nm = _linf(img.pixels, ref)
+    assert nm == 0 and err < TOL, f"{name}: L-inf {err:.3e}"
+
+
+def test_env_zero_is_fully_deterministic_scene_function():
+    """env_color = 0 makes the reference itself deterministic."""
+    path = scene_path("many_gaussians.txt")
+    gpu, _ = _render_gpu_gmm(path, 64, 64, env=(0, 0, 0))
+    ref = _oracle_gmm(path, 64, 64, env=(0, 0, 0))
+    err, nm = _linf(gpu, ref)
+    assert nm == 0 and err < TOL
+
+
+@pytest.mark.parametrize("W,H", [(1, 1), (17, 5), (40, 23), (160, 90)])
+def test_odd_and_non_square_frames(W, H):
+    """Frames that are not tile multiples; non-square frames are stretched (no aspect correction)."""
+    path = scene_path("2_gaussian.txt")
+    gpu, _ = _render_gpu_gmm(path, W, H)
+    ref = _oracle_gmm(path, W, H)
+    err, nm = _linf(gpu, ref)
+    assert nm == 0 and err < TOL
+
+
+@pytest.mark.parametrize("es", [1, 5, 37])
+def test_env_sample_counts(es):
+    path = scene_path("many_gaussians.txt")
+    gpu, _ = _render_gpu_gmm(path, 48, 48, env_samples=es)
+    ref = _oracle_gmm(path, 48, 48, env_samples=es)
+    err, nm = _linf(gpu, ref)
+    assert nm == 0 and err < TOL
+
+
+def test_env_samples_zero_reproduces_reference_nan():
+    """env_samples = 0 divides 0/0 in the reference (test_integrators.h:274): NaN where light scatters."""
+    path = scene_path("2_gaussian.txt")
+    gpu, _ = _render_gpu_gmm(path, 32, 32, env_samples=0)
+    ref = _oracle_gmm(path, 32, 32, env_samples=0)
+    assert np.array_equal(np.isnan(gpu), np.isnan(ref))
+    assert np.isnan(ref).any()
+    err, nm = _linf(gpu, ref)
+    assert err < TOL
+
+
+def test_orthographic_gaussians_and_other_step():
+    path = scene_path("many_gaussians.txt")
+    vd = np.array([0.3, -0.2, -1.0], np.float32)
+    pos = np.array([-1.0, 1.5, 5.0], np.float32)
+    cam = vr.Orthographic_Camera(pos, vd)
+    gpu, _ = _render_gpu_gmm(path, 64, 64, cam=cam, step=0.02)
+    ref = _oracle_gmm(path, 64, 64, cam_type=O.ORTHO, pos=pos, vd=vd, step=0.02)
+    err, nm = _linf(gpu, ref)
+    assert nm == 0 and err < TOL
+
+
+def _synthetic(n, seed, spread=1.0, sigma=(0.05, 0.175)):
+    rng = np.random.default_rng(seed)
+    mean = np.stack([rng.uniform(-spread, spread, n), rng.uniform(1 - spread, 1 + spread, n),
+                     rng.uniform(-spread, spread, n)], 1).astype(np.float32)
+    s = rng.uniform(*sigma, size=(n, 3))
+    cov = []
+    for i in range(n):
+        q, _ = np.linalg.qr(rng.normal(size=(3, 3)))
+        c = q @ np.diag(s[i] ** 2) @ q.T
+        cov.append([c[0, 0], c[0, 1], c[0, 2], c[1, 1], c[1, 2], c[2, 2]])
+    cov = np.asarray(cov, np.float32)
+    dens = rng.uniform(0.2, 2.5, n).astype(np.float32)
+    alb = rng.uniform(0.0, 1.0, n).astype(np.float32)
+    return mean, cov, dens, alb
+
+
+def _both(mean, cov, dens, alb, lpos, lint, W, H, pos=CAM_POS, vd=None, env_samples=8):
+    vd = main_view_dir() if vd is None else vd
+    scene = vr.Scene.from_gaussians(mean, cov, dens, alb, [vr.Light(p, i) for p, i in zip(lpos, lint)])
+    img = vr.Image(W, H)
+    integ = vr.RayMarchingGaussians(vr.Pinhole_Camera(pos, vd, FOV), env_samples=env_samples)
+    integ.render(scene, img)
+    os_ = O.OracleScene.from_gaussians(mean, cov, dens, alb, lpos, lint)
+    ref = O.render(os_, O.PINHOLE, pos, vd, FOV, W, H, O.RAYMARCH_GAUSSIANS, 0.01, env_samples)
+    return img.pixels, ref, integ.last_stats
+
+
+def test_light_inside_gaussian_and_camera_inside_gaussian():
+    """Straddling Gaussians (light inside) need the 'first event past the light' stop; camera inside
+    a Gaussian starts the march with an active set at t = 0."""
+    mean, cov, dens, alb = _synthetic(12, 3)
+    mean = np.vstack([mean, [[0.0, 3.0, 0.0], [0.0, 1.0, 5.0]]]).astype(np.float32)
+    cov = np.vstack([cov, [[0.5, 0, 0, 0.5, 0, 0.5], [0.3, 0.0, 0.0, 0.3, 0.0, 0.6]]]).astype(np.float32)
+    dens = np.append(dens, [0.05, 0.02]).astype(np.float32)
+    alb = np.append(alb, [0.7, 0.9]).astype(np.float32)
+    lpos = np.array([[0.0, 3.1, 0.1], [2.0, 2.0, 2.0]], np.float32)
+    lint = np.array([[40, 40, 40], [10, 20, 30]], np.float32)
+    got, ref, st = _both(mean, cov, dens, alb, lpos, lint, 48, 48)
+    err, nm = _linf(got, ref)
+    assert nm == 0 and err < TOL, err
+
+
+def test_dense_overlap_uses_fallback_path_and_still_matches():
+    """More than 16 simultaneously active Gaussians overflow the fast path's LDS list; those pixels
+    are re-run by the large-capacity kernel and must still match."""
+    n = 40
+    rng = np.random.default_rng(7)
+    mean = (np.array([0.0, 1.0, 0.0]) + rng.normal(scale=0.02, size=(n, 3))).astype(np.float32)
+    sig = rng.uniform(0.2, 0.35, n)
+    cov = np.stack([sig ** 2, 0 * sig, 0 * sig, sig ** 2, 0 * sig, sig ** 2], 1).astype(np.float32)
+    dens = np.full(n, 0.002, np.float32)
+    alb = rng.uniform(0.2, 0.9, n).astype(np.float32)
+    lpos = np.array([[0.0, 5.0, 0.1]], np.float32)
+    lint = np.array([[50, 50, 50]], np.float32)
+    got, ref, st = _both(mean, cov, dens, alb, lpos, lint, 32, 32, env_samples=2)
+    assert st["fallback_pixels"] > 0
+    assert st["error_pixels"] == 0
+    err, nm = _linf(got, ref)
+    assert nm == 0 and err < TOL, err
+
+
+def test_overflow_beyond_every_capacity_fails_loudly():
+    n = 80
+    mean = np.tile(np.array([[0.0, 1.0, 0.0]], np.float32), (n, 1))
+    sig = np.linspace(0.3, 0.4, n)
+    cov = np.stack([sig ** 2, 0 * sig, 0 * sig, sig ** 2, 0 * sig, sig ** 2], 1).astype(np.float32)
+    scene = vr.Scene.from_gaussians(mean, cov, np.full(n, 1e-4, np.float32), np.full(n, 0.5, np.float32),
+                                    [vr.Light([0, 5, 0], [1, 1, 1])])
+    with pytest.raises(vr.VRError) as e:
+        vr.RayMarchingGaussians(vr.Pinhole_Camera(CAM_POS, main_view_dir(), FOV), env_samples=1).render(
+            scene, vr.Image(16, 16))
+    assert e.value.status == 6
+
+
+def test_render_is_bitwise_deterministic():
+    path = scene_path("50_random.txt")
+    a, _ = _render_gpu_gmm(path, 64, 64)
+    b, _ = _render_gpu_gmm(path, 64, 64)
+    assert np.array_equal(a, b)
+
+
+def test_empty_scene_renders_env():
+    scene = vr.Scene.from_gaussians(np.zeros((0, 3)), np.zeros((0, 6)), [], [], [vr.Light([0, 1, 0], [1, 1, 1])])
+    img = vr.Image(20, 20)
+    vr.RayMarchingGaussians(vr.Pinhole_Camera(CAM_POS, main_view_dir(), FOV)).render(scene, img)
+    assert np.array_equal(img.pixels, np.broadcast_to(np.array([0.53, 0.81, 0.92], np.float32), img.pixels.shape))
+
+
+def test_test_integrator_hitmask_covers_lit_pixels():
+    path = scene_path("many_gaussians.txt")
+    scene = vr.Scene.load_GMM(path)
+    cam = vr.Pinhole_Camera(CAM_POS, main_view_dir(), FOV)
+    mask = vr.Image(64, 64)
+    vr.TestIntegrator(cam).render(scene, mask)
+    ref = _oracle_gmm(path, 64, 64)
+    env = np.array([0.53, 0.81, 0.92], np.float32)
+    hit = np.all(mask.pixels == np.array([1, 0, 1], np.float32), axis=-1)
+    miss = np.all(mask.pixels == env, axis=-1)
+    assert np.all(hit | miss)
+    # every pixel that is not exactly the env colour in the oracle must be a hit
+    not_env = ~np.all(ref == env, axis=-1)
+    assert np.all(hit[not_env])
+
+
+def test_tiles_api_packed_slabs_unshuffle_bitwise():
+    """Multi-GPU building block on one device: rank r of R renders tiles r, r+R, ... into a packed
+    slab; the unshuffled frame equals the single-call frame bit for bit."""
+    torch = pytest.importorskip("torch")
+    path = scene_path("50_random.txt")
+    W, H = 100, 70
+    scene = vr.Scene.load_GMM(path)
+    cam = vr.Pinhole_Camera(CAM_POS, main_view_dir(), FOV)
+    integ = vr.RayMarchingGaussians(cam)
+    full = vr.Image(W, H)
+    integ.render(scene, full)
+    dev = vr.Device.get(0)
+    dev.upload(scene)
+    nt = vr.num_tiles(W, H)
+    R = 3
+    per = (nt + R - 1) // R
+    slabs = torch.zeros((R, per * 256 * 3), dtype=torch.float32, device="cuda")
+    stream = torch.cuda.current_stream().cuda_stream
+    for r in range(R):
+        cnt = len(range(r, nt, R))
+        dev.render_tiles_device(cam, integ.params, W, H, r, R, cnt, True, slabs[r].data_ptr(), stream)
+    img = torch.zeros((H, W, 3), dtype=torch.float32, device="cuda")
+    dev.unshuffle_tiles_device(slabs.data_ptr(), R, per, W, H, img.data_ptr(), stream)
+    torch.cuda.synchronize()
+    assert np.array_equal(img.cpu().numpy(), full.pixels)
