@@ -1,5 +1,6 @@
 // Device context: scene upload (BVH build + HBM layout), step tables, launch and statistics.
-// Host C++ over the HIP runtime; the kernels live in kernels/vr_kernels.hip.
+// Host C++ over the HIP runtime; the kernels live in kernels/vr_gauss.hip (RayMarchingGaussians
+// wavefront pipeline) and kernels/vr_spheres.hip (RayMarchingSpheres, TestIntegrator, unshuffle).
 #include <hip/hip_runtime_api.h>
 
 #include <algorithm>
@@ -12,6 +13,11 @@
 
 namespace vr {
 hipError_t launch_render(const RenderArgs& A, hipStream_t stream, int volume_type, int integrator);
+hipError_t gauss_march(const RenderArgs& A, hipStream_t stream, int mode, bool stats);
+hipError_t gauss_scan(const RenderArgs& A, uint32_t npix, void* temp, size_t& temp_bytes, uint32_t* totals,
+                      hipStream_t stream);
+hipError_t gauss_secondary(const RenderArgs& A, uint32_t nrec, hipStream_t stream, bool stats);
+hipError_t gauss_accumulate(const RenderArgs& A, uint32_t nrec, hipStream_t stream);
 hipError_t launch_unshuffle(const float* slabs, uint32_t nslabs, uint32_t tiles_per_slab, uint32_t tiles_x, uint32_t W,
                             uint32_t H, float* img, hipStream_t stream);
 }  // namespace vr
@@ -50,6 +56,14 @@ struct vr_ctx {
     hipEvent_t ev_start = nullptr, ev_stop = nullptr;
     bool stats_pending = false;
     int64_t last_pixels = 0;
+    // wavefront pipeline buffers (grown on demand, never shrunk)
+    struct Buf {
+        void* p = nullptr;
+        size_t bytes = 0;
+    };
+    Buf px_cnt, px_acnt, px_off, px_aoff, px_T, scan_tmp, rec_pos, rec_meta, rec_act, tr, totals;
+    uint32_t* h_totals = nullptr;  // pinned [0] records, [1] act entries
+    int64_t last_records = 0, last_secondary = 0;
 };
 
 namespace {
@@ -176,7 +190,64 @@ vr_status fill_args(vr_ctx* c, const vr_camera* cam, const vr_render_params* p, 
     return VR_OK;
 }
 
-vr_status launch(vr_ctx* c, RenderArgs& A, const vr_render_params* p, hipStream_t s) {
+vr_status grow(vr_ctx::Buf& b, size_t bytes, const char* what) {
+    if (bytes <= b.bytes && b.p) return VR_OK;
+    if (b.p) (void)hipFree(b.p);
+    b.p = nullptr;
+    b.bytes = 0;
+    size_t want = std::max<size_t>(bytes + bytes / 4, 256);
+    hipError_t e = hipMalloc(&b.p, want);
+    if (e != hipSuccess) return hip_fail(e, what);
+    b.bytes = want;
+    return VR_OK;
+}
+
+// RayMarchingGaussians: march (count) -> scan -> march (write) -> secondary rays -> accumulate.
+vr_status gauss_pipeline(vr_ctx* c, RenderArgs& A, hipStream_t s, bool stats) {
+    const uint32_t npix = A.num_tiles * 256u;
+    vr_status st;
+    if ((st = grow(c->px_cnt, npix * 4ull, "hipMalloc(px_cnt)")) != VR_OK) return st;
+    if ((st = grow(c->px_acnt, npix * 4ull, "hipMalloc(px_acnt)")) != VR_OK) return st;
+    if ((st = grow(c->px_off, npix * 4ull, "hipMalloc(px_off)")) != VR_OK) return st;
+    if ((st = grow(c->px_aoff, npix * 4ull, "hipMalloc(px_aoff)")) != VR_OK) return st;
+    if ((st = grow(c->px_T, npix * 4ull, "hipMalloc(px_T)")) != VR_OK) return st;
+    if ((st = grow(c->totals, 16, "hipMalloc(totals)")) != VR_OK) return st;
+    A.px_cnt = (uint32_t*)c->px_cnt.p;
+    A.px_acnt = (uint32_t*)c->px_acnt.p;
+    A.px_off = (uint32_t*)c->px_off.p;
+    A.px_aoff = (uint32_t*)c->px_aoff.p;
+    A.px_T = (float*)c->px_T.p;
+    A.totals = (const uint32_t*)c->totals.p;
+    size_t tmp_bytes = 0;
+    HIP_TRY(gauss_scan(A, npix, nullptr, tmp_bytes, nullptr, s), "scan size");
+    if ((st = grow(c->scan_tmp, tmp_bytes, "hipMalloc(scan)")) != VR_OK) return st;
+    tmp_bytes = c->scan_tmp.bytes;
+    HIP_TRY(gauss_march(A, s, 0, stats), "march (count)");
+    HIP_TRY(gauss_scan(A, npix, c->scan_tmp.p, tmp_bytes, (uint32_t*)c->totals.p, s), "scan");
+    HIP_TRY(hipMemcpyAsync(c->h_totals, c->totals.p, 2 * sizeof(uint32_t), hipMemcpyDeviceToHost, s), "totals D2H");
+    HIP_TRY(hipStreamSynchronize(s), "march (count)");
+    const uint32_t nrec = c->h_totals[0], nact = c->h_totals[1];
+    const uint64_t nsec = (uint64_t)nrec * (uint64_t)(A.num_lights + A.env_samples);
+    if ((st = grow(c->rec_pos, std::max<uint64_t>(nrec, 1) * 16ull, "hipMalloc(records)")) != VR_OK) return st;
+    if ((st = grow(c->rec_meta, std::max<uint64_t>(nrec, 1) * 16ull, "hipMalloc(records)")) != VR_OK) return st;
+    if ((st = grow(c->rec_act, std::max<uint64_t>(nact, 1) * 4ull, "hipMalloc(active lists)")) != VR_OK) return st;
+    if ((st = grow(c->tr, std::max<uint64_t>(nsec, 1) * 4ull, "hipMalloc(secondary)")) != VR_OK) return st;
+    A.rec_pos = (float4*)c->rec_pos.p;
+    A.rec_meta = (uint4*)c->rec_meta.p;
+    A.rec_act = (int32_t*)c->rec_act.p;
+    A.tr = (float*)c->tr.p;
+    A.rec_cap = nrec;
+    A.act_cap = nact;
+    HIP_TRY(hipMemsetAsync(c->d_queue, 0, sizeof(uint32_t), s), "hipMemsetAsync(queue)");
+    HIP_TRY(gauss_march(A, s, 1, stats), "march (write)");
+    HIP_TRY(gauss_secondary(A, nrec, s, stats), "secondary rays");
+    HIP_TRY(gauss_accumulate(A, nrec, s), "accumulate");
+    c->last_records = nrec;
+    c->last_secondary = (int64_t)nsec;
+    return VR_OK;
+}
+
+vr_status launch(vr_ctx* c, RenderArgs& A, const vr_render_params* p, hipStream_t s, bool stats = false) {
     vr_status st = ensure_queue(c, (uint64_t)A.num_tiles * 256u);
     if (st != VR_OK) return st;
     A.queue = c->d_queue;
@@ -188,7 +259,12 @@ vr_status launch(vr_ctx* c, RenderArgs& A, const vr_render_params* p, hipStream_
     HIP_TRY(hipMemsetAsync(c->d_queue, 0, sizeof(uint32_t), s), "hipMemsetAsync(queue)");
     HIP_TRY(hipMemsetAsync(c->d_counters, 0, 4 * sizeof(uint32_t), s), "hipMemsetAsync(counters)");
     HIP_TRY(hipEventRecord(c->ev_start, s), "hipEventRecord");
-    HIP_TRY(launch_render(A, s, c->type, p->integrator), "kernel launch");
+    if (c->type == VR_VOLUME_GAUSSIANS && p->integrator == VR_RAYMARCH_GAUSSIANS) {
+        st = gauss_pipeline(c, A, s, stats);
+        if (st != VR_OK) return st;
+    } else {
+        HIP_TRY(launch_render(A, s, c->type, p->integrator), "kernel launch");
+    }
     HIP_TRY(hipEventRecord(c->ev_stop, s), "hipEventRecord");
     HIP_TRY(hipMemcpyAsync(&c->h_counters[0], c->d_queue, sizeof(uint32_t), hipMemcpyDeviceToHost, s), "hipMemcpyAsync(stats)");
     HIP_TRY(hipMemcpyAsync(&c->h_counters[1], c->d_counters, sizeof(uint32_t), hipMemcpyDeviceToHost, s), "hipMemcpyAsync(stats)");
@@ -213,6 +289,7 @@ vr_status vr_init(int device, vr_ctx** out) {
     if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
         hipMalloc(&c->d_counters, 4 * sizeof(uint32_t)) != hipSuccess ||
         hipHostMalloc(&c->h_counters, 4 * sizeof(uint32_t), hipHostMallocDefault) != hipSuccess ||
+        hipHostMalloc(&c->h_totals, 4 * sizeof(uint32_t), hipHostMallocDefault) != hipSuccess ||
         hipEventCreate(&c->ev_start) != hipSuccess || hipEventCreate(&c->ev_stop) != hipSuccess) {
         vr_destroy(c);
         return fail(VR_ERR_HIP, "vr_init: failed to create stream/workspace");
@@ -231,6 +308,10 @@ void vr_destroy(vr_ctx* c) {
     if (c->d_queue) (void)hipFree(c->d_queue);
     if (c->d_counters) (void)hipFree(c->d_counters);
     if (c->h_counters) (void)hipHostFree(c->h_counters);
+    if (c->h_totals) (void)hipHostFree(c->h_totals);
+    for (vr_ctx::Buf* b : {&c->px_cnt, &c->px_acnt, &c->px_off, &c->px_aoff, &c->px_T, &c->scan_tmp, &c->rec_pos,
+                           &c->rec_meta, &c->rec_act, &c->tr, &c->totals})
+        if (b->p) (void)hipFree(b->p);
     if (c->d_frame) (void)hipFree(c->d_frame);
     if (c->ev_start) (void)hipEventDestroy(c->ev_start);
     if (c->ev_stop) (void)hipEventDestroy(c->ev_stop);
@@ -354,6 +435,42 @@ vr_status vr_render_tiles_device(vr_ctx* c, const vr_camera* cam, const vr_rende
     A.packed = packed ? 1 : 0;
     A.out = d_out;
     return launch(c, A, p, (hipStream_t)stream);
+}
+
+vr_status vr_count_work(vr_ctx* c, const vr_camera* cam, const vr_render_params* p, uint32_t W, uint32_t H,
+                        uint32_t first_tile, uint32_t tile_stride, uint32_t num_tiles, uint64_t counts[8]) {
+    if (!c || !counts) return fail(VR_ERR_INVALID, "vr_count_work: NULL argument");
+    HIP_TRY(hipSetDevice(c->device), "hipSetDevice");
+    RenderArgs A;
+    vr_status st = fill_args(c, cam, p, W, H, A);
+    if (st != VR_OK) return st;
+    if (p->integrator != VR_RAYMARCH_GAUSSIANS) return fail(VR_ERR_UNSUPPORTED, "vr_count_work: RayMarchingGaussians only");
+    uint32_t total = vr_num_tiles(W, H);
+    if (tile_stride == 0 || num_tiles == 0 || (uint64_t)first_tile + (uint64_t)(num_tiles - 1) * tile_stride >= total)
+        return fail(VR_ERR_INVALID, "vr_count_work: bad tile range");
+    float* d_out = nullptr;
+    unsigned long long* d_work = nullptr;
+    HIP_TRY(hipMalloc(&d_out, (size_t)num_tiles * 256 * 3 * sizeof(float)), "hipMalloc(count_work out)");
+    HIP_TRY(hipMalloc(&d_work, 8 * sizeof(unsigned long long)), "hipMalloc(count_work)");
+    HIP_TRY(hipMemsetAsync(d_work, 0, 8 * sizeof(unsigned long long), c->stream), "hipMemsetAsync");
+    A.first_tile = first_tile;
+    A.tile_stride = tile_stride;
+    A.num_tiles = num_tiles;
+    A.packed = 1;
+    A.out = d_out;
+    A.work = d_work;
+    st = launch(c, A, p, c->stream, true);
+    unsigned long long h[8] = {0};
+    if (st == VR_OK) {
+        hipError_t e = hipMemcpyAsync(h, d_work, sizeof(h), hipMemcpyDeviceToHost, c->stream);
+        if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+        if (e != hipSuccess) st = hip_fail(e, "vr_count_work");
+    }
+    c->stats_pending = false;
+    (void)hipFree(d_out);
+    (void)hipFree(d_work);
+    for (int i = 0; i < 8; ++i) counts[i] = h[i];
+    return st;
 }
 
 vr_status vr_unshuffle_tiles_device(vr_ctx* c, const float* d_slabs, uint32_t nslabs, uint32_t tiles_per_slab, uint32_t W,

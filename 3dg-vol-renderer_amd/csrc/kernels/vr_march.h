@@ -209,11 +209,16 @@ __device__ __forceinline__ void slab(const float* b, const Ray& r, float ix, flo
 
 // Generic stack traversal of the child-pair BVH. `prune(tmin, tmax)` says whether a child box
 // whose ray interval is [tmin, tmax] (already known to satisfy tmax >= max(tmin, 0)) must be
-// visited; `leaf(first, count)` handles a leaf's primitive range. The stack lives in LDS with a
+// visited; `leaf(first, count)` handles a leaf's primitive range and returns false to stop the
+// whole traversal. The stack lives in LDS with a
 // per-thread stride (bank-conflict-free: lane i uses word i of every row).
-template <class Prune, class Leaf>
+struct NoCount {
+    __device__ __forceinline__ void operator()() const {}
+};
+
+template <class Prune, class Leaf, class OnNode = NoCount>
 __device__ __forceinline__ void traverse(const BVHNode* __restrict__ nodes, const Ray& r, int* stack, int stride,
-                                         Prune prune, Leaf leaf) {
+                                         Prune prune, Leaf leaf, OnNode on_node = OnNode()) {
     const float ix = __frcp_rn(r.dx), iy = __frcp_rn(r.dy), iz = __frcp_rn(r.dz);
     int sp = 0;
     int node = 0;
@@ -221,6 +226,7 @@ __device__ __forceinline__ void traverse(const BVHNode* __restrict__ nodes, cons
         const float4* np = reinterpret_cast<const float4*>(nodes + node);
         float4 n0 = np[0], n1 = np[1], n2 = np[2];
         int4 nc = reinterpret_cast<const int4*>(nodes + node)[3];
+        on_node();
         float bl[6] = {n0.x, n0.y, n0.z, n0.w, n1.x, n1.y};
         float br[6] = {n1.z, n1.w, n2.x, n2.y, n2.z, n2.w};
         float lmin, lmax, rmin, rmax;
@@ -228,13 +234,19 @@ __device__ __forceinline__ void traverse(const BVHNode* __restrict__ nodes, cons
         slab(br, r, ix, iy, iz, rmin, rmax);
         bool hl = nc.x != 0 && lmax >= fmaxf(lmin, 0.0f) && prune(lmin, lmax);
         bool hr = nc.y != 0 && rmax >= fmaxf(rmin, 0.0f) && prune(rmin, rmax);
-        if (hl && ref_is_leaf(nc.x)) {
-            leaf(leaf_first(nc.x), leaf_count(nc.x));
-            hl = false;
-        }
-        if (hr && ref_is_leaf(nc.y)) {
-            leaf(leaf_first(nc.y), leaf_count(nc.y));
-            hr = false;
+        // leaf children are handled at once, nearer first; a leaf callback returning false ends
+        // the traversal (used by the optical-depth cut-off of the secondary rays)
+        const bool ll = hl && ref_is_leaf(nc.x), lr = hr && ref_is_leaf(nc.y);
+        if (ll || lr) {
+            const bool r_first = lr && (!ll || rmin < lmin);
+            const int32_t first_ref = r_first ? nc.y : nc.x;
+            if (!leaf(leaf_first(first_ref), leaf_count(first_ref))) return;
+            if (ll && lr) {
+                const int32_t second_ref = r_first ? nc.x : nc.y;
+                if (!leaf(leaf_first(second_ref), leaf_count(second_ref))) return;
+            }
+            if (ll) hl = false;
+            if (lr) hr = false;
         }
         if (hl && hr) {
             int nearer = nc.x, farther = nc.y;

@@ -1,6 +1,7 @@
 // Internal layouts shared by the host side (scene prep, BVH build, launch) and the HIP kernels.
 // Everything here is plain data: it is the HBM image of a scene.
 #pragma once
+#include <hip/hip_vector_types.h>
 #include <stdint.h>
 
 namespace vr {
@@ -85,6 +86,20 @@ struct RenderArgs {
     uint32_t* queue;       // [0] = count, [1..] = packed pixel ids (tile_local << 8 | lane)
     uint32_t queue_cap;
     uint32_t* counters;    // [0] = error pixels
+    unsigned long long* work;  // instrumented build only: 8 work counters (vr_count_work)
+
+    // ---- wavefront buffers (RayMarchingGaussians), pixel-local index p = tile_local * 256 + lane ----
+    uint32_t* px_cnt;   // scatter records of pixel p (march steps with sigma_s > 0)
+    uint32_t* px_acnt;  // active-list entries over those records
+    uint32_t* px_off;   // exclusive scan of px_cnt
+    uint32_t* px_aoff;  // exclusive scan of px_acnt
+    float* px_T;        // transmittance left after the march (multiplies env_color at the end)
+    float4* rec_pos;    // per record: pos.xyz, T * sigma_s
+    uint4* rec_meta;    // per record: x | y << 16, step index k, act offset, act count
+    int32_t* rec_act;   // active Gaussians (leaf-order ids) of each record, sorted
+    float* tr;          // per secondary ray: transmittance, [sample][record]
+    const uint32_t* totals;  // device: [0] records, [1] act entries
+    uint32_t rec_cap, act_cap;
 };
 
 }  // namespace vr

@@ -114,6 +114,12 @@ class Scene:
         check(lib().vr_scene_add_gaussians(self._h, arr, n))
         self.version += 1
 
+    def add_random_gaussians(self, n, seed=0, variant=0):
+        """Synthetic Gaussians with make_random.py's (variant 0) or make_nonuniform_random.py's
+        (variant 1) distribution, generated natively (vr_scene_add_random_gaussians)."""
+        check(lib().vr_scene_add_random_gaussians(self._h, int(n), int(seed), int(variant)))
+        self.version += 1
+
     def add_spheres(self, center, radius, sigma_a, sigma_s):
         center = np.asarray(center, np.float32).reshape(-1, 3)
         n = center.shape[0]
@@ -330,6 +336,23 @@ class Device:
                                            height, first_tile, tile_stride, num_tiles, int(packed),
                                            ctypes.c_void_p(out_ptr), ctypes.c_void_p(stream_ptr)))
 
+    # Algorithmic FP32 work per counted operation (SURVEY.md §8(d) accounting; sqrt, div, exp and
+    # erf counted at 4 flops each = quarter-rate transcendental model). See DESIGN.md §Roofline.
+    FLOP_WEIGHTS = {"node_pair_tests": 44, "gaussian_tests": 72, "optical_depths": 98, "densities": 34}
+    WORK_NAMES = ("node_pair_tests", "gaussian_tests", "optical_depths", "densities", "secondary_rays",
+                  "active_steps", "primary_queries", "pixels")
+
+    def count_work(self, camera, params, width, height, first_tile=0, tile_stride=1, num_tiles=None):
+        """Instrumented (untimed) render of the given tiles; returns counts + algorithmic flops."""
+        if num_tiles is None:
+            num_tiles = len(range(first_tile, num_tiles_of(width, height), tile_stride))
+        arr = (ctypes.c_uint64 * 8)()
+        check(lib().vr_count_work(self._h, ctypes.byref(camera.struct), ctypes.byref(params), width, height,
+                                  first_tile, tile_stride, num_tiles, arr))
+        out = {k: int(arr[i]) for i, k in enumerate(self.WORK_NAMES)}
+        out["flops"] = float(sum(self.FLOP_WEIGHTS[k] * out[k] for k in self.FLOP_WEIGHTS))
+        return out
+
     def unshuffle_tiles_device(self, slabs_ptr, nslabs, tiles_per_slab, width, height, image_ptr, stream_ptr=0):
         check(lib().vr_unshuffle_tiles_device(self._h, ctypes.c_void_p(slabs_ptr), nslabs, tiles_per_slab, width,
                                               height, ctypes.c_void_p(image_ptr), ctypes.c_void_p(stream_ptr)))
@@ -343,6 +366,9 @@ class Device:
 
 def num_tiles(width, height):
     return int(lib().vr_num_tiles(width, height))
+
+
+num_tiles_of = num_tiles
 
 
 class Integrator:

@@ -70,6 +70,7 @@ SIGNATURES = {
     "vr_scene_load_xml": (ST, [ctypes.c_char_p, PP, ctypes.POINTER(vr_camera), U32P, U32P,
                                ctypes.POINTER(vr_render_params)]),
     "vr_scene_add_gaussians": (ST, [P, ctypes.POINTER(vr_gaussian), ctypes.c_size_t]),
+    "vr_scene_add_random_gaussians": (ST, [P, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_int32]),
     "vr_scene_add_spheres": (ST, [P, ctypes.POINTER(vr_sphere), ctypes.c_size_t]),
     "vr_scene_add_lights": (ST, [P, ctypes.POINTER(vr_light), ctypes.c_size_t]),
     "vr_scene_set_env_color": (ST, [P, FP]),
@@ -94,6 +95,9 @@ SIGNATURES = {
                                     ctypes.c_uint32, ctypes.c_int32, P, P]),
     "vr_unshuffle_tiles_device": (ST, [P, P, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,
                                        P, P]),
+    "vr_count_work": (ST, [P, ctypes.POINTER(vr_camera), ctypes.POINTER(vr_render_params), ctypes.c_uint32,
+                           ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,
+                           ctypes.POINTER(ctypes.c_uint64)]),
     "vr_num_tiles": (ctypes.c_uint32, [ctypes.c_uint32, ctypes.c_uint32]),
     "vr_synchronize": (ST, [P]),
     "vr_get_stats": (ST, [P, ctypes.POINTER(vr_render_stats)]),

@@ -1,0 +1,222 @@
+#!/usr/bin/env python3
+"""Benchmark: RayMarchingGaussians forward render (the north-star path) on MI355X.
+
+One "step" = one full frame rendered through the C ABI (vr_render_tiles_device) with the scene
+already resident in HBM; at N > 1 GPUs (one process per GPU, torchrun) every rank renders an
+interleaved 1/N of the frame's 16x16 tiles into a packed slab, the slabs are gathered to rank 0
+over RCCL and unshuffled into the row-major frame there (timed: render + gather + unshuffle).
+
+Workload (BASELINE.json metric): 4096 x 4096 pinhole render (tests/main.cpp camera) of 1,000,000
+synthetic Gaussians with make_random.py's distribution and 1000_random.txt's three lights,
+step 0.01, 20 environment samples per scattering step.
+
+Prints ONE JSON line on rank 0 (contract in the task statement); roofline and cpu_baseline
+objects are documented in DESIGN.md.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path[:0] = [os.path.join(ROOT, "3dg-vol-renderer_amd")]
+
+import torch  # noqa: E402  (first: its HIP runtime is the process runtime, see vr_amd/_lib.py)
+import torch.distributed as dist  # noqa: E402
+
+import vr_amd as vr  # noqa: E402
+
+CONFIGS = {
+    # name: (W, H, n_gaussians or scene file, description)
+    "c4": (4096, 4096, 1_000_000, "4096x4096, 1M Gaussians (make_random distribution)"),
+    "c3": (1920, 1080, 100_000, "1920x1080, 100k Gaussians (make_random distribution)"),
+    "c2": (512, 512, "1000_random.txt", "512x512, scenes/gaussians/1000_random.txt"),
+}
+LIGHTS = [((0.0, 5.0, 0.1), (50.0, 0.0, 0.0)), ((-3.0, 3.0, 0.3), (0.0, 30.0, 0.0)),
+          ((3.0, 3.0, -0.2), (0.0, 0.0, 30.0))]  # scenes/gaussians/1000_random.txt:1-3
+CAM_POS = np.array([0.0, 1.0, 6.0], np.float32)  # tests/main.cpp:21-34
+CAM_VIEW = np.array([0.0, 0.0, -1.0], np.float32)
+FOV = np.float32(0.25 * np.pi)
+HBM_PEAK_GBPS = 8000.0   # MI355X_MICROARCH.md: 8.0 TB/s spec
+FP32_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md: FP32 vector = FP32-input MFMA peak
+
+
+def build_scene(cfg, seed):
+    W, H, src, _ = CONFIGS[cfg]
+    if isinstance(src, str):
+        scene = vr.Scene.load_GMM(os.path.join(ROOT, "tests", "golden", "scenes", src))
+    else:
+        scene = vr.Scene(vr.Scene.GAUSSIANS)
+        scene.add_random_gaussians(src, seed=seed, variant=0)
+        for p, i in LIGHTS:
+            scene.add_light(vr.Light(p, i))
+    return scene, W, H
+
+
+def cpu_baseline(scene, W, H, env_samples, budget_s, threads):
+    """The CPU restatement (oracle, test infrastructure) timed on this host on a bounded pixel
+    sample of the same workload; Mrays/s extrapolated from the sample."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import pyoracle as O
+    g = scene.gaussians()
+    lights = scene.lights
+    osc = O.OracleScene.from_gaussians(g[:, 0:3], g[:, 3:9], g[:, 9], g[:, 10],
+                                       np.array([l.position for l in lights], np.float32),
+                                       np.array([l.intensity for l in lights], np.float32))
+    rng = np.random.default_rng(1234)
+    done, t_total = 0, 0.0
+    batch = max(1, threads)
+    while t_total < budget_s and done < 4096:
+        idx = rng.choice(W * H, size=batch, replace=False)
+        pix = np.stack([idx % W, idx // W], 1).astype(np.int32)
+        t0 = time.perf_counter()
+        O.render(osc, O.PINHOLE, CAM_POS, CAM_VIEW, FOV, W, H, O.RAYMARCH_GAUSSIANS, 0.01, env_samples,
+                 pixels=pix, nthreads=threads)
+        t_total += time.perf_counter() - t0
+        done += batch
+    return {"value": done / t_total / 1e6, "unit": "Mrays/s", "cores": threads, "kind": "port",
+            "sample": f"{done} uniformly random pixels of the {W}x{H} frame ({t_total:.1f} s of CPU time on "
+                      f"{threads} threads, OpenMP schedule(dynamic,1)); faithful restatement incl. the "
+                      f"reference's O(N) per-step mask scans"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--config", default="c4", choices=sorted(CONFIGS))
+    ap.add_argument("--env-samples", type=int, default=20)
+    ap.add_argument("--t-eps", type=float, default=0.0)
+    ap.add_argument("--seed", type=int, default=2025)
+    ap.add_argument("--cpu-budget", type=float, default=20.0, help="seconds of CPU-baseline work (0 = skip)")
+    ap.add_argument("--cpu-threads", type=int, default=min(16, os.cpu_count() or 1))
+    ap.add_argument("--flops", type=int, default=1, help="run one instrumented frame to count algorithmic work")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
+    torch.cuda.set_device(local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+
+    t_setup = time.perf_counter()
+    scene, W, H = build_scene(args.config, args.seed)
+    camera = vr.Pinhole_Camera(CAM_POS, CAM_VIEW, FOV)
+    integ = vr.RayMarchingGaussians(camera, step_size=0.01, env_samples=args.env_samples, t_eps=args.t_eps,
+                                    device=local)
+    dev = vr.Device.get(local)
+    dev.upload(scene)
+    t_setup = time.perf_counter() - t_setup
+
+    ntiles = vr.num_tiles(W, H)
+    per = (ntiles + world - 1) // world
+    mine = len(range(rank, ntiles, world))
+    stream = torch.cuda.current_stream()
+    sp = stream.cuda_stream
+    if world == 1:
+        frame = torch.empty((H, W, 3), dtype=torch.float32, device="cuda")
+    else:
+        slab = torch.zeros((per * 256 * 3,), dtype=torch.float32, device="cuda")
+        slabs = torch.empty((world, per * 256 * 3), dtype=torch.float32, device="cuda") if rank == 0 else None
+        frame = torch.empty((H, W, 3), dtype=torch.float32, device="cuda") if rank == 0 else None
+
+    kev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+
+    def step(i=None):
+        if i is not None:
+            kev[i][0].record(stream)
+        if world == 1:
+            dev.render_tiles_device(camera, integ.params, W, H, 0, 1, ntiles, False, frame.data_ptr(), sp)
+        else:
+            dev.render_tiles_device(camera, integ.params, W, H, rank, world, mine, True, slab.data_ptr(), sp)
+        if i is not None:
+            kev[i][1].record(stream)
+        if world > 1:
+            dist.gather(slab, list(slabs.unbind(0)) if rank == 0 else None, dst=0)
+            if rank == 0:
+                dev.unshuffle_tiles_device(slabs.data_ptr(), world, per, W, H, frame.data_ptr(), sp)
+
+    def log(msg):
+        if rank == 0:
+            print(f"[bench] {msg}", file=sys.stderr, flush=True)
+
+    log(f"setup {t_setup:.1f}s: {scene.get_num_primitives()} Gaussians, {W}x{H}, {world} GPU(s)")
+    for i in range(args.warmup):
+        step()
+        torch.cuda.synchronize()
+        log(f"warmup {i} done")
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        step(i)
+        if args.steps > 1 and world == 1:
+            log(f"step {i} enqueued")
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    st = dev.stats()
+    if st["error_pixels"]:
+        raise SystemExit(f"rank {rank}: {st['error_pixels']} pixels exceeded every capacity")
+    kernel_ms = float(np.mean([a.elapsed_time(b) for a, b in kev]))
+    t = torch.tensor([elapsed, kernel_ms], dtype=torch.float64, device="cuda")
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    elapsed, kernel_ms_max = float(t[0]), float(t[1])
+    ms_per_step = elapsed / args.steps * 1e3
+    rays = W * H  # whole frame per step, all ranks together (1 primary ray per pixel)
+    value = rays / (ms_per_step * 1e-3) / 1e6
+
+    # ---- algorithmic work of one frame (instrumented counters, untimed) ----
+    work = None
+    if args.flops and rank == 0:
+        work = dev.count_work(camera, integ.params, W, H, first_tile=rank, tile_stride=world, num_tiles=mine)
+
+    if rank == 0:
+        n_g = scene.get_num_primitives()
+        # compulsory HBM bytes of one launch on this rank: every 48-B record read once, every
+        # 12-B output pixel written once
+        alg_bytes = 48.0 * n_g + 12.0 * mine * 256
+        hbm_gbps = alg_bytes / (kernel_ms * 1e-3) / 1e9
+        roof = {"bound": "mfma", "roof": "fp32 vector (= f32 MFMA) peak; no MFMA used (VALU/latency-bound "
+                "traversal + transcendentals)", "unit": "TFLOP/s", "peak": FP32_PEAK_TFLOPS,
+                "achieved": None, "frac": None, "traffic": None,
+                "hbm": {"achieved": hbm_gbps, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+                        "frac": hbm_gbps / HBM_PEAK_GBPS, "alg_bytes": alg_bytes},
+                "kernel": "rm_gaussians_kernel", "kernel_ms": kernel_ms}
+        if work is not None:
+            tflops = work["flops"] / (kernel_ms * 1e-3) / 1e12
+            roof.update(achieved=tflops, frac=tflops / FP32_PEAK_TFLOPS, work=work)
+        cpu = None
+        if world == 1 and args.cpu_budget > 0:
+            cpu = cpu_baseline(scene, W, H, args.env_samples, args.cpu_budget, args.cpu_threads)
+        out = {
+            "metric": "Mrays/s + achieved HBM GB/s, 4096² render of 1M Gaussians, 1/2/4/8 GPU",
+            "value": value, "unit": "Mrays/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": ms_per_step, "higher_is_better": True, "scaling": "strong", "vs_baseline": None,
+            "dtype": "f32", "data": "synthetic (seeded make_random.py distribution)",
+            "config": {"workload": CONFIGS[args.config][3], "width": W, "height": H, "gaussians": n_g,
+                       "integrator": "RayMarchingGaussians", "step_size": 0.01, "env_samples": args.env_samples,
+                       "t_eps": args.t_eps, "lights": len(LIGHTS), "parallelism": f"tiles{world}",
+                       "setup_s": t_setup, "fallback_pixels": st["fallback_pixels"]},
+            "roofline": roof,
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

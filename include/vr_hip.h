@@ -132,6 +132,14 @@ vr_status vr_scene_load_smm(const char* path, vr_scene** out);
 vr_status vr_scene_load_xml(const char* path, vr_scene** out, vr_camera* camera, uint32_t* width,
                             uint32_t* height, vr_render_params* params);
 vr_status vr_scene_add_gaussians(vr_scene* s, const vr_gaussian* g, size_t n);
+/* Synthetic scenes of the reference generators' distribution (tests/make_random.py:21-45 for
+ * variant 0, tests/make_nonuniform_random.py:19-30 (y biased towards 0) for variant 1): mean
+ * x,z ~ U(-1,1), y ~ U(0,2); per-axis diameter ~ U(0.01, 0.035); covariance
+ * Q diag((d/2)^2) Q^T with Q from the QR of a 3x3 standard-normal matrix (det fixed to +1);
+ * density ~ U(0.2, 0.5); albedo ~ U(0.25, 0.95); emission ~ U(0,1)^3. Values are rounded exactly as
+ * the generators print them (%.4f / %.6f) and then read back as floats, so a generated scene is
+ * the scene load_GMM would produce from the generator's text file. Seeded PCG32 (rng.h). */
+vr_status vr_scene_add_random_gaussians(vr_scene* s, uint64_t n, uint64_t seed, int32_t variant);
 vr_status vr_scene_add_spheres(vr_scene* s, const vr_sphere* sp, size_t n);
 vr_status vr_scene_add_lights(vr_scene* s, const vr_light* l, size_t n);
 vr_status vr_scene_set_env_color(vr_scene* s, const float rgb[3]);
@@ -181,6 +189,14 @@ vr_status vr_render_tiles_device(vr_ctx* ctx, const vr_camera* cam, const vr_ren
 vr_status vr_unshuffle_tiles_device(vr_ctx* ctx, const float* d_slabs, uint32_t nslabs,
                                     uint32_t tiles_per_slab, uint32_t width, uint32_t height,
                                     float* d_image, void* stream);
+/* Diagnostics (untimed): render the given tiles once with the instrumented kernel build and return
+ * the algorithmic work it executed: counts[0] BVH node-pair tests, [1] ray-Gaussian quadratic +
+ * intersect evaluations, [2] optical-depth evaluations, [3] density (mu_t) evaluations,
+ * [4] secondary (light + environment) rays, [5] active march steps, [6] primary-ray BVH queries,
+ * [7] pixels completed. Synchronous; RayMarchingGaussians only. Used for the roofline report. */
+vr_status vr_count_work(vr_ctx* ctx, const vr_camera* cam, const vr_render_params* p, uint32_t width,
+                        uint32_t height, uint32_t first_tile, uint32_t tile_stride, uint32_t num_tiles,
+                        uint64_t counts[8]);
 /* Number of 16x16 tiles of a W x H frame. */
 uint32_t vr_num_tiles(uint32_t width, uint32_t height);
 vr_status vr_synchronize(vr_ctx* ctx);
