@@ -61,7 +61,9 @@ struct vr_ctx {
         void* p = nullptr;
         size_t bytes = 0;
     };
-    Buf px_cnt, px_acnt, px_off, px_aoff, px_T, scan_tmp, rec_pos, rec_meta, rec_act, tr, totals;
+    Buf px_cnt, px_acnt, px_off, px_aoff, px_T, scan_tmp, rec_pos, rec_meta, rec_act, tr, totals, rec_bloom, slowq;
+    Buf pcg_jump;
+    int pcg_jump_n = -1;
     uint32_t* h_totals = nullptr;  // pinned [0] records, [1] act entries
     int64_t last_records = 0, last_secondary = 0;
 };
@@ -218,6 +220,22 @@ vr_status gauss_pipeline(vr_ctx* c, RenderArgs& A, hipStream_t s, bool stats) {
     A.px_aoff = (uint32_t*)c->px_aoff.p;
     A.px_T = (float*)c->px_T.p;
     A.totals = (const uint32_t*)c->totals.p;
+    // PCG32 (rng.h:20-50, seq 1 -> inc 3) jump-ahead table for the environment samples
+    if (c->pcg_jump_n < 2 * A.env_samples + 2) {
+        const int n = 2 * A.env_samples + 2;
+        std::vector<unsigned long long> tab(2 * (size_t)n);
+        unsigned long long m = 1ull, a = 0ull;
+        for (int k = 0; k < n; ++k) {
+            tab[2 * k] = m;
+            tab[2 * k + 1] = a;
+            m *= 6364136223846793005ull;
+            a = a * 6364136223846793005ull + 3ull;
+        }
+        if ((st = grow(c->pcg_jump, tab.size() * 8, "hipMalloc(pcg)")) != VR_OK) return st;
+        HIP_TRY(hipMemcpy(c->pcg_jump.p, tab.data(), tab.size() * 8, hipMemcpyHostToDevice), "hipMemcpy(pcg)");
+        c->pcg_jump_n = n;
+    }
+    A.pcg_jump = (const unsigned long long*)c->pcg_jump.p;
     size_t tmp_bytes = 0;
     HIP_TRY(gauss_scan(A, npix, nullptr, tmp_bytes, nullptr, s), "scan size");
     if ((st = grow(c->scan_tmp, tmp_bytes, "hipMalloc(scan)")) != VR_OK) return st;
@@ -232,6 +250,14 @@ vr_status gauss_pipeline(vr_ctx* c, RenderArgs& A, hipStream_t s, bool stats) {
     if ((st = grow(c->rec_meta, std::max<uint64_t>(nrec, 1) * 16ull, "hipMalloc(records)")) != VR_OK) return st;
     if ((st = grow(c->rec_act, std::max<uint64_t>(nact, 1) * 4ull, "hipMalloc(active lists)")) != VR_OK) return st;
     if ((st = grow(c->tr, std::max<uint64_t>(nsec, 1) * 4ull, "hipMalloc(secondary)")) != VR_OK) return st;
+    if (nsec >= 0xffffffffull) return fail(VR_ERR_UNSUPPORTED, "more than 2^32 secondary rays in one call (split the frame)");
+    const uint64_t nslow = (uint64_t)nrec * (uint64_t)A.num_lights;
+    if ((st = grow(c->rec_bloom, std::max<uint64_t>(nrec, 1) * 8ull, "hipMalloc(record blooms)")) != VR_OK) return st;
+    if ((st = grow(c->slowq, (nslow + 1) * 4ull, "hipMalloc(slow queue)")) != VR_OK) return st;
+    A.rec_bloom = (unsigned long long*)c->rec_bloom.p;
+    A.slowq = (uint32_t*)c->slowq.p;
+    A.slowq_cap = (uint32_t)nslow;
+    HIP_TRY(hipMemsetAsync(A.slowq, 0, sizeof(uint32_t), s), "hipMemsetAsync(slow queue)");
     A.rec_pos = (float4*)c->rec_pos.p;
     A.rec_meta = (uint4*)c->rec_meta.p;
     A.rec_act = (int32_t*)c->rec_act.p;
@@ -310,7 +336,7 @@ void vr_destroy(vr_ctx* c) {
     if (c->h_counters) (void)hipHostFree(c->h_counters);
     if (c->h_totals) (void)hipHostFree(c->h_totals);
     for (vr_ctx::Buf* b : {&c->px_cnt, &c->px_acnt, &c->px_off, &c->px_aoff, &c->px_T, &c->scan_tmp, &c->rec_pos,
-                           &c->rec_meta, &c->rec_act, &c->tr, &c->totals})
+                           &c->rec_meta, &c->rec_act, &c->tr, &c->totals, &c->rec_bloom, &c->slowq, &c->pcg_jump})
         if (b->p) (void)hipFree(b->p);
     if (c->d_frame) (void)hipFree(c->d_frame);
     if (c->ev_start) (void)hipEventDestroy(c->ev_start);

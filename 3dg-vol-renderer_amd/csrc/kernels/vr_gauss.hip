@@ -9,9 +9,9 @@
 //      step index k, the active Gaussian set). Run twice: MODE 0 counts records per pixel, an
 //      exclusive scan places them, MODE 1 writes them — so the record order is a pure function of
 //      the frame, and the final image is bitwise reproducible.
-//   2. secondary_kernel (one thread per secondary ray, sample-major order so that consecutive
-//      lanes trace rays towards the same light from neighbouring pixels): transmittance of every
-//      light / environment ray of every record.
+//   2. secondary_persistent_kernel (every light / environment ray of every record; ray ids in
+//      sample-major order so that neighbouring lanes trace rays from neighbouring pixels towards the
+//      same light): transmittance of each secondary ray, see Stage 2 below.
 //   3. accumulate_kernel (one thread per pixel): L += T*sigma_s*(Li + Le)*dt/(4 pi) over the
 //      pixel's records in step order, then L += T*env — the reference's operation order.
 //
@@ -32,6 +32,9 @@
 #include <hip/hip_runtime.h>
 #include <hipcub/hipcub.hpp>
 
+#include <cstdio>
+#include <cstdlib>
+
 #include "vr_dev_common.h"
 
 namespace vr {
@@ -44,7 +47,7 @@ namespace dev {
 constexpr float kTauCut = 104.0f;
 
 // ---------------------------------------------------------------------------------------------
-// Secondary-ray transmittance (shared by the secondary kernel)
+// Exact light-ray transmittance (the slow path of Stage 2)
 // ---------------------------------------------------------------------------------------------
 
 // Towards a point light at distance `dist` (test_integrators.h:202-237).
@@ -135,49 +138,6 @@ __device__ float light_transmittance(const RenderArgs& A, const Ray& sr, float d
             if constexpr (S) c.v[kCtrOD]++;
             tau += optical_depth(g, q, 0.0f, tstop);
         }
-    }
-    return expf(-tau);
-}
-
-// Environment ray, to its last event (test_integrators.h:241-273).
-template <bool S>
-__device__ float env_transmittance(const RenderArgs& A, const Ray& er, const ActList& act, int* stack, int stride,
-                                   Ctr& c) {
-    const GaussianRecord* __restrict__ G = A.gauss;
-    float tau = 0.0f, tlast = 0.0f;
-    uint64_t hitmask = 0;
-    traverse(
-        A.nodes, er, stack, stride, [&](float, float) { return true; },
-        [&](uint32_t first, uint32_t count) {
-            for (uint32_t j = first; j < first + count; ++j) {
-                if constexpr (S) c.v[kCtrPrims]++;
-                GRec g = load_rec(G, j);
-                Quad q = quad(g, er);
-                float a, b;
-                if (!intersect(q, a, b)) continue;
-                int slot = act.find((int)j);
-                float lo = a;
-                if (slot >= 0) {
-                    lo = 0.0f;
-                    hitmask |= 1ull << slot;
-                }
-                if constexpr (S) c.v[kCtrOD]++;
-                tau += optical_depth(g, q, lo, b);
-                tlast = fmaxf(tlast, b);
-            }
-            return tau < kTauCut;
-        },
-        NodeCount<S>{&c});
-    if (tau >= kTauCut) return 0.0f;
-    uint64_t all = act.n >= 64 ? ~0ull : ((1ull << act.n) - 1ull);
-    uint64_t missed = all & ~hitmask;
-    while (missed) {
-        int s = __ffsll((unsigned long long)missed) - 1;
-        missed &= missed - 1;
-        GRec g = load_rec(G, act.get(s));
-        Quad q = quad(g, er);
-        if constexpr (S) c.v[kCtrOD]++;
-        tau += optical_depth(g, q, 0.0f, tlast);
     }
     return expf(-tau);
 }
@@ -304,7 +264,13 @@ __device__ int march(const RenderArgs& A, uint32_t p, int px, int py, int* act_b
                     uint32_t r = rbase + nrec;
                     A.rec_pos[r] = make_float4(px_, py_, pz_, T * sigma_s);
                     A.rec_meta[r] = make_uint4((uint32_t)px | ((uint32_t)py << 16), (uint32_t)k, abase + nact, (uint32_t)w);
-                    for (int i = 0; i < w; ++i) A.rec_act[abase + nact + i] = act.get(i);
+                    uint64_t bl = 0;
+                    for (int i = 0; i < w; ++i) {
+                        const int j = act.get(i);
+                        A.rec_act[abase + nact + i] = j;
+                        bl |= 1ull << (j & 63);
+                    }
+                    A.rec_bloom[r] = bl;
                 }
                 nrec++;
                 nact += (uint32_t)w;
@@ -389,51 +355,379 @@ __global__ void totals_kernel(const uint32_t* cnt, const uint32_t* off, const ui
 }
 
 // ---------------------------------------------------------------------------------------------
-// Stage 2: one thread per secondary ray. Ray id t = s * nrec + r (sample-major).
+// Stage 2: persistent "while-while" tracing of all secondary rays, per-lane ray refill.
+//
+// Secondary rays have very uneven lengths (the optical-depth cut-off ends a ray after a few
+// dense hits, a ray through empty space walks many nodes), so one ray per lane per round leaves
+// most of a wave idle behind its slowest lane. Here every wave owns a contiguous chunk of ray
+// ids (sample-major: neighbouring pixels, same light / same env sample index) and each lane
+// pulls the next id from it the moment its ray completes; one loop iteration = one BVH node
+// pair (+ the primitives of a leaf child). Light rays whose result depends on the first event
+// past the light (a Gaussian straddling the light, or a pre-activated Gaussian the ray misses
+// through rounding) are rare; they go to a queue served by secondary_slow_kernel's exact
+// three-pass light_transmittance.
 // ---------------------------------------------------------------------------------------------
+struct SecRay {
+    Ray ray;
+    float ix, iy, iz, oxi, oyi, ozi;  // 1/d and o/d for the slab test
+    float tau, lim;                   // optical depth so far; light: dist, env: +inf
+    float tlast;                      // env: last event
+    uint64_t hitmask, bloom;
+    uint32_t act_off, act_n;
+    bool light, needs_stop;
+};
+
+__device__ __forceinline__ int act_find(const RenderArgs& A, const SecRay& R, int j) {
+    if (!((R.bloom >> (j & 63)) & 1ull)) return -1;
+    for (uint32_t i = 0; i < R.act_n; ++i)
+        if (A.rec_act[R.act_off + i] == j) return (int)i;
+    return -1;
+}
+
+// Direction of environment sample e of a record: PCG32 keyed by (pixel, step) as the oracle does;
+// the 2e draws of the earlier samples are skipped by LCG jump-ahead s -> M s + C (host table).
+__device__ __forceinline__ void env_sample_dir(const RenderArgs& A, const uint4& meta, uint32_t e, float& wx, float& wy,
+                                               float& wz) {
+    const int px = (int)(meta.x & 0xffffu), py = (int)(meta.x >> 16);
+    PCG32 rng(derive_path_seed(px, py, (int)meta.y), 1);
+    rng.state = A.pcg_jump[4 * e] * rng.state + A.pcg_jump[4 * e + 1];
+    float xi1 = rng.uniform();
+    float xi2 = rng.uniform();
+    env_dir(xi1, xi2, wx, wy, wz);
+}
+
+// Octahedral direction cell (8 x 8) used to group environment rays for coherent traversal.
+__device__ __forceinline__ uint32_t dir_cell(float x, float y, float z) {
+    const float n = fabsf(x) + fabsf(y) + fabsf(z);
+    float u = x / n, v = y / n;
+    if (z < 0.0f) {
+        const float uu = (1.0f - fabsf(v)) * (u >= 0.0f ? 1.0f : -1.0f);
+        const float vv = (1.0f - fabsf(u)) * (v >= 0.0f ? 1.0f : -1.0f);
+        u = uu;
+        v = vv;
+    }
+    const int cu = min(7, max(0, (int)((u + 1.0f) * 4.0f)));
+    const int cv = min(7, max(0, (int)((v + 1.0f) * 4.0f)));
+    return (uint32_t)(cu * 8 + cv);
+}
+
+// Start ray t = s * nrec + r. Returns false if the ray is already complete (Tr written).
+__device__ __forceinline__ bool sec_init(const RenderArgs& A, uint32_t nrec, uint64_t t, SecRay& R) {
+    const uint32_t s = (uint32_t)(t / nrec);
+    const uint32_t r = (uint32_t)(t - (uint64_t)s * nrec);
+    const float4 pos = A.rec_pos[r];
+    const uint4 meta = A.rec_meta[r];
+    R.act_off = meta.z;
+    R.act_n = meta.w;
+    R.bloom = A.rec_bloom[r];
+    R.hitmask = 0;
+    R.tau = 0.0f;
+    R.tlast = 0.0f;
+    R.needs_stop = false;
+    if (s < (uint32_t)A.num_lights) {
+        const LightRecord& lr = A.lights[s];
+        float dx = lr.px - pos.x, dy = lr.py - pos.y, dz = lr.pz - pos.z;
+        float dist = sqrtf(dot3(dx, dy, dz, dx, dy, dz));
+        normalize3(dx, dy, dz);
+        R.ray = make_ray(pos.x, pos.y, pos.z, dx, dy, dz);
+        R.light = true;
+        R.lim = dist;
+        if (!(dist > 0.0f)) {  // `while (t_prev < dist)` never runs
+            A.tr[t] = 1.0f;
+            return false;
+        }
+    } else {
+        float wx, wy, wz;
+        env_sample_dir(A, meta, s - (uint32_t)A.num_lights, wx, wy, wz);
+        R.ray = make_ray(pos.x, pos.y, pos.z, wx, wy, wz);
+        R.light = false;
+        R.lim = INFINITY;
+    }
+    // |d| clamped away from 0: the fma slab form b/d - o/d must never see inf - inf
+    R.ix = __frcp_rn(fabsf(R.ray.dx) > 1e-30f ? R.ray.dx : copysignf(1e-30f, R.ray.dx));
+    R.iy = __frcp_rn(fabsf(R.ray.dy) > 1e-30f ? R.ray.dy : copysignf(1e-30f, R.ray.dy));
+    R.iz = __frcp_rn(fabsf(R.ray.dz) > 1e-30f ? R.ray.dz : copysignf(1e-30f, R.ray.dz));
+    R.oxi = R.ray.ox * R.ix;
+    R.oyi = R.ray.oy * R.iy;
+    R.ozi = R.ray.oz * R.iz;
+    return true;
+}
+
+template <bool S>
+__device__ __forceinline__ void sec_leaf(const RenderArgs& A, SecRay& R, int32_t ref, Ctr& c) {
+    const uint32_t first = leaf_first(ref), count = leaf_count(ref);
+    for (uint32_t j = first; j < first + count; ++j) {
+        if constexpr (S) c.v[kCtrPrims]++;
+        GRec g = load_rec(A.gauss, j);
+        Quad q = quad(g, R.ray);
+        float a, b;
+        if (!intersect(q, a, b)) continue;
+        int slot = act_find(A, R, (int)j);
+        float lo = a;
+        if (slot >= 0) {
+            lo = 0.0f;
+            R.hitmask |= 1ull << slot;
+        }
+        if (!R.light || b < R.lim) {
+            if constexpr (S) c.v[kCtrOD]++;
+            R.tau += optical_depth(g, q, lo, b);
+            R.tlast = fmaxf(R.tlast, b);
+        } else if (lo < R.lim) {
+            R.needs_stop = true;
+        }
+    }
+}
+
+// Ray complete: write its transmittance (or hand it to the exact slow path).
+template <bool S>
+__device__ __forceinline__ void sec_finish(const RenderArgs& A, uint64_t t, SecRay& R, Ctr& c) {
+    if (R.tau >= kTauCut) {
+        A.tr[t] = 0.0f;
+        return;
+    }
+    const uint64_t all = R.act_n >= 64 ? ~0ull : ((1ull << R.act_n) - 1ull);
+    uint64_t missed = all & ~R.hitmask;
+    if (R.light) {
+        if (R.needs_stop || missed) {
+            uint32_t slot = atomicAdd(A.slowq, 1u);
+            if (slot < A.slowq_cap) A.slowq[1 + slot] = (uint32_t)t;
+            else {
+                atomicAdd(A.counters, 1u);
+                A.tr[t] = __builtin_nanf("");
+            }
+            return;
+        }
+    } else {
+        while (missed) {  // pre-activated, missed through rounding: active up to the last event
+            int s = __ffsll((unsigned long long)missed) - 1;
+            missed &= missed - 1;
+            GRec g = load_rec(A.gauss, A.rec_act[R.act_off + s]);
+            Quad q = quad(g, R.ray);
+            if constexpr (S) c.v[kCtrOD]++;
+            R.tau += optical_depth(g, q, 0.0f, R.tlast);
+        }
+    }
+    A.tr[t] = expf(-R.tau);
+}
+
+// One BVH node pair of secondary ray R (plus the primitives of leaf children). Returns true when
+// the ray is complete (stack exhausted or optical depth past the cut-off).
 template <int BLOCK, bool S>
-__global__ __launch_bounds__(BLOCK) void secondary_kernel(RenderArgs A, uint32_t nrec) {
+__device__ __forceinline__ bool sec_step(const RenderArgs& A, SecRay& R, int* stack, int& sp, int& node, Ctr& c) {
+    if constexpr (S) c.v[kCtrNodes]++;
+    const float4* np = reinterpret_cast<const float4*>(A.nodes + node);
+    const float4 n0 = np[0], n1 = np[1], n2 = np[2];
+    const int4 nc = reinterpret_cast<const int4*>(A.nodes + node)[3];
+    float lmin, lmax, rmin, rmax;
+    {
+        float tx1 = fmaf(n0.x, R.ix, -R.oxi), tx2 = fmaf(n0.w, R.ix, -R.oxi);
+        float ty1 = fmaf(n0.y, R.iy, -R.oyi), ty2 = fmaf(n1.x, R.iy, -R.oyi);
+        float tz1 = fmaf(n0.z, R.iz, -R.ozi), tz2 = fmaf(n1.y, R.iz, -R.ozi);
+        lmin = fmaxf(fmaxf(fminf(tx1, tx2), fminf(ty1, ty2)), fminf(tz1, tz2));
+        lmax = fminf(fminf(fmaxf(tx1, tx2), fmaxf(ty1, ty2)), fmaxf(tz1, tz2));
+        float ux1 = fmaf(n1.z, R.ix, -R.oxi), ux2 = fmaf(n2.y, R.ix, -R.oxi);
+        float uy1 = fmaf(n1.w, R.iy, -R.oyi), uy2 = fmaf(n2.z, R.iy, -R.oyi);
+        float uz1 = fmaf(n2.x, R.iz, -R.ozi), uz2 = fmaf(n2.w, R.iz, -R.ozi);
+        rmin = fmaxf(fmaxf(fminf(ux1, ux2), fminf(uy1, uy2)), fminf(uz1, uz2));
+        rmax = fminf(fminf(fmaxf(ux1, ux2), fmaxf(uy1, uy2)), fmaxf(uz1, uz2));
+    }
+    const float lim = R.lim + kTPad * (1.0f + R.lim);
+    bool hl = nc.x != 0 && lmax >= fmaxf(lmin, 0.0f) && lmin <= lim;
+    bool hr = nc.y != 0 && rmax >= fmaxf(rmin, 0.0f) && rmin <= lim;
+    const bool ll = hl && ref_is_leaf(nc.x), lr = hr && ref_is_leaf(nc.y);
+    if (ll || lr) {
+        const bool r_first = lr && (!ll || rmin < lmin);
+        sec_leaf<S>(A, R, r_first ? nc.y : nc.x, c);
+        if (ll && lr && R.tau < kTauCut) sec_leaf<S>(A, R, r_first ? nc.x : nc.y, c);
+        if (ll) hl = false;
+        if (lr) hr = false;
+    }
+    bool done = R.tau >= kTauCut;
+    if (!done) {
+        if (hl && hr) {
+            int nearer = nc.x, farther = nc.y;
+            if (rmin < lmin) {
+                nearer = nc.y;
+                farther = nc.x;
+            }
+            stack[sp * BLOCK] = farther;
+            ++sp;
+            node = nearer;
+        } else if (hl) {
+            node = nc.x;
+        } else if (hr) {
+            node = nc.y;
+        } else if (sp > 0) {
+            --sp;
+            node = stack[sp * BLOCK];
+        } else {
+            done = true;
+        }
+    }
+    return done;
+}
+
+// One ray per lane, grid-stride over ray ids [t_begin, t_end) (light rays: already coherent —
+// neighbouring lanes trace from neighbouring pixels towards the same light).
+template <int BLOCK, bool S>
+__global__ __launch_bounds__(BLOCK) void secondary_simple_kernel(RenderArgs A, uint32_t nrec, uint64_t t_begin,
+                                                                 uint64_t t_end) {
     __shared__ int s_stack[kStackSize * BLOCK];
     int* stack = s_stack + threadIdx.x;
-    const uint32_t nsamp = (uint32_t)(A.num_lights + A.env_samples);
-    const uint64_t total = (uint64_t)nrec * nsamp;
     Ctr c{};
     const uint64_t stride_t = (uint64_t)gridDim.x * BLOCK;
-    const uint64_t t0 = (uint64_t)blockIdx.x * BLOCK + threadIdx.x;
-    const uint64_t rounds = (total + stride_t - 1) / stride_t;  // uniform trip count (all lanes flush)
-    for (uint64_t it = 0; it < rounds; ++it) {
-        const uint64_t t = t0 + it * stride_t;
-        if (t >= total) continue;
+    for (uint64_t t = t_begin + (uint64_t)blockIdx.x * BLOCK + threadIdx.x; t < t_end; t += stride_t) {
+        SecRay R;
+        if constexpr (S) c.v[kCtrSecRays]++;
+        if (!sec_init(A, nrec, t, R)) continue;
+        int sp = 0, node = 0;
+        while (!sec_step<BLOCK, S>(A, R, stack, sp, node, c)) {
+        }
+        sec_finish<S>(A, t, R, c);
+    }
+    if constexpr (S)
+        for (int i = 0; i < kNumCtr; ++i)
+            if (c.v[i]) atomicAdd(A.work + i, (unsigned long long)c.v[i]);
+}
+
+// Environment rays: their directions are independent per (pixel, step, sample), so lanes of a wave
+// taking consecutive ray ids fetch unrelated BVH nodes (measured: ~7x the cost per node step of
+// the coherent light rays). Each workgroup takes CHUNK consecutive env-ray ids (neighbouring
+// pixels, same sample index), counting-sorts them in LDS by octahedral direction cell, and traces
+// them in that order, so a wave's rays share origin neighbourhood AND direction cone. Each ray
+// still writes its own slot, so the result does not depend on the order.
+template <int BLOCK, int PER, bool S>
+__global__ __launch_bounds__(BLOCK) void secondary_binned_kernel(RenderArgs A, uint32_t nrec, uint64_t t_begin,
+                                                                 uint64_t t_end) {
+    constexpr int CHUNK = BLOCK * PER;
+    constexpr int NBIN = 64;
+    __shared__ int s_stack[kStackSize * BLOCK];
+    __shared__ uint32_t s_sorted[CHUNK];
+    __shared__ uint32_t s_hist[NBIN];
+    int* stack = s_stack + threadIdx.x;
+    Ctr c{};
+    const uint64_t nchunks = (t_end - t_begin + CHUNK - 1) / CHUNK;
+    for (uint64_t ch = blockIdx.x; ch < nchunks; ch += gridDim.x) {
+        const uint64_t base = t_begin + ch * CHUNK;
+        if (threadIdx.x < NBIN) s_hist[threadIdx.x] = 0;
+        __syncthreads();
+        uint32_t cell[PER];
+        #pragma unroll
+        for (int i = 0; i < PER; ++i) {
+            const uint64_t t = base + (uint64_t)i * BLOCK + threadIdx.x;
+            cell[i] = NBIN;  // past the end
+            if (t < t_end) {
+                const uint32_t s = (uint32_t)(t / nrec);
+                const uint32_t r = (uint32_t)(t - (uint64_t)s * nrec);
+                float wx, wy, wz;
+                env_sample_dir(A, A.rec_meta[r], s - (uint32_t)A.num_lights, wx, wy, wz);
+                cell[i] = dir_cell(wx, wy, wz);
+                atomicAdd(&s_hist[cell[i]], 1u);
+            }
+        }
+        __syncthreads();
+        if (threadIdx.x < 64) {  // exclusive scan of the 64 cell counts (one wave)
+            uint32_t v = s_hist[threadIdx.x], x = v;
+            for (int o = 1; o < 64; o <<= 1) {
+                uint32_t y = __shfl_up(x, o, 64);
+                if ((int)threadIdx.x >= o) x += y;
+            }
+            s_hist[threadIdx.x] = x - v;
+        }
+        __syncthreads();
+        uint32_t valid = 0;
+        #pragma unroll
+        for (int i = 0; i < PER; ++i)
+            if (cell[i] < NBIN) {
+                const uint32_t slot = atomicAdd(&s_hist[cell[i]], 1u);
+                s_sorted[slot] = (uint32_t)(i * BLOCK + threadIdx.x);
+                ++valid;
+            }
+        __syncthreads();
+        const uint32_t n = (uint32_t)min((uint64_t)CHUNK, t_end - base);
+        for (uint32_t q = threadIdx.x; q < n; q += BLOCK) {
+            const uint64_t t = base + s_sorted[q];
+            SecRay R;
+            if constexpr (S) c.v[kCtrSecRays]++;
+            if (!sec_init(A, nrec, t, R)) continue;
+            int sp = 0, node = 0;
+            while (!sec_step<BLOCK, S>(A, R, stack, sp, node, c)) {
+            }
+            sec_finish<S>(A, t, R, c);
+        }
+        __syncthreads();
+    }
+    if constexpr (S)
+        for (int i = 0; i < kNumCtr; ++i)
+            if (c.v[i]) atomicAdd(A.work + i, (unsigned long long)c.v[i]);
+}
+
+template <int BLOCK, bool S>
+__global__ __launch_bounds__(BLOCK) void secondary_persistent_kernel(RenderArgs A, uint32_t nrec, uint64_t total,
+                                                                     uint64_t chunk) {
+    __shared__ int s_stack[kStackSize * BLOCK];
+    int* stack = s_stack + threadIdx.x;
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint64_t wave = ((uint64_t)blockIdx.x * BLOCK + threadIdx.x) >> 6;
+    const uint64_t begin = wave * chunk;
+    const uint64_t end = begin + chunk < total ? begin + chunk : total;
+    uint64_t next = begin;  // wave-uniform
+    Ctr c{};
+    SecRay R;
+    bool live = false;
+    uint64_t t = 0;
+    int sp = 0, node = 0;
+    for (;;) {
+        // refill lanes whose ray is done from the wave's chunk
+        // refill once a quarter of the wave is idle (amortises the ray set-up over many lanes)
+        const uint64_t need = __ballot(!live);
+        if (__popcll(need) >= 16 || need == ~0ull) {
+            const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(need >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)need, 0u));
+            if (!live) {
+                t = next + rank;
+                if (t < end) {
+                    if constexpr (S) c.v[kCtrSecRays]++;
+                    live = sec_init(A, nrec, t, R);
+                    sp = 0;
+                    node = 0;
+                }
+            }
+            next += (uint64_t)__popcll(need);
+        }
+        if (!__any(live)) break;
+        if (!live) continue;
+        if (sec_step<BLOCK, S>(A, R, stack, sp, node, c)) {
+            sec_finish<S>(A, t, R, c);
+            live = false;
+        }
+    }
+    if constexpr (S) flush_counters(A.work, c);
+}
+
+// Exact three-pass light transmittance for the queued rays (see light_transmittance).
+template <int BLOCK, bool S>
+__global__ __launch_bounds__(BLOCK) void secondary_slow_kernel(RenderArgs A, uint32_t nrec) {
+    __shared__ int s_stack[kStackSize * BLOCK];
+    int* stack = s_stack + threadIdx.x;
+    const uint32_t n = min(A.slowq[0], A.slowq_cap);
+    Ctr c{};
+    for (uint32_t q = blockIdx.x * BLOCK + threadIdx.x; q < n; q += gridDim.x * BLOCK) {
+        const uint64_t t = A.slowq[1 + q];
         const uint32_t s = (uint32_t)(t / nrec);
         const uint32_t r = (uint32_t)(t - (uint64_t)s * nrec);
         const float4 pos = A.rec_pos[r];
         const uint4 meta = A.rec_meta[r];
-        ActList act{A.rec_act + meta.z, 1, (int)meta.w, 0};
-        act.rebuild_bloom();
-        if constexpr (S) c.v[kCtrSecRays]++;
-        float Tr;
-        if (s < (uint32_t)A.num_lights) {
-            const LightRecord& lr = A.lights[s];
-            float dx = lr.px - pos.x, dy = lr.py - pos.y, dz = lr.pz - pos.z;
-            float dist = sqrtf(dot3(dx, dy, dz, dx, dy, dz));
-            normalize3(dx, dy, dz);
-            Ray sr = make_ray(pos.x, pos.y, pos.z, dx, dy, dz);
-            Tr = light_transmittance<S>(A, sr, dist, act, stack, BLOCK, c);
-        } else {
-            const uint32_t e = s - (uint32_t)A.num_lights;
-            const int px = (int)(meta.x & 0xffffu), py = (int)(meta.x >> 16);
-            PCG32 rng(derive_path_seed(px, py, (int)meta.y), 1);
-            for (uint32_t i = 0; i < 2 * e; ++i) rng.next_u32();
-            float xi1 = rng.uniform();
-            float xi2 = rng.uniform();
-            float wx, wy, wz;
-            env_dir(xi1, xi2, wx, wy, wz);
-            Ray er = make_ray(pos.x, pos.y, pos.z, wx, wy, wz);
-            Tr = env_transmittance<S>(A, er, act, stack, BLOCK, c);
-        }
-        A.tr[t] = Tr;
+        ActList act{A.rec_act + meta.z, 1, (int)meta.w, A.rec_bloom[r]};
+        const LightRecord& lr = A.lights[s];
+        float dx = lr.px - pos.x, dy = lr.py - pos.y, dz = lr.pz - pos.z;
+        float dist = sqrtf(dot3(dx, dy, dz, dx, dy, dz));
+        normalize3(dx, dy, dz);
+        Ray sr = make_ray(pos.x, pos.y, pos.z, dx, dy, dz);
+        A.tr[t] = light_transmittance<S>(A, sr, dist, act, stack, BLOCK, c);
     }
-    if constexpr (S) flush_counters(A.work, c);
+    if constexpr (S)
+        for (int i = 0; i < kNumCtr; ++i)
+            if (c.v[i]) atomicAdd(A.work + i, (unsigned long long)c.v[i]);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -528,18 +822,63 @@ hipError_t gauss_scan(const RenderArgs& A, uint32_t npix, void* temp, size_t& te
     return hipGetLastError();
 }
 
-hipError_t gauss_secondary(const RenderArgs& A, uint32_t nrec, hipStream_t stream, bool stats) {
-    uint64_t total = (uint64_t)nrec * (uint64_t)(A.num_lights + A.env_samples);
-    if (total == 0) return hipSuccess;
-    uint64_t blocks = (total + kBlockSecondary - 1) / kBlockSecondary;
-    if (blocks > 65536ull * 16ull) blocks = 65536ull * 16ull;
-    if (stats)
-        hipLaunchKernelGGL((dev::secondary_kernel<kBlockSecondary, true>), dim3((unsigned)blocks), dim3(kBlockSecondary), 0,
-                           stream, A, nrec);
-    else
-        hipLaunchKernelGGL((dev::secondary_kernel<kBlockSecondary, false>), dim3((unsigned)blocks), dim3(kBlockSecondary), 0,
-                           stream, A, nrec);
+template <bool S>
+static hipError_t secondary_launch(const RenderArgs& A, uint32_t nrec, uint64_t total, hipStream_t stream) {
+    // Kernel choice (measured on C4, 4096^2 / 1M Gaussians: simple 2.13 s, env-binned 2.30 s,
+    // persistent 3.57 s): one thread per secondary ray in record order is fastest, because
+    // neighbouring records are neighbouring pixels and their rays already share BVH paths.
+    // VR_SECONDARY=b / p select the direction-binned or persistent variants for A/B runs.
+    static int variant = -1;  // 0 simple, 1 light simple + env binned, 2 persistent
+    if (variant < 0) {
+        const char* v = getenv("VR_SECONDARY");
+        variant = (v && v[0] == 'b') ? 1 : (v && v[0] == 'p') ? 2 : 0;
+    }
+    static int grid = 0;  // persistent grid: every CU filled to its occupancy limit
+    if (variant == 2 && grid == 0) {
+        int dev = 0, cus = 0, per_cu = 0;
+        if (hipGetDevice(&dev) != hipSuccess) return hipErrorUnknown;
+        if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return hipErrorUnknown;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, dev::secondary_persistent_kernel<kBlockSecondary, S>,
+                                                         kBlockSecondary, 0) != hipSuccess || per_cu < 1)
+            per_cu = 1;
+        grid = cus * per_cu;
+        if (getenv("VR_DEBUG")) fprintf(stderr, "[vr] persistent secondary grid: %d CUs x %d blocks\n", cus, per_cu);
+    }
+    const uint64_t nlight = (uint64_t)nrec * (uint64_t)A.num_lights;
+    auto simple = [&](uint64_t b0, uint64_t b1) {
+        if (b1 <= b0) return;
+        uint64_t blocks = (b1 - b0 + kBlockSecondary - 1) / kBlockSecondary;
+        if (blocks > 65536ull * 16ull) blocks = 65536ull * 16ull;
+        hipLaunchKernelGGL((dev::secondary_simple_kernel<kBlockSecondary, S>), dim3((unsigned)blocks), dim3(kBlockSecondary), 0,
+                           stream, A, nrec, b0, b1);
+    };
+    if (variant == 0) {
+        simple(0, total);
+    } else if (variant == 2) {
+        const uint64_t waves = (uint64_t)grid * (kBlockSecondary / 64);
+        const uint64_t chunk = (total + waves - 1) / waves;
+        hipLaunchKernelGGL((dev::secondary_persistent_kernel<kBlockSecondary, S>), dim3(grid), dim3(kBlockSecondary), 0,
+                           stream, A, nrec, total, chunk);
+    } else {
+        simple(0, nlight);
+        if (total > nlight) {
+            constexpr int kPer = 8;
+            uint64_t chunks = (total - nlight + kBlockSecondary * kPer - 1) / (kBlockSecondary * kPer);
+            if (chunks > 65536ull * 8ull) chunks = 65536ull * 8ull;
+            hipLaunchKernelGGL((dev::secondary_binned_kernel<kBlockSecondary, kPer, S>), dim3((unsigned)chunks),
+                               dim3(kBlockSecondary), 0, stream, A, nrec, nlight, total);
+        }
+    }
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL((dev::secondary_slow_kernel<64, S>), dim3(512), dim3(64), 0, stream, A, nrec);
     return hipGetLastError();
+}
+
+hipError_t gauss_secondary(const RenderArgs& A, uint32_t nrec, hipStream_t stream, bool stats) {
+    const uint64_t total = (uint64_t)nrec * (uint64_t)(A.num_lights + A.env_samples);
+    if (total == 0) return hipSuccess;
+    return stats ? secondary_launch<true>(A, nrec, total, stream) : secondary_launch<false>(A, nrec, total, stream);
 }
 
 hipError_t gauss_accumulate(const RenderArgs& A, uint32_t nrec, hipStream_t stream) {

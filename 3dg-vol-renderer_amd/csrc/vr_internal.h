@@ -100,6 +100,10 @@ struct RenderArgs {
     float* tr;          // per secondary ray: transmittance, [sample][record]
     const uint32_t* totals;  // device: [0] records, [1] act entries
     uint32_t rec_cap, act_cap;
+    unsigned long long* rec_bloom;  // per record: 64-bit membership mask of its active list
+    uint32_t* slowq;                // light rays needing the exact stopping event: [0] count, [1..] ray ids
+    uint32_t slowq_cap;
+    const unsigned long long* pcg_jump;  // [2k] = A^k, [2k+1] = inc (A^(k-1) + ... + 1): PCG32 state after k draws
 };
 
 }  // namespace vr

@@ -28,6 +28,7 @@ import torch  # noqa: E402  (first: its HIP runtime is the process runtime, see 
 import torch.distributed as dist  # noqa: E402
 
 import vr_amd as vr  # noqa: E402
+from vr_amd import tiles  # noqa: E402
 
 CONFIGS = {
     # name: (W, H, n_gaussians or scene file, description)
@@ -132,16 +133,11 @@ def main():
     def step(i=None):
         if i is not None:
             kev[i][0].record(stream)
-        if world == 1:
-            dev.render_tiles_device(camera, integ.params, W, H, 0, 1, ntiles, False, frame.data_ptr(), sp)
-        else:
-            dev.render_tiles_device(camera, integ.params, W, H, rank, world, mine, True, slab.data_ptr(), sp)
+        tiles.render_local(dev, camera, integ.params, W, H, rank, world, None if world == 1 else slab, frame, sp)
         if i is not None:
             kev[i][1].record(stream)
         if world > 1:
-            dist.gather(slab, list(slabs.unbind(0)) if rank == 0 else None, dst=0)
-            if rank == 0:
-                dev.unshuffle_tiles_device(slabs.data_ptr(), world, per, W, H, frame.data_ptr(), sp)
+            tiles.gather_frame(dev, W, H, rank, world, slab, slabs, frame, sp, dist)
 
     def log(msg):
         if rank == 0:

@@ -1,0 +1,77 @@
+"""Multi-process tile sharding on CPU (torch.distributed gloo, world size 2 and 3).
+
+Each rank renders its interleaved tile share with the CPU oracle (a stand-in for the device
+renderer, which tests/test_gpu_parity.py checks bit-for-bit against the single-call frame),
+packs it into a slab exactly as vr_render_tiles_device does, the slabs are gathered to rank 0 and
+unshuffled; the reassembled frame must equal the oracle's full frame bit for bit.
+"""
+import os
+import socket
+import sys
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, W, H, q):
+    for p in (os.path.join(ROOT, "3dg-vol-renderer_amd"), os.path.join(ROOT, "oracle"), os.path.join(ROOT, "tests")):
+        sys.path.insert(0, p)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import pyoracle as O
+        from helpers import CAM_POS, FOV, main_view_dir, scene_path
+        from vr_amd import tiles
+
+        first, stride, count, per = tiles.rank_tiles(W, H, rank, world)
+        x, y = tiles.tile_pixels(W, H, first, stride, count)
+        inside = x >= 0
+        s = O.OracleScene.load_gmm(scene_path("many_gaussians.txt"))
+        rgb = O.render(s, O.PINHOLE, CAM_POS, main_view_dir(), FOV, W, H, env_samples=4,
+                       pixels=np.stack([x[inside], y[inside]], 1), nthreads=1)
+        slab = torch.zeros((per * 256, 3), dtype=torch.float32)
+        slab[: count * 256][torch.from_numpy(inside)] = torch.from_numpy(rgb)
+        gathered = [torch.zeros_like(slab) for _ in range(world)] if rank == 0 else None
+        dist.gather(slab, gathered, dst=0)
+        if rank == 0:
+            img = tiles.unshuffle_reference(torch.stack(gathered).numpy(), W, H)
+            full = O.render(s, O.PINHOLE, CAM_POS, main_view_dir(), FOV, W, H, env_samples=4, nthreads=1)
+            q.put(bool(np.array_equal(img, full)))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,W,H", [(2, 40, 24), (3, 33, 50)])
+def test_tile_sharding_gather_unshuffle_gloo(world, W, H):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    mp.start_processes(_worker, args=(world, port, W, H, q), nprocs=world, join=True, start_method="spawn")
+    assert q.get(timeout=60) is True
+
+
+def test_rank_tiles_partition_covers_frame_once():
+    sys.path.insert(0, os.path.join(ROOT, "3dg-vol-renderer_amd"))
+    from vr_amd import tiles
+    for W, H, R in [(4096, 4096, 8), (1920, 1080, 3), (17, 5, 4), (100, 70, 7)]:
+        seen = np.zeros((H, W), np.int32)
+        for r in range(R):
+            first, stride, count, per = tiles.rank_tiles(W, H, r, R)
+            assert count <= per
+            x, y = tiles.tile_pixels(W, H, first, stride, count)
+            m = x >= 0
+            np.add.at(seen, (y[m], x[m]), 1)
+        assert np.all(seen == 1)

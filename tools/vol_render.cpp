@@ -1,0 +1,107 @@
+// vol_render: command-line renderer over the C++ host API (the role of the reference's
+// tests/main.cpp, which hard-codes scene, camera and integrator; here they are arguments).
+//
+//   vol_render --scene scenes/many_gaussians.txt [--spheres] [--xml] [--size 512x512]
+//              [--integrator gaussians|spheres|test] [--step 0.01] [--env 20]
+//              [--camera pinhole|ortho] [--pos 0,1,6] [--lookat 0,1,0] [--fov 0.785398]
+//              [--out output.ppm] [--dump-rays N]
+//
+// --dump-rays N prints the first N primary rays (host only, no GPU) — used by the CPU tests.
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
+#include <iostream>
+#include <numbers>
+#include <string>
+
+#include "vr/integrator.h"
+#include "vr/test_integrators.h"
+
+static Eigen::Vector3f parse3(const char* s) {
+    float a = 0, b = 0, c = 0;
+    if (std::sscanf(s, "%f,%f,%f", &a, &b, &c) != 3) throw std::runtime_error(std::string("bad vector: ") + s);
+    return Eigen::Vector3f(a, b, c);
+}
+
+int main(int argc, char** argv) try {
+    std::string scene_path, out = "output.ppm", integ = "gaussians", cam_type = "pinhole";
+    bool spheres = false, xml = false;
+    unsigned W = 512, H = 512;
+    float step = 0.01f, fov = 0.25f * std::numbers::pi_v<float>;
+    int env = -1, dump = 0;
+    Eigen::Vector3f pos(0, 1, 6), lookat(0, 1, 0);
+    for (int i = 1; i < argc; ++i) {
+        std::string a = argv[i];
+        auto next = [&]() -> const char* {
+            if (i + 1 >= argc) throw std::runtime_error("missing value for " + a);
+            return argv[++i];
+        };
+        if (a == "--scene") scene_path = next();
+        else if (a == "--spheres") spheres = true;
+        else if (a == "--xml") xml = true;
+        else if (a == "--size") { if (std::sscanf(next(), "%ux%u", &W, &H) != 2) throw std::runtime_error("bad --size"); }
+        else if (a == "--integrator") integ = next();
+        else if (a == "--step") step = std::strtof(next(), nullptr);
+        else if (a == "--env") env = std::atoi(next());
+        else if (a == "--camera") cam_type = next();
+        else if (a == "--pos") pos = parse3(next());
+        else if (a == "--lookat") lookat = parse3(next());
+        else if (a == "--fov") fov = std::strtof(next(), nullptr);
+        else if (a == "--out") out = next();
+        else if (a == "--dump-rays") dump = std::atoi(next());
+        else throw std::runtime_error("unknown argument " + a);
+    }
+    if (scene_path.empty()) throw std::runtime_error("--scene is required");
+
+    std::shared_ptr<Camera> camera;
+    Scene scene;
+    vr_render_params xml_params{};
+    if (xml) {
+        vr_camera st{};
+        uint32_t w = 0, h = 0;
+        scene = Scene::load_XML(scene_path, &st, &w, &h, &xml_params);
+        camera = std::make_shared<State_Camera>(st);
+        W = w;
+        H = h;
+        integ = xml_params.integrator == VR_RAYMARCH_SPHERES ? "spheres" : "gaussians";
+        if (env < 0) env = xml_params.env_samples;
+        step = xml_params.step_size;
+    } else {
+        scene = spheres ? Scene::load_SMM(scene_path) : Scene::load_GMM(scene_path);
+        Eigen::Vector3f view_dir = (lookat - pos).normalized();
+        if (cam_type == "ortho") camera = std::make_shared<Orthographic_Camera>(pos, view_dir);
+        else camera = std::make_shared<Pinhole_Camera>(pos, view_dir, fov);
+    }
+    std::printf("scene: %zu primitives, %zu lights\n", scene.get_num_primitives(), scene.lights.size());
+
+    if (dump > 0) {  // host-only: primary rays through pixel centres, row-major
+        for (int k = 0; k < dump; ++k) {
+            unsigned x = k % W, y = k / W;
+            Eigen::Vector2d uv((x + 0.5) / W, (y + 0.5) / H);
+            Ray r = camera->sample_ray(uv);
+            std::printf("ray %u %u %.9g %.9g %.9g %.9g %.9g %.9g\n", x, y, r.origin.x(), r.origin.y(), r.origin.z(),
+                        r.direction.x(), r.direction.y(), r.direction.z());
+        }
+        return 0;
+    }
+
+    std::unique_ptr<HipIntegrator> integrator;
+    if (integ == "gaussians") integrator = std::make_unique<RayMarchingGaussians>(camera, step, env < 0 ? 20 : env);
+    else if (integ == "spheres") integrator = std::make_unique<RayMarchingSpheres>(camera, step, env < 0 ? 5 : env);
+    else if (integ == "test") integrator = std::make_unique<TestIntegrator>(camera);
+    else throw std::runtime_error("unknown integrator " + integ);
+
+    Image image(W, H);
+    auto t0 = std::chrono::high_resolution_clock::now();
+    integrator->render(scene, image);
+    auto t1 = std::chrono::high_resolution_clock::now();
+    vr_render_stats st = integrator->stats();
+    std::printf("Render time: %.6f seconds (device %.3f ms, %lld pixels, %lld fallback)\n",
+                std::chrono::duration<double>(t1 - t0).count(), st.kernel_ms, (long long)st.pixels,
+                (long long)st.fallback_pixels);
+    image.make_PPM(out);
+    return 0;
+} catch (const std::exception& e) {
+    std::fprintf(stderr, "vol_render: %s\n", e.what());
+    return 1;
+}
