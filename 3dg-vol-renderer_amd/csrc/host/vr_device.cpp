@@ -54,6 +54,8 @@ struct vr_ctx {
     float* d_frame = nullptr;
     size_t frame_cap = 0;
     hipEvent_t ev_start = nullptr, ev_stop = nullptr;
+    hipEvent_t ev_stage[4] = {nullptr, nullptr, nullptr, nullptr};  // stage boundaries of gauss_pipeline
+    bool staged = false;                                            // last launch recorded ev_stage
     bool stats_pending = false;
     int64_t last_pixels = 0;
     // wavefront pipeline buffers (grown on demand, never shrunk)
@@ -241,6 +243,7 @@ vr_status gauss_pipeline(vr_ctx* c, RenderArgs& A, hipStream_t s, bool stats) {
     if ((st = grow(c->scan_tmp, tmp_bytes, "hipMalloc(scan)")) != VR_OK) return st;
     tmp_bytes = c->scan_tmp.bytes;
     HIP_TRY(gauss_march(A, s, 0, stats), "march (count)");
+    HIP_TRY(hipEventRecord(c->ev_stage[0], s), "hipEventRecord");
     HIP_TRY(gauss_scan(A, npix, c->scan_tmp.p, tmp_bytes, (uint32_t*)c->totals.p, s), "scan");
     HIP_TRY(hipMemcpyAsync(c->h_totals, c->totals.p, 2 * sizeof(uint32_t), hipMemcpyDeviceToHost, s), "totals D2H");
     HIP_TRY(hipStreamSynchronize(s), "march (count)");
@@ -265,9 +268,13 @@ vr_status gauss_pipeline(vr_ctx* c, RenderArgs& A, hipStream_t s, bool stats) {
     A.rec_cap = nrec;
     A.act_cap = nact;
     HIP_TRY(hipMemsetAsync(c->d_queue, 0, sizeof(uint32_t), s), "hipMemsetAsync(queue)");
+    HIP_TRY(hipEventRecord(c->ev_stage[1], s), "hipEventRecord");
     HIP_TRY(gauss_march(A, s, 1, stats), "march (write)");
+    HIP_TRY(hipEventRecord(c->ev_stage[2], s), "hipEventRecord");
     HIP_TRY(gauss_secondary(A, nrec, s, stats), "secondary rays");
+    HIP_TRY(hipEventRecord(c->ev_stage[3], s), "hipEventRecord");
     HIP_TRY(gauss_accumulate(A, nrec, s), "accumulate");
+    c->staged = true;
     c->last_records = nrec;
     c->last_secondary = (int64_t)nsec;
     return VR_OK;
@@ -285,6 +292,9 @@ vr_status launch(vr_ctx* c, RenderArgs& A, const vr_render_params* p, hipStream_
     HIP_TRY(hipMemsetAsync(c->d_queue, 0, sizeof(uint32_t), s), "hipMemsetAsync(queue)");
     HIP_TRY(hipMemsetAsync(c->d_counters, 0, 4 * sizeof(uint32_t), s), "hipMemsetAsync(counters)");
     HIP_TRY(hipEventRecord(c->ev_start, s), "hipEventRecord");
+    c->staged = false;
+    c->last_records = 0;
+    c->last_secondary = 0;
     if (c->type == VR_VOLUME_GAUSSIANS && p->integrator == VR_RAYMARCH_GAUSSIANS) {
         st = gauss_pipeline(c, A, s, stats);
         if (st != VR_OK) return st;
@@ -316,7 +326,9 @@ vr_status vr_init(int device, vr_ctx** out) {
         hipMalloc(&c->d_counters, 4 * sizeof(uint32_t)) != hipSuccess ||
         hipHostMalloc(&c->h_counters, 4 * sizeof(uint32_t), hipHostMallocDefault) != hipSuccess ||
         hipHostMalloc(&c->h_totals, 4 * sizeof(uint32_t), hipHostMallocDefault) != hipSuccess ||
-        hipEventCreate(&c->ev_start) != hipSuccess || hipEventCreate(&c->ev_stop) != hipSuccess) {
+        hipEventCreate(&c->ev_start) != hipSuccess || hipEventCreate(&c->ev_stop) != hipSuccess ||
+        hipEventCreate(&c->ev_stage[0]) != hipSuccess || hipEventCreate(&c->ev_stage[1]) != hipSuccess ||
+        hipEventCreate(&c->ev_stage[2]) != hipSuccess || hipEventCreate(&c->ev_stage[3]) != hipSuccess) {
         vr_destroy(c);
         return fail(VR_ERR_HIP, "vr_init: failed to create stream/workspace");
     }
@@ -341,6 +353,8 @@ void vr_destroy(vr_ctx* c) {
     if (c->d_frame) (void)hipFree(c->d_frame);
     if (c->ev_start) (void)hipEventDestroy(c->ev_start);
     if (c->ev_stop) (void)hipEventDestroy(c->ev_stop);
+    for (hipEvent_t e : c->ev_stage)
+        if (e) (void)hipEventDestroy(e);
     if (c->stream) (void)hipStreamDestroy(c->stream);
     delete c;
 }
@@ -464,7 +478,7 @@ vr_status vr_render_tiles_device(vr_ctx* c, const vr_camera* cam, const vr_rende
 }
 
 vr_status vr_count_work(vr_ctx* c, const vr_camera* cam, const vr_render_params* p, uint32_t W, uint32_t H,
-                        uint32_t first_tile, uint32_t tile_stride, uint32_t num_tiles, uint64_t counts[8]) {
+                        uint32_t first_tile, uint32_t tile_stride, uint32_t num_tiles, uint64_t counts[16]) {
     if (!c || !counts) return fail(VR_ERR_INVALID, "vr_count_work: NULL argument");
     HIP_TRY(hipSetDevice(c->device), "hipSetDevice");
     RenderArgs A;
@@ -477,8 +491,8 @@ vr_status vr_count_work(vr_ctx* c, const vr_camera* cam, const vr_render_params*
     float* d_out = nullptr;
     unsigned long long* d_work = nullptr;
     HIP_TRY(hipMalloc(&d_out, (size_t)num_tiles * 256 * 3 * sizeof(float)), "hipMalloc(count_work out)");
-    HIP_TRY(hipMalloc(&d_work, 8 * sizeof(unsigned long long)), "hipMalloc(count_work)");
-    HIP_TRY(hipMemsetAsync(d_work, 0, 8 * sizeof(unsigned long long), c->stream), "hipMemsetAsync");
+    HIP_TRY(hipMalloc(&d_work, 16 * sizeof(unsigned long long)), "hipMalloc(count_work)");
+    HIP_TRY(hipMemsetAsync(d_work, 0, 16 * sizeof(unsigned long long), c->stream), "hipMemsetAsync");
     A.first_tile = first_tile;
     A.tile_stride = tile_stride;
     A.num_tiles = num_tiles;
@@ -486,7 +500,7 @@ vr_status vr_count_work(vr_ctx* c, const vr_camera* cam, const vr_render_params*
     A.out = d_out;
     A.work = d_work;
     st = launch(c, A, p, c->stream, true);
-    unsigned long long h[8] = {0};
+    unsigned long long h[16] = {0};
     if (st == VR_OK) {
         hipError_t e = hipMemcpyAsync(h, d_work, sizeof(h), hipMemcpyDeviceToHost, c->stream);
         if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
@@ -495,7 +509,7 @@ vr_status vr_count_work(vr_ctx* c, const vr_camera* cam, const vr_render_params*
     c->stats_pending = false;
     (void)hipFree(d_out);
     (void)hipFree(d_work);
-    for (int i = 0; i < 8; ++i) counts[i] = h[i];
+    for (int i = 0; i < 16; ++i) counts[i] = h[i];
     return st;
 }
 
@@ -526,6 +540,17 @@ vr_status vr_get_stats(vr_ctx* c, vr_render_stats* o) {
     o->pixels = c->last_pixels;
     o->fallback_pixels = c->h_counters[0];
     o->error_pixels = c->h_counters[1];
+    for (double& v : o->stage_ms) v = 0.0;
+    if (c->staged) {
+        hipEvent_t b[6] = {c->ev_start, c->ev_stage[0], c->ev_stage[1], c->ev_stage[2], c->ev_stage[3], c->ev_stop};
+        for (int i = 0; i < 5; ++i) {
+            float m = 0.0f;
+            HIP_TRY(hipEventElapsedTime(&m, b[i], b[i + 1]), "hipEventElapsedTime");
+            o->stage_ms[i] = m;
+        }
+    }
+    o->scatter_records = c->last_records;
+    o->secondary_rays = c->last_secondary;
     return VR_OK;
 }
 

@@ -587,7 +587,7 @@ __global__ __launch_bounds__(BLOCK) void secondary_simple_kernel(RenderArgs A, u
     }
     if constexpr (S)
         for (int i = 0; i < kNumCtr; ++i)
-            if (c.v[i]) atomicAdd(A.work + i, (unsigned long long)c.v[i]);
+            if (c.v[i]) atomicAdd(A.work + kNumCtr + i, (unsigned long long)c.v[i]);
 }
 
 // Environment rays: their directions are independent per (pixel, step, sample), so lanes of a wave
@@ -659,7 +659,7 @@ __global__ __launch_bounds__(BLOCK) void secondary_binned_kernel(RenderArgs A, u
     }
     if constexpr (S)
         for (int i = 0; i < kNumCtr; ++i)
-            if (c.v[i]) atomicAdd(A.work + i, (unsigned long long)c.v[i]);
+            if (c.v[i]) atomicAdd(A.work + kNumCtr + i, (unsigned long long)c.v[i]);
 }
 
 template <int BLOCK, bool S>
@@ -701,7 +701,7 @@ __global__ __launch_bounds__(BLOCK) void secondary_persistent_kernel(RenderArgs 
             live = false;
         }
     }
-    if constexpr (S) flush_counters(A.work, c);
+    if constexpr (S) flush_counters(A.work + kNumCtr, c);
 }
 
 // Exact three-pass light transmittance for the queued rays (see light_transmittance).
@@ -727,7 +727,7 @@ __global__ __launch_bounds__(BLOCK) void secondary_slow_kernel(RenderArgs A, uin
     }
     if constexpr (S)
         for (int i = 0; i < kNumCtr; ++i)
-            if (c.v[i]) atomicAdd(A.work + i, (unsigned long long)c.v[i]);
+            if (c.v[i]) atomicAdd(A.work + kNumCtr + i, (unsigned long long)c.v[i]);
 }
 
 // ---------------------------------------------------------------------------------------------

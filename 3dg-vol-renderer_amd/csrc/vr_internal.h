@@ -86,7 +86,7 @@ struct RenderArgs {
     uint32_t* queue;       // [0] = count, [1..] = packed pixel ids (tile_local << 8 | lane)
     uint32_t queue_cap;
     uint32_t* counters;    // [0] = error pixels
-    unsigned long long* work;  // instrumented build only: 8 work counters (vr_count_work)
+    unsigned long long* work;  // instrumented build only: [0..7] march-kernel counters, [8..15] secondary-kernel counters
 
     // ---- wavefront buffers (RayMarchingGaussians), pixel-local index p = tile_local * 256 + lane ----
     uint32_t* px_cnt;   // scatter records of pixel p (march steps with sigma_s > 0)

@@ -325,7 +325,11 @@ class Device:
         s = L.vr_render_stats()
         check(lib().vr_get_stats(self._h, ctypes.byref(s)))
         return {"kernel_ms": s.kernel_ms, "pixels": s.pixels, "fallback_pixels": s.fallback_pixels,
-                "error_pixels": s.error_pixels}
+                "error_pixels": s.error_pixels, "stage_ms": dict(zip(self.STAGES, list(s.stage_ms))),
+                "scatter_records": s.scatter_records, "secondary_rays": s.secondary_rays}
+
+    # vr_render_stats.stage_ms (include/vr_hip.h)
+    STAGES = ("march_count", "scan", "march_write", "secondary", "accumulate")
 
     def synchronize(self):
         check(lib().vr_synchronize(self._h))
@@ -346,11 +350,15 @@ class Device:
         """Instrumented (untimed) render of the given tiles; returns counts + algorithmic flops."""
         if num_tiles is None:
             num_tiles = len(range(first_tile, num_tiles_of(width, height), tile_stride))
-        arr = (ctypes.c_uint64 * 8)()
+        arr = (ctypes.c_uint64 * 16)()
         check(lib().vr_count_work(self._h, ctypes.byref(camera.struct), ctypes.byref(params), width, height,
                                   first_tile, tile_stride, num_tiles, arr))
-        out = {k: int(arr[i]) for i, k in enumerate(self.WORK_NAMES)}
-        out["flops"] = float(sum(self.FLOP_WEIGHTS[k] * out[k] for k in self.FLOP_WEIGHTS))
+        out = {}
+        for s, stage in enumerate(("march", "secondary")):
+            d = {k: int(arr[8 * s + i]) for i, k in enumerate(self.WORK_NAMES)}
+            d["flops"] = float(sum(self.FLOP_WEIGHTS[k] * d[k] for k in self.FLOP_WEIGHTS))
+            out[stage] = d
+        out["flops"] = out["march"]["flops"] + out["secondary"]["flops"]
         return out
 
     def unshuffle_tiles_device(self, slabs_ptr, nslabs, tiles_per_slab, width, height, image_ptr, stream_ptr=0):

@@ -52,7 +52,8 @@ class vr_scene_info(ctypes.Structure):
 
 class vr_render_stats(ctypes.Structure):
     _fields_ = [("kernel_ms", ctypes.c_double), ("pixels", ctypes.c_int64), ("fallback_pixels", ctypes.c_int64),
-                ("error_pixels", ctypes.c_int64)]
+                ("error_pixels", ctypes.c_int64), ("stage_ms", ctypes.c_double * 5),
+                ("scatter_records", ctypes.c_int64), ("secondary_rays", ctypes.c_int64)]
 
 
 # name -> (restype, argtypes). Every symbol declared in include/vr_hip.h.

@@ -110,6 +110,12 @@ typedef struct vr_render_stats {
     int64_t pixels;           /* pixels rendered */
     int64_t fallback_pixels;  /* pixels re-run on the large-capacity path (active-set overflow) */
     int64_t error_pixels;     /* pixels that exceeded every capacity (output NaN) */
+    /* RayMarchingGaussians stages (HIP events on the render stream; 0 for the other integrators):
+     * [0] march (count pass), [1] scan + record allocation (includes one host sync),
+     * [2] march (write pass), [3] secondary-ray transmittance, [4] accumulate. */
+    double stage_ms[5];
+    int64_t scatter_records;  /* march steps with sigma_s > 0 (each spawns lights + env_samples rays) */
+    int64_t secondary_rays;   /* records * (lights + env_samples) */
 } vr_render_stats;
 
 typedef struct vr_scene vr_scene; /* host-side scene: primitives, lights, env colour */
@@ -190,13 +196,15 @@ vr_status vr_unshuffle_tiles_device(vr_ctx* ctx, const float* d_slabs, uint32_t 
                                     uint32_t tiles_per_slab, uint32_t width, uint32_t height,
                                     float* d_image, void* stream);
 /* Diagnostics (untimed): render the given tiles once with the instrumented kernel build and return
- * the algorithmic work it executed: counts[0] BVH node-pair tests, [1] ray-Gaussian quadratic +
- * intersect evaluations, [2] optical-depth evaluations, [3] density (mu_t) evaluations,
- * [4] secondary (light + environment) rays, [5] active march steps, [6] primary-ray BVH queries,
- * [7] pixels completed. Synchronous; RayMarchingGaussians only. Used for the roofline report. */
+ * the algorithmic work it executed, per stage: counts[0..7] the march kernels (both passes),
+ * counts[8..15] the secondary-ray kernels. Within a stage: [0] BVH node-pair tests,
+ * [1] ray-Gaussian quadratic + intersect evaluations, [2] optical-depth evaluations, [3] density
+ * (mu_t) evaluations, [4] secondary (light + environment) rays, [5] active march steps,
+ * [6] primary-ray BVH queries, [7] pixels completed. Synchronous; RayMarchingGaussians only. Used
+ * for the roofline report. */
 vr_status vr_count_work(vr_ctx* ctx, const vr_camera* cam, const vr_render_params* p, uint32_t width,
                         uint32_t height, uint32_t first_tile, uint32_t tile_stride, uint32_t num_tiles,
-                        uint64_t counts[8]);
+                        uint64_t counts[16]);
 /* Number of 16x16 tiles of a W x H frame. */
 uint32_t vr_num_tiles(uint32_t width, uint32_t height);
 vr_status vr_synchronize(vr_ctx* ctx);

@@ -16,6 +16,7 @@ _lib = None
 
 RAYMARCH_GAUSSIANS = 0
 RAYMARCH_SPHERES = 1
+RAYMARCH_GAUSSIANS_LISTS = 2  # same algorithm, sparse active sets + stop at T == 0 (bit-identical)
 PINHOLE = 0
 ORTHO = 1
 

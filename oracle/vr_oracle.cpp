@@ -665,6 +665,135 @@ static V3 rm_gaussians_pixel(const Scene& scene, const Camera& cam, int x, int y
     return L;
 }
 
+// ---------------------------------------------------------------------------------------------
+// Same per-pixel algorithm as rm_gaussians_pixel, for the CPU *baseline* of bench.py only.
+// Two changes, both bit-neutral (tests/test_oracle_golden.py checks bitwise equality with the
+// faithful function above):
+//   * the reference's O(N) std::vector<bool> active masks (test_integrators.h:181, 224, 262,
+//     281-283; gmm.h:108-113) are kept as an index-sorted list plus a byte mask, so every sum runs
+//     over exactly the same indices in exactly the same (ascending) order;
+//   * the march stops once T == 0: every later term is T*sigma_s*(...) = +0 and the final T*env is
+//     +0, so L is unchanged (the device path stops at the same point).
+// Without them one 1M-Gaussian pixel costs minutes of mask scans (DESIGN.md §CPU baseline).
+// ---------------------------------------------------------------------------------------------
+struct SparseSet {
+    std::vector<uint8_t>* mask;  // shared scratch of size N, all zero outside `list`
+    std::vector<size_t> list;    // ascending indices i with mask[i] == 1
+    void set(size_t i, bool v) {
+        uint8_t& m = (*mask)[i];
+        if ((m != 0) == v) return;
+        m = v ? 1 : 0;
+        auto it = std::lower_bound(list.begin(), list.end(), i);
+        if (v) list.insert(it, i);
+        else list.erase(it);
+    }
+    void clear() {
+        for (size_t i : list) (*mask)[i] = 0;
+        list.clear();
+    }
+};
+
+static V3 rm_gaussians_pixel_lists(const Scene& scene, const Camera& cam, int x, int y, int W, int H,
+                                   float step_size, int env_samples) {
+    const GMM& gmm = scene.gmm;
+    static thread_local std::vector<uint8_t> mask_a, mask_b;
+    if (mask_a.size() != gmm.gaussians.size()) mask_a.assign(gmm.gaussians.size(), 0);
+    if (mask_b.size() != gmm.gaussians.size()) mask_b.assign(gmm.gaussians.size(), 0);
+    float u = (x + 0.5f) / W, v = (y + 0.5f) / H;
+    Ray ray = cam.sample_ray(u, v);
+    std::vector<PrimitiveHitEvent> events;
+    gmm.intersect_events(ray, events);
+    if (events.empty()) return scene.env_color;
+    float t_end = events.back().t;
+    SparseSet active{&mask_a, {}};
+    size_t evt_i = 0;
+    float t = 0.0f, T = 1.0f;
+    V3 L{0, 0, 0};
+    int k = 0;
+    // secondary-ray segment loop on a copy of the primary active set (test_integrators.h:208-235, 255-271)
+    auto secondary = [&](const Ray& r, std::vector<PrimitiveHitEvent>& ev, bool to_light, float dist) {
+        for (size_t i : active.list) ev.insert(ev.begin(), {0.0f, true, i});
+        SparseSet mask{&mask_b, active.list};
+        for (size_t i : mask.list) mask_b[i] = 1;
+        float t_prev = 0, Tr = 1.0f;
+        size_t ei = 0;
+        if (to_light) {
+            while (t_prev < dist) {
+                float t_next = (ei < ev.size() ? ev[ei].t : dist);
+                Tr *= gmm.transmittance_over_segment(r, t_prev, t_next, mask.list);
+                if (ei < ev.size()) {
+                    mask.set(ev[ei].index, ev[ei].entering);
+                    ++ei;
+                }
+                t_prev = t_next;
+            }
+        } else {
+            while (ei < ev.size()) {
+                float t_next = ev[ei].t;
+                Tr *= gmm.transmittance_over_segment(r, t_prev, t_next, mask.list);
+                mask.set(ev[ei].index, ev[ei].entering);
+                t_prev = t_next;
+                ++ei;
+            }
+        }
+        mask.clear();
+        return Tr;
+    };
+    while (t < t_end) {
+        while (evt_i < events.size() && events[evt_i].t <= t) {
+            active.set(events[evt_i].index, events[evt_i].entering);
+            ++evt_i;
+        }
+        V3 pos = ray.origin + t * ray.direction;
+        float sum_mu_t = 0.0f, sum_mu_t_alb = 0.0f, sigma_s = 0.0f;  // gmm.h:98-126 over the list
+        for (size_t i : active.list) {
+            float mu_t_i = gmm.gaussians[i].mu_t(pos);
+            sum_mu_t += mu_t_i;
+            sum_mu_t_alb += mu_t_i * gmm.gaussians[i].albedo;
+        }
+        if (!(sum_mu_t <= 0.0f)) {
+            float a_mix = sum_mu_t_alb / sum_mu_t;
+            sigma_s = a_mix * sum_mu_t;
+        }
+        if (sigma_s > 0.0f) {
+            V3 Li{0, 0, 0};
+            for (const auto& light : scene.lights) {
+                V3 wi = normalized(light.position - pos);
+                float dist = norm(light.position - pos);
+                Ray shadow_ray(pos, wi);
+                std::vector<PrimitiveHitEvent> shadow_ev;
+                gmm.intersect_events(shadow_ray, shadow_ev);
+                float Tr = secondary(shadow_ray, shadow_ev, true, dist);
+                float d2 = dist * dist;
+                Li = Li + V3{(Tr * light.intensity.x) / d2, (Tr * light.intensity.y) / d2, (Tr * light.intensity.z) / d2};
+            }
+            V3 Le{0, 0, 0};
+            PCG32 rng(derive_path_seed(x, y, k), 1);
+            for (int si = 0; si < env_samples; ++si) {
+                float xi1 = rng.uniform();
+                float xi2 = rng.uniform();
+                Ray env_ray(pos, env_dir(xi1, xi2));
+                std::vector<PrimitiveHitEvent> env_ev;
+                gmm.intersect_events(env_ray, env_ev);
+                float Tr_env = secondary(env_ray, env_ev, false, 0.0f);
+                Le = Le + Tr_env * scene.env_color;
+            }
+            float fs = float(env_samples);
+            Le = V3{(Le.x / fs) * k4Pi, (Le.y / fs) * k4Pi, (Le.z / fs) * k4Pi};
+            float Ts = T * sigma_s;
+            V3 S = Li + Le;
+            L = L + V3{((Ts * S.x) * step_size) * kInv4Pi, ((Ts * S.y) * step_size) * kInv4Pi, ((Ts * S.z) * step_size) * kInv4Pi};
+        }
+        T *= gmm.transmittance_over_segment(ray, t, t + step_size, active.list);
+        t += step_size;
+        ++k;
+        if (T == 0.0f) break;
+    }
+    active.clear();
+    L = L + T * scene.env_color;
+    return L;
+}
+
 // test_integrators.h:23-135 — RayMarchingSpheres per pixel.
 static V3 rm_spheres_pixel(const Scene& scene, const Camera& cam, int i, int j, int W, int H,
                            float step_size, int env_samples) {
@@ -937,7 +1066,8 @@ void orc_env_dir(float xi1, float xi2, float* out) {
     out[0] = d.x; out[1] = d.y; out[2] = d.z;
 }
 
-// integrator: 0 RayMarchingGaussians, 1 RayMarchingSpheres.
+// integrator: 0 RayMarchingGaussians, 1 RayMarchingSpheres, 2 RayMarchingGaussians with sorted
+// active lists + stop at T == 0 (bit-identical to 0; bench.py's CPU baseline).
 // If pix != nullptr, render only the npix pixels pix[2k]=x, pix[2k+1]=y into out[3*npix];
 // otherwise the whole W*H frame into out[3*W*H] (row-major, image.h:13-17).
 int orc_render(void* sp, int cam_type, const float* pos, const float* vd, float fov, int integrator,
@@ -947,15 +1077,17 @@ int orc_render(void* sp, int cam_type, const float* pos, const float* vd, float 
         Scene* s = (Scene*)sp;
         Camera c = cam_type == 0 ? Camera::make_pinhole({pos[0], pos[1], pos[2]}, {vd[0], vd[1], vd[2]}, fov)
                                  : Camera::make_ortho({pos[0], pos[1], pos[2]}, {vd[0], vd[1], vd[2]});
-        if ((integrator == 0) != (s->volume_type == 0)) { g_err = "integrator/scene type mismatch"; return 1; }
+        if (integrator < 0 || integrator > 2) { g_err = "unknown integrator"; return 1; }
+        if ((integrator != 1) != (s->volume_type == 0)) { g_err = "integrator/scene type mismatch"; return 1; }
         int64_t total = pix ? npix : (int64_t)W * H;
         if (nthreads > 0) omp_set_num_threads(nthreads);
 #pragma omp parallel for schedule(dynamic, 1)
         for (int64_t q = 0; q < total; ++q) {
             int x = pix ? pix[2 * q] : (int)(q % W);
             int y = pix ? pix[2 * q + 1] : (int)(q / W);
-            V3 L = integrator == 0 ? rm_gaussians_pixel(*s, c, x, y, W, H, step_size, env_samples)
-                                   : rm_spheres_pixel(*s, c, x, y, W, H, step_size, env_samples);
+            V3 L = integrator == 0   ? rm_gaussians_pixel(*s, c, x, y, W, H, step_size, env_samples)
+                   : integrator == 2 ? rm_gaussians_pixel_lists(*s, c, x, y, W, H, step_size, env_samples)
+                                     : rm_spheres_pixel(*s, c, x, y, W, H, step_size, env_samples);
             out[3 * q] = L.x; out[3 * q + 1] = L.y; out[3 * q + 2] = L.z;
         }
         return 0;

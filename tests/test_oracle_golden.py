@@ -73,6 +73,20 @@ def test_miss_mask_known_answer(golden, scene):
     assert np.all(out == np.float32([0.53, 0.81, 0.92]))
 
 
+@pytest.mark.parametrize("scene,W,env", [("many_gaussians.txt", 64, None), ("50_random.txt", 48, None),
+                                         ("1000_random.txt", 32, None), ("2_gaussian.txt", 48, (0.0, 0.0, 0.0))])
+def test_sparse_list_baseline_bitwise_equals_faithful(scene, W, env):
+    """The CPU-baseline variant (sorted active lists instead of O(N) masks, stop at T == 0) is the
+    same function bit for bit: bench.py times it because the faithful O(N) scans take minutes per
+    pixel at 1M Gaussians."""
+    s = O.OracleScene.load_gmm(scene_path(scene))
+    if env is not None:
+        s.set_env(env)
+    a = O.render(s, O.PINHOLE, CAM_POS, main_view_dir(), FOV, W, W, O.RAYMARCH_GAUSSIANS, 0.01, 6)
+    b = O.render(s, O.PINHOLE, CAM_POS, main_view_dir(), FOV, W, W, O.RAYMARCH_GAUSSIANS_LISTS, 0.01, 6)
+    assert a.tobytes() == b.tobytes()
+
+
 def test_ortho_sphere_matches_reference_render():
     """RayMarchingSpheres on the ortho XML scene (== scenes/spheres/1_spheres.txt) vs
     tests/renders/env_test_orthographic.ppm (mean 0.44 with many env samples)."""
