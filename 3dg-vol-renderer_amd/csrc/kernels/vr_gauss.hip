@@ -453,15 +453,15 @@ __device__ __forceinline__ bool sec_init(const RenderArgs& A, uint32_t nrec, uin
     return true;
 }
 
-template <bool S>
+template <bool S, bool FAST>
 __device__ __forceinline__ void sec_leaf(const RenderArgs& A, SecRay& R, int32_t ref, Ctr& c) {
     const uint32_t first = leaf_first(ref), count = leaf_count(ref);
     for (uint32_t j = first; j < first + count; ++j) {
         if constexpr (S) c.v[kCtrPrims]++;
         GRec g = load_rec(A.gauss, j);
-        Quad q = quad(g, R.ray);
+        Quad q = FAST ? quad_fast(g, R.ray) : quad(g, R.ray);
         float a, b;
-        if (!intersect(q, a, b)) continue;
+        if (!(FAST ? intersect_fast(q, a, b) : intersect(q, a, b))) continue;
         int slot = act_find(A, R, (int)j);
         float lo = a;
         if (slot >= 0) {
@@ -470,7 +470,7 @@ __device__ __forceinline__ void sec_leaf(const RenderArgs& A, SecRay& R, int32_t
         }
         if (!R.light || b < R.lim) {
             if constexpr (S) c.v[kCtrOD]++;
-            R.tau += optical_depth(g, q, lo, b);
+            R.tau += FAST ? optical_depth_fast(g, q, lo, b) : optical_depth(g, q, lo, b);
             R.tlast = fmaxf(R.tlast, b);
         } else if (lo < R.lim) {
             R.needs_stop = true;
@@ -479,7 +479,7 @@ __device__ __forceinline__ void sec_leaf(const RenderArgs& A, SecRay& R, int32_t
 }
 
 // Ray complete: write its transmittance (or hand it to the exact slow path).
-template <bool S>
+template <bool S, bool FAST>
 __device__ __forceinline__ void sec_finish(const RenderArgs& A, uint64_t t, SecRay& R, Ctr& c) {
     if (R.tau >= kTauCut) {
         A.tr[t] = 0.0f;
@@ -502,9 +502,9 @@ __device__ __forceinline__ void sec_finish(const RenderArgs& A, uint64_t t, SecR
             int s = __ffsll((unsigned long long)missed) - 1;
             missed &= missed - 1;
             GRec g = load_rec(A.gauss, A.rec_act[R.act_off + s]);
-            Quad q = quad(g, R.ray);
+            Quad q = FAST ? quad_fast(g, R.ray) : quad(g, R.ray);
             if constexpr (S) c.v[kCtrOD]++;
-            R.tau += optical_depth(g, q, 0.0f, R.tlast);
+            R.tau += FAST ? optical_depth_fast(g, q, 0.0f, R.tlast) : optical_depth(g, q, 0.0f, R.tlast);
         }
     }
     A.tr[t] = expf(-R.tau);
@@ -512,7 +512,7 @@ __device__ __forceinline__ void sec_finish(const RenderArgs& A, uint64_t t, SecR
 
 // One BVH node pair of secondary ray R (plus the primitives of leaf children). Returns true when
 // the ray is complete (stack exhausted or optical depth past the cut-off).
-template <int BLOCK, bool S>
+template <int BLOCK, bool S, bool FAST>
 __device__ __forceinline__ bool sec_step(const RenderArgs& A, SecRay& R, int* stack, int& sp, int& node, Ctr& c) {
     if constexpr (S) c.v[kCtrNodes]++;
     const float4* np = reinterpret_cast<const float4*>(A.nodes + node);
@@ -537,8 +537,8 @@ __device__ __forceinline__ bool sec_step(const RenderArgs& A, SecRay& R, int* st
     const bool ll = hl && ref_is_leaf(nc.x), lr = hr && ref_is_leaf(nc.y);
     if (ll || lr) {
         const bool r_first = lr && (!ll || rmin < lmin);
-        sec_leaf<S>(A, R, r_first ? nc.y : nc.x, c);
-        if (ll && lr && R.tau < kTauCut) sec_leaf<S>(A, R, r_first ? nc.x : nc.y, c);
+        sec_leaf<S, FAST>(A, R, r_first ? nc.y : nc.x, c);
+        if (ll && lr && R.tau < kTauCut) sec_leaf<S, FAST>(A, R, r_first ? nc.x : nc.y, c);
         if (ll) hl = false;
         if (lr) hr = false;
     }
@@ -569,7 +569,7 @@ __device__ __forceinline__ bool sec_step(const RenderArgs& A, SecRay& R, int* st
 
 // One ray per lane, grid-stride over ray ids [t_begin, t_end) (light rays: already coherent —
 // neighbouring lanes trace from neighbouring pixels towards the same light).
-template <int BLOCK, bool S>
+template <int BLOCK, bool S, bool FAST>
 __global__ __launch_bounds__(BLOCK) void secondary_simple_kernel(RenderArgs A, uint32_t nrec, uint64_t t_begin,
                                                                  uint64_t t_end) {
     __shared__ int s_stack[kStackSize * BLOCK];
@@ -581,93 +581,20 @@ __global__ __launch_bounds__(BLOCK) void secondary_simple_kernel(RenderArgs A, u
         if constexpr (S) c.v[kCtrSecRays]++;
         if (!sec_init(A, nrec, t, R)) continue;
         int sp = 0, node = 0;
-        while (!sec_step<BLOCK, S>(A, R, stack, sp, node, c)) {
+        while (!sec_step<BLOCK, S, FAST>(A, R, stack, sp, node, c)) {
         }
-        sec_finish<S>(A, t, R, c);
+        sec_finish<S, FAST>(A, t, R, c);
     }
     if constexpr (S)
         for (int i = 0; i < kNumCtr; ++i)
             if (c.v[i]) atomicAdd(A.work + kNumCtr + i, (unsigned long long)c.v[i]);
 }
 
-// Environment rays: their directions are independent per (pixel, step, sample), so lanes of a wave
-// taking consecutive ray ids fetch unrelated BVH nodes (measured: ~7x the cost per node step of
-// the coherent light rays). Each workgroup takes CHUNK consecutive env-ray ids (neighbouring
-// pixels, same sample index), counting-sorts them in LDS by octahedral direction cell, and traces
-// them in that order, so a wave's rays share origin neighbourhood AND direction cone. Each ray
-// still writes its own slot, so the result does not depend on the order.
-template <int BLOCK, int PER, bool S>
-__global__ __launch_bounds__(BLOCK) void secondary_binned_kernel(RenderArgs A, uint32_t nrec, uint64_t t_begin,
-                                                                 uint64_t t_end) {
-    constexpr int CHUNK = BLOCK * PER;
-    constexpr int NBIN = 64;
-    __shared__ int s_stack[kStackSize * BLOCK];
-    __shared__ uint32_t s_sorted[CHUNK];
-    __shared__ uint32_t s_hist[NBIN];
-    int* stack = s_stack + threadIdx.x;
-    Ctr c{};
-    const uint64_t nchunks = (t_end - t_begin + CHUNK - 1) / CHUNK;
-    for (uint64_t ch = blockIdx.x; ch < nchunks; ch += gridDim.x) {
-        const uint64_t base = t_begin + ch * CHUNK;
-        if (threadIdx.x < NBIN) s_hist[threadIdx.x] = 0;
-        __syncthreads();
-        uint32_t cell[PER];
-        #pragma unroll
-        for (int i = 0; i < PER; ++i) {
-            const uint64_t t = base + (uint64_t)i * BLOCK + threadIdx.x;
-            cell[i] = NBIN;  // past the end
-            if (t < t_end) {
-                const uint32_t s = (uint32_t)(t / nrec);
-                const uint32_t r = (uint32_t)(t - (uint64_t)s * nrec);
-                float wx, wy, wz;
-                env_sample_dir(A, A.rec_meta[r], s - (uint32_t)A.num_lights, wx, wy, wz);
-                cell[i] = dir_cell(wx, wy, wz);
-                atomicAdd(&s_hist[cell[i]], 1u);
-            }
-        }
-        __syncthreads();
-        if (threadIdx.x < 64) {  // exclusive scan of the 64 cell counts (one wave)
-            uint32_t v = s_hist[threadIdx.x], x = v;
-            for (int o = 1; o < 64; o <<= 1) {
-                uint32_t y = __shfl_up(x, o, 64);
-                if ((int)threadIdx.x >= o) x += y;
-            }
-            s_hist[threadIdx.x] = x - v;
-        }
-        __syncthreads();
-        uint32_t valid = 0;
-        #pragma unroll
-        for (int i = 0; i < PER; ++i)
-            if (cell[i] < NBIN) {
-                const uint32_t slot = atomicAdd(&s_hist[cell[i]], 1u);
-                s_sorted[slot] = (uint32_t)(i * BLOCK + threadIdx.x);
-                ++valid;
-            }
-        __syncthreads();
-        const uint32_t n = (uint32_t)min((uint64_t)CHUNK, t_end - base);
-        for (uint32_t q = threadIdx.x; q < n; q += BLOCK) {
-            const uint64_t t = base + s_sorted[q];
-            SecRay R;
-            if constexpr (S) c.v[kCtrSecRays]++;
-            if (!sec_init(A, nrec, t, R)) continue;
-            int sp = 0, node = 0;
-            while (!sec_step<BLOCK, S>(A, R, stack, sp, node, c)) {
-            }
-            sec_finish<S>(A, t, R, c);
-        }
-        __syncthreads();
-    }
-    if constexpr (S)
-        for (int i = 0; i < kNumCtr; ++i)
-            if (c.v[i]) atomicAdd(A.work + kNumCtr + i, (unsigned long long)c.v[i]);
-}
-
-template <int BLOCK, bool S>
+template <int BLOCK, bool S, bool FAST>
 __global__ __launch_bounds__(BLOCK) void secondary_persistent_kernel(RenderArgs A, uint32_t nrec, uint64_t total,
                                                                      uint64_t chunk) {
     __shared__ int s_stack[kStackSize * BLOCK];
     int* stack = s_stack + threadIdx.x;
-    const uint32_t lane = threadIdx.x & 63u;
     const uint64_t wave = ((uint64_t)blockIdx.x * BLOCK + threadIdx.x) >> 6;
     const uint64_t begin = wave * chunk;
     const uint64_t end = begin + chunk < total ? begin + chunk : total;
@@ -696,8 +623,8 @@ __global__ __launch_bounds__(BLOCK) void secondary_persistent_kernel(RenderArgs 
         }
         if (!__any(live)) break;
         if (!live) continue;
-        if (sec_step<BLOCK, S>(A, R, stack, sp, node, c)) {
-            sec_finish<S>(A, t, R, c);
+        if (sec_step<BLOCK, S, FAST>(A, R, stack, sp, node, c)) {
+            sec_finish<S, FAST>(A, t, R, c);
             live = false;
         }
     }
@@ -822,52 +749,29 @@ hipError_t gauss_scan(const RenderArgs& A, uint32_t npix, void* temp, size_t& te
     return hipGetLastError();
 }
 
-template <bool S>
-static hipError_t secondary_launch(const RenderArgs& A, uint32_t nrec, uint64_t total, hipStream_t stream) {
-    // Kernel choice (measured on C4, 4096^2 / 1M Gaussians: simple 2.13 s, env-binned 2.30 s,
-    // persistent 3.57 s): one thread per secondary ray in record order is fastest, because
-    // neighbouring records are neighbouring pixels and their rays already share BVH paths.
-    // VR_SECONDARY=b / p select the direction-binned or persistent variants for A/B runs.
-    static int variant = -1;  // 0 simple, 1 light simple + env binned, 2 persistent
-    if (variant < 0) {
-        const char* v = getenv("VR_SECONDARY");
-        variant = (v && v[0] == 'b') ? 1 : (v && v[0] == 'p') ? 2 : 0;
-    }
-    static int grid = 0;  // persistent grid: every CU filled to its occupancy limit
-    if (variant == 2 && grid == 0) {
+template <bool S, bool FAST>
+static hipError_t secondary_launch(const RenderArgs& A, uint32_t nrec, uint64_t total, hipStream_t stream, int variant) {
+    // Kernel choice (C4, 4096^2 / 1M Gaussians, round 1: simple 2.13 s, persistent 3.57 s): one
+    // thread per secondary ray in record order, because neighbouring records are neighbouring
+    // pixels and their rays already share BVH paths. VR_SECONDARY=p selects the persistent
+    // variant for A/B runs.
+    if (variant == 0) {
+        uint64_t blocks = (total + kBlockSecondary - 1) / kBlockSecondary;
+        if (blocks > 65536ull * 16ull) blocks = 65536ull * 16ull;
+        hipLaunchKernelGGL((dev::secondary_simple_kernel<kBlockSecondary, S, FAST>), dim3((unsigned)blocks),
+                           dim3(kBlockSecondary), 0, stream, A, nrec, (uint64_t)0, total);
+    } else {
         int dev = 0, cus = 0, per_cu = 0;
         if (hipGetDevice(&dev) != hipSuccess) return hipErrorUnknown;
         if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return hipErrorUnknown;
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, dev::secondary_persistent_kernel<kBlockSecondary, S>,
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, dev::secondary_persistent_kernel<kBlockSecondary, S, FAST>,
                                                          kBlockSecondary, 0) != hipSuccess || per_cu < 1)
             per_cu = 1;
-        grid = cus * per_cu;
-        if (getenv("VR_DEBUG")) fprintf(stderr, "[vr] persistent secondary grid: %d CUs x %d blocks\n", cus, per_cu);
-    }
-    const uint64_t nlight = (uint64_t)nrec * (uint64_t)A.num_lights;
-    auto simple = [&](uint64_t b0, uint64_t b1) {
-        if (b1 <= b0) return;
-        uint64_t blocks = (b1 - b0 + kBlockSecondary - 1) / kBlockSecondary;
-        if (blocks > 65536ull * 16ull) blocks = 65536ull * 16ull;
-        hipLaunchKernelGGL((dev::secondary_simple_kernel<kBlockSecondary, S>), dim3((unsigned)blocks), dim3(kBlockSecondary), 0,
-                           stream, A, nrec, b0, b1);
-    };
-    if (variant == 0) {
-        simple(0, total);
-    } else if (variant == 2) {
-        const uint64_t waves = (uint64_t)grid * (kBlockSecondary / 64);
+        const uint64_t grid = (uint64_t)cus * (uint64_t)per_cu;
+        const uint64_t waves = grid * (kBlockSecondary / 64);
         const uint64_t chunk = (total + waves - 1) / waves;
-        hipLaunchKernelGGL((dev::secondary_persistent_kernel<kBlockSecondary, S>), dim3(grid), dim3(kBlockSecondary), 0,
-                           stream, A, nrec, total, chunk);
-    } else {
-        simple(0, nlight);
-        if (total > nlight) {
-            constexpr int kPer = 8;
-            uint64_t chunks = (total - nlight + kBlockSecondary * kPer - 1) / (kBlockSecondary * kPer);
-            if (chunks > 65536ull * 8ull) chunks = 65536ull * 8ull;
-            hipLaunchKernelGGL((dev::secondary_binned_kernel<kBlockSecondary, kPer, S>), dim3((unsigned)chunks),
-                               dim3(kBlockSecondary), 0, stream, A, nrec, nlight, total);
-        }
+        hipLaunchKernelGGL((dev::secondary_persistent_kernel<kBlockSecondary, S, FAST>), dim3((unsigned)grid),
+                           dim3(kBlockSecondary), 0, stream, A, nrec, total, chunk);
     }
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
@@ -878,7 +782,20 @@ static hipError_t secondary_launch(const RenderArgs& A, uint32_t nrec, uint64_t 
 hipError_t gauss_secondary(const RenderArgs& A, uint32_t nrec, hipStream_t stream, bool stats) {
     const uint64_t total = (uint64_t)nrec * (uint64_t)(A.num_lights + A.env_samples);
     if (total == 0) return hipSuccess;
-    return stats ? secondary_launch<true>(A, nrec, total, stream) : secondary_launch<false>(A, nrec, total, stream);
+    // A/B switches (read once): VR_SECONDARY=p persistent kernel; VR_SEC_EXACT=1 correctly rounded
+    // secondary-ray arithmetic (the fast form is the default).
+    static const int variant = [] {
+        const char* v = getenv("VR_SECONDARY");
+        return (v && v[0] == 'p') ? 1 : 0;
+    }();
+    static const bool exact = [] {
+        const char* v = getenv("VR_SEC_EXACT");
+        return v && v[0] == '1';
+    }();
+    if (stats) return exact ? secondary_launch<true, false>(A, nrec, total, stream, variant)
+                            : secondary_launch<true, true>(A, nrec, total, stream, variant);
+    return exact ? secondary_launch<false, false>(A, nrec, total, stream, variant)
+                 : secondary_launch<false, true>(A, nrec, total, stream, variant);
 }
 
 hipError_t gauss_accumulate(const RenderArgs& A, uint32_t nrec, hipStream_t stream) {

@@ -132,6 +132,55 @@ __device__ __forceinline__ float optical_depth(const GRec& g, const Quad& q, flo
     return pref * e * (F1 - F0);
 }
 
+// ---- secondary-ray variants ------------------------------------------------------------------
+// Light / environment rays only feed transmittances (continuous) and decisions at the 3-sigma
+// boundary whose optical-depth weight is ~0, so they may round differently from the reference:
+// FMA-contracted products and hardware reciprocal / square root (1 ulp) instead of correctly
+// rounded division and sqrt — about half the VALU instructions of the exact forms. The primary
+// march keeps the exact forms (its activation decisions must match the oracle bit for bit).
+__device__ __forceinline__ Quad quad_fast(const GRec& g, const Ray& r) {
+    const float px = r.ox - g.mx, py = r.oy - g.my, pz = r.oz - g.mz;
+    const float mdx = fmaf(g.m00, r.dx, fmaf(g.m01, r.dy, g.m02 * r.dz));
+    const float mdy = fmaf(g.m01, r.dx, fmaf(g.m11, r.dy, g.m12 * r.dz));
+    const float mdz = fmaf(g.m02, r.dx, fmaf(g.m12, r.dy, g.m22 * r.dz));
+    const float mpx = fmaf(g.m00, px, fmaf(g.m01, py, g.m02 * pz));
+    const float mpy = fmaf(g.m01, px, fmaf(g.m11, py, g.m12 * pz));
+    const float mpz = fmaf(g.m02, px, fmaf(g.m12, py, g.m22 * pz));
+    Quad q;
+    q.A = fmaf(r.dx, mdx, fmaf(r.dy, mdy, r.dz * mdz));
+    q.B = 2.0f * fmaf(px, mdx, fmaf(py, mdy, pz * mdz));
+    q.Cq = fmaf(px, mpx, fmaf(py, mpy, pz * mpz));
+    return q;
+}
+
+__device__ __forceinline__ bool intersect_fast(const Quad& q, float& t_enter, float& t_exit) {
+    const float disc = fmaf(q.B, q.B, -4.0f * q.A * (q.Cq - 9.0f));
+    if (disc < 0.0f) return false;
+    const float s = __builtin_amdgcn_sqrtf(disc);
+    const float inv2A = __builtin_amdgcn_rcpf(2.0f * q.A);  // A = d.Md > 0 (M positive definite)
+    float t0 = (-q.B - s) * inv2A, t1 = (-q.B + s) * inv2A;
+    if (t0 > t1) {
+        const float tmp = t0;
+        t0 = t1;
+        t1 = tmp;
+    }
+    if (t1 < 0.0f) return false;
+    t_enter = t0 >= 0.0f ? t0 : 0.0f;
+    t_exit = t1;
+    return true;
+}
+
+__device__ __forceinline__ float optical_depth_fast(const GRec& g, const Quad& q, float t0, float t1) {
+    const float twoA = 2.0f * q.A;
+    const float r2A = __builtin_amdgcn_rcpf(twoA);
+    const float pref = (g.density * g.norm) * __builtin_amdgcn_sqrtf(3.14159265358979323846f * r2A);
+    const float inv_den = 0.5f * __builtin_amdgcn_rsqf(twoA);  // 1 / (2 sqrt(2A))
+    const float F1 = erff(fmaf(twoA, t1, q.B) * inv_den);
+    const float F0 = erff(fmaf(twoA, t0, q.B) * inv_den);
+    const float e = __expf(-0.5f * fmaf(-q.B * q.B, 0.5f * r2A, q.Cq));  // C - B^2 / (4A)
+    return pref * e * (F1 - F0);
+}
+
 // Gaussian::mu_t = density * evaluate(x) (gaussian.h:111-117), exponent -0.5 d^T M d with
 // Eigen's lazy-product order.
 __device__ __forceinline__ float mu_t(const GRec& g, float x, float y, float z) {
@@ -285,4 +334,5 @@ __device__ __forceinline__ int kfirst(const float* __restrict__ ts, int n, float
 // NOTE on rounding: HIP's __fsqrt_rn maps to __ocml_native_sqrt_f32 (approximate) unless
 // OCML_BASIC_ROUNDED_OPERATIONS is defined; plain sqrtf / '/' are correctly rounded under hipcc's
 // default -fhip-fp32-correctly-rounded-divide-sqrt, which is what the bit-exactness relies on
-// (verified against the CPU oracle by tests/test_gpu_parity.py::test_device_geometry_bit_exact).
+// (host side: tests/test_host_abi.py::test_camera_and_primary_rays_bit_identical; device side: the
+// L-inf parity tests of tests/test_gpu_parity.py, which a flipped activation decision would break).

@@ -14,8 +14,10 @@
 #pragma once
 
 #include <algorithm>
+#include <atomic>
 #include <cstdint>
 #include <cstring>
+#include <map>
 #include <memory>
 #include <mutex>
 #include <optional>
@@ -44,6 +46,11 @@ inline vr_ctx* device(int dev = 0) {
         ctxs[dev].reset(c);
     }
     return ctxs[dev].get();
+}
+
+inline uint64_t next_serial() {
+    static std::atomic<uint64_t> serial{0};
+    return ++serial;
 }
 
 inline uint64_t fnv1a(const void* p, size_t n, uint64_t h = 1469598103934665603ull) {
@@ -238,10 +245,11 @@ struct Scene {
             const float env[3] = {env_color[0], env_color[1], env_color[2]};
             vr_cpp::check(vr_scene_set_env_color(h, env));
             native_fp_ = fp;
-            ++native_version_;
+            native_version_ = vr_cpp::next_serial();
         }
         return native_.get();
     }
+    // process-unique id of the current native copy (a freed handle's address may be reused)
     uint64_t native_version() const { return native_version_; }
 
 private:
@@ -299,6 +307,7 @@ private:
         }
         s.native_ = owner;  // the loaded native scene is already up to date
         s.native_fp_ = s.fingerprint();
+        s.native_version_ = vr_cpp::next_serial();
         return s;
     }
 };
@@ -377,13 +386,16 @@ public:
     void render(const Scene& scene, Image& image) override {
         vr_ctx* ctx = vr_cpp::device(device_);
         // re-upload when the scene (or the scene object) changed since the last render on this device
-        static thread_local const void* last_obj = nullptr;
-        static thread_local uint64_t last_version = ~0ull;
+        static std::mutex mu;
+        static std::map<vr_ctx*, std::pair<const void*, uint64_t>> uploaded;  // per device context
         vr_scene* ns = scene.native();
-        if (last_obj != (const void*)ns || last_version != scene.native_version()) {
-            vr_cpp::check(vr_upload_scene(ctx, ns));
-            last_obj = ns;
-            last_version = scene.native_version();
+        {
+            std::lock_guard<std::mutex> lock(mu);
+            auto it = uploaded.find(ctx);
+            if (it == uploaded.end() || it->second.first != (const void*)ns || it->second.second != scene.native_version()) {
+                vr_cpp::check(vr_upload_scene(ctx, ns));
+                uploaded[ctx] = {ns, scene.native_version()};
+            }
         }
         vr_cpp::check(vr_render(ctx, &camera->state(), &params_, image.get_width(), image.get_height(), image.data()));
     }

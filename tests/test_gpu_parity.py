@@ -286,3 +286,60 @@ def test_tiles_api_packed_slabs_unshuffle_bitwise():
     dev.unshuffle_tiles_device(slabs.data_ptr(), R, per, W, H, img.data_ptr(), stream)
     torch.cuda.synchronize()
     assert np.array_equal(img.cpu().numpy(), full.pixels)
+
+
+# ---- BASELINE.json configs 3 and 4 at full size -------------------------------------------------
+# The faithful oracle needs minutes per pixel at these sizes (O(N) mask scans), so the check uses
+# its bit-identical sparse-list variant (test_sparse_list_baseline_bitwise_equals_faithful) on a
+# seeded pixel sample, plus size-independent properties of the whole frame.
+LIGHTS_1000 = [((0.0, 5.0, 0.1), (50.0, 0.0, 0.0)), ((-3.0, 3.0, 0.3), (0.0, 30.0, 0.0)),
+               ((3.0, 3.0, -0.2), (0.0, 0.0, 30.0))]  # scenes/gaussians/1000_random.txt:1-3
+
+
+def _synthetic_scene(n, seed=2025):
+    scene = vr.Scene(vr.Scene.GAUSSIANS)
+    scene.add_random_gaussians(n, seed=seed, variant=0)
+    for p, i in LIGHTS_1000:
+        scene.add_light(vr.Light(p, i))
+    g = scene.gaussians()
+    osc = O.OracleScene.from_gaussians(g[:, 0:3], g[:, 3:9], g[:, 9], g[:, 10],
+                                       np.array([l[0] for l in LIGHTS_1000], np.float32),
+                                       np.array([l[1] for l in LIGHTS_1000], np.float32))
+    return scene, osc
+
+
+@pytest.mark.parametrize("W,H,n,npix", [(1920, 1080, 100_000, 384), (4096, 4096, 1_000_000, 160)])
+def test_full_size_configs_match_oracle_on_sampled_pixels(W, H, n, npix):
+    scene, osc = _synthetic_scene(n)
+    cam = vr.Pinhole_Camera(CAM_POS, main_view_dir(), FOV)
+    img = vr.Image(W, H)
+    integ = vr.RayMarchingGaussians(cam)
+    integ.render(scene, img)
+    st = integ.last_stats
+    assert st["error_pixels"] == 0
+    px = img.pixels
+    assert np.isfinite(px).all() and (px >= 0).all()
+    pix = _pixels(W, H, npix, seed=11)
+    ref = O.render(osc, O.PINHOLE, CAM_POS, main_view_dir(), FOV, W, H, O.RAYMARCH_GAUSSIANS_LISTS, 0.01, 20,
+                   pixels=pix)
+    err, nm = _linf(px[pix[:, 1], pix[:, 0]], ref)
+    assert nm == 0 and err < TOL, f"{W}x{H}/{n}: L-inf {err:.3e}"
+    # a pixel whose centre ray misses everything is env colour exactly (test_integrators.h:172-176)
+    env = np.array([0.53, 0.81, 0.92], np.float32)
+    is_env = np.all(ref == env, axis=-1)
+    assert np.all(px[pix[is_env, 1], pix[is_env, 0]] == env)
+
+
+@pytest.mark.parametrize("t_eps", [1e-6, 1e-5])
+def test_transmittance_early_out_error_bound(t_eps):
+    """Stopping a ray once T <= t_eps (the wave-wide early-out) changes a pixel by at most
+    ~t_eps x (brightest in-scattered radiance); stays far inside the 1e-4 parity bar."""
+    path = scene_path("1000_random.txt")
+    W = H = 256
+    scene = vr.Scene.load_GMM(path)
+    img = vr.Image(W, H)
+    vr.RayMarchingGaussians(vr.Pinhole_Camera(CAM_POS, main_view_dir(), FOV), t_eps=t_eps).render(scene, img)
+    pix = _pixels(W, H, 96, seed=5)
+    ref = _oracle_gmm(path, W, H, pixels=pix)
+    err, nm = _linf(img.pixels[pix[:, 1], pix[:, 0]], ref)
+    assert nm == 0 and err < TOL, f"t_eps {t_eps}: L-inf {err:.3e}"
