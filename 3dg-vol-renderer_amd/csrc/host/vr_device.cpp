@@ -64,7 +64,7 @@ struct vr_ctx {
         size_t bytes = 0;
     };
     Buf px_cnt, px_acnt, px_off, px_aoff, px_T, scan_tmp, rec_pos, rec_meta, rec_act, tr, totals, rec_bloom, slowq;
-    Buf pcg_jump;
+    Buf pcg_jump, ray_next;
     int pcg_jump_n = -1;
     uint32_t* h_totals = nullptr;  // pinned [0] records, [1] act entries
     int64_t last_records = 0, last_secondary = 0;
@@ -261,6 +261,8 @@ vr_status gauss_pipeline(vr_ctx* c, RenderArgs& A, hipStream_t s, bool stats) {
     A.slowq = (uint32_t*)c->slowq.p;
     A.slowq_cap = (uint32_t)nslow;
     HIP_TRY(hipMemsetAsync(A.slowq, 0, sizeof(uint32_t), s), "hipMemsetAsync(slow queue)");
+    if ((st = grow(c->ray_next, 8, "hipMalloc(ray counter)")) != VR_OK) return st;
+    A.ray_next = (unsigned long long*)c->ray_next.p;
     A.rec_pos = (float4*)c->rec_pos.p;
     A.rec_meta = (uint4*)c->rec_meta.p;
     A.rec_act = (int32_t*)c->rec_act.p;
@@ -348,7 +350,7 @@ void vr_destroy(vr_ctx* c) {
     if (c->h_counters) (void)hipHostFree(c->h_counters);
     if (c->h_totals) (void)hipHostFree(c->h_totals);
     for (vr_ctx::Buf* b : {&c->px_cnt, &c->px_acnt, &c->px_off, &c->px_aoff, &c->px_T, &c->scan_tmp, &c->rec_pos,
-                           &c->rec_meta, &c->rec_act, &c->tr, &c->totals, &c->rec_bloom, &c->slowq, &c->pcg_jump})
+                           &c->rec_meta, &c->rec_act, &c->tr, &c->totals, &c->rec_bloom, &c->slowq, &c->pcg_jump, &c->ray_next})
         if (b->p) (void)hipFree(b->p);
     if (c->d_frame) (void)hipFree(c->d_frame);
     if (c->ev_start) (void)hipEventDestroy(c->ev_start);

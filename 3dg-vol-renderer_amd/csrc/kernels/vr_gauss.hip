@@ -567,6 +567,172 @@ __device__ __forceinline__ bool sec_step(const RenderArgs& A, SecRay& R, int* st
     return done;
 }
 
+// ---------------------------------------------------------------------------------------------
+// Stage 2 (default): persistent while-while tracing with postponed leaves.
+//
+// One ray per lane, but a wave never runs the node code and the primitive code in the same
+// iteration: every iteration is either a NODE iteration (lanes with room in their leaf queue take
+// one child-pair step; leaf children are queued, not tested) or a PRIM iteration (lanes with a
+// queued leaf test ONE primitive), whichever more lanes can use. A lane whose ray completes is
+// refilled from the wave's pool of ray ids (64 consecutive ids per atomic fetch: neighbouring
+// records, same light / env-sample index, so a wave's rays stay spatially coherent). This removes
+// the two divergence costs of one-ray-per-lane traversal: a wave no longer waits for its longest
+// ray, and a leaf visit no longer stalls the lanes that are still walking inner nodes.
+// ---------------------------------------------------------------------------------------------
+struct LeafQueue {  // FIFO of up to 4 leaf refs (registers) + the leaf being tested
+    int32_t q0, q1, q2, q3;
+    int n;
+    uint32_t j, end;  // current primitive range [j, end)
+    __device__ __forceinline__ void push(int32_t r) {
+        if (n == 0) q0 = r;
+        else if (n == 1) q1 = r;
+        else if (n == 2) q2 = r;
+        else q3 = r;
+        ++n;
+    }
+    __device__ __forceinline__ bool has_prim() const { return j < end || n > 0; }
+    __device__ __forceinline__ uint32_t next() {  // requires has_prim()
+        if (j == end) {
+            j = leaf_first(q0);
+            end = j + leaf_count(q0);
+            q0 = q1;
+            q1 = q2;
+            q2 = q3;
+            --n;
+        }
+        return j++;
+    }
+};
+
+// One child-pair step of the postponed-leaf traversal: leaf children go to the queue (nearer
+// first); node < 0 afterwards means the traversal is finished.
+template <int BLOCK, bool S>
+__device__ __forceinline__ void sec_node(const RenderArgs& A, const SecRay& R, int* stack, int& sp, int& node,
+                                         LeafQueue& Q, Ctr& c) {
+    if constexpr (S) c.v[kCtrNodes]++;
+    const float4* np = reinterpret_cast<const float4*>(A.nodes + node);
+    const float4 n0 = np[0], n1 = np[1], n2 = np[2];
+    const int4 nc = reinterpret_cast<const int4*>(A.nodes + node)[3];
+    const float tx1 = fmaf(n0.x, R.ix, -R.oxi), tx2 = fmaf(n0.w, R.ix, -R.oxi);
+    const float ty1 = fmaf(n0.y, R.iy, -R.oyi), ty2 = fmaf(n1.x, R.iy, -R.oyi);
+    const float tz1 = fmaf(n0.z, R.iz, -R.ozi), tz2 = fmaf(n1.y, R.iz, -R.ozi);
+    const float lmin = fmaxf(fmaxf(fminf(tx1, tx2), fminf(ty1, ty2)), fminf(tz1, tz2));
+    const float lmax = fminf(fminf(fmaxf(tx1, tx2), fmaxf(ty1, ty2)), fmaxf(tz1, tz2));
+    const float ux1 = fmaf(n1.z, R.ix, -R.oxi), ux2 = fmaf(n2.y, R.ix, -R.oxi);
+    const float uy1 = fmaf(n1.w, R.iy, -R.oyi), uy2 = fmaf(n2.z, R.iy, -R.oyi);
+    const float uz1 = fmaf(n2.x, R.iz, -R.ozi), uz2 = fmaf(n2.w, R.iz, -R.ozi);
+    const float rmin = fmaxf(fmaxf(fminf(ux1, ux2), fminf(uy1, uy2)), fminf(uz1, uz2));
+    const float rmax = fminf(fminf(fmaxf(ux1, ux2), fmaxf(uy1, uy2)), fmaxf(uz1, uz2));
+    const float lim = R.lim + kTPad * (1.0f + R.lim);
+    bool hl = nc.x != 0 && lmax >= fmaxf(lmin, 0.0f) && lmin <= lim;
+    bool hr = nc.y != 0 && rmax >= fmaxf(rmin, 0.0f) && rmin <= lim;
+    const bool r_near = rmin < lmin;
+    const bool ll = hl && ref_is_leaf(nc.x), lr = hr && ref_is_leaf(nc.y);
+    if (ll && lr) {
+        Q.push(r_near ? nc.y : nc.x);
+        Q.push(r_near ? nc.x : nc.y);
+    } else if (ll) {
+        Q.push(nc.x);
+    } else if (lr) {
+        Q.push(nc.y);
+    }
+    hl = hl && !ll;
+    hr = hr && !lr;
+    if (hl && hr) {
+        stack[sp * BLOCK] = r_near ? nc.x : nc.y;
+        ++sp;
+        node = r_near ? nc.y : nc.x;
+    } else if (hl) {
+        node = nc.x;
+    } else if (hr) {
+        node = nc.y;
+    } else if (sp > 0) {
+        --sp;
+        node = stack[sp * BLOCK];
+    } else {
+        node = -1;
+    }
+}
+
+template <int BLOCK, bool S>
+__global__ __launch_bounds__(BLOCK) void secondary_ww_kernel(RenderArgs A, uint32_t nrec, uint64_t total) {
+    __shared__ int s_stack[kStackSize * BLOCK];
+    int* stack = s_stack + threadIdx.x;
+    const uint32_t lane = threadIdx.x & 63u;
+    Ctr c{};
+    SecRay R;
+    LeafQueue Q{0, 0, 0, 0, 0, 0u, 0u};
+    uint64_t t = 0;
+    int sp = 0, node = -1;
+    bool live = false;
+    uint64_t pool = 0, pool_end = 0;  // wave-uniform: ray ids fetched but not yet handed out
+    bool counter_done = false;        // wave-uniform: the global ray counter has passed `total`
+    for (;;) {
+        const uint64_t idle = __ballot(!live);
+        if (__popcll(idle) >= 32) {  // refill once half the wave is idle (amortises sec_init)
+            if (pool == pool_end && !counter_done) {
+                uint64_t base = 0;
+                if (lane == 0) base = atomicAdd(A.ray_next, 64ull);
+                const uint32_t lo = __shfl((uint32_t)base, 0, 64), hi = __shfl((uint32_t)(base >> 32), 0, 64);
+                base = ((uint64_t)hi << 32) | lo;
+                pool = base < total ? base : total;
+                pool_end = base + 64 < total ? base + 64 : total;
+                counter_done = base + 64 >= total;
+            }
+            const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(idle >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)idle, 0u));
+            if (!live && pool + rank < pool_end) {
+                t = pool + rank;
+                if constexpr (S) c.v[kCtrSecRays]++;
+                live = sec_init(A, nrec, t, R);  // false: complete already (Tr written)
+                sp = 0;
+                node = 0;
+                Q.n = 0;
+                Q.j = Q.end = 0;
+            }
+            const uint64_t handed = (uint64_t)__popcll(idle);
+            pool = pool + handed < pool_end ? pool + handed : pool_end;
+        }
+        if (!__any(live)) {
+            if (counter_done && pool == pool_end) break;
+            continue;
+        }
+        const bool has_prim = live && Q.has_prim();
+        const bool can_node = live && node >= 0 && Q.n <= 2;
+        const int np = __popcll(__ballot(has_prim)), nn = __popcll(__ballot(can_node));
+        if (np >= nn) {  // PRIM iteration
+            if (has_prim) {
+                const uint32_t j = Q.next();
+                if constexpr (S) c.v[kCtrPrims]++;
+                const GRec g = load_rec(A.gauss, (int)j);
+                const Quad q = quad_fast(g, R.ray);
+                float a, b;
+                if (intersect_fast(q, a, b)) {
+                    const int slot = act_find(A, R, (int)j);
+                    float lo = a;
+                    if (slot >= 0) {
+                        lo = 0.0f;
+                        R.hitmask |= 1ull << slot;
+                    }
+                    if (!R.light || b < R.lim) {
+                        if constexpr (S) c.v[kCtrOD]++;
+                        R.tau += optical_depth_fast(g, q, lo, b);
+                        R.tlast = fmaxf(R.tlast, b);
+                    } else if (lo < R.lim) {
+                        R.needs_stop = true;
+                    }
+                }
+            }
+        } else {  // NODE iteration
+            if (can_node) sec_node<BLOCK, S>(A, R, stack, sp, node, Q, c);
+        }
+        if (live && (R.tau >= kTauCut || (node < 0 && !Q.has_prim()))) {
+            sec_finish<S, true>(A, t, R, c);
+            live = false;
+        }
+    }
+    if constexpr (S) flush_counters(A.work + kNumCtr, c);
+}
+
 // One ray per lane, grid-stride over ray ids [t_begin, t_end) (light rays: already coherent —
 // neighbouring lanes trace from neighbouring pixels towards the same light).
 template <int BLOCK, bool S, bool FAST>
@@ -755,7 +921,21 @@ static hipError_t secondary_launch(const RenderArgs& A, uint32_t nrec, uint64_t 
     // thread per secondary ray in record order, because neighbouring records are neighbouring
     // pixels and their rays already share BVH paths. VR_SECONDARY=p selects the persistent
     // variant for A/B runs.
-    if (variant == 0) {
+    if (variant == 2) {
+        int dev = 0, cus = 0, per_cu = 0;
+        if (hipGetDevice(&dev) != hipSuccess) return hipErrorUnknown;
+        if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return hipErrorUnknown;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, dev::secondary_ww_kernel<kBlockSecondary, S>,
+                                                         kBlockSecondary, 0) != hipSuccess || per_cu < 1)
+            per_cu = 1;
+        uint64_t grid = (uint64_t)cus * (uint64_t)per_cu;
+        const uint64_t need = (total + kBlockSecondary - 1) / kBlockSecondary;
+        if (grid > need) grid = need;
+        hipError_t e = hipMemsetAsync(A.ray_next, 0, sizeof(unsigned long long), stream);
+        if (e != hipSuccess) return e;
+        hipLaunchKernelGGL((dev::secondary_ww_kernel<kBlockSecondary, S>), dim3((unsigned)grid), dim3(kBlockSecondary), 0,
+                           stream, A, nrec, total);
+    } else if (variant == 0) {
         uint64_t blocks = (total + kBlockSecondary - 1) / kBlockSecondary;
         if (blocks > 65536ull * 16ull) blocks = 65536ull * 16ull;
         hipLaunchKernelGGL((dev::secondary_simple_kernel<kBlockSecondary, S, FAST>), dim3((unsigned)blocks),
@@ -782,11 +962,11 @@ static hipError_t secondary_launch(const RenderArgs& A, uint32_t nrec, uint64_t 
 hipError_t gauss_secondary(const RenderArgs& A, uint32_t nrec, hipStream_t stream, bool stats) {
     const uint64_t total = (uint64_t)nrec * (uint64_t)(A.num_lights + A.env_samples);
     if (total == 0) return hipSuccess;
-    // A/B switches (read once): VR_SECONDARY=p persistent kernel; VR_SEC_EXACT=1 correctly rounded
+    // A/B switches (read once): VR_SECONDARY=s one ray per thread, =p refill-only persistent kernel; VR_SEC_EXACT=1 correctly rounded
     // secondary-ray arithmetic (the fast form is the default).
-    static const int variant = [] {
+    static const int variant = [] {  // 2: while-while persistent (default), 0: one ray per thread, 1: old persistent
         const char* v = getenv("VR_SECONDARY");
-        return (v && v[0] == 'p') ? 1 : 0;
+        return (v && v[0] == 'p') ? 1 : (v && v[0] == 's') ? 0 : 2;
     }();
     static const bool exact = [] {
         const char* v = getenv("VR_SEC_EXACT");

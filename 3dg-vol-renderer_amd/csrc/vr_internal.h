@@ -103,6 +103,7 @@ struct RenderArgs {
     unsigned long long* rec_bloom;  // per record: 64-bit membership mask of its active list
     uint32_t* slowq;                // light rays needing the exact stopping event: [0] count, [1..] ray ids
     uint32_t slowq_cap;
+    unsigned long long* ray_next;   // persistent secondary kernel: next unclaimed ray id
     const unsigned long long* pcg_jump;  // [2k] = A^k, [2k+1] = inc (A^(k-1) + ... + 1): PCG32 state after k draws
 };
 

@@ -95,7 +95,8 @@ def main():
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--config", default="c4", choices=sorted(CONFIGS))
     ap.add_argument("--env-samples", type=int, default=20)
-    ap.add_argument("--t-eps", type=float, default=0.0)
+    ap.add_argument("--t-eps", type=float, default=1e-6,
+                    help="stop a ray once T <= t_eps (SURVEY §8(d) benchmark setting; error bound in DESIGN.md)")
     ap.add_argument("--seed", type=int, default=2025)
     ap.add_argument("--cpu-budget", type=float, default=20.0, help="seconds of CPU-baseline work (0 = skip)")
     ap.add_argument("--cpu-threads", type=int, default=min(16, os.cpu_count() or 1))
