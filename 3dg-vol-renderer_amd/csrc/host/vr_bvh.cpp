@@ -81,6 +81,11 @@ BVHBuild build_bvh(const std::vector<float>& boxes) {
     }
     uint32_t* ord = out.order.data();
     constexpr int kBins = 16;
+    // Depth budget: SAH may go kSlack levels deeper than a perfectly balanced tree, but never past
+    // kMaxDepth. Shallow trees let the secondary-ray kernel use a 24-entry LDS stack (more waves per
+    // CU); very large scenes fall back to the 32-entry stack.
+    constexpr int kSlack = 6;
+    const int depth_cap = std::min(kMaxDepth, std::max(kShallowDepth, ceil_log2((N + kLeafMax - 1) / kLeafMax + 1) + kSlack));
     while (!work.empty()) {
         Work w = work.back();
         work.pop_back();
@@ -99,7 +104,7 @@ BVHBuild build_bvh(const std::vector<float>& boxes) {
         if (ext[1] > ext[axis]) axis = 1;
         if (ext[2] > ext[axis]) axis = 2;
         uint32_t mid = 0;
-        const bool balanced = w.depth + ceil_log2((count + kLeafMax - 1) / kLeafMax) >= kMaxDepth - 1;
+        const bool balanced = w.depth + ceil_log2((count + kLeafMax - 1) / kLeafMax) >= depth_cap - 1;
         if (!balanced && ext[axis] > 0.0f) {
             // binned SAH over all three axes
             float best_cost = INFINITY;

@@ -5,6 +5,8 @@
 
 #include <algorithm>
 #include <cmath>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <map>
 #include <mutex>
@@ -176,6 +178,7 @@ vr_status fill_args(vr_ctx* c, const vr_camera* cam, const vr_render_params* p, 
     A.nodes = c->d_nodes;
     A.spheres = c->d_spheres;
     A.num_prims = c->num_prims;
+    A.bvh_depth = c->bvh_depth;
     A.num_lights = (int32_t)c->lights.size();
     for (size_t l = 0; l < c->lights.size(); ++l) A.lights[l] = c->lights[l];
     for (int k = 0; k < 3; ++k) A.env[k] = c->env[k];
@@ -402,6 +405,8 @@ vr_status vr_upload_scene(vr_ctx* c, const vr_scene* sc) {
         HIP_TRY(hipMemcpy(c->d_nodes, b.nodes.data(), b.nodes.size() * sizeof(BVHNode), hipMemcpyHostToDevice), "hipMemcpy(nodes)");
         c->num_prims = (int32_t)N;
         c->bvh_depth = b.max_depth;
+        if (getenv("VR_DEBUG"))
+            fprintf(stderr, "[vr] BVH: %zu prims, %zu nodes, depth %d\n", N, b.nodes.size(), b.max_depth);
         c->num_nodes = b.nodes.size();
     } else {
         const size_t N = s.spheres.size();

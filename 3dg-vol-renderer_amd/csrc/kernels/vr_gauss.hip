@@ -654,9 +654,11 @@ __device__ __forceinline__ void sec_node(const RenderArgs& A, const SecRay& R, i
     }
 }
 
-template <int BLOCK, bool S>
-__global__ __launch_bounds__(BLOCK) void secondary_ww_kernel(RenderArgs A, uint32_t nrec, uint64_t total) {
-    __shared__ int s_stack[kStackSize * BLOCK];
+template <int BLOCK, int STACK, bool S>
+__global__ __launch_bounds__(BLOCK, STACK == kShallowStack ? 6 : 5) void secondary_ww_kernel(RenderArgs A, uint32_t nrec,
+                                                                                            uint64_t total, int refill_min,
+                                                                                            int prim_bias) {
+    __shared__ int s_stack[STACK * BLOCK];
     int* stack = s_stack + threadIdx.x;
     const uint32_t lane = threadIdx.x & 63u;
     Ctr c{};
@@ -669,7 +671,7 @@ __global__ __launch_bounds__(BLOCK) void secondary_ww_kernel(RenderArgs A, uint3
     bool counter_done = false;        // wave-uniform: the global ray counter has passed `total`
     for (;;) {
         const uint64_t idle = __ballot(!live);
-        if (__popcll(idle) >= 32) {  // refill once half the wave is idle (amortises sec_init)
+        if (__popcll(idle) >= refill_min) {  // refill once enough lanes are idle (amortises sec_init)
             if (pool == pool_end && !counter_done) {
                 uint64_t base = 0;
                 if (lane == 0) base = atomicAdd(A.ray_next, 64ull);
@@ -699,7 +701,8 @@ __global__ __launch_bounds__(BLOCK) void secondary_ww_kernel(RenderArgs A, uint3
         const bool has_prim = live && Q.has_prim();
         const bool can_node = live && node >= 0 && Q.n <= 2;
         const int np = __popcll(__ballot(has_prim)), nn = __popcll(__ballot(can_node));
-        if (np >= nn) {  // PRIM iteration
+        // whichever kind more lanes can use; never a kind no lane can use (that would not progress)
+        if (nn == 0 || (np > 0 && np + prim_bias >= nn)) {  // PRIM iteration
             if (has_prim) {
                 const uint32_t j = Q.next();
                 if constexpr (S) c.v[kCtrPrims]++;
@@ -922,19 +925,29 @@ static hipError_t secondary_launch(const RenderArgs& A, uint32_t nrec, uint64_t 
     // pixels and their rays already share BVH paths. VR_SECONDARY=p selects the persistent
     // variant for A/B runs.
     if (variant == 2) {
-        int dev = 0, cus = 0, per_cu = 0;
-        if (hipGetDevice(&dev) != hipSuccess) return hipErrorUnknown;
-        if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return hipErrorUnknown;
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, dev::secondary_ww_kernel<kBlockSecondary, S>,
-                                                         kBlockSecondary, 0) != hipSuccess || per_cu < 1)
+        static const int refill_min = getenv("VR_WW_REFILL") ? atoi(getenv("VR_WW_REFILL")) : 32;
+        static const int prim_bias = getenv("VR_WW_BIAS") ? atoi(getenv("VR_WW_BIAS")) : 0;
+        const int rmin = refill_min < 1 ? 1 : (refill_min > 64 ? 64 : refill_min);
+        hipError_t e = hipMemsetAsync(A.ray_next, 0, sizeof(unsigned long long), stream);
+        if (e != hipSuccess) return e;
+        static const bool force_deep = getenv("VR_WW_STACK") && atoi(getenv("VR_WW_STACK")) == kStackSize;
+        const bool shallow = A.bvh_depth <= kShallowStack + 1 && !force_deep;  // pushes <= depth - 1
+        const void* fn = shallow ? (const void*)dev::secondary_ww_kernel<kBlockSecondary, kShallowStack, S>
+                                 : (const void*)dev::secondary_ww_kernel<kBlockSecondary, kStackSize, S>;
+        int dv = 0, cus = 0, per_cu = 0;
+        if (hipGetDevice(&dv) != hipSuccess) return hipErrorUnknown;
+        if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dv) != hipSuccess) return hipErrorUnknown;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, kBlockSecondary, 0) != hipSuccess || per_cu < 1)
             per_cu = 1;
         uint64_t grid = (uint64_t)cus * (uint64_t)per_cu;
         const uint64_t need = (total + kBlockSecondary - 1) / kBlockSecondary;
         if (grid > need) grid = need;
-        hipError_t e = hipMemsetAsync(A.ray_next, 0, sizeof(unsigned long long), stream);
-        if (e != hipSuccess) return e;
-        hipLaunchKernelGGL((dev::secondary_ww_kernel<kBlockSecondary, S>), dim3((unsigned)grid), dim3(kBlockSecondary), 0,
-                           stream, A, nrec, total);
+        if (shallow)
+            hipLaunchKernelGGL((dev::secondary_ww_kernel<kBlockSecondary, kShallowStack, S>), dim3((unsigned)grid),
+                               dim3(kBlockSecondary), 0, stream, A, nrec, total, rmin, prim_bias);
+        else
+            hipLaunchKernelGGL((dev::secondary_ww_kernel<kBlockSecondary, kStackSize, S>), dim3((unsigned)grid),
+                               dim3(kBlockSecondary), 0, stream, A, nrec, total, rmin, prim_bias);
     } else if (variant == 0) {
         uint64_t blocks = (total + kBlockSecondary - 1) / kBlockSecondary;
         if (blocks > 65536ull * 16ull) blocks = 65536ull * 16ull;

@@ -38,6 +38,8 @@ static_assert(sizeof(BVHNode) == 64, "node must be 64 B");
 constexpr int kLeafMax = 4;          // primitives per leaf
 constexpr int kMaxDepth = 30;        // builder guarantees node depth <= kMaxDepth
 constexpr int kStackSize = 32;       // traversal stack entries (>= kMaxDepth + 1)
+constexpr int kShallowDepth = 24;    // trees this shallow use the 24-entry stack variant
+constexpr int kShallowStack = 24;    // (a child-pair traversal pushes at most depth - 1 entries)
 constexpr int kTile = 16;            // pixel tile edge (one 256-thread workgroup per tile)
 
 __host__ __device__ inline bool ref_is_leaf(int32_t r) { return r < 0; }
@@ -73,6 +75,7 @@ struct RenderArgs {
     const BVHNode* nodes;
     const SphereRecord* spheres;
     int32_t num_prims;
+    int32_t bvh_depth;  // deepest node level of the uploaded BVH (root = 1)
     int32_t num_lights;
     LightRecord lights[kMaxLights];
     float env[3];
