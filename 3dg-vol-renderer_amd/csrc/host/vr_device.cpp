@@ -66,7 +66,8 @@ struct vr_ctx {
         size_t bytes = 0;
     };
     Buf px_cnt, px_acnt, px_off, px_aoff, px_T, scan_tmp, rec_pos, rec_meta, rec_act, tr, totals, rec_bloom, slowq;
-    Buf pcg_jump, ray_next;
+    Buf pcg_jump, ray_next, rec_list, rec_nlist;
+    bool list_ok = false;  // all covariances positive definite: neighbour lists are exact
     int pcg_jump_n = -1;
     uint32_t* h_totals = nullptr;  // pinned [0] records, [1] act entries
     int64_t last_records = 0, last_secondary = 0;
@@ -185,6 +186,11 @@ vr_status fill_args(vr_ctx* c, const vr_camera* cam, const vr_render_params* p, 
     A.step_size = p->step_size;
     A.env_samples = p->env_samples;
     A.t_eps = p->t_eps;
+    // Secondary-ray optical-depth cut-off. Exact mode (t_eps = 0): 104, where expf(-tau) is already
+    // 0 in f32, so stopping is bit-neutral. With an early-out budget t_eps > 0 the cut-off is
+    // ln(1/t_eps) + ln(1000): a dropped transmittance is <= 1e-3 * t_eps, a thousandth of the error
+    // the primary early-out itself is allowed (DESIGN.md §Error budget).
+    A.tau_cut = p->t_eps > 0.0f ? std::min(104.0f, (float)(std::log(1.0 / p->t_eps) + std::log(1000.0))) : 104.0f;
     if (p->integrator != VR_TEST_HITMASK) {
         const float* d;
         int n;
@@ -266,6 +272,15 @@ vr_status gauss_pipeline(vr_ctx* c, RenderArgs& A, hipStream_t s, bool stats) {
     HIP_TRY(hipMemsetAsync(A.slowq, 0, sizeof(uint32_t), s), "hipMemsetAsync(slow queue)");
     if ((st = grow(c->ray_next, 8, "hipMalloc(ray counter)")) != VR_OK) return st;
     A.ray_next = (unsigned long long*)c->ray_next.p;
+    static const bool no_list = getenv("VR_NOLIST") && getenv("VR_NOLIST")[0] == '1';
+    A.list_ok = c->list_ok && !no_list && (uint64_t)nrec * kListCap < 0xffffffffull;
+    if (A.list_ok) {
+        if ((st = grow(c->rec_list, std::max<uint64_t>(nrec, 1) * kListCap * 4ull, "hipMalloc(record lists)")) != VR_OK)
+            return st;
+        if ((st = grow(c->rec_nlist, std::max<uint64_t>(nrec, 1) * 4ull, "hipMalloc(record lists)")) != VR_OK) return st;
+        A.rec_list = (int32_t*)c->rec_list.p;
+        A.rec_nlist = (uint32_t*)c->rec_nlist.p;
+    }
     A.rec_pos = (float4*)c->rec_pos.p;
     A.rec_meta = (uint4*)c->rec_meta.p;
     A.rec_act = (int32_t*)c->rec_act.p;
@@ -353,7 +368,7 @@ void vr_destroy(vr_ctx* c) {
     if (c->h_counters) (void)hipHostFree(c->h_counters);
     if (c->h_totals) (void)hipHostFree(c->h_totals);
     for (vr_ctx::Buf* b : {&c->px_cnt, &c->px_acnt, &c->px_off, &c->px_aoff, &c->px_T, &c->scan_tmp, &c->rec_pos,
-                           &c->rec_meta, &c->rec_act, &c->tr, &c->totals, &c->rec_bloom, &c->slowq, &c->pcg_jump, &c->ray_next})
+                           &c->rec_meta, &c->rec_act, &c->tr, &c->totals, &c->rec_bloom, &c->slowq, &c->pcg_jump, &c->ray_next, &c->rec_list, &c->rec_nlist})
         if (b->p) (void)hipFree(b->p);
     if (c->d_frame) (void)hipFree(c->d_frame);
     if (c->ev_start) (void)hipEventDestroy(c->ev_start);
@@ -405,6 +420,18 @@ vr_status vr_upload_scene(vr_ctx* c, const vr_scene* sc) {
         HIP_TRY(hipMemcpy(c->d_nodes, b.nodes.data(), b.nodes.size() * sizeof(BVHNode), hipMemcpyHostToDevice), "hipMemcpy(nodes)");
         c->num_prims = (int32_t)N;
         c->bvh_depth = b.max_depth;
+        // neighbour lists rely on the 3.15-sigma boxes bounding {q <= kListR2}: true for positive
+        // definite covariances with a finite inverse
+        c->list_ok = true;
+        for (size_t i = 0; i < N && c->list_ok; ++i) {
+            const GaussianPre& p = s.pre[i];
+            const double a = p.cov[0], b2 = p.cov[1], c2 = p.cov[2], d = p.cov[3], e = p.cov[4], f = p.cov[5];
+            const double m2 = a * d - b2 * b2;
+            const double det = a * (d * f - e * e) - b2 * (b2 * f - e * c2) + c2 * (b2 * e - d * c2);
+            bool ok = a > 0.0 && m2 > 0.0 && det > 0.0;
+            for (int k = 0; k < 6; ++k) ok = ok && std::isfinite(p.inv_cov[k]);
+            c->list_ok = ok;
+        }
         if (getenv("VR_DEBUG"))
             fprintf(stderr, "[vr] BVH: %zu prims, %zu nodes, depth %d\n", N, b.nodes.size(), b.max_depth);
         c->num_nodes = b.nodes.size();

@@ -375,6 +375,11 @@ struct SecRay {
     uint64_t hitmask, bloom;
     uint32_t act_off, act_n;
     bool light, needs_stop;
+    uint32_t nsteps;  // instrumented build only: node steps taken by this ray
+    uint32_t rec;     // record index
+    int lmode;        // neighbour-list phase: 1 central members, 2 other members, 0 done / none
+    bool listed;      // the record has a neighbour list (tree leaves then skip its members)
+    uint32_t lnb;     // number of "other" members (tested after the central ones)
 };
 
 __device__ __forceinline__ int act_find(const RenderArgs& A, const SecRay& R, int j) {
@@ -417,10 +422,12 @@ __device__ __forceinline__ bool sec_init(const RenderArgs& A, uint32_t nrec, uin
     const uint32_t r = (uint32_t)(t - (uint64_t)s * nrec);
     const float4 pos = A.rec_pos[r];
     const uint4 meta = A.rec_meta[r];
+    R.rec = r;
     R.act_off = meta.z;
     R.act_n = meta.w;
     R.bloom = A.rec_bloom[r];
     R.hitmask = 0;
+    R.nsteps = 0;
     R.tau = 0.0f;
     R.tlast = 0.0f;
     R.needs_stop = false;
@@ -481,7 +488,15 @@ __device__ __forceinline__ void sec_leaf(const RenderArgs& A, SecRay& R, int32_t
 // Ray complete: write its transmittance (or hand it to the exact slow path).
 template <bool S, bool FAST>
 __device__ __forceinline__ void sec_finish(const RenderArgs& A, uint64_t t, SecRay& R, Ctr& c) {
-    if (R.tau >= kTauCut) {
+    if constexpr (S) {  // secondary-stage diagnostics in otherwise unused counter slots
+        if (R.tau >= A.tau_cut) {
+            c.v[kCtrSteps]++;                 // rays ended by the optical-depth cut-off
+            c.v[kCtrPrimQueries] += R.nsteps;  // ... and their node steps
+        } else {
+            c.v[kCtrPixels] += R.nsteps;       // node steps of rays that ran to the end of the tree
+        }
+    }
+    if (R.tau >= A.tau_cut) {
         A.tr[t] = 0.0f;
         return;
     }
@@ -538,11 +553,11 @@ __device__ __forceinline__ bool sec_step(const RenderArgs& A, SecRay& R, int* st
     if (ll || lr) {
         const bool r_first = lr && (!ll || rmin < lmin);
         sec_leaf<S, FAST>(A, R, r_first ? nc.y : nc.x, c);
-        if (ll && lr && R.tau < kTauCut) sec_leaf<S, FAST>(A, R, r_first ? nc.x : nc.y, c);
+        if (ll && lr && R.tau < A.tau_cut) sec_leaf<S, FAST>(A, R, r_first ? nc.x : nc.y, c);
         if (ll) hl = false;
         if (lr) hr = false;
     }
-    bool done = R.tau >= kTauCut;
+    bool done = R.tau >= A.tau_cut;
     if (!done) {
         if (hl && hr) {
             int nearer = nc.x, farther = nc.y;
@@ -583,12 +598,12 @@ struct LeafQueue {  // FIFO of up to 4 leaf refs (registers) + the leaf being te
     int32_t q0, q1, q2, q3;
     int n;
     uint32_t j, end;  // current primitive range [j, end)
-    __device__ __forceinline__ void push(int32_t r) {
-        if (n == 0) q0 = r;
-        else if (n == 1) q1 = r;
-        else if (n == 2) q2 = r;
-        else q3 = r;
-        ++n;
+    // branch-free: writes r at slot `idx` (no slot matches idx < 0)
+    __device__ __forceinline__ void put(int idx, int32_t r) {
+        q0 = idx == 0 ? r : q0;
+        q1 = idx == 1 ? r : q1;
+        q2 = idx == 2 ? r : q2;
+        q3 = idx == 3 ? r : q3;
     }
     __device__ __forceinline__ bool has_prim() const { return j < end || n > 0; }
     __device__ __forceinline__ uint32_t next() {  // requires has_prim()
@@ -605,11 +620,15 @@ struct LeafQueue {  // FIFO of up to 4 leaf refs (registers) + the leaf being te
 };
 
 // One child-pair step of the postponed-leaf traversal: leaf children go to the queue (nearer
-// first); node < 0 afterwards means the traversal is finished.
+// first); node < 0 afterwards means the traversal is finished. Written branch-free (bitwise
+// predicates, selects) so a wave does not split inside the step.
 template <int BLOCK, bool S>
-__device__ __forceinline__ void sec_node(const RenderArgs& A, const SecRay& R, int* stack, int& sp, int& node,
-                                         LeafQueue& Q, Ctr& c) {
-    if constexpr (S) c.v[kCtrNodes]++;
+__device__ __forceinline__ void sec_node(const RenderArgs& A, SecRay& R, int* stack, int& sp, int& node, LeafQueue& Q,
+                                         Ctr& c) {
+    if constexpr (S) {
+        c.v[kCtrNodes]++;
+        ++R.nsteps;
+    }
     const float4* np = reinterpret_cast<const float4*>(A.nodes + node);
     const float4 n0 = np[0], n1 = np[1], n2 = np[2];
     const int4 nc = reinterpret_cast<const int4*>(A.nodes + node)[3];
@@ -624,33 +643,133 @@ __device__ __forceinline__ void sec_node(const RenderArgs& A, const SecRay& R, i
     const float rmin = fmaxf(fmaxf(fminf(ux1, ux2), fminf(uy1, uy2)), fminf(uz1, uz2));
     const float rmax = fminf(fminf(fmaxf(ux1, ux2), fmaxf(uy1, uy2)), fmaxf(uz1, uz2));
     const float lim = R.lim + kTPad * (1.0f + R.lim);
-    bool hl = nc.x != 0 && lmax >= fmaxf(lmin, 0.0f) && lmin <= lim;
-    bool hr = nc.y != 0 && rmax >= fmaxf(rmin, 0.0f) && rmin <= lim;
+    const bool hl = (nc.x != 0) & (lmax >= fmaxf(lmin, 0.0f)) & (lmin <= lim);
+    const bool hr = (nc.y != 0) & (rmax >= fmaxf(rmin, 0.0f)) & (rmin <= lim);
     const bool r_near = rmin < lmin;
-    const bool ll = hl && ref_is_leaf(nc.x), lr = hr && ref_is_leaf(nc.y);
-    if (ll && lr) {
-        Q.push(r_near ? nc.y : nc.x);
-        Q.push(r_near ? nc.x : nc.y);
-    } else if (ll) {
-        Q.push(nc.x);
-    } else if (lr) {
-        Q.push(nc.y);
-    }
-    hl = hl && !ll;
-    hr = hr && !lr;
-    if (hl && hr) {
-        stack[sp * BLOCK] = r_near ? nc.x : nc.y;
+    const bool ll = hl & (nc.x < 0), lr = hr & (nc.y < 0);  // leaf refs are negative
+    const int32_t near_ref = r_near ? nc.y : nc.x, far_ref = r_near ? nc.x : nc.y;
+    // leaves -> queue, nearer first
+    const int32_t first_leaf = (ll & lr) ? near_ref : (ll ? nc.x : nc.y);
+    Q.put((ll | lr) ? Q.n : -1, first_leaf);
+    Q.put((ll & lr) ? Q.n + 1 : -1, far_ref);
+    Q.n += (int)ll + (int)lr;
+    // inner children -> continue / stack
+    const bool il = hl & !ll, ir = hr & !lr;
+    if (il & ir) {
+        stack[sp * BLOCK] = far_ref;
         ++sp;
-        node = r_near ? nc.y : nc.x;
-    } else if (hl) {
-        node = nc.x;
-    } else if (hr) {
-        node = nc.y;
+    }
+    if (il | ir) {
+        node = (il & ir) ? near_ref : (il ? nc.x : nc.y);
     } else if (sp > 0) {
         --sp;
         node = stack[sp * BLOCK];
     } else {
         node = -1;
+    }
+}
+
+// Neighbour list of every record: a point query of the BVH at the record position collecting
+// each Gaussian with q_j(pos) <= kListR2, central ones (q <= kListCentral, the largest optical
+// depths from pos) at the front of the record's slots, the others at the back. All secondary rays
+// of the record test this list first — most of them become opaque right there, without touching
+// the tree — and the tree walk that follows skips exactly these members (same q, bit for bit).
+template <int BLOCK>
+__global__ __launch_bounds__(BLOCK) void record_list_kernel(RenderArgs A, uint32_t nrec) {
+    __shared__ int s_stack[kStackSize * BLOCK];
+    int* stack = s_stack + threadIdx.x;
+    for (uint32_t r = blockIdx.x * BLOCK + threadIdx.x; r < nrec; r += gridDim.x * BLOCK) {
+        const float4 pos = A.rec_pos[r];
+        int32_t* slot = A.rec_list + (size_t)r * kListCap;
+        uint32_t nc = 0, nb = 0;
+        bool ovf = false;
+        int sp = 0, node = 0;
+        for (;;) {
+            const float4* np = reinterpret_cast<const float4*>(A.nodes + node);
+            const float4 n0 = np[0], n1 = np[1], n2 = np[2];
+            const int4 ncr = reinterpret_cast<const int4*>(A.nodes + node)[3];
+            const bool inl = (ncr.x != 0) & (n0.x <= pos.x) & (pos.x <= n0.w) & (n0.y <= pos.y) & (pos.y <= n1.x) &
+                             (n0.z <= pos.z) & (pos.z <= n1.y);
+            const bool inr = (ncr.y != 0) & (n1.z <= pos.x) & (pos.x <= n2.y) & (n1.w <= pos.y) & (pos.y <= n2.z) &
+                             (n2.x <= pos.z) & (pos.z <= n2.w);
+            int32_t leaves[2];
+            int nleaf = 0;
+            if (inl && ncr.x < 0) leaves[nleaf++] = ncr.x;
+            if (inr && ncr.y < 0) leaves[nleaf++] = ncr.y;
+            for (int li = 0; li < nleaf; ++li) {
+                const uint32_t first = leaf_first(leaves[li]), count = leaf_count(leaves[li]);
+                for (uint32_t j = first; j < first + count; ++j) {
+                    const GRec g = load_rec(A.gauss, (int)j);
+                    const float q = cq_fast(g, pos.x - g.mx, pos.y - g.my, pos.z - g.mz);
+                    if (!(q <= kListR2)) continue;
+                    if (nc + nb >= (uint32_t)kListCap) {
+                        ovf = true;
+                    } else if (q <= kListCentral) {
+                        slot[nc++] = (int32_t)j;
+                    } else {
+                        slot[kListCap - 1 - nb++] = (int32_t)j;
+                    }
+                }
+            }
+            const bool il = inl && ncr.x > 0, ir = inr && ncr.y > 0;
+            if (il && ir) {
+                stack[sp * BLOCK] = ncr.y;
+                ++sp;
+                node = ncr.x;
+            } else if (il) {
+                node = ncr.x;
+            } else if (ir) {
+                node = ncr.y;
+            } else if (sp > 0) {
+                --sp;
+                node = stack[sp * BLOCK];
+            } else {
+                break;
+            }
+        }
+        A.rec_nlist[r] = ovf ? 0xffffffffu : (nc | (nb << 16));
+    }
+}
+
+// Start ray R's neighbour-list phase (or go straight to the tree).
+__device__ __forceinline__ void list_begin(const RenderArgs& A, SecRay& R, LeafQueue& Q, int& node) {
+    Q.n = 0;
+    Q.j = Q.end = 0;
+    R.lmode = 0;
+    R.listed = false;
+    node = 0;
+    if (!A.list_ok) return;
+    const uint32_t nl = A.rec_nlist[R.rec];
+    if (nl == 0xffffffffu) return;
+    R.listed = true;
+    const uint32_t nc = nl & 0xffffu;
+    R.lnb = nl >> 16;
+    const uint32_t base = R.rec * (uint32_t)kListCap;
+    if (nc > 0) {
+        R.lmode = 1;
+        Q.j = base;
+        Q.end = base + nc;
+        node = -2;
+    } else if (R.lnb > 0) {
+        R.lmode = 2;
+        Q.j = base + kListCap - R.lnb;
+        Q.end = base + kListCap;
+        node = -2;
+    }
+}
+
+// After a list slot was consumed: move to the other members, then to the tree.
+__device__ __forceinline__ void list_advance(SecRay& R, LeafQueue& Q, int& node) {
+    if (R.lmode == 0 || Q.j < Q.end) return;
+    if (R.lmode == 1 && R.lnb > 0) {
+        R.lmode = 2;
+        const uint32_t base = R.rec * (uint32_t)kListCap;
+        Q.j = base + kListCap - R.lnb;
+        Q.end = base + kListCap;
+    } else {
+        R.lmode = 0;
+        Q.j = Q.end = 0;
+        node = 0;
     }
 }
 
@@ -687,9 +806,7 @@ __global__ __launch_bounds__(BLOCK, STACK == kShallowStack ? 6 : 5) void seconda
                 if constexpr (S) c.v[kCtrSecRays]++;
                 live = sec_init(A, nrec, t, R);  // false: complete already (Tr written)
                 sp = 0;
-                node = 0;
-                Q.n = 0;
-                Q.j = Q.end = 0;
+                list_begin(A, R, Q, node);
             }
             const uint64_t handed = (uint64_t)__popcll(idle);
             pool = pool + handed < pool_end ? pool + handed : pool_end;
@@ -704,12 +821,14 @@ __global__ __launch_bounds__(BLOCK, STACK == kShallowStack ? 6 : 5) void seconda
         // whichever kind more lanes can use; never a kind no lane can use (that would not progress)
         if (nn == 0 || (np > 0 && np + prim_bias >= nn)) {  // PRIM iteration
             if (has_prim) {
-                const uint32_t j = Q.next();
+                const bool from_list = R.lmode != 0;
+                const uint32_t j = from_list ? (uint32_t)A.rec_list[Q.j++] : Q.next();
                 if constexpr (S) c.v[kCtrPrims]++;
                 const GRec g = load_rec(A.gauss, (int)j);
                 const Quad q = quad_fast(g, R.ray);
                 float a, b;
-                if (intersect_fast(q, a, b)) {
+                // a tree leaf skips the record's list members (already summed)
+                if (!(R.listed && !from_list && q.Cq <= kListR2) && intersect_fast(q, a, b)) {
                     const int slot = act_find(A, R, (int)j);
                     float lo = a;
                     if (slot >= 0) {
@@ -724,11 +843,12 @@ __global__ __launch_bounds__(BLOCK, STACK == kShallowStack ? 6 : 5) void seconda
                         R.needs_stop = true;
                     }
                 }
+                list_advance(R, Q, node);
             }
         } else {  // NODE iteration
             if (can_node) sec_node<BLOCK, S>(A, R, stack, sp, node, Q, c);
         }
-        if (live && (R.tau >= kTauCut || (node < 0 && !Q.has_prim()))) {
+        if (live && (R.tau >= A.tau_cut || (node < 0 && !Q.has_prim()))) {
             sec_finish<S, true>(A, t, R, c);
             live = false;
         }
@@ -932,6 +1052,15 @@ static hipError_t secondary_launch(const RenderArgs& A, uint32_t nrec, uint64_t 
         if (e != hipSuccess) return e;
         static const bool force_deep = getenv("VR_WW_STACK") && atoi(getenv("VR_WW_STACK")) == kStackSize;
         const bool shallow = A.bvh_depth <= kShallowStack + 1 && !force_deep;  // pushes <= depth - 1
+        if (A.list_ok) {
+            uint64_t lb = ((uint64_t)nrec + kBlockSecondary - 1) / kBlockSecondary;
+            if (lb > 65536ull * 4ull) lb = 65536ull * 4ull;
+            if (lb > 0)
+                hipLaunchKernelGGL((dev::record_list_kernel<kBlockSecondary>), dim3((unsigned)lb), dim3(kBlockSecondary), 0,
+                                   stream, A, nrec);
+            e = hipGetLastError();
+            if (e != hipSuccess) return e;
+        }
         const void* fn = shallow ? (const void*)dev::secondary_ww_kernel<kBlockSecondary, kShallowStack, S>
                                  : (const void*)dev::secondary_ww_kernel<kBlockSecondary, kStackSize, S>;
         int dv = 0, cus = 0, per_cu = 0;

@@ -138,18 +138,24 @@ __device__ __forceinline__ float optical_depth(const GRec& g, const Quad& q, flo
 // FMA-contracted products and hardware reciprocal / square root (1 ulp) instead of correctly
 // rounded division and sqrt — about half the VALU instructions of the exact forms. The primary
 // march keeps the exact forms (its activation decisions must match the oracle bit for bit).
+// p^T M p with p = origin - mean, in exactly the arithmetic quad_fast uses for Cq (the record
+// neighbour lists compare it bit for bit against the value a secondary ray computes).
+__device__ __forceinline__ float cq_fast(const GRec& g, float px, float py, float pz) {
+    const float mpx = fmaf(g.m00, px, fmaf(g.m01, py, g.m02 * pz));
+    const float mpy = fmaf(g.m01, px, fmaf(g.m11, py, g.m12 * pz));
+    const float mpz = fmaf(g.m02, px, fmaf(g.m12, py, g.m22 * pz));
+    return fmaf(px, mpx, fmaf(py, mpy, pz * mpz));
+}
+
 __device__ __forceinline__ Quad quad_fast(const GRec& g, const Ray& r) {
     const float px = r.ox - g.mx, py = r.oy - g.my, pz = r.oz - g.mz;
     const float mdx = fmaf(g.m00, r.dx, fmaf(g.m01, r.dy, g.m02 * r.dz));
     const float mdy = fmaf(g.m01, r.dx, fmaf(g.m11, r.dy, g.m12 * r.dz));
     const float mdz = fmaf(g.m02, r.dx, fmaf(g.m12, r.dy, g.m22 * r.dz));
-    const float mpx = fmaf(g.m00, px, fmaf(g.m01, py, g.m02 * pz));
-    const float mpy = fmaf(g.m01, px, fmaf(g.m11, py, g.m12 * pz));
-    const float mpz = fmaf(g.m02, px, fmaf(g.m12, py, g.m22 * pz));
     Quad q;
     q.A = fmaf(r.dx, mdx, fmaf(r.dy, mdy, r.dz * mdz));
     q.B = 2.0f * fmaf(px, mdx, fmaf(py, mdy, pz * mdz));
-    q.Cq = fmaf(px, mpx, fmaf(py, mpy, pz * mpz));
+    q.Cq = cq_fast(g, px, py, pz);
     return q;
 }
 

@@ -59,6 +59,14 @@ struct LightRecord {
 };
 
 constexpr int kMaxLights = 16;
+
+// Record neighbour lists (secondary rays): every Gaussian j whose scaled Mahalanobis distance at
+// the record position satisfies q_j(pos) <= kListR2 (pos inside its 3.08-sigma ellipsoid). The
+// BVH boxes bound the 3.15-sigma ellipsoid, so a point query can never miss a member of a
+// scene whose covariances are all positive definite (checked at upload, else lists are off).
+constexpr int kListCap = 48;
+constexpr float kListR2 = 9.5f;
+constexpr float kListCentral = 4.0f;  // members with q <= 4 (inside 2 sigma) are tested first
 constexpr int kMaxSpheres = 64;
 
 // Kernel launch parameters (passed by value).
@@ -83,6 +91,7 @@ struct RenderArgs {
     float step_size;
     int32_t env_samples;
     float t_eps;
+    float tau_cut;        // secondary rays: Tr := 0 once the optical depth reaches this (see vr_device.cpp)
     const float* tsteps;  // iterated float step sequence t_k (test_integrators.h:184,289)
     int32_t num_tsteps;
     // fallback queue (active-set overflow) and error counters
@@ -107,6 +116,9 @@ struct RenderArgs {
     uint32_t* slowq;                // light rays needing the exact stopping event: [0] count, [1..] ray ids
     uint32_t slowq_cap;
     unsigned long long* ray_next;   // persistent secondary kernel: next unclaimed ray id
+    int32_t* rec_list;              // per record kListCap slots: central members from the front, others from the back
+    uint32_t* rec_nlist;            // per record: central count | others << 16; 0xffffffff = no list (overflow)
+    int32_t list_ok;                // scene allows neighbour lists (all covariances positive definite)
     const unsigned long long* pcg_jump;  // [2k] = A^k, [2k+1] = inc (A^(k-1) + ... + 1): PCG32 state after k draws
 };
 
