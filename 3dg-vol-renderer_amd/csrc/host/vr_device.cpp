@@ -15,9 +15,8 @@
 
 namespace vr {
 hipError_t launch_render(const RenderArgs& A, hipStream_t stream, int volume_type, int integrator);
-hipError_t gauss_march(const RenderArgs& A, hipStream_t stream, int mode, bool stats);
-hipError_t gauss_scan(const RenderArgs& A, uint32_t npix, void* temp, size_t& temp_bytes, uint32_t* totals,
-                      hipStream_t stream);
+hipError_t gauss_march(const RenderArgs& A, hipStream_t stream, bool stats);
+hipError_t gauss_lists(const RenderArgs& A, uint32_t nrec, hipStream_t stream);
 hipError_t gauss_secondary(const RenderArgs& A, uint32_t nrec, hipStream_t stream, bool stats);
 hipError_t gauss_accumulate(const RenderArgs& A, uint32_t nrec, hipStream_t stream);
 hipError_t launch_unshuffle(const float* slabs, uint32_t nslabs, uint32_t tiles_per_slab, uint32_t tiles_x, uint32_t W,
@@ -65,12 +64,13 @@ struct vr_ctx {
         void* p = nullptr;
         size_t bytes = 0;
     };
-    Buf px_cnt, px_acnt, px_off, px_aoff, px_T, scan_tmp, rec_pos, rec_meta, rec_act, tr, totals, rec_bloom, slowq;
+    Buf px_first, px_T, rec_pos, rec_meta, rec_next, rec_act, tr, rec_alloc, rec_bloom, slowq;
     Buf pcg_jump, ray_next, rec_list, rec_nlist;
     bool list_ok = false;  // all covariances positive definite: neighbour lists are exact
     int pcg_jump_n = -1;
-    uint32_t* h_totals = nullptr;  // pinned [0] records, [1] act entries
+    uint32_t* h_totals = nullptr;  // pinned copy of rec_alloc: [0] records, [1] overflow-pool entries, [2] exceeded
     int64_t last_records = 0, last_secondary = 0;
+    uint64_t rec_hint = 0, ovf_hint = 0;  // record / overflow-pool capacities that sufficed last time
 };
 
 namespace {
@@ -215,22 +215,16 @@ vr_status grow(vr_ctx::Buf& b, size_t bytes, const char* what) {
     return VR_OK;
 }
 
-// RayMarchingGaussians: march (count) -> scan -> march (write) -> secondary rays -> accumulate.
+// RayMarchingGaussians: march (records) -> neighbour lists -> secondary rays -> accumulate.
 vr_status gauss_pipeline(vr_ctx* c, RenderArgs& A, hipStream_t s, bool stats) {
     const uint32_t npix = A.num_tiles * 256u;
     vr_status st;
-    if ((st = grow(c->px_cnt, npix * 4ull, "hipMalloc(px_cnt)")) != VR_OK) return st;
-    if ((st = grow(c->px_acnt, npix * 4ull, "hipMalloc(px_acnt)")) != VR_OK) return st;
-    if ((st = grow(c->px_off, npix * 4ull, "hipMalloc(px_off)")) != VR_OK) return st;
-    if ((st = grow(c->px_aoff, npix * 4ull, "hipMalloc(px_aoff)")) != VR_OK) return st;
+    if ((st = grow(c->px_first, npix * 4ull, "hipMalloc(px_first)")) != VR_OK) return st;
     if ((st = grow(c->px_T, npix * 4ull, "hipMalloc(px_T)")) != VR_OK) return st;
-    if ((st = grow(c->totals, 16, "hipMalloc(totals)")) != VR_OK) return st;
-    A.px_cnt = (uint32_t*)c->px_cnt.p;
-    A.px_acnt = (uint32_t*)c->px_acnt.p;
-    A.px_off = (uint32_t*)c->px_off.p;
-    A.px_aoff = (uint32_t*)c->px_aoff.p;
+    if ((st = grow(c->rec_alloc, 16, "hipMalloc(rec_alloc)")) != VR_OK) return st;
+    A.px_first = (uint32_t*)c->px_first.p;
     A.px_T = (float*)c->px_T.p;
-    A.totals = (const uint32_t*)c->totals.p;
+    A.rec_alloc = (uint32_t*)c->rec_alloc.p;
     // PCG32 (rng.h:20-50, seq 1 -> inc 3) jump-ahead table for the environment samples
     if (c->pcg_jump_n < 2 * A.env_samples + 2) {
         const int n = 2 * A.env_samples + 2;
@@ -247,26 +241,49 @@ vr_status gauss_pipeline(vr_ctx* c, RenderArgs& A, hipStream_t s, bool stats) {
         c->pcg_jump_n = n;
     }
     A.pcg_jump = (const unsigned long long*)c->pcg_jump.p;
-    size_t tmp_bytes = 0;
-    HIP_TRY(gauss_scan(A, npix, nullptr, tmp_bytes, nullptr, s), "scan size");
-    if ((st = grow(c->scan_tmp, tmp_bytes, "hipMalloc(scan)")) != VR_OK) return st;
-    tmp_bytes = c->scan_tmp.bytes;
-    HIP_TRY(gauss_march(A, s, 0, stats), "march (count)");
-    HIP_TRY(hipEventRecord(c->ev_stage[0], s), "hipEventRecord");
-    HIP_TRY(gauss_scan(A, npix, c->scan_tmp.p, tmp_bytes, (uint32_t*)c->totals.p, s), "scan");
-    HIP_TRY(hipMemcpyAsync(c->h_totals, c->totals.p, 2 * sizeof(uint32_t), hipMemcpyDeviceToHost, s), "totals D2H");
-    HIP_TRY(hipStreamSynchronize(s), "march (count)");
-    const uint32_t nrec = c->h_totals[0], nact = c->h_totals[1];
+
+    // One march pass; record capacity from the last frame (re-run with the exact need on overflow).
+    uint64_t cap = std::max<uint64_t>({c->rec_hint, 2ull * npix, 4096ull});
+    uint64_t ovf = std::max<uint64_t>({c->ovf_hint, cap, 4096ull});
+    uint32_t nrec = 0;
+    for (int attempt = 0;; ++attempt) {
+        if (cap > 0xffffffffull / kActInline || ovf > 0xffffffffull - cap * kActInline)
+            return fail(VR_ERR_UNSUPPORTED, "too many scatter records in one call (split the frame)");
+        if ((st = grow(c->rec_pos, cap * 16ull, "hipMalloc(records)")) != VR_OK) return st;
+        if ((st = grow(c->rec_meta, cap * 16ull, "hipMalloc(records)")) != VR_OK) return st;
+        if ((st = grow(c->rec_next, cap * 4ull, "hipMalloc(records)")) != VR_OK) return st;
+        if ((st = grow(c->rec_bloom, cap * 8ull, "hipMalloc(record blooms)")) != VR_OK) return st;
+        if ((st = grow(c->rec_act, (cap * kActInline + ovf) * 4ull, "hipMalloc(active lists)")) != VR_OK) return st;
+        A.rec_pos = (float4*)c->rec_pos.p;
+        A.rec_meta = (uint4*)c->rec_meta.p;
+        A.rec_next = (uint32_t*)c->rec_next.p;
+        A.rec_bloom = (unsigned long long*)c->rec_bloom.p;
+        A.rec_act = (int32_t*)c->rec_act.p;
+        A.rec_cap = (uint32_t)cap;
+        A.act_ovf_cap = (uint32_t)ovf;
+        HIP_TRY(hipMemsetAsync(A.rec_alloc, 0, 16, s), "hipMemsetAsync(rec_alloc)");
+        HIP_TRY(hipMemsetAsync(c->d_queue, 0, sizeof(uint32_t), s), "hipMemsetAsync(queue)");
+        HIP_TRY(gauss_march(A, s, stats), "march");
+        if (attempt == 0) HIP_TRY(hipEventRecord(c->ev_stage[0], s), "hipEventRecord");
+        HIP_TRY(hipMemcpyAsync(c->h_totals, A.rec_alloc, 3 * sizeof(uint32_t), hipMemcpyDeviceToHost, s), "rec_alloc D2H");
+        HIP_TRY(hipStreamSynchronize(s), "march");
+        if (c->h_totals[2] == 0) {
+            nrec = c->h_totals[0];
+            break;
+        }
+        if (attempt >= 3) return fail(VR_ERR_OVERFLOW, "scatter-record capacity could not be sized");
+        cap = std::max<uint64_t>(2 * cap, (uint64_t)c->h_totals[0] + c->h_totals[0] / 4 + 1024);
+        ovf = std::max<uint64_t>(2 * ovf, (uint64_t)c->h_totals[1] + c->h_totals[1] / 4 + 1024);
+    }
+    c->rec_hint = (uint64_t)nrec + nrec / 8;
+    c->ovf_hint = std::max<uint64_t>(c->ovf_hint, (uint64_t)c->h_totals[1] + c->h_totals[1] / 8);
+
     const uint64_t nsec = (uint64_t)nrec * (uint64_t)(A.num_lights + A.env_samples);
-    if ((st = grow(c->rec_pos, std::max<uint64_t>(nrec, 1) * 16ull, "hipMalloc(records)")) != VR_OK) return st;
-    if ((st = grow(c->rec_meta, std::max<uint64_t>(nrec, 1) * 16ull, "hipMalloc(records)")) != VR_OK) return st;
-    if ((st = grow(c->rec_act, std::max<uint64_t>(nact, 1) * 4ull, "hipMalloc(active lists)")) != VR_OK) return st;
-    if ((st = grow(c->tr, std::max<uint64_t>(nsec, 1) * 4ull, "hipMalloc(secondary)")) != VR_OK) return st;
     if (nsec >= 0xffffffffull) return fail(VR_ERR_UNSUPPORTED, "more than 2^32 secondary rays in one call (split the frame)");
+    if ((st = grow(c->tr, std::max<uint64_t>(nsec, 1) * 4ull, "hipMalloc(secondary)")) != VR_OK) return st;
+    A.tr = (float*)c->tr.p;
     const uint64_t nslow = (uint64_t)nrec * (uint64_t)A.num_lights;
-    if ((st = grow(c->rec_bloom, std::max<uint64_t>(nrec, 1) * 8ull, "hipMalloc(record blooms)")) != VR_OK) return st;
     if ((st = grow(c->slowq, (nslow + 1) * 4ull, "hipMalloc(slow queue)")) != VR_OK) return st;
-    A.rec_bloom = (unsigned long long*)c->rec_bloom.p;
     A.slowq = (uint32_t*)c->slowq.p;
     A.slowq_cap = (uint32_t)nslow;
     HIP_TRY(hipMemsetAsync(A.slowq, 0, sizeof(uint32_t), s), "hipMemsetAsync(slow queue)");
@@ -281,15 +298,8 @@ vr_status gauss_pipeline(vr_ctx* c, RenderArgs& A, hipStream_t s, bool stats) {
         A.rec_list = (int32_t*)c->rec_list.p;
         A.rec_nlist = (uint32_t*)c->rec_nlist.p;
     }
-    A.rec_pos = (float4*)c->rec_pos.p;
-    A.rec_meta = (uint4*)c->rec_meta.p;
-    A.rec_act = (int32_t*)c->rec_act.p;
-    A.tr = (float*)c->tr.p;
-    A.rec_cap = nrec;
-    A.act_cap = nact;
-    HIP_TRY(hipMemsetAsync(c->d_queue, 0, sizeof(uint32_t), s), "hipMemsetAsync(queue)");
     HIP_TRY(hipEventRecord(c->ev_stage[1], s), "hipEventRecord");
-    HIP_TRY(gauss_march(A, s, 1, stats), "march (write)");
+    HIP_TRY(gauss_lists(A, nrec, s), "neighbour lists");
     HIP_TRY(hipEventRecord(c->ev_stage[2], s), "hipEventRecord");
     HIP_TRY(gauss_secondary(A, nrec, s, stats), "secondary rays");
     HIP_TRY(hipEventRecord(c->ev_stage[3], s), "hipEventRecord");
@@ -367,8 +377,8 @@ void vr_destroy(vr_ctx* c) {
     if (c->d_counters) (void)hipFree(c->d_counters);
     if (c->h_counters) (void)hipHostFree(c->h_counters);
     if (c->h_totals) (void)hipHostFree(c->h_totals);
-    for (vr_ctx::Buf* b : {&c->px_cnt, &c->px_acnt, &c->px_off, &c->px_aoff, &c->px_T, &c->scan_tmp, &c->rec_pos,
-                           &c->rec_meta, &c->rec_act, &c->tr, &c->totals, &c->rec_bloom, &c->slowq, &c->pcg_jump, &c->ray_next, &c->rec_list, &c->rec_nlist})
+    for (vr_ctx::Buf* b : {&c->px_first, &c->px_T, &c->rec_pos, &c->rec_meta, &c->rec_next, &c->rec_act, &c->tr,
+                           &c->rec_alloc, &c->rec_bloom, &c->slowq, &c->pcg_jump, &c->ray_next, &c->rec_list, &c->rec_nlist})
         if (b->p) (void)hipFree(b->p);
     if (c->d_frame) (void)hipFree(c->d_frame);
     if (c->ev_start) (void)hipEventDestroy(c->ev_start);

@@ -30,7 +30,6 @@
 // Pixels whose active set outgrows the fast path's LDS list (32) are queued and re-run by the
 // fallback kernels (64), so results never depend on capacity.
 #include <hip/hip_runtime.h>
-#include <hipcub/hipcub.hpp>
 
 #include <cstdio>
 #include <cstdlib>
@@ -145,9 +144,11 @@ __device__ float light_transmittance(const RenderArgs& A, const Ray& sr, float d
 // ---------------------------------------------------------------------------------------------
 // Stage 1: primary march
 // ---------------------------------------------------------------------------------------------
-// MODE 0: count scatter records / active entries of pixel p. MODE 1: write them (offsets from the
-// scan of MODE 0's counts). Both modes run the identical march, so they agree record for record.
-template <int ACT, int MODE, bool S>
+// One pass: each scattering step allocates its record with a wave-aggregated atomic and links it
+// to the pixel's previous record (px_first / rec_next), so a pixel's records are visited in step
+// order by accumulate_kernel wherever they landed in memory. Records that do not fit the
+// capacity raise rec_alloc[2]; the host then grows the buffers and re-runs the march.
+template <int ACT, bool S>
 __device__ int march(const RenderArgs& A, uint32_t p, int px, int py, int* act_base, int* stack, int stride, Ctr& c) {
     const Ray ray = primary_ray(A, px, py);
     const GaussianRecord* __restrict__ G = A.gauss;
@@ -155,12 +156,8 @@ __device__ int march(const RenderArgs& A, uint32_t p, int px, int py, int* act_b
     const int nts = A.num_tsteps;
     const float step = A.step_size;
     float T = 1.0f;
-    uint32_t nrec = 0, nact = 0;
-    uint32_t rbase = 0, abase = 0;
-    if constexpr (MODE == 1) {
-        rbase = A.px_off[p];
-        abase = A.px_aoff[p];
-    }
+    uint32_t prev = kNoRecord;  // this pixel's last record
+    A.px_first[p] = kNoRecord;
     ActList act{act_base, stride, 0, 0};
     int kq = 0;
     if (A.num_prims > 0) {
@@ -258,48 +255,53 @@ __device__ int march(const RenderArgs& A, uint32_t p, int px, int py, int* act_b
                 sigma_s = a_mix * smu;
             }
             if (sigma_s > 0.0f) {  // scattering step -> one record
-                if constexpr (MODE == 1) {
-                    // never write past the slots MODE 0 reserved for this pixel
-                    if (nrec >= A.px_cnt[p] || nact + (uint32_t)w > A.px_acnt[p]) return kError;
-                    uint32_t r = rbase + nrec;
+                // lanes emitting now share one atomic (this branch is divergent: ballot = them)
+                const uint64_t m = __ballot(true);
+                const uint32_t leader = (uint32_t)__ffsll((unsigned long long)m) - 1u;
+                uint32_t base = 0;
+                if (__lane_id() == leader) base = atomicAdd(&A.rec_alloc[0], (uint32_t)__popcll(m));
+                base = (uint32_t)__builtin_amdgcn_readlane((int)base, (int)leader);
+                const uint32_t r = base + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+                uint32_t aoff = r * (uint32_t)kActInline;
+                bool fits = r < A.rec_cap;
+                if (w > kActInline) {  // rare: long active lists go to the overflow pool
+                    const uint32_t o = atomicAdd(&A.rec_alloc[1], (uint32_t)w);
+                    aoff = A.rec_cap * (uint32_t)kActInline + o;
+                    fits = fits && o + (uint32_t)w <= A.act_ovf_cap;
+                }
+                if (fits) {
                     A.rec_pos[r] = make_float4(px_, py_, pz_, T * sigma_s);
-                    A.rec_meta[r] = make_uint4((uint32_t)px | ((uint32_t)py << 16), (uint32_t)k, abase + nact, (uint32_t)w);
+                    A.rec_meta[r] = make_uint4((uint32_t)px | ((uint32_t)py << 16), (uint32_t)k, aoff, (uint32_t)w);
                     uint64_t bl = 0;
                     for (int i = 0; i < w; ++i) {
                         const int j = act.get(i);
-                        A.rec_act[abase + nact + i] = j;
+                        A.rec_act[aoff + i] = j;
                         bl |= 1ull << (j & 63);
                     }
                     A.rec_bloom[r] = bl;
+                    A.rec_next[r] = kNoRecord;
+                    if (prev == kNoRecord) A.px_first[p] = r;
+                    else A.rec_next[prev] = r;
+                    prev = r;
+                } else {
+                    A.rec_alloc[2] = 1u;  // capacity exceeded: the host re-runs the march
                 }
-                nrec++;
-                nact += (uint32_t)w;
             }
             T *= expf(-tau_seg);
             if (T <= A.t_eps) break;
         }
     }
-    if constexpr (MODE == 0) {
-        A.px_cnt[p] = nrec;
-        A.px_acnt[p] = nact;
-    } else {
-        A.px_T[p] = T;
-        if constexpr (S) c.v[kCtrPixels]++;
-    }
+    A.px_T[p] = T;
+    if constexpr (S) c.v[kCtrPixels]++;
     return kOK;
 }
 
-__device__ __forceinline__ void mark_error(const RenderArgs& A, uint32_t p, int mode) {
+__device__ __forceinline__ void mark_error(const RenderArgs& A, uint32_t p) {
     atomicAdd(A.counters, 1u);
-    if (mode == 0) {
-        A.px_cnt[p] = 0;
-        A.px_acnt[p] = 0;
-    } else {
-        A.px_T[p] = __builtin_nanf("");
-    }
+    A.px_T[p] = __builtin_nanf("");
 }
 
-template <int ACT, int BLOCK, int MODE, bool S>
+template <int ACT, int BLOCK, bool S>
 __global__ __launch_bounds__(BLOCK) void march_kernel(RenderArgs A) {
     __shared__ int s_act[ACT * BLOCK];
     __shared__ int s_stack[kStackSize * BLOCK];
@@ -311,24 +313,22 @@ __global__ __launch_bounds__(BLOCK) void march_kernel(RenderArgs A) {
     Ctr c{};
     int st = kOK;
     if (x < (int)A.width && y < (int)A.height) {
-        st = march<ACT, MODE, S>(A, p, x, y, s_act + tid, s_stack + tid, BLOCK, c);
-    } else if constexpr (MODE == 0) {
-        A.px_cnt[p] = 0;
-        A.px_acnt[p] = 0;
+        st = march<ACT, S>(A, p, x, y, s_act + tid, s_stack + tid, BLOCK, c);
     } else {
+        A.px_first[p] = kNoRecord;
         A.px_T[p] = 0.0f;
     }
     if constexpr (S) flush_counters(A.work, c);
     if (st == kOverflow) {
         uint32_t slot = atomicAdd(A.queue, 1u);
         if (slot < A.queue_cap) A.queue[1 + slot] = p;
-        else mark_error(A, p, MODE);
+        else mark_error(A, p);
     } else if (st == kError) {
-        mark_error(A, p, MODE);
+        mark_error(A, p);
     }
 }
 
-template <int ACT, int BLOCK, int MODE, bool S>
+template <int ACT, int BLOCK, bool S>
 __global__ __launch_bounds__(BLOCK) void march_fallback_kernel(RenderArgs A) {
     __shared__ int s_act[ACT * BLOCK];
     __shared__ int s_stack[kStackSize * BLOCK];
@@ -339,18 +339,10 @@ __global__ __launch_bounds__(BLOCK) void march_fallback_kernel(RenderArgs A) {
         int lx, ly, x, y;
         tile_pixel(A, p >> 8, (int)(p & 255u), lx, ly, x, y);
         Ctr c{};
-        int st = march<ACT, MODE, S>(A, p, x, y, s_act + tid, s_stack + tid, BLOCK, c);
+        int st = march<ACT, S>(A, p, x, y, s_act + tid, s_stack + tid, BLOCK, c);  // re-links px_first
         if constexpr (S)
             for (int i = 0; i < kNumCtr; ++i) atomicAdd(A.work + i, (unsigned long long)c.v[i]);
-        if (st != kOK) mark_error(A, p, MODE);
-    }
-}
-
-__global__ void totals_kernel(const uint32_t* cnt, const uint32_t* off, const uint32_t* acnt, const uint32_t* aoff,
-                              uint32_t n, uint32_t* totals) {
-    if (threadIdx.x == 0 && blockIdx.x == 0) {
-        totals[0] = n ? off[n - 1] + cnt[n - 1] : 0u;
-        totals[1] = n ? aoff[n - 1] + acnt[n - 1] : 0u;
+        if (st != kOK) mark_error(A, p);
     }
 }
 
@@ -959,12 +951,10 @@ __global__ __launch_bounds__(256) void accumulate_kernel(RenderArgs A, uint32_t 
         store_px(A, tile_local, lx, ly, x, y, 0.0f, 0.0f, 0.0f);
         return;
     }
-    const uint32_t n = A.px_cnt[p], o = A.px_off[p];
     const float fs = (float)A.env_samples;
     const float step = A.step_size;
     float L0 = 0.0f, L1 = 0.0f, L2 = 0.0f;
-    for (uint32_t i = 0; i < n; ++i) {
-        const uint32_t r = o + i;
+    for (uint32_t r = A.px_first[p]; r != kNoRecord; r = A.rec_next[r]) {  // step order
         const float4 pos = A.rec_pos[r];
         float Li0 = 0.0f, Li1 = 0.0f, Li2 = 0.0f;
         for (int l = 0; l < A.num_lights; ++l) {
@@ -1005,37 +995,18 @@ constexpr int kActFast = 32, kBlockFast = 256;
 constexpr int kActFallback = 64, kBlockFallback = 64;
 constexpr int kBlockSecondary = 256;
 
-template <int MODE, bool S>
+template <bool S>
 static hipError_t march_pass(const RenderArgs& A, hipStream_t stream) {
-    hipLaunchKernelGGL((dev::march_kernel<kActFast, kBlockFast, MODE, S>), dim3(A.num_tiles), dim3(kBlockFast), 0, stream, A);
+    hipLaunchKernelGGL((dev::march_kernel<kActFast, kBlockFast, S>), dim3(A.num_tiles), dim3(kBlockFast), 0, stream, A);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL((dev::march_fallback_kernel<kActFallback, kBlockFallback, MODE, S>), dim3(1024), dim3(kBlockFallback),
-                       0, stream, A);
+    hipLaunchKernelGGL((dev::march_fallback_kernel<kActFallback, kBlockFallback, S>), dim3(1024), dim3(kBlockFallback), 0,
+                       stream, A);
     return hipGetLastError();
 }
 
-hipError_t gauss_march(const RenderArgs& A, hipStream_t stream, int mode, bool stats) {
-    if (mode == 0) return stats ? march_pass<0, true>(A, stream) : march_pass<0, false>(A, stream);
-    return stats ? march_pass<1, true>(A, stream) : march_pass<1, false>(A, stream);
-}
-
-// Exclusive scans of the per-pixel counts + totals. temp == nullptr queries temp_bytes.
-hipError_t gauss_scan(const RenderArgs& A, uint32_t npix, void* temp, size_t& temp_bytes, uint32_t* totals,
-                      hipStream_t stream) {
-    if (!temp) {
-        size_t b = 0;
-        hipError_t e = hipcub::DeviceScan::ExclusiveSum(nullptr, b, A.px_cnt, A.px_off, (int)npix, stream);
-        temp_bytes = b;
-        return e;
-    }
-    hipError_t e = hipcub::DeviceScan::ExclusiveSum(temp, temp_bytes, A.px_cnt, A.px_off, (int)npix, stream);
-    if (e != hipSuccess) return e;
-    e = hipcub::DeviceScan::ExclusiveSum(temp, temp_bytes, A.px_acnt, A.px_aoff, (int)npix, stream);
-    if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(dev::totals_kernel, dim3(1), dim3(64), 0, stream, A.px_cnt, A.px_off, A.px_acnt, A.px_aoff, npix,
-                       totals);
-    return hipGetLastError();
+hipError_t gauss_march(const RenderArgs& A, hipStream_t stream, bool stats) {
+    return stats ? march_pass<true>(A, stream) : march_pass<false>(A, stream);
 }
 
 template <bool S, bool FAST>
@@ -1052,15 +1023,6 @@ static hipError_t secondary_launch(const RenderArgs& A, uint32_t nrec, uint64_t 
         if (e != hipSuccess) return e;
         static const bool force_deep = getenv("VR_WW_STACK") && atoi(getenv("VR_WW_STACK")) == kStackSize;
         const bool shallow = A.bvh_depth <= kShallowStack + 1 && !force_deep;  // pushes <= depth - 1
-        if (A.list_ok) {
-            uint64_t lb = ((uint64_t)nrec + kBlockSecondary - 1) / kBlockSecondary;
-            if (lb > 65536ull * 4ull) lb = 65536ull * 4ull;
-            if (lb > 0)
-                hipLaunchKernelGGL((dev::record_list_kernel<kBlockSecondary>), dim3((unsigned)lb), dim3(kBlockSecondary), 0,
-                                   stream, A, nrec);
-            e = hipGetLastError();
-            if (e != hipSuccess) return e;
-        }
         const void* fn = shallow ? (const void*)dev::secondary_ww_kernel<kBlockSecondary, kShallowStack, S>
                                  : (const void*)dev::secondary_ww_kernel<kBlockSecondary, kStackSize, S>;
         int dv = 0, cus = 0, per_cu = 0;
@@ -1098,6 +1060,15 @@ static hipError_t secondary_launch(const RenderArgs& A, uint32_t nrec, uint64_t 
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL((dev::secondary_slow_kernel<64, S>), dim3(512), dim3(64), 0, stream, A, nrec);
+    return hipGetLastError();
+}
+
+hipError_t gauss_lists(const RenderArgs& A, uint32_t nrec, hipStream_t stream) {
+    if (!A.list_ok || nrec == 0) return hipSuccess;
+    uint64_t lb = ((uint64_t)nrec + kBlockSecondary - 1) / kBlockSecondary;
+    if (lb > 65536ull * 4ull) lb = 65536ull * 4ull;
+    hipLaunchKernelGGL((dev::record_list_kernel<kBlockSecondary>), dim3((unsigned)lb), dim3(kBlockSecondary), 0, stream, A,
+                       nrec);
     return hipGetLastError();
 }
 

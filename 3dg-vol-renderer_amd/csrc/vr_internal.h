@@ -59,6 +59,8 @@ struct LightRecord {
 };
 
 constexpr int kMaxLights = 16;
+constexpr uint32_t kNoRecord = 0xffffffffu;
+constexpr int kActInline = 4;  // active-list slots stored with each scatter record
 
 // Record neighbour lists (secondary rays): every Gaussian j whose scaled Mahalanobis distance at
 // the record position satisfies q_j(pos) <= kListR2 (pos inside its 3.08-sigma ellipsoid). The
@@ -101,17 +103,16 @@ struct RenderArgs {
     unsigned long long* work;  // instrumented build only: [0..7] march-kernel counters, [8..15] secondary-kernel counters
 
     // ---- wavefront buffers (RayMarchingGaussians), pixel-local index p = tile_local * 256 + lane ----
-    uint32_t* px_cnt;   // scatter records of pixel p (march steps with sigma_s > 0)
-    uint32_t* px_acnt;  // active-list entries over those records
-    uint32_t* px_off;   // exclusive scan of px_cnt
-    uint32_t* px_aoff;  // exclusive scan of px_acnt
+    uint32_t* px_first; // first scatter record of pixel p (kNoRecord: none); later ones via rec_next
     float* px_T;        // transmittance left after the march (multiplies env_color at the end)
     float4* rec_pos;    // per record: pos.xyz, T * sigma_s
     uint4* rec_meta;    // per record: x | y << 16, step index k, act offset, act count
-    int32_t* rec_act;   // active Gaussians (leaf-order ids) of each record, sorted
+    uint32_t* rec_next; // per record: the pixel's next record in step order (kNoRecord: last)
+    int32_t* rec_act;   // active Gaussians (leaf-order ids) of each record, sorted: kActInline slots per
+                        // record, longer lists in the overflow pool after rec_cap * kActInline
     float* tr;          // per secondary ray: transmittance, [sample][record]
-    const uint32_t* totals;  // device: [0] records, [1] act entries
-    uint32_t rec_cap, act_cap;
+    uint32_t* rec_alloc;  // [0] records allocated, [1] overflow-pool entries allocated, [2] capacity exceeded
+    uint32_t rec_cap, act_ovf_cap;
     unsigned long long* rec_bloom;  // per record: 64-bit membership mask of its active list
     uint32_t* slowq;                // light rays needing the exact stopping event: [0] count, [1..] ray ids
     uint32_t slowq_cap;

@@ -329,7 +329,7 @@ class Device:
                 "scatter_records": s.scatter_records, "secondary_rays": s.secondary_rays}
 
     # vr_render_stats.stage_ms (include/vr_hip.h)
-    STAGES = ("march_count", "scan", "march_write", "secondary", "accumulate")
+    STAGES = ("march", "sizing", "lists", "secondary", "accumulate")
 
     def synchronize(self):
         check(lib().vr_synchronize(self._h))

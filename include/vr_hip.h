@@ -111,8 +111,9 @@ typedef struct vr_render_stats {
     int64_t fallback_pixels;  /* pixels re-run on the large-capacity path (active-set overflow) */
     int64_t error_pixels;     /* pixels that exceeded every capacity (output NaN) */
     /* RayMarchingGaussians stages (HIP events on the render stream; 0 for the other integrators):
-     * [0] march (count pass), [1] scan + record allocation (includes one host sync),
-     * [2] march (write pass), [3] secondary-ray transmittance, [4] accumulate. */
+     * [0] primary march (scatter records), [1] record-buffer sizing (one host sync; a re-run of
+     * the march if the capacity carried over from the last frame was too small), [2] record
+     * neighbour lists, [3] secondary-ray transmittance, [4] accumulate. */
     double stage_ms[5];
     int64_t scatter_records;  /* march steps with sigma_s > 0 (each spawns lights + env_samples rays) */
     int64_t secondary_rays;   /* records * (lights + env_samples) */
