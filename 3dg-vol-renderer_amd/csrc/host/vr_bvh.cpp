@@ -13,6 +13,7 @@
 //   * primitives reordered so every leaf is a contiguous run of 48-B records.
 #include <algorithm>
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 #include <limits>
 
@@ -41,6 +42,13 @@ struct Box {
         float d0 = mx[0] - mn[0], d1 = mx[1] - mn[1], d2 = mx[2] - mn[2];
         if (!(d0 >= 0.0f) || !(d1 >= 0.0f) || !(d2 >= 0.0f)) return 0.0f;
         return 2.0f * (d0 * d1 + d0 * d2 + d1 * d2);
+    }
+    // Probability-of-visit metric: surface area (long rays) + vol_w * volume (rays that start
+    // inside the volume: a short ray of length l hits a box with probability ~ V + S l / 4).
+    float metric(float vol_w) const {
+        float d0 = mx[0] - mn[0], d1 = mx[1] - mn[1], d2 = mx[2] - mn[2];
+        if (!(d0 >= 0.0f) || !(d1 >= 0.0f) || !(d2 >= 0.0f)) return 0.0f;
+        return 2.0f * (d0 * d1 + d0 * d2 + d1 * d2) + vol_w * (d0 * d1 * d2);
     }
 };
 
@@ -80,18 +88,26 @@ BVHBuild build_bvh(const std::vector<float>& boxes) {
         work.push_back({0, 1});
     }
     uint32_t* ord = out.order.data();
-    constexpr int kBins = 16;
+    auto env_or = [](const char* name, double def) {
+        const char* v = getenv(name);
+        return v ? atof(v) : def;
+    };
+    static const int kBins = std::min(64, std::max(4, (int)env_or("VR_BVH_BINS", 16)));
+    static const float vol_w = (float)env_or("VR_BVH_VOL", 0.0);
+    static const uint32_t leaf_max = (uint32_t)std::min(kLeafMax, std::max(1, (int)env_or("VR_BVH_LEAF", kLeafMax)));
     // Depth budget: SAH may go kSlack levels deeper than a perfectly balanced tree, but never past
     // kMaxDepth. Shallow trees let the secondary-ray kernel use a 24-entry LDS stack (more waves per
     // CU); very large scenes fall back to the 32-entry stack.
     constexpr int kSlack = 6;
-    const int depth_cap = std::min(kMaxDepth, std::max(kShallowDepth, ceil_log2((N + kLeafMax - 1) / kLeafMax + 1) + kSlack));
+    static const int depth_env = getenv("VR_BVH_DEPTH") ? atoi(getenv("VR_BVH_DEPTH")) : 0;  // A/B override
+    const int depth_cap = depth_env > 0 ? std::min(kMaxDepth, depth_env)
+                                        : std::min(kMaxDepth, std::max(kShallowDepth, ceil_log2((N + kLeafMax - 1) / kLeafMax + 1) + kSlack));
     while (!work.empty()) {
         Work w = work.back();
         work.pop_back();
         const uint32_t first = t[w.node].first, count = t[w.node].count;
         out.max_depth = std::max(out.max_depth, w.depth);
-        if (count <= (uint32_t)kLeafMax) continue;
+        if (count <= leaf_max) continue;
         Box cb;
         for (uint32_t j = first; j < first + count; ++j) {
             const float* c = &cen[3 * ord[j]];
@@ -111,8 +127,8 @@ BVHBuild build_bvh(const std::vector<float>& boxes) {
             int best_axis = -1, best_split = -1;
             for (int a = 0; a < 3; ++a) {
                 if (!(ext[a] > 0.0f)) continue;
-                Box bb[kBins];
-                uint32_t bn[kBins] = {0};
+                Box bb[64];
+                uint32_t bn[64] = {0};
                 const float scale = kBins / ext[a];
                 for (uint32_t j = first; j < first + count; ++j) {
                     uint32_t p = ord[j];
@@ -121,14 +137,14 @@ BVHBuild build_bvh(const std::vector<float>& boxes) {
                     bb[b].grow(&boxes[6 * p]);
                     bn[b]++;
                 }
-                float ra[kBins];
-                uint32_t rn[kBins];
+                float ra[64];
+                uint32_t rn[64];
                 Box acc;
                 uint32_t n = 0;
                 for (int b = kBins - 1; b > 0; --b) {
                     acc.grow(bb[b]);
                     n += bn[b];
-                    ra[b] = acc.area();
+                    ra[b] = acc.metric(vol_w);
                     rn[b] = n;
                 }
                 Box lacc;
@@ -137,7 +153,7 @@ BVHBuild build_bvh(const std::vector<float>& boxes) {
                     lacc.grow(bb[b]);
                     ln += bn[b];
                     if (ln == 0 || rn[b + 1] == 0) continue;
-                    float c = lacc.area() * ln + ra[b + 1] * rn[b + 1];
+                    float c = lacc.metric(vol_w) * ln + ra[b + 1] * rn[b + 1];
                     if (c < best_cost) {
                         best_cost = c;
                         best_axis = a;

@@ -766,7 +766,7 @@ __device__ __forceinline__ void list_advance(SecRay& R, LeafQueue& Q, int& node)
 }
 
 template <int BLOCK, int STACK, bool S>
-__global__ __launch_bounds__(BLOCK, STACK == kShallowStack ? 6 : 5) void secondary_ww_kernel(RenderArgs A, uint32_t nrec,
+__global__ __launch_bounds__(BLOCK, STACK <= kShallowStack ? 6 : 5) void secondary_ww_kernel(RenderArgs A, uint32_t nrec,
                                                                                             uint64_t total, int refill_min,
                                                                                             int prim_bias) {
     __shared__ int s_stack[STACK * BLOCK];
@@ -1022,9 +1022,11 @@ static hipError_t secondary_launch(const RenderArgs& A, uint32_t nrec, uint64_t 
         hipError_t e = hipMemsetAsync(A.ray_next, 0, sizeof(unsigned long long), stream);
         if (e != hipSuccess) return e;
         static const bool force_deep = getenv("VR_WW_STACK") && atoi(getenv("VR_WW_STACK")) == kStackSize;
-        const bool shallow = A.bvh_depth <= kShallowStack + 1 && !force_deep;  // pushes <= depth - 1
-        const void* fn = shallow ? (const void*)dev::secondary_ww_kernel<kBlockSecondary, kShallowStack, S>
-                                 : (const void*)dev::secondary_ww_kernel<kBlockSecondary, kStackSize, S>;
+        // smallest LDS stack the tree fits (a child-pair traversal pushes at most depth - 1 entries):
+        // 24 entries -> 6 waves/SIMD, 32 -> 5 (a 20-entry / 8-wave variant spills and loses)
+        const int stack = (force_deep || A.bvh_depth > kShallowStack + 1) ? kStackSize : kShallowStack;
+        const void* fn = stack == kShallowStack ? (const void*)dev::secondary_ww_kernel<kBlockSecondary, kShallowStack, S>
+                                                : (const void*)dev::secondary_ww_kernel<kBlockSecondary, kStackSize, S>;
         int dv = 0, cus = 0, per_cu = 0;
         if (hipGetDevice(&dv) != hipSuccess) return hipErrorUnknown;
         if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dv) != hipSuccess) return hipErrorUnknown;
@@ -1033,7 +1035,7 @@ static hipError_t secondary_launch(const RenderArgs& A, uint32_t nrec, uint64_t 
         uint64_t grid = (uint64_t)cus * (uint64_t)per_cu;
         const uint64_t need = (total + kBlockSecondary - 1) / kBlockSecondary;
         if (grid > need) grid = need;
-        if (shallow)
+        if (stack == kShallowStack)
             hipLaunchKernelGGL((dev::secondary_ww_kernel<kBlockSecondary, kShallowStack, S>), dim3((unsigned)grid),
                                dim3(kBlockSecondary), 0, stream, A, nrec, total, rmin, prim_bias);
         else

@@ -343,3 +343,18 @@ def test_transmittance_early_out_error_bound(t_eps):
     ref = _oracle_gmm(path, W, H, pixels=pix)
     err, nm = _linf(img.pixels[pix[:, 1], pix[:, 0]], ref)
     assert nm == 0 and err < TOL, f"t_eps {t_eps}: L-inf {err:.3e}"
+
+
+@pytest.mark.parametrize("W,H,n,npix", [(1920, 1080, 100_000, 384), (4096, 4096, 1_000_000, 256)])
+def test_full_size_benchmark_settings_match_exact_oracle(W, H, n, npix):
+    """bench.py's settings (early-out t_eps = 1e-6 and the secondary optical-depth cut-off tied to
+    it) against the exact restatement, on the benchmark scenes themselves."""
+    scene, osc = _synthetic_scene(n)
+    img = vr.Image(W, H)
+    vr.RayMarchingGaussians(vr.Pinhole_Camera(CAM_POS, main_view_dir(), FOV), t_eps=1e-6).render(scene, img)
+    pix = _pixels(W, H, npix, seed=23)
+    ref = O.render(osc, O.PINHOLE, CAM_POS, main_view_dir(), FOV, W, H, O.RAYMARCH_GAUSSIANS_LISTS, 0.01, 20,
+                   pixels=pix)
+    err, nm = _linf(img.pixels[pix[:, 1], pix[:, 0]], ref)
+    print(f"{W}x{H}/{n} t_eps=1e-6: L-inf {err:.3e}")
+    assert nm == 0 and err < TOL, f"{W}x{H}/{n}: L-inf {err:.3e}"
