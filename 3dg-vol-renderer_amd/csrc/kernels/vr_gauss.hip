@@ -369,6 +369,7 @@ struct SecRay {
     bool light, needs_stop;
     uint32_t nsteps;  // instrumented build only: node steps taken by this ray
     uint32_t rec;     // record index
+    uint32_t slot;    // result slot s * nrec + rec in tr
     int lmode;        // neighbour-list phase: 1 central members, 2 other members, 0 done / none
     bool listed;      // the record has a neighbour list (tree leaves then skip its members)
     uint32_t lnb;     // number of "other" members (tested after the central ones)
@@ -409,9 +410,24 @@ __device__ __forceinline__ uint32_t dir_cell(float x, float y, float z) {
 }
 
 // Start ray t = s * nrec + r. Returns false if the ray is already complete (Tr written).
+// Ray ids are scheduled record-chunk-major: id t covers record r = 64 * chunk + (t mod 64) and
+// sample s (light, then environment), where chunk = t / (64 * NS) and s = (t mod 64 NS) / 64. The
+// 64 * NS rays of a chunk share 64 records' data (position, active list, neighbour list), so a
+// wave that takes consecutive ids reads each record from its cache instead of once per sample.
+// The result slot stays sample-major: tr[s * nrec + r].
+__device__ __forceinline__ bool ray_slot(uint32_t t, uint32_t nrec, uint32_t ns, uint32_t& s, uint32_t& r) {
+    const uint32_t per = 64u * ns;
+    const uint32_t chunk = t / per;
+    const uint32_t rem = t - chunk * per;
+    s = rem >> 6;
+    r = chunk * 64u + (rem & 63u);
+    return r < nrec;
+}
+
 __device__ __forceinline__ bool sec_init(const RenderArgs& A, uint32_t nrec, uint64_t t, SecRay& R) {
-    const uint32_t s = (uint32_t)(t / nrec);
-    const uint32_t r = (uint32_t)(t - (uint64_t)s * nrec);
+    uint32_t s, r;
+    if (!ray_slot((uint32_t)t, nrec, (uint32_t)(A.num_lights + A.env_samples), s, r)) return false;  // padding id
+    R.slot = s * nrec + r;
     const float4 pos = A.rec_pos[r];
     const uint4 meta = A.rec_meta[r];
     R.rec = r;
@@ -432,7 +448,7 @@ __device__ __forceinline__ bool sec_init(const RenderArgs& A, uint32_t nrec, uin
         R.light = true;
         R.lim = dist;
         if (!(dist > 0.0f)) {  // `while (t_prev < dist)` never runs
-            A.tr[t] = 1.0f;
+            A.tr[R.slot] = 1.0f;
             return false;
         }
     } else {
@@ -489,7 +505,7 @@ __device__ __forceinline__ void sec_finish(const RenderArgs& A, uint64_t t, SecR
         }
     }
     if (R.tau >= A.tau_cut) {
-        A.tr[t] = 0.0f;
+        A.tr[R.slot] = 0.0f;
         return;
     }
     const uint64_t all = R.act_n >= 64 ? ~0ull : ((1ull << R.act_n) - 1ull);
@@ -497,10 +513,10 @@ __device__ __forceinline__ void sec_finish(const RenderArgs& A, uint64_t t, SecR
     if (R.light) {
         if (R.needs_stop || missed) {
             uint32_t slot = atomicAdd(A.slowq, 1u);
-            if (slot < A.slowq_cap) A.slowq[1 + slot] = (uint32_t)t;
+            if (slot < A.slowq_cap) A.slowq[1 + slot] = R.slot;
             else {
                 atomicAdd(A.counters, 1u);
-                A.tr[t] = __builtin_nanf("");
+                A.tr[R.slot] = __builtin_nanf("");
             }
             return;
         }
@@ -514,7 +530,7 @@ __device__ __forceinline__ void sec_finish(const RenderArgs& A, uint64_t t, SecR
             R.tau += FAST ? optical_depth_fast(g, q, 0.0f, R.tlast) : optical_depth(g, q, 0.0f, R.tlast);
         }
     }
-    A.tr[t] = expf(-R.tau);
+    A.tr[R.slot] = expf(-R.tau);
 }
 
 // One BVH node pair of secondary ray R (plus the primitives of leaf children). Returns true when
@@ -785,20 +801,25 @@ __global__ __launch_bounds__(BLOCK, STACK <= kShallowStack ? 6 : 5) void seconda
         if (__popcll(idle) >= refill_min) {  // refill once enough lanes are idle (amortises sec_init)
             if (pool == pool_end && !counter_done) {
                 uint64_t base = 0;
-                if (lane == 0) base = atomicAdd(A.ray_next, 64ull);
+                // a whole record chunk (64 records x all their samples, see ray_slot) per fetch
+                const uint64_t fetch = 64ull * (uint64_t)(A.num_lights + A.env_samples);
+                if (lane == 0) base = atomicAdd(A.ray_next, fetch);
                 const uint32_t lo = __shfl((uint32_t)base, 0, 64), hi = __shfl((uint32_t)(base >> 32), 0, 64);
                 base = ((uint64_t)hi << 32) | lo;
                 pool = base < total ? base : total;
-                pool_end = base + 64 < total ? base + 64 : total;
-                counter_done = base + 64 >= total;
+                pool_end = base + fetch < total ? base + fetch : total;
+                counter_done = base + fetch >= total;
             }
             const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(idle >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)idle, 0u));
             if (!live && pool + rank < pool_end) {
                 t = pool + rank;
                 if constexpr (S) c.v[kCtrSecRays]++;
-                live = sec_init(A, nrec, t, R);  // false: complete already (Tr written)
+                live = sec_init(A, nrec, t, R);  // false: padding id, or complete already (Tr written)
                 sp = 0;
-                list_begin(A, R, Q, node);
+                node = -1;
+                Q.n = 0;
+                Q.j = Q.end = 0;
+                if (live) list_begin(A, R, Q, node);
             }
             const uint64_t handed = (uint64_t)__popcll(idle);
             pool = pool + handed < pool_end ? pool + handed : pool_end;
@@ -920,7 +941,7 @@ __global__ __launch_bounds__(BLOCK) void secondary_slow_kernel(RenderArgs A, uin
     const uint32_t n = min(A.slowq[0], A.slowq_cap);
     Ctr c{};
     for (uint32_t q = blockIdx.x * BLOCK + threadIdx.x; q < n; q += gridDim.x * BLOCK) {
-        const uint64_t t = A.slowq[1 + q];
+        const uint64_t t = A.slowq[1 + q];  // result slot s * nrec + r
         const uint32_t s = (uint32_t)(t / nrec);
         const uint32_t r = (uint32_t)(t - (uint64_t)s * nrec);
         const float4 pos = A.rec_pos[r];
@@ -1075,8 +1096,10 @@ hipError_t gauss_lists(const RenderArgs& A, uint32_t nrec, hipStream_t stream) {
 }
 
 hipError_t gauss_secondary(const RenderArgs& A, uint32_t nrec, hipStream_t stream, bool stats) {
-    const uint64_t total = (uint64_t)nrec * (uint64_t)(A.num_lights + A.env_samples);
+    // padded ray-id space of the record-chunk schedule (see ray_slot)
+    const uint64_t total = ((uint64_t)nrec + 63u) / 64u * 64u * (uint64_t)(A.num_lights + A.env_samples);
     if (total == 0) return hipSuccess;
+    if (total >= 0xffffffffull) return hipErrorInvalidValue;
     // A/B switches (read once): VR_SECONDARY=s one ray per thread, =p refill-only persistent kernel; VR_SEC_EXACT=1 correctly rounded
     // secondary-ray arithmetic (the fast form is the default).
     static const int variant = [] {  // 2: while-while persistent (default), 0: one ray per thread, 1: old persistent
@@ -1087,8 +1110,12 @@ hipError_t gauss_secondary(const RenderArgs& A, uint32_t nrec, hipStream_t strea
         const char* v = getenv("VR_SEC_EXACT");
         return v && v[0] == '1';
     }();
-    if (stats) return exact ? secondary_launch<true, false>(A, nrec, total, stream, variant)
-                            : secondary_launch<true, true>(A, nrec, total, stream, variant);
+    // The instrumented (work-counting) run uses the one-ray-per-thread kernel: its counts are the
+    // canonical, non-speculative work of a near-first BVH traversal per secondary ray, which is
+    // what the roofline's algorithmic flops are defined on (the persistent kernel's postponed
+    // leaves make it do a little more, speculatively).
+    if (stats) return exact ? secondary_launch<true, false>(A, nrec, total, stream, 0)
+                            : secondary_launch<true, true>(A, nrec, total, stream, 0);
     return exact ? secondary_launch<false, false>(A, nrec, total, stream, variant)
                  : secondary_launch<false, true>(A, nrec, total, stream, variant);
 }
