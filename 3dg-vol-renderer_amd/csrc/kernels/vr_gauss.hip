@@ -301,10 +301,10 @@ __device__ __forceinline__ void mark_error(const RenderArgs& A, uint32_t p) {
     A.px_T[p] = __builtin_nanf("");
 }
 
-template <int ACT, int BLOCK, bool S>
+template <int ACT, int BLOCK, bool S, int STACK = kStackSize>
 __global__ __launch_bounds__(BLOCK) void march_kernel(RenderArgs A) {
     __shared__ int s_act[ACT * BLOCK];
-    __shared__ int s_stack[kStackSize * BLOCK];
+    __shared__ int s_stack[STACK * BLOCK];
     const int tid = threadIdx.x;
     const uint32_t tile_local = xcd_tile(blockIdx.x, gridDim.x);
     const uint32_t p = tile_local * 256u + (uint32_t)tid;
@@ -781,8 +781,10 @@ __device__ __forceinline__ void list_advance(SecRay& R, LeafQueue& Q, int& node)
     }
 }
 
-template <int BLOCK, int STACK, bool S>
-__global__ __launch_bounds__(BLOCK, STACK <= kShallowStack ? 6 : 5) void secondary_ww_kernel(RenderArgs A, uint32_t nrec,
+// 5 waves/SIMD: the register allocation this kernel needs without spilling (a 6-wave build
+// spills ~6 VGPRs to scratch and measured 9 % slower on C4).
+template <int BLOCK, int STACK, bool S, int WAVES = 5>
+__global__ __launch_bounds__(BLOCK, WAVES) void secondary_ww_kernel(RenderArgs A, uint32_t nrec,
                                                                                             uint64_t total, int refill_min,
                                                                                             int prim_bias) {
     __shared__ int s_stack[STACK * BLOCK];
@@ -1012,13 +1014,23 @@ __global__ __launch_bounds__(256) void accumulate_kernel(RenderArgs A, uint32_t 
 // ---------------------------------------------------------------------------------------------
 // Host launchers
 // ---------------------------------------------------------------------------------------------
-constexpr int kActFast = 32, kBlockFast = 256;
+constexpr int kActFast = 16, kBlockFast = 256;
 constexpr int kActFallback = 64, kBlockFallback = 64;
 constexpr int kBlockSecondary = 256;
 
 template <bool S>
 static hipError_t march_pass(const RenderArgs& A, hipStream_t stream) {
-    hipLaunchKernelGGL((dev::march_kernel<kActFast, kBlockFast, S>), dim3(A.num_tiles), dim3(kBlockFast), 0, stream, A);
+    // LDS per 256-lane workgroup = (active-list slots + stack entries) * 1 KiB. Shallow trees use a
+    // 24-entry stack; the 16-slot active list overflows to the 64-slot fallback kernel.
+    static const int act_env = getenv("VR_MARCH_ACT") ? atoi(getenv("VR_MARCH_ACT")) : 16;  // A/B
+    const bool shallow = A.bvh_depth <= kShallowStack + 1;
+    if (act_env == 32)
+        hipLaunchKernelGGL((dev::march_kernel<32, kBlockFast, S>), dim3(A.num_tiles), dim3(kBlockFast), 0, stream, A);
+    else if (shallow)
+        hipLaunchKernelGGL((dev::march_kernel<kActFast, kBlockFast, S, kShallowStack>), dim3(A.num_tiles),
+                           dim3(kBlockFast), 0, stream, A);
+    else
+        hipLaunchKernelGGL((dev::march_kernel<kActFast, kBlockFast, S>), dim3(A.num_tiles), dim3(kBlockFast), 0, stream, A);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL((dev::march_fallback_kernel<kActFallback, kBlockFallback, S>), dim3(1024), dim3(kBlockFallback), 0,
