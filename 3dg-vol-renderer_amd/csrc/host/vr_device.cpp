@@ -111,6 +111,11 @@ float scene_tmax(const vr_ctx* c, const vr_camera* cam) {
                         best = std::max(best, (float)std::sqrt(d));
                     }
         }
+    // secondary rays start inside the scene box: a Gaussian interval on them ends within one
+    // box diagonal (PureRayMarching marches them over the same step table)
+    double diag = 0.0;
+    for (int k = 0; k < 3; ++k) diag += (double)(c->bmax[k] - c->bmin[k]) * (c->bmax[k] - c->bmin[k]);
+    best = std::max(best, (float)std::sqrt(diag));
     return best * 1.01f + 1.0f;
 }
 
@@ -155,11 +160,12 @@ vr_status fill_args(vr_ctx* c, const vr_camera* cam, const vr_render_params* p, 
     if (W == 0 || H == 0 || W > 65535 || H > 65535) return fail(VR_ERR_INVALID, "width/height must be in [1, 65535]");
     if (cam->type != VR_CAMERA_PINHOLE && cam->type != VR_CAMERA_ORTHOGRAPHIC) return fail(VR_ERR_INVALID, "unknown camera type");
     if (p->flags != 0) return fail(VR_ERR_INVALID, "vr_render_params.flags must be 0");
-    if (p->integrator == VR_RAYMARCH_GAUSSIANS && c->type != VR_VOLUME_GAUSSIANS)
+    if ((p->integrator == VR_RAYMARCH_GAUSSIANS || p->integrator == VR_PURE_RAYMARCH) && c->type != VR_VOLUME_GAUSSIANS)
         return fail(VR_ERR_INVALID, "RayMarchingGaussians needs a Gaussian scene");
     if (p->integrator == VR_RAYMARCH_SPHERES && c->type != VR_VOLUME_SPHERES)
         return fail(VR_ERR_INVALID, "RayMarchingSpheres needs a sphere scene");
-    if (p->integrator != VR_RAYMARCH_GAUSSIANS && p->integrator != VR_RAYMARCH_SPHERES && p->integrator != VR_TEST_HITMASK)
+    if (p->integrator != VR_RAYMARCH_GAUSSIANS && p->integrator != VR_RAYMARCH_SPHERES && p->integrator != VR_TEST_HITMASK &&
+        p->integrator != VR_PURE_RAYMARCH)
         return fail(VR_ERR_UNSUPPORTED, "integrator has no device implementation");
     if (p->integrator != VR_TEST_HITMASK && p->env_samples < 0) return fail(VR_ERR_INVALID, "env_samples must be >= 0");
     if (!(p->t_eps >= 0.0f) || p->t_eps >= 1.0f) return fail(VR_ERR_INVALID, "t_eps must be in [0, 1)");
@@ -186,6 +192,7 @@ vr_status fill_args(vr_ctx* c, const vr_camera* cam, const vr_render_params* p, 
     A.step_size = p->step_size;
     A.env_samples = p->env_samples;
     A.t_eps = p->t_eps;
+    A.pure = p->integrator == VR_PURE_RAYMARCH ? 1 : 0;
     // Secondary-ray optical-depth cut-off. Exact mode (t_eps = 0): 104, where expf(-tau) is already
     // 0 in f32, so stopping is bit-neutral. With an early-out budget t_eps > 0 the cut-off is
     // ln(1/t_eps) + ln(1000): a dropped transmittance is <= 1e-3 * t_eps, a thousandth of the error
@@ -325,7 +332,7 @@ vr_status launch(vr_ctx* c, RenderArgs& A, const vr_render_params* p, hipStream_
     c->staged = false;
     c->last_records = 0;
     c->last_secondary = 0;
-    if (c->type == VR_VOLUME_GAUSSIANS && p->integrator == VR_RAYMARCH_GAUSSIANS) {
+    if (c->type == VR_VOLUME_GAUSSIANS && (p->integrator == VR_RAYMARCH_GAUSSIANS || p->integrator == VR_PURE_RAYMARCH)) {
         st = gauss_pipeline(c, A, s, stats);
         if (st != VR_OK) return st;
     } else {
@@ -528,7 +535,8 @@ vr_status vr_count_work(vr_ctx* c, const vr_camera* cam, const vr_render_params*
     RenderArgs A;
     vr_status st = fill_args(c, cam, p, W, H, A);
     if (st != VR_OK) return st;
-    if (p->integrator != VR_RAYMARCH_GAUSSIANS) return fail(VR_ERR_UNSUPPORTED, "vr_count_work: RayMarchingGaussians only");
+    if (p->integrator != VR_RAYMARCH_GAUSSIANS && p->integrator != VR_PURE_RAYMARCH)
+        return fail(VR_ERR_UNSUPPORTED, "vr_count_work: Gaussian ray-march integrators only");
     uint32_t total = vr_num_tiles(W, H);
     if (tile_stride == 0 || num_tiles == 0 || (uint64_t)first_tile + (uint64_t)(num_tiles - 1) * tile_stride >= total)
         return fail(VR_ERR_INVALID, "vr_count_work: bad tile range");

@@ -239,7 +239,7 @@ __device__ int march(const RenderArgs& A, uint32_t p, int px, int py, int* act_b
                 float m = mu_t(g, px_, py_, pz_);
                 smu += m;
                 smua += m * g.albedo;
-                tau_seg += optical_depth(g, q, t_k, t_k1);
+                if (!A.pure) tau_seg += optical_depth(g, q, t_k, t_k1);
                 if constexpr (S) {
                     c.v[kCtrMu]++;
                     c.v[kCtrOD]++;
@@ -287,7 +287,17 @@ __device__ int march(const RenderArgs& A, uint32_t p, int px, int py, int* act_b
                     A.rec_alloc[2] = 1u;  // capacity exceeded: the host re-runs the march
                 }
             }
-            T *= expf(-tau_seg);
+            if (A.pure) {  // integrator.h:196-198, 259: T *= exp(-sigma_t * step), sigma_t = sigma_a + sigma_s
+                float sa = 0.0f, ss = 0.0f;
+                if (smu > 0.0f) {
+                    const float a_mix = smua / smu;
+                    ss = a_mix * smu;
+                    sa = (1.0f - a_mix) * smu;
+                }
+                T *= expf(-(sa + ss) * step);
+            } else {
+                T *= expf(-tau_seg);
+            }
             if (T <= A.t_eps) break;
         }
     }
@@ -468,6 +478,45 @@ __device__ __forceinline__ bool sec_init(const RenderArgs& A, uint32_t nrec, uin
     return true;
 }
 
+// PureRayMarching (integrator.h:105-135): the marched transmittance multiplies exp(-sigma_t dt)
+// over the iterated steps t_k = 0, dt, 2dt, ... of the secondary ray; grouped per Gaussian that is
+// dt * sum of its mu_t at the steps t_k in [lo, hi) where it is active.
+__device__ __forceinline__ float marched_depth(const RenderArgs& A, const GRec& g, const Ray& r, float lo, float hi) {
+    const float* __restrict__ ts = A.tsteps;
+    float s = 0.0f;
+    for (int k = kfirst(ts, A.num_tsteps, A.step_size, lo); k < A.num_tsteps; ++k) {
+        const float t = ts[k];
+        if (!(t < hi)) break;
+        s += mu_t(g, r.ox + t * r.dx, r.oy + t * r.dy, r.oz + t * r.dz);
+    }
+    return s * A.step_size;
+}
+
+// Adds Gaussian g (active on the secondary ray over [lo, b)) to the ray's optical depth.
+//   RayMarchingGaussians: analytic segment depth; a light ray's Gaussian straddling the light
+//   needs the first event past the light (test_integrators.h:220-235) -> exact slow path.
+//   PureRayMarching: marched to t < dist (light) / t < last event (environment, b <= tlast).
+template <bool S, bool FAST>
+__device__ __forceinline__ void sec_add(const RenderArgs& A, SecRay& R, const GRec& g, const Quad& q, float lo, float b,
+                                        Ctr& c) {
+    if constexpr (S) c.v[kCtrOD]++;
+    if (A.pure) {
+        if (!R.light) {
+            R.tau += marched_depth(A, g, R.ray, lo, b);
+            R.tlast = fmaxf(R.tlast, b);
+        } else if (lo < R.lim) {
+            R.tau += marched_depth(A, g, R.ray, lo, fminf(b, R.lim));
+        }
+        return;
+    }
+    if (!R.light || b < R.lim) {
+        R.tau += FAST ? optical_depth_fast(g, q, lo, b) : optical_depth(g, q, lo, b);
+        R.tlast = fmaxf(R.tlast, b);
+    } else if (lo < R.lim) {
+        R.needs_stop = true;
+    }
+}
+
 template <bool S, bool FAST>
 __device__ __forceinline__ void sec_leaf(const RenderArgs& A, SecRay& R, int32_t ref, Ctr& c) {
     const uint32_t first = leaf_first(ref), count = leaf_count(ref);
@@ -483,13 +532,7 @@ __device__ __forceinline__ void sec_leaf(const RenderArgs& A, SecRay& R, int32_t
             lo = 0.0f;
             R.hitmask |= 1ull << slot;
         }
-        if (!R.light || b < R.lim) {
-            if constexpr (S) c.v[kCtrOD]++;
-            R.tau += FAST ? optical_depth_fast(g, q, lo, b) : optical_depth(g, q, lo, b);
-            R.tlast = fmaxf(R.tlast, b);
-        } else if (lo < R.lim) {
-            R.needs_stop = true;
-        }
+        sec_add<S, FAST>(A, R, g, q, lo, b, c);
     }
 }
 
@@ -510,7 +553,14 @@ __device__ __forceinline__ void sec_finish(const RenderArgs& A, uint64_t t, SecR
     }
     const uint64_t all = R.act_n >= 64 ? ~0ull : ((1ull << R.act_n) - 1ull);
     uint64_t missed = all & ~R.hitmask;
-    if (R.light) {
+    if (A.pure) {  // pre-activated, missed through rounding: active to the end of the march
+        while (missed) {
+            int s = __ffsll((unsigned long long)missed) - 1;
+            missed &= missed - 1;
+            GRec g = load_rec(A.gauss, A.rec_act[R.act_off + s]);
+            R.tau += marched_depth(A, g, R.ray, 0.0f, R.light ? R.lim : R.tlast);
+        }
+    } else if (R.light) {
         if (R.needs_stop || missed) {
             uint32_t slot = atomicAdd(A.slowq, 1u);
             if (slot < A.slowq_cap) A.slowq[1 + slot] = R.slot;
@@ -850,13 +900,7 @@ __global__ __launch_bounds__(BLOCK, WAVES) void secondary_ww_kernel(RenderArgs A
                         lo = 0.0f;
                         R.hitmask |= 1ull << slot;
                     }
-                    if (!R.light || b < R.lim) {
-                        if constexpr (S) c.v[kCtrOD]++;
-                        R.tau += optical_depth_fast(g, q, lo, b);
-                        R.tlast = fmaxf(R.tlast, b);
-                    } else if (lo < R.lim) {
-                        R.needs_stop = true;
-                    }
+                    sec_add<S, true>(A, R, g, q, lo, b, c);
                 }
                 list_advance(R, Q, node);
             }

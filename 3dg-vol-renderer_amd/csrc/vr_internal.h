@@ -93,7 +93,8 @@ struct RenderArgs {
     float step_size;
     int32_t env_samples;
     float t_eps;
-    float tau_cut;        // secondary rays: Tr := 0 once the optical depth reaches this (see vr_device.cpp)
+    float tau_cut;
+    int32_t pure;         // PureRayMarching: marched (point-sampled) transmittance, integrator.h:100-267        // secondary rays: Tr := 0 once the optical depth reaches this (see vr_device.cpp)
     const float* tsteps;  // iterated float step sequence t_k (test_integrators.h:184,289)
     int32_t num_tsteps;
     // fallback queue (active-set overflow) and error counters

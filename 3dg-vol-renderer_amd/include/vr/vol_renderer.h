@@ -414,6 +414,13 @@ public:
         : HipIntegrator(camera, VR_RAYMARCH_GAUSSIANS, step_size, env_samples, dev) {}
 };
 
+// integrator.h:100-142 — PureRayMarching(camera, step_size = 0.01, env_samples = 20)
+class PureRayMarching : public HipIntegrator {
+public:
+    PureRayMarching(const std::shared_ptr<Camera>& camera, float step_size = 0.01f, int env_samples = 20, int dev = 0)
+        : HipIntegrator(camera, VR_PURE_RAYMARCH, step_size, env_samples, dev) {}
+};
+
 // test_integrators.h:11-21 — RayMarchingSpheres(camera, step_size = 0.01, env_samples = 5)
 class RayMarchingSpheres : public HipIntegrator {
 public:

@@ -21,7 +21,8 @@ from ._lib import VRError, check, fptr, lib
 
 __all__ = [
     "VRError", "Light", "Scene", "Camera", "Pinhole_Camera", "Orthographic_Camera", "Ray", "Image",
-    "Integrator", "RayMarchingGaussians", "RayMarchingSpheres", "TestIntegrator", "Device", "load_xml",
+    "Integrator", "RayMarchingGaussians", "PureRayMarching", "RayMarchingSpheres", "TestIntegrator", "Device",
+    "load_xml",
     "num_tiles",
 ]
 
@@ -410,6 +411,16 @@ class RayMarchingGaussians(Integrator):
     """test_integrators.h:143-297: RayMarchingGaussians(camera, step_size=0.01, env_samples=20)."""
 
     integrator_id = L.VR_RAYMARCH_GAUSSIANS
+
+    def __init__(self, camera, step_size=0.01, env_samples=20, t_eps=0.0, device=0):
+        super().__init__(camera, step_size, env_samples, t_eps, device)
+
+
+class PureRayMarching(Integrator):
+    """integrator.h:100-267: PureRayMarching(camera, step_size=0.01, env_samples=20) — primary and
+    shadow/environment transmittance marched at step_size (T *= exp(-sigma_t dt))."""
+
+    integrator_id = L.VR_PURE_RAYMARCH
 
     def __init__(self, camera, step_size=0.01, env_samples=20, t_eps=0.0, device=0):
         super().__init__(camera, step_size, env_samples, t_eps, device)

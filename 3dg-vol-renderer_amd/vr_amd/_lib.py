@@ -16,7 +16,7 @@ STATUS_NAMES = {
 }
 VR_VOLUME_GAUSSIANS, VR_VOLUME_SPHERES = 0, 1
 VR_CAMERA_PINHOLE, VR_CAMERA_ORTHOGRAPHIC = 0, 1
-VR_RAYMARCH_GAUSSIANS, VR_RAYMARCH_SPHERES, VR_TEST_HITMASK = 0, 1, 2
+VR_RAYMARCH_GAUSSIANS, VR_RAYMARCH_SPHERES, VR_TEST_HITMASK, VR_PURE_RAYMARCH = 0, 1, 2, 3
 
 f3 = ctypes.c_float * 3
 

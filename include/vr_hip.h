@@ -46,7 +46,8 @@ typedef enum vr_camera_type { VR_CAMERA_PINHOLE = 0, VR_CAMERA_ORTHOGRAPHIC = 1 
 typedef enum vr_integrator {
     VR_RAYMARCH_GAUSSIANS = 0, /* RayMarchingGaussians  test_integrators.h:143-297 */
     VR_RAYMARCH_SPHERES = 1,   /* RayMarchingSpheres    test_integrators.h:11-136  */
-    VR_TEST_HITMASK = 2        /* TestIntegrator        integrator.h:65-94         */
+    VR_TEST_HITMASK = 2,       /* TestIntegrator        integrator.h:65-94         */
+    VR_PURE_RAYMARCH = 3       /* PureRayMarching       integrator.h:100-267       */
 } vr_integrator;
 
 /* Light (scene.h:12-15). */

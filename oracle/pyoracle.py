@@ -17,6 +17,7 @@ _lib = None
 RAYMARCH_GAUSSIANS = 0
 RAYMARCH_SPHERES = 1
 RAYMARCH_GAUSSIANS_LISTS = 2  # same algorithm, sparse active sets + stop at T == 0 (bit-identical)
+PURE_RAYMARCH = 3  # PureRayMarching (integrator.h:100-267): marched primary and shadow transmittance
 PINHOLE = 0
 ORTHO = 1
 

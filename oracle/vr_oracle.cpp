@@ -665,6 +665,96 @@ static V3 rm_gaussians_pixel(const Scene& scene, const Camera& cam, int x, int y
     return L;
 }
 
+// integrator.h:105-135 — PureRayMarching::march_transmittance: marched transmittance on [0, t_max).
+static float march_transmittance(const Scene& scene, const Ray& ray, float t_max, const std::vector<PrimitiveHitEvent>& events,
+                                 const std::vector<bool>& active0, float step_size) {
+    const GMM& gmm = scene.gmm;
+    std::vector<bool> active = active0;
+    float T = 1.0f;
+    size_t evt_idx = 0, n_evt = events.size();
+    for (float t = 0.0f; t < t_max; t += step_size) {
+        while (evt_idx < n_evt && events[evt_idx].t <= t) {
+            active[events[evt_idx].index] = events[evt_idx].entering;
+            ++evt_idx;
+        }
+        V3 pos = ray.origin + t * ray.direction;
+        float sigma_a, sigma_s;
+        gmm.evaluate_sigma(active, pos, sigma_a, sigma_s);
+        float sigma_t = sigma_a + sigma_s;
+        T *= std::exp(-sigma_t * step_size);
+    }
+    return T;
+}
+
+// integrator.h:150-265 — PureRayMarching::render per pixel (environment directions from the same
+// deterministic PCG32 sampler as rm_gaussians_pixel, keyed by the step index).
+static V3 rm_pure_pixel(const Scene& scene, const Camera& cam, int x, int y, int W, int H, float step_size,
+                        int env_samples) {
+    const GMM& gmm = scene.gmm;
+    float u = (x + 0.5f) / W, v = (y + 0.5f) / H;
+    Ray ray = cam.sample_ray(u, v);
+    std::vector<PrimitiveHitEvent> primary_events;
+    gmm.intersect_events(ray, primary_events);
+    if (primary_events.empty()) return scene.env_color;
+    float t_end = primary_events.back().t;
+    std::vector<bool> primary_active(gmm.gaussians.size(), false);
+    for (auto& e : primary_events)
+        if (e.t == 0.0f && e.entering) primary_active[e.index] = true;
+    float T = 1.0f;
+    V3 L{0, 0, 0};
+    size_t idx_evt = 0, n_evt = primary_events.size();
+    int k = 0;
+    for (float t = 0.0f; t < t_end; t += step_size, ++k) {
+        while (idx_evt < n_evt && primary_events[idx_evt].t <= t) {
+            primary_active[primary_events[idx_evt].index] = primary_events[idx_evt].entering;
+            ++idx_evt;
+        }
+        V3 pos = ray.origin + t * ray.direction;
+        float sigma_a, sigma_s;
+        gmm.evaluate_sigma(primary_active, pos, sigma_a, sigma_s);
+        float sigma_t = sigma_a + sigma_s;
+        if (sigma_s > 0.0f) {
+            V3 Li{0, 0, 0};
+            for (const auto& light : scene.lights) {
+                V3 wi = normalized(light.position - pos);
+                float dist = norm(light.position - pos);
+                Ray shadow_ray(pos, wi);
+                std::vector<PrimitiveHitEvent> shadow_events;
+                gmm.intersect_events(shadow_ray, shadow_events);
+                std::vector<bool> shadow_active = primary_active;
+                for (size_t i = 0; i < shadow_active.size(); ++i)
+                    if (primary_active[i]) shadow_events.insert(shadow_events.begin(), {0.0f, true, i});
+                float Tr = march_transmittance(scene, shadow_ray, dist, shadow_events, shadow_active, step_size);
+                float d2 = dist * dist;
+                Li = Li + V3{(Tr * light.intensity.x) / d2, (Tr * light.intensity.y) / d2, (Tr * light.intensity.z) / d2};
+            }
+            V3 Le{0, 0, 0};
+            PCG32 rng(derive_path_seed(x, y, k), 1);
+            for (int s = 0; s < env_samples; ++s) {
+                float xi1 = rng.uniform();
+                float xi2 = rng.uniform();
+                Ray env_ray(pos, env_dir(xi1, xi2));
+                std::vector<PrimitiveHitEvent> env_events;
+                gmm.intersect_events(env_ray, env_events);
+                std::vector<bool> env_active = primary_active;
+                for (size_t i = 0; i < env_active.size(); ++i)
+                    if (primary_active[i]) env_events.insert(env_events.begin(), {0.0f, true, i});
+                float t_env_end = env_events.empty() ? 0.0f : env_events.back().t;
+                float Tr_env = march_transmittance(scene, env_ray, t_env_end, env_events, env_active, step_size);
+                Le = Le + Tr_env * scene.env_color;
+            }
+            float fs = float(env_samples);
+            Le = V3{(Le.x / fs) * k4Pi, (Le.y / fs) * k4Pi, (Le.z / fs) * k4Pi};
+            float Ts = T * sigma_s;
+            V3 S = Li + Le;
+            L = L + V3{((Ts * S.x) * step_size) * kInv4Pi, ((Ts * S.y) * step_size) * kInv4Pi, ((Ts * S.z) * step_size) * kInv4Pi};
+        }
+        T *= std::exp(-sigma_t * step_size);
+    }
+    L = L + T * scene.env_color;
+    return L;
+}
+
 // ---------------------------------------------------------------------------------------------
 // Same per-pixel algorithm as rm_gaussians_pixel, for the CPU *baseline* of bench.py only.
 // Two changes, both bit-neutral (tests/test_oracle_golden.py checks bitwise equality with the
@@ -1067,7 +1157,7 @@ void orc_env_dir(float xi1, float xi2, float* out) {
 }
 
 // integrator: 0 RayMarchingGaussians, 1 RayMarchingSpheres, 2 RayMarchingGaussians with sorted
-// active lists + stop at T == 0 (bit-identical to 0; bench.py's CPU baseline).
+// active lists + stop at T == 0 (bit-identical to 0; bench.py's CPU baseline), 3 PureRayMarching.
 // If pix != nullptr, render only the npix pixels pix[2k]=x, pix[2k+1]=y into out[3*npix];
 // otherwise the whole W*H frame into out[3*W*H] (row-major, image.h:13-17).
 int orc_render(void* sp, int cam_type, const float* pos, const float* vd, float fov, int integrator,
@@ -1077,7 +1167,7 @@ int orc_render(void* sp, int cam_type, const float* pos, const float* vd, float 
         Scene* s = (Scene*)sp;
         Camera c = cam_type == 0 ? Camera::make_pinhole({pos[0], pos[1], pos[2]}, {vd[0], vd[1], vd[2]}, fov)
                                  : Camera::make_ortho({pos[0], pos[1], pos[2]}, {vd[0], vd[1], vd[2]});
-        if (integrator < 0 || integrator > 2) { g_err = "unknown integrator"; return 1; }
+        if (integrator < 0 || integrator > 3) { g_err = "unknown integrator"; return 1; }
         if ((integrator != 1) != (s->volume_type == 0)) { g_err = "integrator/scene type mismatch"; return 1; }
         int64_t total = pix ? npix : (int64_t)W * H;
         if (nthreads > 0) omp_set_num_threads(nthreads);
@@ -1087,6 +1177,7 @@ int orc_render(void* sp, int cam_type, const float* pos, const float* vd, float 
             int y = pix ? pix[2 * q + 1] : (int)(q / W);
             V3 L = integrator == 0   ? rm_gaussians_pixel(*s, c, x, y, W, H, step_size, env_samples)
                    : integrator == 2 ? rm_gaussians_pixel_lists(*s, c, x, y, W, H, step_size, env_samples)
+                   : integrator == 3 ? rm_pure_pixel(*s, c, x, y, W, H, step_size, env_samples)
                                      : rm_spheres_pixel(*s, c, x, y, W, H, step_size, env_samples);
             out[3 * q] = L.x; out[3 * q + 1] = L.y; out[3 * q + 2] = L.z;
         }

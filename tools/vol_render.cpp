@@ -2,7 +2,7 @@
 // tests/main.cpp, which hard-codes scene, camera and integrator; here they are arguments).
 //
 //   vol_render --scene scenes/many_gaussians.txt [--spheres] [--xml] [--size 512x512]
-//              [--integrator gaussians|spheres|test] [--step 0.01] [--env 20]
+//              [--integrator gaussians|pure|spheres|test] [--step 0.01] [--env 20]
 //              [--camera pinhole|ortho] [--pos 0,1,6] [--lookat 0,1,0] [--fov 0.785398]
 //              [--out output.ppm] [--dump-rays N]
 //
@@ -88,6 +88,7 @@ int main(int argc, char** argv) try {
     std::unique_ptr<HipIntegrator> integrator;
     if (integ == "gaussians") integrator = std::make_unique<RayMarchingGaussians>(camera, step, env < 0 ? 20 : env);
     else if (integ == "spheres") integrator = std::make_unique<RayMarchingSpheres>(camera, step, env < 0 ? 5 : env);
+    else if (integ == "pure") integrator = std::make_unique<PureRayMarching>(camera, step, env < 0 ? 20 : env);
     else if (integ == "test") integrator = std::make_unique<TestIntegrator>(camera);
     else throw std::runtime_error("unknown integrator " + integ);
 
