@@ -496,11 +496,11 @@ __device__ __forceinline__ float marched_depth(const RenderArgs& A, const GRec& 
 //   RayMarchingGaussians: analytic segment depth; a light ray's Gaussian straddling the light
 //   needs the first event past the light (test_integrators.h:220-235) -> exact slow path.
 //   PureRayMarching: marched to t < dist (light) / t < last event (environment, b <= tlast).
-template <bool S, bool FAST>
+template <bool S, bool FAST, bool PURE>
 __device__ __forceinline__ void sec_add(const RenderArgs& A, SecRay& R, const GRec& g, const Quad& q, float lo, float b,
                                         Ctr& c) {
     if constexpr (S) c.v[kCtrOD]++;
-    if (A.pure) {
+    if constexpr (PURE) {
         if (!R.light) {
             R.tau += marched_depth(A, g, R.ray, lo, b);
             R.tlast = fmaxf(R.tlast, b);
@@ -517,7 +517,7 @@ __device__ __forceinline__ void sec_add(const RenderArgs& A, SecRay& R, const GR
     }
 }
 
-template <bool S, bool FAST>
+template <bool S, bool FAST, bool PURE>
 __device__ __forceinline__ void sec_leaf(const RenderArgs& A, SecRay& R, int32_t ref, Ctr& c) {
     const uint32_t first = leaf_first(ref), count = leaf_count(ref);
     for (uint32_t j = first; j < first + count; ++j) {
@@ -532,12 +532,12 @@ __device__ __forceinline__ void sec_leaf(const RenderArgs& A, SecRay& R, int32_t
             lo = 0.0f;
             R.hitmask |= 1ull << slot;
         }
-        sec_add<S, FAST>(A, R, g, q, lo, b, c);
+        sec_add<S, FAST, PURE>(A, R, g, q, lo, b, c);
     }
 }
 
 // Ray complete: write its transmittance (or hand it to the exact slow path).
-template <bool S, bool FAST>
+template <bool S, bool FAST, bool PURE>
 __device__ __forceinline__ void sec_finish(const RenderArgs& A, uint64_t t, SecRay& R, Ctr& c) {
     if constexpr (S) {  // secondary-stage diagnostics in otherwise unused counter slots
         if (R.tau >= A.tau_cut) {
@@ -553,7 +553,7 @@ __device__ __forceinline__ void sec_finish(const RenderArgs& A, uint64_t t, SecR
     }
     const uint64_t all = R.act_n >= 64 ? ~0ull : ((1ull << R.act_n) - 1ull);
     uint64_t missed = all & ~R.hitmask;
-    if (A.pure) {  // pre-activated, missed through rounding: active to the end of the march
+    if constexpr (PURE) {  // pre-activated, missed through rounding: active to the end of the march
         while (missed) {
             int s = __ffsll((unsigned long long)missed) - 1;
             missed &= missed - 1;
@@ -585,7 +585,7 @@ __device__ __forceinline__ void sec_finish(const RenderArgs& A, uint64_t t, SecR
 
 // One BVH node pair of secondary ray R (plus the primitives of leaf children). Returns true when
 // the ray is complete (stack exhausted or optical depth past the cut-off).
-template <int BLOCK, bool S, bool FAST>
+template <int BLOCK, bool S, bool FAST, bool PURE>
 __device__ __forceinline__ bool sec_step(const RenderArgs& A, SecRay& R, int* stack, int& sp, int& node, Ctr& c) {
     if constexpr (S) c.v[kCtrNodes]++;
     const float4* np = reinterpret_cast<const float4*>(A.nodes + node);
@@ -610,8 +610,8 @@ __device__ __forceinline__ bool sec_step(const RenderArgs& A, SecRay& R, int* st
     const bool ll = hl && ref_is_leaf(nc.x), lr = hr && ref_is_leaf(nc.y);
     if (ll || lr) {
         const bool r_first = lr && (!ll || rmin < lmin);
-        sec_leaf<S, FAST>(A, R, r_first ? nc.y : nc.x, c);
-        if (ll && lr && R.tau < A.tau_cut) sec_leaf<S, FAST>(A, R, r_first ? nc.x : nc.y, c);
+        sec_leaf<S, FAST, PURE>(A, R, r_first ? nc.y : nc.x, c);
+        if (ll && lr && R.tau < A.tau_cut) sec_leaf<S, FAST, PURE>(A, R, r_first ? nc.x : nc.y, c);
         if (ll) hl = false;
         if (lr) hr = false;
     }
@@ -833,7 +833,7 @@ __device__ __forceinline__ void list_advance(SecRay& R, LeafQueue& Q, int& node)
 
 // 5 waves/SIMD: the register allocation this kernel needs without spilling (a 6-wave build
 // spills ~6 VGPRs to scratch and measured 9 % slower on C4).
-template <int BLOCK, int STACK, bool S, int WAVES = 5>
+template <int BLOCK, int STACK, bool S, bool PURE, int WAVES = 5>
 __global__ __launch_bounds__(BLOCK, WAVES) void secondary_ww_kernel(RenderArgs A, uint32_t nrec,
                                                                                             uint64_t total, int refill_min,
                                                                                             int prim_bias) {
@@ -900,7 +900,7 @@ __global__ __launch_bounds__(BLOCK, WAVES) void secondary_ww_kernel(RenderArgs A
                         lo = 0.0f;
                         R.hitmask |= 1ull << slot;
                     }
-                    sec_add<S, true>(A, R, g, q, lo, b, c);
+                    sec_add<S, true, PURE>(A, R, g, q, lo, b, c);
                 }
                 list_advance(R, Q, node);
             }
@@ -908,7 +908,7 @@ __global__ __launch_bounds__(BLOCK, WAVES) void secondary_ww_kernel(RenderArgs A
             if (can_node) sec_node<BLOCK, S>(A, R, stack, sp, node, Q, c);
         }
         if (live && (R.tau >= A.tau_cut || (node < 0 && !Q.has_prim()))) {
-            sec_finish<S, true>(A, t, R, c);
+            sec_finish<S, true, PURE>(A, t, R, c);
             live = false;
         }
     }
@@ -917,7 +917,7 @@ __global__ __launch_bounds__(BLOCK, WAVES) void secondary_ww_kernel(RenderArgs A
 
 // One ray per lane, grid-stride over ray ids [t_begin, t_end) (light rays: already coherent —
 // neighbouring lanes trace from neighbouring pixels towards the same light).
-template <int BLOCK, bool S, bool FAST>
+template <int BLOCK, bool S, bool FAST, bool PURE>
 __global__ __launch_bounds__(BLOCK) void secondary_simple_kernel(RenderArgs A, uint32_t nrec, uint64_t t_begin,
                                                                  uint64_t t_end) {
     __shared__ int s_stack[kStackSize * BLOCK];
@@ -929,55 +929,15 @@ __global__ __launch_bounds__(BLOCK) void secondary_simple_kernel(RenderArgs A, u
         if constexpr (S) c.v[kCtrSecRays]++;
         if (!sec_init(A, nrec, t, R)) continue;
         int sp = 0, node = 0;
-        while (!sec_step<BLOCK, S, FAST>(A, R, stack, sp, node, c)) {
+        while (!sec_step<BLOCK, S, FAST, PURE>(A, R, stack, sp, node, c)) {
         }
-        sec_finish<S, FAST>(A, t, R, c);
+        sec_finish<S, FAST, PURE>(A, t, R, c);
     }
     if constexpr (S)
         for (int i = 0; i < kNumCtr; ++i)
             if (c.v[i]) atomicAdd(A.work + kNumCtr + i, (unsigned long long)c.v[i]);
 }
 
-template <int BLOCK, bool S, bool FAST>
-__global__ __launch_bounds__(BLOCK) void secondary_persistent_kernel(RenderArgs A, uint32_t nrec, uint64_t total,
-                                                                     uint64_t chunk) {
-    __shared__ int s_stack[kStackSize * BLOCK];
-    int* stack = s_stack + threadIdx.x;
-    const uint64_t wave = ((uint64_t)blockIdx.x * BLOCK + threadIdx.x) >> 6;
-    const uint64_t begin = wave * chunk;
-    const uint64_t end = begin + chunk < total ? begin + chunk : total;
-    uint64_t next = begin;  // wave-uniform
-    Ctr c{};
-    SecRay R;
-    bool live = false;
-    uint64_t t = 0;
-    int sp = 0, node = 0;
-    for (;;) {
-        // refill lanes whose ray is done from the wave's chunk
-        // refill once a quarter of the wave is idle (amortises the ray set-up over many lanes)
-        const uint64_t need = __ballot(!live);
-        if (__popcll(need) >= 16 || need == ~0ull) {
-            const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(need >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)need, 0u));
-            if (!live) {
-                t = next + rank;
-                if (t < end) {
-                    if constexpr (S) c.v[kCtrSecRays]++;
-                    live = sec_init(A, nrec, t, R);
-                    sp = 0;
-                    node = 0;
-                }
-            }
-            next += (uint64_t)__popcll(need);
-        }
-        if (!__any(live)) break;
-        if (!live) continue;
-        if (sec_step<BLOCK, S, FAST>(A, R, stack, sp, node, c)) {
-            sec_finish<S, FAST>(A, t, R, c);
-            live = false;
-        }
-    }
-    if constexpr (S) flush_counters(A.work + kNumCtr, c);
-}
 
 // Exact three-pass light transmittance for the queued rays (see light_transmittance).
 template <int BLOCK, bool S>
@@ -1086,24 +1046,19 @@ hipError_t gauss_march(const RenderArgs& A, hipStream_t stream, bool stats) {
     return stats ? march_pass<true>(A, stream) : march_pass<false>(A, stream);
 }
 
-template <bool S, bool FAST>
+template <bool S, bool FAST, bool PURE>
 static hipError_t secondary_launch(const RenderArgs& A, uint32_t nrec, uint64_t total, hipStream_t stream, int variant) {
-    // Kernel choice (C4, 4096^2 / 1M Gaussians, round 1: simple 2.13 s, persistent 3.57 s): one
-    // thread per secondary ray in record order, because neighbouring records are neighbouring
-    // pixels and their rays already share BVH paths. VR_SECONDARY=p selects the persistent
-    // variant for A/B runs.
-    if (variant == 2) {
+    if (variant == 2) {  // persistent while-while kernel (default)
         static const int refill_min = getenv("VR_WW_REFILL") ? atoi(getenv("VR_WW_REFILL")) : 32;
         static const int prim_bias = getenv("VR_WW_BIAS") ? atoi(getenv("VR_WW_BIAS")) : 0;
         const int rmin = refill_min < 1 ? 1 : (refill_min > 64 ? 64 : refill_min);
         hipError_t e = hipMemsetAsync(A.ray_next, 0, sizeof(unsigned long long), stream);
         if (e != hipSuccess) return e;
         static const bool force_deep = getenv("VR_WW_STACK") && atoi(getenv("VR_WW_STACK")) == kStackSize;
-        // smallest LDS stack the tree fits (a child-pair traversal pushes at most depth - 1 entries):
-        // 24 entries -> 6 waves/SIMD, 32 -> 5 (a 20-entry / 8-wave variant spills and loses)
-        const int stack = (force_deep || A.bvh_depth > kShallowStack + 1) ? kStackSize : kShallowStack;
-        const void* fn = stack == kShallowStack ? (const void*)dev::secondary_ww_kernel<kBlockSecondary, kShallowStack, S>
-                                                : (const void*)dev::secondary_ww_kernel<kBlockSecondary, kStackSize, S>;
+        // smallest LDS stack the tree fits (a child-pair traversal pushes at most depth - 1 entries)
+        const bool shallow = !force_deep && A.bvh_depth <= kShallowStack + 1;
+        const void* fn = shallow ? (const void*)dev::secondary_ww_kernel<kBlockSecondary, kShallowStack, S, PURE>
+                                 : (const void*)dev::secondary_ww_kernel<kBlockSecondary, kStackSize, S, PURE>;
         int dv = 0, cus = 0, per_cu = 0;
         if (hipGetDevice(&dv) != hipSuccess) return hipErrorUnknown;
         if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dv) != hipSuccess) return hipErrorUnknown;
@@ -1112,34 +1067,25 @@ static hipError_t secondary_launch(const RenderArgs& A, uint32_t nrec, uint64_t 
         uint64_t grid = (uint64_t)cus * (uint64_t)per_cu;
         const uint64_t need = (total + kBlockSecondary - 1) / kBlockSecondary;
         if (grid > need) grid = need;
-        if (stack == kShallowStack)
-            hipLaunchKernelGGL((dev::secondary_ww_kernel<kBlockSecondary, kShallowStack, S>), dim3((unsigned)grid),
+        if (shallow)
+            hipLaunchKernelGGL((dev::secondary_ww_kernel<kBlockSecondary, kShallowStack, S, PURE>), dim3((unsigned)grid),
                                dim3(kBlockSecondary), 0, stream, A, nrec, total, rmin, prim_bias);
         else
-            hipLaunchKernelGGL((dev::secondary_ww_kernel<kBlockSecondary, kStackSize, S>), dim3((unsigned)grid),
+            hipLaunchKernelGGL((dev::secondary_ww_kernel<kBlockSecondary, kStackSize, S, PURE>), dim3((unsigned)grid),
                                dim3(kBlockSecondary), 0, stream, A, nrec, total, rmin, prim_bias);
-    } else if (variant == 0) {
+    } else {  // one ray per thread
         uint64_t blocks = (total + kBlockSecondary - 1) / kBlockSecondary;
         if (blocks > 65536ull * 16ull) blocks = 65536ull * 16ull;
-        hipLaunchKernelGGL((dev::secondary_simple_kernel<kBlockSecondary, S, FAST>), dim3((unsigned)blocks),
+        hipLaunchKernelGGL((dev::secondary_simple_kernel<kBlockSecondary, S, FAST, PURE>), dim3((unsigned)blocks),
                            dim3(kBlockSecondary), 0, stream, A, nrec, (uint64_t)0, total);
-    } else {
-        int dev = 0, cus = 0, per_cu = 0;
-        if (hipGetDevice(&dev) != hipSuccess) return hipErrorUnknown;
-        if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return hipErrorUnknown;
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, dev::secondary_persistent_kernel<kBlockSecondary, S, FAST>,
-                                                         kBlockSecondary, 0) != hipSuccess || per_cu < 1)
-            per_cu = 1;
-        const uint64_t grid = (uint64_t)cus * (uint64_t)per_cu;
-        const uint64_t waves = grid * (kBlockSecondary / 64);
-        const uint64_t chunk = (total + waves - 1) / waves;
-        hipLaunchKernelGGL((dev::secondary_persistent_kernel<kBlockSecondary, S, FAST>), dim3((unsigned)grid),
-                           dim3(kBlockSecondary), 0, stream, A, nrec, total, chunk);
     }
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL((dev::secondary_slow_kernel<64, S>), dim3(512), dim3(64), 0, stream, A, nrec);
-    return hipGetLastError();
+    if (!PURE) {  // PureRayMarching has no first-event-past-the-light quirk, hence no slow path
+        hipLaunchKernelGGL((dev::secondary_slow_kernel<64, S>), dim3(512), dim3(64), 0, stream, A, nrec);
+        e = hipGetLastError();
+    }
+    return e;
 }
 
 hipError_t gauss_lists(const RenderArgs& A, uint32_t nrec, hipStream_t stream) {
@@ -1158,9 +1104,9 @@ hipError_t gauss_secondary(const RenderArgs& A, uint32_t nrec, hipStream_t strea
     if (total >= 0xffffffffull) return hipErrorInvalidValue;
     // A/B switches (read once): VR_SECONDARY=s one ray per thread, =p refill-only persistent kernel; VR_SEC_EXACT=1 correctly rounded
     // secondary-ray arithmetic (the fast form is the default).
-    static const int variant = [] {  // 2: while-while persistent (default), 0: one ray per thread, 1: old persistent
+    static const int variant = [] {  // 2: while-while persistent (default), 0: one ray per thread
         const char* v = getenv("VR_SECONDARY");
-        return (v && v[0] == 'p') ? 1 : (v && v[0] == 's') ? 0 : 2;
+        return (v && v[0] == 's') ? 0 : 2;
     }();
     static const bool exact = [] {
         const char* v = getenv("VR_SEC_EXACT");
@@ -1170,10 +1116,15 @@ hipError_t gauss_secondary(const RenderArgs& A, uint32_t nrec, hipStream_t strea
     // canonical, non-speculative work of a near-first BVH traversal per secondary ray, which is
     // what the roofline's algorithmic flops are defined on (the persistent kernel's postponed
     // leaves make it do a little more, speculatively).
-    if (stats) return exact ? secondary_launch<true, false>(A, nrec, total, stream, 0)
-                            : secondary_launch<true, true>(A, nrec, total, stream, 0);
-    return exact ? secondary_launch<false, false>(A, nrec, total, stream, variant)
-                 : secondary_launch<false, true>(A, nrec, total, stream, variant);
+    const int v = stats ? 0 : variant;
+    if (A.pure) {
+        if (stats) return secondary_launch<true, true, true>(A, nrec, total, stream, v);
+        return secondary_launch<false, true, true>(A, nrec, total, stream, v);
+    }
+    if (stats) return exact ? secondary_launch<true, false, false>(A, nrec, total, stream, v)
+                            : secondary_launch<true, true, false>(A, nrec, total, stream, v);
+    return exact ? secondary_launch<false, false, false>(A, nrec, total, stream, v)
+                 : secondary_launch<false, true, false>(A, nrec, total, stream, v);
 }
 
 hipError_t gauss_accumulate(const RenderArgs& A, uint32_t nrec, hipStream_t stream) {
