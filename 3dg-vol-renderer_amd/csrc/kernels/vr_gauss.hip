@@ -373,16 +373,15 @@ struct SecRay {
     Ray ray;
     float ix, iy, iz, oxi, oyi, ozi;  // 1/d and o/d for the slab test
     float tau, lim;                   // optical depth so far; light: dist, env: +inf
-    float tlast;                      // env: last event
+    // `lim`: a light ray's distance to the light; an environment ray's last event so far (the
+    // reference's t_env_end, test_integrators.h:258-271), which bounds nothing during traversal
     uint64_t hitmask, bloom;
     uint32_t act_off, act_n;
     bool light, needs_stop;
     uint32_t nsteps;  // instrumented build only: node steps taken by this ray
     uint32_t rec;     // record index
     uint32_t slot;    // result slot s * nrec + rec in tr
-    int lmode;        // neighbour-list phase: 1 central members, 2 other members, 0 done / none
     bool listed;      // the record has a neighbour list (tree leaves then skip its members)
-    uint32_t lnb;     // number of "other" members (tested after the central ones)
 };
 
 __device__ __forceinline__ int act_find(const RenderArgs& A, const SecRay& R, int j) {
@@ -447,7 +446,6 @@ __device__ __forceinline__ bool sec_init(const RenderArgs& A, uint32_t nrec, uin
     R.hitmask = 0;
     R.nsteps = 0;
     R.tau = 0.0f;
-    R.tlast = 0.0f;
     R.needs_stop = false;
     if (s < (uint32_t)A.num_lights) {
         const LightRecord& lr = A.lights[s];
@@ -466,7 +464,7 @@ __device__ __forceinline__ bool sec_init(const RenderArgs& A, uint32_t nrec, uin
         env_sample_dir(A, meta, s - (uint32_t)A.num_lights, wx, wy, wz);
         R.ray = make_ray(pos.x, pos.y, pos.z, wx, wy, wz);
         R.light = false;
-        R.lim = INFINITY;
+        R.lim = 0.0f;  // last event so far
     }
     // |d| clamped away from 0: the fma slab form b/d - o/d must never see inf - inf
     R.ix = __frcp_rn(fabsf(R.ray.dx) > 1e-30f ? R.ray.dx : copysignf(1e-30f, R.ray.dx));
@@ -503,15 +501,17 @@ __device__ __forceinline__ void sec_add(const RenderArgs& A, SecRay& R, const GR
     if constexpr (PURE) {
         if (!R.light) {
             R.tau += marched_depth(A, g, R.ray, lo, b);
-            R.tlast = fmaxf(R.tlast, b);
+            R.lim = fmaxf(R.lim, b);
         } else if (lo < R.lim) {
             R.tau += marched_depth(A, g, R.ray, lo, fminf(b, R.lim));
         }
         return;
     }
-    if (!R.light || b < R.lim) {
+    if (!R.light) {
         R.tau += FAST ? optical_depth_fast(g, q, lo, b) : optical_depth(g, q, lo, b);
-        R.tlast = fmaxf(R.tlast, b);
+        R.lim = fmaxf(R.lim, b);
+    } else if (b < R.lim) {
+        R.tau += FAST ? optical_depth_fast(g, q, lo, b) : optical_depth(g, q, lo, b);
     } else if (lo < R.lim) {
         R.needs_stop = true;
     }
@@ -558,7 +558,7 @@ __device__ __forceinline__ void sec_finish(const RenderArgs& A, uint64_t t, SecR
             int s = __ffsll((unsigned long long)missed) - 1;
             missed &= missed - 1;
             GRec g = load_rec(A.gauss, A.rec_act[R.act_off + s]);
-            R.tau += marched_depth(A, g, R.ray, 0.0f, R.light ? R.lim : R.tlast);
+            R.tau += marched_depth(A, g, R.ray, 0.0f, R.lim);  // dist (light) / last event (environment)
         }
     } else if (R.light) {
         if (R.needs_stop || missed) {
@@ -577,7 +577,7 @@ __device__ __forceinline__ void sec_finish(const RenderArgs& A, uint64_t t, SecR
             GRec g = load_rec(A.gauss, A.rec_act[R.act_off + s]);
             Quad q = FAST ? quad_fast(g, R.ray) : quad(g, R.ray);
             if constexpr (S) c.v[kCtrOD]++;
-            R.tau += FAST ? optical_depth_fast(g, q, 0.0f, R.tlast) : optical_depth(g, q, 0.0f, R.tlast);
+            R.tau += FAST ? optical_depth_fast(g, q, 0.0f, R.lim) : optical_depth(g, q, 0.0f, R.lim);
         }
     }
     A.tr[R.slot] = expf(-R.tau);
@@ -604,7 +604,7 @@ __device__ __forceinline__ bool sec_step(const RenderArgs& A, SecRay& R, int* st
         rmin = fmaxf(fmaxf(fminf(ux1, ux2), fminf(uy1, uy2)), fminf(uz1, uz2));
         rmax = fminf(fminf(fmaxf(ux1, ux2), fmaxf(uy1, uy2)), fmaxf(uz1, uz2));
     }
-    const float lim = R.lim + kTPad * (1.0f + R.lim);
+    const float lim = R.light ? R.lim + kTPad * (1.0f + R.lim) : INFINITY;
     bool hl = nc.x != 0 && lmax >= fmaxf(lmin, 0.0f) && lmin <= lim;
     bool hr = nc.y != 0 && rmax >= fmaxf(rmin, 0.0f) && rmin <= lim;
     const bool ll = hl && ref_is_leaf(nc.x), lr = hr && ref_is_leaf(nc.y);
@@ -652,16 +652,14 @@ __device__ __forceinline__ bool sec_step(const RenderArgs& A, SecRay& R, int* st
 // the two divergence costs of one-ray-per-lane traversal: a wave no longer waits for its longest
 // ray, and a leaf visit no longer stalls the lanes that are still walking inner nodes.
 // ---------------------------------------------------------------------------------------------
-struct LeafQueue {  // FIFO of up to 4 leaf refs (registers) + the leaf being tested
-    int32_t q0, q1, q2, q3;
+struct LeafQueue {  // FIFO of up to 2 leaf refs (registers) + the leaf being tested
+    int32_t q0, q1;
     int n;
     uint32_t j, end;  // current primitive range [j, end)
     // branch-free: writes r at slot `idx` (no slot matches idx < 0)
     __device__ __forceinline__ void put(int idx, int32_t r) {
         q0 = idx == 0 ? r : q0;
         q1 = idx == 1 ? r : q1;
-        q2 = idx == 2 ? r : q2;
-        q3 = idx == 3 ? r : q3;
     }
     __device__ __forceinline__ bool has_prim() const { return j < end || n > 0; }
     __device__ __forceinline__ uint32_t next() {  // requires has_prim()
@@ -669,8 +667,6 @@ struct LeafQueue {  // FIFO of up to 4 leaf refs (registers) + the leaf being te
             j = leaf_first(q0);
             end = j + leaf_count(q0);
             q0 = q1;
-            q1 = q2;
-            q2 = q3;
             --n;
         }
         return j++;
@@ -700,7 +696,7 @@ __device__ __forceinline__ void sec_node(const RenderArgs& A, SecRay& R, int* st
     const float uz1 = fmaf(n2.x, R.iz, -R.ozi), uz2 = fmaf(n2.w, R.iz, -R.ozi);
     const float rmin = fmaxf(fmaxf(fminf(ux1, ux2), fminf(uy1, uy2)), fminf(uz1, uz2));
     const float rmax = fminf(fminf(fmaxf(ux1, ux2), fmaxf(uy1, uy2)), fmaxf(uz1, uz2));
-    const float lim = R.lim + kTPad * (1.0f + R.lim);
+    const float lim = R.light ? R.lim + kTPad * (1.0f + R.lim) : INFINITY;
     const bool hl = (nc.x != 0) & (lmax >= fmaxf(lmin, 0.0f)) & (lmin <= lim);
     const bool hr = (nc.y != 0) & (rmax >= fmaxf(rmin, 0.0f)) & (rmin <= lim);
     const bool r_near = rmin < lmin;
@@ -789,51 +785,50 @@ __global__ __launch_bounds__(BLOCK) void record_list_kernel(RenderArgs A, uint32
     }
 }
 
+// Neighbour-list phases live in `node`: kListCentral_ (-2) walks the central members [Q.j, Q.end),
+// kListOther_ (-3) the other members, whose slot range waits in the (then unused) leaf-queue
+// registers q0 / q1; node >= 0 is the tree walk, -1 the end.
+constexpr int kNodeListCentral = -2, kNodeListOther = -3;
+
 // Start ray R's neighbour-list phase (or go straight to the tree).
 __device__ __forceinline__ void list_begin(const RenderArgs& A, SecRay& R, LeafQueue& Q, int& node) {
     Q.n = 0;
     Q.j = Q.end = 0;
-    R.lmode = 0;
     R.listed = false;
     node = 0;
     if (!A.list_ok) return;
     const uint32_t nl = A.rec_nlist[R.rec];
     if (nl == 0xffffffffu) return;
     R.listed = true;
-    const uint32_t nc = nl & 0xffffu;
-    R.lnb = nl >> 16;
+    const uint32_t nc = nl & 0xffffu, nb = nl >> 16;
     const uint32_t base = R.rec * (uint32_t)kListCap;
+    Q.q0 = (int32_t)(base + kListCap - nb);  // other members: [q0, q1)
+    Q.q1 = (int32_t)(base + kListCap);
     if (nc > 0) {
-        R.lmode = 1;
         Q.j = base;
         Q.end = base + nc;
-        node = -2;
-    } else if (R.lnb > 0) {
-        R.lmode = 2;
-        Q.j = base + kListCap - R.lnb;
-        Q.end = base + kListCap;
-        node = -2;
+        node = kNodeListCentral;
+    } else if (nb > 0) {
+        Q.j = (uint32_t)Q.q0;
+        Q.end = (uint32_t)Q.q1;
+        node = kNodeListOther;
     }
 }
 
 // After a list slot was consumed: move to the other members, then to the tree.
-__device__ __forceinline__ void list_advance(SecRay& R, LeafQueue& Q, int& node) {
-    if (R.lmode == 0 || Q.j < Q.end) return;
-    if (R.lmode == 1 && R.lnb > 0) {
-        R.lmode = 2;
-        const uint32_t base = R.rec * (uint32_t)kListCap;
-        Q.j = base + kListCap - R.lnb;
-        Q.end = base + kListCap;
+__device__ __forceinline__ void list_advance(LeafQueue& Q, int& node) {
+    if (node > kNodeListCentral || Q.j < Q.end) return;
+    if (node == kNodeListCentral && Q.q0 < Q.q1) {
+        Q.j = (uint32_t)Q.q0;
+        Q.end = (uint32_t)Q.q1;
+        node = kNodeListOther;
     } else {
-        R.lmode = 0;
         Q.j = Q.end = 0;
         node = 0;
     }
 }
 
-// 5 waves/SIMD: the register allocation this kernel needs without spilling (a 6-wave build
-// spills ~6 VGPRs to scratch and measured 9 % slower on C4).
-template <int BLOCK, int STACK, bool S, bool PURE, int WAVES = 5>
+template <int BLOCK, int STACK, bool S, bool PURE, int WAVES = 6>
 __global__ __launch_bounds__(BLOCK, WAVES) void secondary_ww_kernel(RenderArgs A, uint32_t nrec,
                                                                                             uint64_t total, int refill_min,
                                                                                             int prim_bias) {
@@ -842,8 +837,8 @@ __global__ __launch_bounds__(BLOCK, WAVES) void secondary_ww_kernel(RenderArgs A
     const uint32_t lane = threadIdx.x & 63u;
     Ctr c{};
     SecRay R;
-    LeafQueue Q{0, 0, 0, 0, 0, 0u, 0u};
-    uint64_t t = 0;
+    LeafQueue Q{0, 0, 0, 0u, 0u};
+    uint32_t t = 0;
     int sp = 0, node = -1;
     bool live = false;
     uint64_t pool = 0, pool_end = 0;  // wave-uniform: ray ids fetched but not yet handed out
@@ -864,7 +859,7 @@ __global__ __launch_bounds__(BLOCK, WAVES) void secondary_ww_kernel(RenderArgs A
             }
             const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(idle >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)idle, 0u));
             if (!live && pool + rank < pool_end) {
-                t = pool + rank;
+                t = (uint32_t)(pool + rank);
                 if constexpr (S) c.v[kCtrSecRays]++;
                 live = sec_init(A, nrec, t, R);  // false: padding id, or complete already (Tr written)
                 sp = 0;
@@ -881,12 +876,12 @@ __global__ __launch_bounds__(BLOCK, WAVES) void secondary_ww_kernel(RenderArgs A
             continue;
         }
         const bool has_prim = live && Q.has_prim();
-        const bool can_node = live && node >= 0 && Q.n <= 2;
+        const bool can_node = live && node >= 0 && Q.n == 0;  // room for the 2 leaves a step can queue
         const int np = __popcll(__ballot(has_prim)), nn = __popcll(__ballot(can_node));
         // whichever kind more lanes can use; never a kind no lane can use (that would not progress)
         if (nn == 0 || (np > 0 && np + prim_bias >= nn)) {  // PRIM iteration
             if (has_prim) {
-                const bool from_list = R.lmode != 0;
+                const bool from_list = node <= kNodeListCentral;
                 const uint32_t j = from_list ? (uint32_t)A.rec_list[Q.j++] : Q.next();
                 if constexpr (S) c.v[kCtrPrims]++;
                 const GRec g = load_rec(A.gauss, (int)j);
@@ -902,12 +897,12 @@ __global__ __launch_bounds__(BLOCK, WAVES) void secondary_ww_kernel(RenderArgs A
                     }
                     sec_add<S, true, PURE>(A, R, g, q, lo, b, c);
                 }
-                list_advance(R, Q, node);
+                list_advance(Q, node);
             }
         } else {  // NODE iteration
             if (can_node) sec_node<BLOCK, S>(A, R, stack, sp, node, Q, c);
         }
-        if (live && (R.tau >= A.tau_cut || (node < 0 && !Q.has_prim()))) {
+        if (live && (R.tau >= A.tau_cut || (node == -1 && !Q.has_prim()))) {
             sec_finish<S, true, PURE>(A, t, R, c);
             live = false;
         }

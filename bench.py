@@ -8,7 +8,12 @@ over RCCL and unshuffled into the row-major frame there (timed: render + gather 
 
 Workload (BASELINE.json metric): 4096 x 4096 pinhole render (tests/main.cpp camera) of 1,000,000
 synthetic Gaussians with make_random.py's distribution and 1000_random.txt's three lights,
-step 0.01, 20 environment samples per scattering step.
+step 0.01, 20 environment samples per scattering step, early-out t_eps = 1e-6 (on
+these scenes the frame is within ~1e-6 of the exact one, tests/test_gpu_parity.py).
+
+Device stages per frame: march_kernel (scatter records) -> record_list_kernel
+(record neighbour lists) -> secondary_ww_kernel (light + environment transmittance, the dominant
+kernel) -> accumulate_kernel.
 
 Prints ONE JSON line on rank 0 (contract in the task statement); roofline and cpu_baseline
 objects are documented in DESIGN.md.
@@ -189,7 +194,7 @@ def main():
         sec_ms = stage_ms["secondary"]
         roof = {"bound": "mfma", "unit": "TFLOP/s", "peak": FP32_PEAK_TFLOPS, "achieved": None, "frac": None,
                 "traffic": None,
-                "kernel": "secondary_simple_kernel + secondary_slow_kernel (stage 'secondary')",
+                "kernel": "secondary_ww_kernel + secondary_slow_kernel (stage 'secondary')",
                 "kernel_ms": sec_ms, "peak_note": "FP32 vector peak (= f32 MFMA peak); VALU-only kernel",
                 "stage_ms": stage_ms, "frame_kernel_ms": kernel_ms,
                 "secondary_rays": per_step[-1]["secondary_rays"], "scatter_records": per_step[-1]["scatter_records"]}
@@ -198,6 +203,16 @@ def main():
             tflops = sec_flops / (sec_ms * 1e-3) / 1e12
             roof.update(achieved=tflops, frac=tflops / FP32_PEAK_TFLOPS, alg_flops=sec_flops, work=work,
                         frame_tflops=work["flops"] / (kernel_ms * 1e-3) / 1e12)
+        # HBM traffic of the dominant kernel: rocprofv3 PMC passes of this same command (FETCH_SIZE x 2,
+        # the gfx950 correction of MI355X_MICROARCH.md, + WRITE_SIZE), committed under profiles/
+        pmc_path = os.path.join(ROOT, "profiles", "r01_c4_pmc_summary.json")
+        if args.config == "c4" and world == 1 and os.path.exists(pmc_path):
+            pmc = json.load(open(pmc_path))
+            for k, d in pmc.items():
+                if k.startswith("vr::dev::secondary_ww_kernel") and "hbm_read_bytes_gfx950_corrected" in d:
+                    roof["traffic"] = d["hbm_read_bytes_gfx950_corrected"] + d.get("hbm_write_bytes", 0.0)
+                    roof["traffic_unit"] = "bytes per launch"
+                    roof["traffic_source"] = "profiles/r01_c4_pmc_summary.json (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE)"
         # HBM view of the whole frame (the north star's requested metric): compulsory bytes = every
         # 48-B Gaussian record read once + every 12-B output pixel written once, over frame time.
         alg_bytes = 48.0 * n_g + 12.0 * mine * 256
