@@ -828,6 +828,8 @@ __device__ __forceinline__ void list_advance(LeafQueue& Q, int& node) {
     }
 }
 
+// 6 waves/SIMD = 80 VGPRs: the ray state is kept small enough for that without scratch spills (a
+// spilling 6-wave build measured 9 % slower than 5 waves; this one is 5 % faster than 5 waves).
 template <int BLOCK, int STACK, bool S, bool PURE, int WAVES = 6>
 __global__ __launch_bounds__(BLOCK, WAVES) void secondary_ww_kernel(RenderArgs A, uint32_t nrec,
                                                                                             uint64_t total, int refill_min,
