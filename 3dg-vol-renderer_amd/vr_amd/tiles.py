@@ -57,11 +57,20 @@ def render_local(dev, camera, params, W, H, rank, world, slab, frame, stream_ptr
         dev.render_tiles_device(camera, params, W, H, first, stride, count, True, slab.data_ptr(), stream_ptr)
 
 
-def gather_frame(dev, W, H, rank, world, slab, slabs, frame, stream_ptr, dist):
-    """Gather every rank's slab to rank 0 (one RCCL gather over xGMI) and unshuffle there."""
+def gather_frame(dev, W, H, rank, world, slab, slabs, frame, stream_ptr, dist, via_host=False):
+    """Gather every rank's slab to rank 0 (one RCCL gather over xGMI) and unshuffle there.
+    via_host: gather CPU copies instead (gloo rehearsal of the N > 1 path on one GPU)."""
     if world == 1:
         return
     per = slab.numel() // (TILE * TILE * 3)
-    dist.gather(slab, list(slabs.unbind(0)) if rank == 0 else None, dst=0)
+    if via_host:
+        import torch
+        torch.cuda.synchronize()
+        host = [torch.empty_like(slab, device="cpu") for _ in range(world)] if rank == 0 else None
+        dist.gather(slab.cpu(), host, dst=0)
+        if rank == 0:
+            slabs.copy_(torch.stack(host).to(slabs.device))
+    else:
+        dist.gather(slab, list(slabs.unbind(0)) if rank == 0 else None, dst=0)
     if rank == 0:
         dev.unshuffle_tiles_device(slabs.data_ptr(), world, per, W, H, frame.data_ptr(), stream_ptr)

@@ -113,9 +113,17 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
+    # VR_BENCH_GLOO=1 (rehearsal only): every rank on cuda:0, slabs gathered through host memory
+    # with gloo, so the N>1 path can be exercised on a one-GPU box. Real runs use RCCL.
+    rehearsal = os.environ.get("VR_BENCH_GLOO") == "1"
+    if rehearsal:
+        local = 0
     torch.cuda.set_device(local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if rehearsal:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
 
     t_setup = time.perf_counter()
     scene, W, H = build_scene(args.config, args.seed)
@@ -141,7 +149,7 @@ def main():
     def step():
         tiles.render_local(dev, camera, integ.params, W, H, rank, world, None if world == 1 else slab, frame, sp)
         if world > 1:
-            tiles.gather_frame(dev, W, H, rank, world, slab, slabs, frame, sp, dist)
+            tiles.gather_frame(dev, W, H, rank, world, slab, slabs, frame, sp, dist, via_host=rehearsal)
 
     def log(msg):
         if rank == 0:
