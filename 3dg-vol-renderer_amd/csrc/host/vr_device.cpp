@@ -65,7 +65,7 @@ struct vr_ctx {
         size_t bytes = 0;
     };
     Buf px_first, px_T, rec_pos, rec_meta, rec_next, rec_act, tr, rec_alloc, rec_bloom, slowq;
-    Buf pcg_jump, ray_next, rec_list, rec_nlist;
+    Buf pcg_jump, ray_next, rec_list, rec_nlist, stack_ovf;
     bool list_ok = false;  // all covariances positive definite: neighbour lists are exact
     int pcg_jump_n = -1;
     uint32_t* h_totals = nullptr;  // pinned copy of rec_alloc: [0] records, [1] overflow-pool entries, [2] exceeded
@@ -296,6 +296,14 @@ vr_status gauss_pipeline(vr_ctx* c, RenderArgs& A, hipStream_t s, bool stats) {
     HIP_TRY(hipMemsetAsync(A.slowq, 0, sizeof(uint32_t), s), "hipMemsetAsync(slow queue)");
     if ((st = grow(c->ray_next, 8, "hipMalloc(ray counter)")) != VR_OK) return st;
     A.ray_next = (unsigned long long*)c->ray_next.p;
+    {  // traversal-stack overflow of the persistent kernel: kMaxDepth entries for every lane it can keep resident
+        int cus = 0;
+        HIP_TRY(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, c->device), "hipDeviceGetAttribute");
+        const uint64_t lanes = (uint64_t)std::max(cus, 1) * 2048ull;  // 32 waves of 64 lanes per CU at most
+        if ((st = grow(c->stack_ovf, lanes * kMaxDepth * 4ull, "hipMalloc(stack overflow)")) != VR_OK) return st;
+        A.stack_ovf = (int32_t*)c->stack_ovf.p;
+        A.stack_ovf_lanes = (uint32_t)lanes;
+    }
     static const bool no_list = getenv("VR_NOLIST") && getenv("VR_NOLIST")[0] == '1';
     A.list_ok = c->list_ok && !no_list && (uint64_t)nrec * kListCap < 0xffffffffull;
     if (A.list_ok) {
@@ -385,7 +393,8 @@ void vr_destroy(vr_ctx* c) {
     if (c->h_counters) (void)hipHostFree(c->h_counters);
     if (c->h_totals) (void)hipHostFree(c->h_totals);
     for (vr_ctx::Buf* b : {&c->px_first, &c->px_T, &c->rec_pos, &c->rec_meta, &c->rec_next, &c->rec_act, &c->tr,
-                           &c->rec_alloc, &c->rec_bloom, &c->slowq, &c->pcg_jump, &c->ray_next, &c->rec_list, &c->rec_nlist})
+                           &c->rec_alloc, &c->rec_bloom, &c->slowq, &c->pcg_jump, &c->ray_next, &c->rec_list, &c->rec_nlist,
+                           &c->stack_ovf})
         if (b->p) (void)hipFree(b->p);
     if (c->d_frame) (void)hipFree(c->d_frame);
     if (c->ev_start) (void)hipEventDestroy(c->ev_start);

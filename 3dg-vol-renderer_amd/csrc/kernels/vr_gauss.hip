@@ -538,7 +538,7 @@ __device__ __forceinline__ void sec_leaf(const RenderArgs& A, SecRay& R, int32_t
 
 // Ray complete: write its transmittance (or hand it to the exact slow path).
 template <bool S, bool FAST, bool PURE>
-__device__ __forceinline__ void sec_finish(const RenderArgs& A, uint64_t t, SecRay& R, Ctr& c) {
+__device__ __forceinline__ void sec_finish(const RenderArgs& A, SecRay& R, Ctr& c) {
     if constexpr (S) {  // secondary-stage diagnostics in otherwise unused counter slots
         if (R.tau >= A.tau_cut) {
             c.v[kCtrSteps]++;                 // rays ended by the optical-depth cut-off
@@ -652,31 +652,72 @@ __device__ __forceinline__ bool sec_step(const RenderArgs& A, SecRay& R, int* st
 // the two divergence costs of one-ray-per-lane traversal: a wave no longer waits for its longest
 // ray, and a leaf visit no longer stalls the lanes that are still walking inner nodes.
 // ---------------------------------------------------------------------------------------------
-struct LeafQueue {  // FIFO of up to 2 leaf refs (registers) + the leaf being tested
+// FIFO of up to QCAP leaf refs + the leaf being tested. QCAP = 2 or 4: the first two entries live
+// in registers (q0, q1), entries 2 and 3 in the two LDS words per lane just above the traversal
+// stack (ext[0], ext[BLOCK]). QCAP = 1 + 2^k (k >= 2): the head entry in q0, the others in an
+// LDS ring of QCAP - 1 words above the stack, ring head in q1. A lane may take a NODE step while
+// the queue has room for the 2 leaves a step can add, so a lane holding queued leaves keeps
+// walking the tree.
+template <int QCAP>
+constexpr bool kQueueRing = QCAP > 4;
+template <int QCAP>
+constexpr int kQueueLds = kQueueRing<QCAP> ? QCAP - 1 : QCAP - 2;  // LDS words per lane of the queue
+
+struct LeafQueue {
     int32_t q0, q1;
     int n;
     uint32_t j, end;  // current primitive range [j, end)
-    // branch-free: writes r at slot `idx` (no slot matches idx < 0)
-    __device__ __forceinline__ void put(int idx, int32_t r) {
-        q0 = idx == 0 ? r : q0;
-        q1 = idx == 1 ? r : q1;
+    // branch-free for the register entries: writes r at slot `idx` (no slot matches idx < 0)
+    template <int QCAP, int BLOCK>
+    __device__ __forceinline__ void put(int idx, int32_t r, int* ext) {
+        if constexpr (kQueueRing<QCAP>) {
+            q0 = idx == 0 ? r : q0;
+            if (idx >= 1) ext[((q1 + idx - 1) & (QCAP - 2)) * BLOCK] = r;
+        } else {
+            q0 = idx == 0 ? r : q0;
+            q1 = idx == 1 ? r : q1;
+            if constexpr (QCAP > 2)
+                if (idx >= 2) ext[(idx - 2) * BLOCK] = r;
+        }
     }
     __device__ __forceinline__ bool has_prim() const { return j < end || n > 0; }
-    __device__ __forceinline__ uint32_t next() {  // requires has_prim()
+    template <int QCAP, int BLOCK>
+    __device__ __forceinline__ uint32_t next(int* ext) {  // requires has_prim()
         if (j == end) {
             j = leaf_first(q0);
             end = j + leaf_count(q0);
-            q0 = q1;
+            if constexpr (kQueueRing<QCAP>) {
+                if (n > 1) {
+                    q0 = ext[(q1 & (QCAP - 2)) * BLOCK];
+                    q1 = (q1 + 1) & (QCAP - 2);
+                }
+            } else {
+                q0 = q1;
+                if constexpr (QCAP > 2) {
+                    if (n > 2) {
+                        q1 = ext[0];
+                        if (n > 3) ext[0] = ext[BLOCK];
+                    }
+                }
+            }
             --n;
         }
         return j++;
     }
 };
 
+// Traversal-stack entries past the STACK held in LDS spill to this lane's slots of the global
+// overflow buffer (kMaxDepth - STACK entries per lane of the resident grid; rarely touched).
+template <int BLOCK, int STACK>
+__device__ __forceinline__ uint32_t ovf_slot(int sp) {
+    const uint32_t lane_id = blockIdx.x * BLOCK + threadIdx.x;
+    return lane_id * (uint32_t)(kMaxDepth - STACK) + (uint32_t)(sp - STACK);
+}
+
 // One child-pair step of the postponed-leaf traversal: leaf children go to the queue (nearer
 // first); node < 0 afterwards means the traversal is finished. Written branch-free (bitwise
 // predicates, selects) so a wave does not split inside the step.
-template <int BLOCK, bool S>
+template <int BLOCK, bool S, int QCAP, int STACK>
 __device__ __forceinline__ void sec_node(const RenderArgs& A, SecRay& R, int* stack, int& sp, int& node, LeafQueue& Q,
                                          Ctr& c) {
     if constexpr (S) {
@@ -704,20 +745,21 @@ __device__ __forceinline__ void sec_node(const RenderArgs& A, SecRay& R, int* st
     const int32_t near_ref = r_near ? nc.y : nc.x, far_ref = r_near ? nc.x : nc.y;
     // leaves -> queue, nearer first
     const int32_t first_leaf = (ll & lr) ? near_ref : (ll ? nc.x : nc.y);
-    Q.put((ll | lr) ? Q.n : -1, first_leaf);
-    Q.put((ll & lr) ? Q.n + 1 : -1, far_ref);
+    Q.put<QCAP, BLOCK>((ll | lr) ? Q.n : -1, first_leaf, stack + STACK * BLOCK);
+    Q.put<QCAP, BLOCK>((ll & lr) ? Q.n + 1 : -1, far_ref, stack + STACK * BLOCK);
     Q.n += (int)ll + (int)lr;
     // inner children -> continue / stack
     const bool il = hl & !ll, ir = hr & !lr;
     if (il & ir) {
-        stack[sp * BLOCK] = far_ref;
+        if (sp < STACK) stack[sp * BLOCK] = far_ref;
+        else A.stack_ovf[ovf_slot<BLOCK, STACK>(sp)] = far_ref;
         ++sp;
     }
     if (il | ir) {
         node = (il & ir) ? near_ref : (il ? nc.x : nc.y);
     } else if (sp > 0) {
         --sp;
-        node = stack[sp * BLOCK];
+        node = sp < STACK ? stack[sp * BLOCK] : A.stack_ovf[ovf_slot<BLOCK, STACK>(sp)];
     } else {
         node = -1;
     }
@@ -794,6 +836,7 @@ constexpr int kNodeListCentral = -2, kNodeListOther = -3;
 __device__ __forceinline__ void list_begin(const RenderArgs& A, SecRay& R, LeafQueue& Q, int& node) {
     Q.n = 0;
     Q.j = Q.end = 0;
+    Q.q1 = 0;  // ring head (ring queues): valid whenever the tree walk starts here
     R.listed = false;
     node = 0;
     if (!A.list_ok) return;
@@ -812,6 +855,8 @@ __device__ __forceinline__ void list_begin(const RenderArgs& A, SecRay& R, LeafQ
         Q.j = (uint32_t)Q.q0;
         Q.end = (uint32_t)Q.q1;
         node = kNodeListOther;
+    } else {
+        Q.q1 = 0;
     }
 }
 
@@ -824,17 +869,31 @@ __device__ __forceinline__ void list_advance(LeafQueue& Q, int& node) {
         node = kNodeListOther;
     } else {
         Q.j = Q.end = 0;
+        Q.q1 = 0;  // ring head (ring queues) / unused
         node = 0;
     }
 }
 
+// Shader clock read ordered after the values a, b exist (diagnostics only: the compiler would
+// otherwise move a plain clock read across the arithmetic it is meant to time).
+__device__ __forceinline__ uint64_t clock_after(float a, int b) {
+    uint64_t t;
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t) : "v"(a), "v"(b) : "memory");
+    return t;
+}
+
+// P = true (diagnostics, VR_WW_PROF=1 on the instrumented run): lane 0 of every wave accumulates
+// into the secondary counter slots: [0] NODE iterations, [1] PRIM iterations, [2] lanes in NODE
+// iterations, [3] lanes in PRIM iterations, [4] live lanes, [5] lanes whose NODE step waits for
+// leaf-queue room, [6] lanes that could take either step, [7] iterations with a refill (sums over
+// iterations). VR_WW_PROF=2: [4] NODE, [5] PRIM, [6] refill + finish shader-clock cycles instead.
 // 6 waves/SIMD = 80 VGPRs: the ray state is kept small enough for that without scratch spills (a
 // spilling 6-wave build measured 9 % slower than 5 waves; this one is 5 % faster than 5 waves).
-template <int BLOCK, int STACK, bool S, bool PURE, int WAVES = 6>
-__global__ __launch_bounds__(BLOCK, WAVES) void secondary_ww_kernel(RenderArgs A, uint32_t nrec,
-                                                                                            uint64_t total, int refill_min,
-                                                                                            int prim_bias) {
-    __shared__ int s_stack[STACK * BLOCK];
+template <int BLOCK, int STACK, bool S, bool PURE, int WAVES = 6, bool P = false, int QCAP = 2>
+__global__ __launch_bounds__(BLOCK, WAVES) void secondary_ww_kernel(RenderArgs A, uint32_t nrec, uint64_t total,
+                                                                    int refill_min, int prim_bias, int prof_clock, int node_steps,
+                                                                    int prim_steps) {
+    __shared__ int s_stack[(STACK + kQueueLds<QCAP>) * BLOCK];
     int* stack = s_stack + threadIdx.x;
     const uint32_t lane = threadIdx.x & 63u;
     Ctr c{};
@@ -845,9 +904,14 @@ __global__ __launch_bounds__(BLOCK, WAVES) void secondary_ww_kernel(RenderArgs A
     bool live = false;
     uint64_t pool = 0, pool_end = 0;  // wave-uniform: ray ids fetched but not yet handed out
     bool counter_done = false;        // wave-uniform: the global ray counter has passed `total`
+    uint64_t pc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    uint64_t tA = 0, tB = 0;
     for (;;) {
+        if constexpr (P)
+            if (prof_clock) tA = clock_after(R.tau, node);
         const uint64_t idle = __ballot(!live);
-        if (__popcll(idle) >= refill_min) {  // refill once enough lanes are idle (amortises sec_init)
+        if (__popcll(idle) >= refill_min) {
+            if constexpr (P) pc[7]++;  // refill once enough lanes are idle (amortises sec_init)
             if (pool == pool_end && !counter_done) {
                 uint64_t base = 0;
                 // a whole record chunk (64 records x all their samples, see ray_slot) per fetch
@@ -877,39 +941,72 @@ __global__ __launch_bounds__(BLOCK, WAVES) void secondary_ww_kernel(RenderArgs A
             if (counter_done && pool == pool_end) break;
             continue;
         }
+        if constexpr (P) {
+            if (prof_clock) {
+                tB = clock_after(R.tau, node + (int)t + (int)live);
+                pc[6] += tB - tA;
+            } else {
+                pc[4] += (uint64_t)__popcll(__ballot(live));
+                pc[5] += (uint64_t)__popcll(__ballot(live && node >= 0 && Q.n > 0));
+                pc[6] += (uint64_t)__popcll(__ballot(live && node >= 0 && Q.n == 0 && Q.has_prim()));
+            }
+        }
         const bool has_prim = live && Q.has_prim();
-        const bool can_node = live && node >= 0 && Q.n == 0;  // room for the 2 leaves a step can queue
+        const bool can_node = live && node >= 0 && (QCAP == 2 ? Q.n == 0 : Q.n <= QCAP - 2);  // room for the 2 leaves a step can queue
         const int np = __popcll(__ballot(has_prim)), nn = __popcll(__ballot(can_node));
         // whichever kind more lanes can use; never a kind no lane can use (that would not progress)
-        if (nn == 0 || (np > 0 && np + prim_bias >= nn)) {  // PRIM iteration
-            if (has_prim) {
-                const bool from_list = node <= kNodeListCentral;
-                const uint32_t j = from_list ? (uint32_t)A.rec_list[Q.j++] : Q.next();
-                if constexpr (S) c.v[kCtrPrims]++;
-                const GRec g = load_rec(A.gauss, (int)j);
-                const Quad q = quad_fast(g, R.ray);
-                float a, b;
-                // a tree leaf skips the record's list members (already summed)
-                if (!(R.listed && !from_list && q.Cq <= kListR2) && intersect_fast(q, a, b)) {
-                    const int slot = act_find(A, R, (int)j);
-                    float lo = a;
-                    if (slot >= 0) {
-                        lo = 0.0f;
-                        R.hitmask |= 1ull << slot;
+        const bool prim_iter = nn == 0 || (np > 0 && np + prim_bias >= nn);
+        if (prim_iter) {  // PRIM iteration: up to `prim_steps` primitive tests per lane
+            bool go = has_prim;
+            for (int k = 0; k < prim_steps; ++k) {
+                if (go) {
+                    const bool from_list = node <= kNodeListCentral;
+                    const uint32_t j = from_list ? (uint32_t)A.rec_list[Q.j++] : Q.next<QCAP, BLOCK>(stack + STACK * BLOCK);
+                    if constexpr (S) c.v[from_list ? kCtrMu : kCtrPrims]++;  // list members counted apart
+                    const GRec g = load_rec(A.gauss, (int)j);
+                    const Quad q = quad_fast(g, R.ray);
+                    float a, b;
+                    // a tree leaf skips the record's list members (already summed)
+                    if (!(R.listed && !from_list && q.Cq <= kListR2) && intersect_fast(q, a, b)) {
+                        const int slot = act_find(A, R, (int)j);
+                        float lo = a;
+                        if (slot >= 0) {
+                            lo = 0.0f;
+                            R.hitmask |= 1ull << slot;
+                        }
+                        sec_add<S, true, PURE>(A, R, g, q, lo, b, c);
                     }
-                    sec_add<S, true, PURE>(A, R, g, q, lo, b, c);
+                    list_advance(Q, node);
                 }
-                list_advance(Q, node);
+                go = go && Q.has_prim() && R.tau < A.tau_cut;
             }
-        } else {  // NODE iteration
-            if (can_node) sec_node<BLOCK, S>(A, R, stack, sp, node, Q, c);
+        } else {  // NODE iteration: up to `node_steps` child-pair steps per lane
+            bool go = can_node;
+            for (int k = 0; k < node_steps; ++k) {
+                if (go) sec_node<BLOCK, S, QCAP, STACK>(A, R, stack, sp, node, Q, c);
+                go = go && node >= 0 && Q.n <= QCAP - 2;
+            }
+        }
+        if constexpr (P) {
+            pc[prim_iter ? 1 : 0]++;
+            pc[prim_iter ? 3 : 2] += (uint64_t)(prim_iter ? np : nn);
+            if (prof_clock) {
+                const uint64_t tC = clock_after(R.tau, node + sp + Q.n + (int)Q.j);
+                pc[prim_iter ? 5 : 4] += tC - tB;
+                tA = tC;
+            }
         }
         if (live && (R.tau >= A.tau_cut || (node == -1 && !Q.has_prim()))) {
-            sec_finish<S, true, PURE>(A, t, R, c);
+            sec_finish<S, true, PURE>(A, R, c);
             live = false;
         }
+        if constexpr (P)
+            if (prof_clock) pc[6] += clock_after(R.tau, (int)live) - tA;
     }
     if constexpr (S) flush_counters(A.work + kNumCtr, c);
+    if constexpr (P)
+        if (lane == 0)
+            for (int i = 0; i < 8; ++i) atomicAdd(A.work + kNumCtr + i, (unsigned long long)pc[i]);
 }
 
 // One ray per lane, grid-stride over ray ids [t_begin, t_end) (light rays: already coherent —
@@ -928,7 +1025,7 @@ __global__ __launch_bounds__(BLOCK) void secondary_simple_kernel(RenderArgs A, u
         int sp = 0, node = 0;
         while (!sec_step<BLOCK, S, FAST, PURE>(A, R, stack, sp, node, c)) {
         }
-        sec_finish<S, FAST, PURE>(A, t, R, c);
+        sec_finish<S, FAST, PURE>(A, R, c);
     }
     if constexpr (S)
         for (int i = 0; i < kNumCtr; ++i)
@@ -1043,33 +1140,59 @@ hipError_t gauss_march(const RenderArgs& A, hipStream_t stream, bool stats) {
     return stats ? march_pass<true>(A, stream) : march_pass<false>(A, stream);
 }
 
+// One launch of the persistent kernel: one resident grid (every CU filled to the kernel's occupancy).
+template <int STACK, bool S, bool PURE, bool P, int QCAP, int WAVES = 6>
+static hipError_t ww_launch(const RenderArgs& A, uint32_t nrec, uint64_t total, hipStream_t stream, int refill_min,
+                            int prim_bias, int prof_clock) {
+    static const int node_steps = getenv("VR_WW_NK") ? atoi(getenv("VR_WW_NK")) : 6;
+    static const int prim_steps = getenv("VR_WW_PK") ? atoi(getenv("VR_WW_PK")) : 6;
+    constexpr int kWaves = PURE ? 5 : WAVES;  // PureRayMarching's marched depth does not fit 80 VGPRs without spills
+    const void* fn = (const void*)dev::secondary_ww_kernel<kBlockSecondary, STACK, S, PURE, kWaves, P, QCAP>;
+    int dv = 0, cus = 0, per_cu = 0;
+    if (hipGetDevice(&dv) != hipSuccess) return hipErrorUnknown;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dv) != hipSuccess) return hipErrorUnknown;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, kBlockSecondary, 0) != hipSuccess || per_cu < 1)
+        per_cu = 1;
+    uint64_t grid = (uint64_t)cus * (uint64_t)per_cu;
+    const uint64_t need = (total + kBlockSecondary - 1) / kBlockSecondary;
+    if (grid > need) grid = need;
+    if (grid * kBlockSecondary > A.stack_ovf_lanes) grid = A.stack_ovf_lanes / kBlockSecondary;  // overflow slots
+    if (grid == 0) return hipErrorInvalidValue;
+    hipLaunchKernelGGL((dev::secondary_ww_kernel<kBlockSecondary, STACK, S, PURE, kWaves, P, QCAP>), dim3((unsigned)grid),
+                       dim3(kBlockSecondary), 0, stream, A, nrec, total, refill_min, prim_bias, prof_clock,
+                       node_steps < 1 ? 1 : node_steps, prim_steps < 1 ? 1 : prim_steps);
+    return hipGetLastError();
+}
+
 template <bool S, bool FAST, bool PURE>
 static hipError_t secondary_launch(const RenderArgs& A, uint32_t nrec, uint64_t total, hipStream_t stream, int variant) {
     if (variant == 2) {  // persistent while-while kernel (default)
-        static const int refill_min = getenv("VR_WW_REFILL") ? atoi(getenv("VR_WW_REFILL")) : 32;
+        static const int refill_min = getenv("VR_WW_REFILL") ? atoi(getenv("VR_WW_REFILL")) : 24;
         static const int prim_bias = getenv("VR_WW_BIAS") ? atoi(getenv("VR_WW_BIAS")) : 0;
+        static const int qcap = getenv("VR_WW_QCAP") ? atoi(getenv("VR_WW_QCAP")) : 9;
+        static const int waves = getenv("VR_WW_WAVES") ? atoi(getenv("VR_WW_WAVES")) : 6;
         const int rmin = refill_min < 1 ? 1 : (refill_min > 64 ? 64 : refill_min);
         hipError_t e = hipMemsetAsync(A.ray_next, 0, sizeof(unsigned long long), stream);
         if (e != hipSuccess) return e;
-        static const bool force_deep = getenv("VR_WW_STACK") && atoi(getenv("VR_WW_STACK")) == kStackSize;
-        // smallest LDS stack the tree fits (a child-pair traversal pushes at most depth - 1 entries)
-        const bool shallow = !force_deep && A.bvh_depth <= kShallowStack + 1;
-        const void* fn = shallow ? (const void*)dev::secondary_ww_kernel<kBlockSecondary, kShallowStack, S, PURE>
-                                 : (const void*)dev::secondary_ww_kernel<kBlockSecondary, kStackSize, S, PURE>;
-        int dv = 0, cus = 0, per_cu = 0;
-        if (hipGetDevice(&dv) != hipSuccess) return hipErrorUnknown;
-        if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dv) != hipSuccess) return hipErrorUnknown;
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, kBlockSecondary, 0) != hipSuccess || per_cu < 1)
-            per_cu = 1;
-        uint64_t grid = (uint64_t)cus * (uint64_t)per_cu;
-        const uint64_t need = (total + kBlockSecondary - 1) / kBlockSecondary;
-        if (grid > need) grid = need;
-        if (shallow)
-            hipLaunchKernelGGL((dev::secondary_ww_kernel<kBlockSecondary, kShallowStack, S, PURE>), dim3((unsigned)grid),
-                               dim3(kBlockSecondary), 0, stream, A, nrec, total, rmin, prim_bias);
+        static const int prof = getenv("VR_WW_PROF") ? atoi(getenv("VR_WW_PROF")) : 0;
+        // LDS words per lane: STACK traversal entries + the leaf queue's LDS part (QCAP 4: 2, ring: QCAP - 1)
+        if (S && prof)  // diagnostics in place of the work counts (S selects the counting run)
+            e = ww_launch<kShallowStack, false, PURE, true, 4>(A, nrec, total, stream, rmin, prim_bias, prof == 2);
+        else if (qcap == 4 && waves == 5)
+            e = ww_launch<kShallowStack, S, PURE, false, 4, 5>(A, nrec, total, stream, rmin, prim_bias, 0);
+        else if (qcap == 9 && waves == 5)
+            e = ww_launch<22, S, PURE, false, 9, 5>(A, nrec, total, stream, rmin, prim_bias, 0);
+        else if (qcap == 17 && waves == 5)
+            e = ww_launch<14, S, PURE, false, 17, 5>(A, nrec, total, stream, rmin, prim_bias, 0);
+        else if (qcap == 17)
+            e = ww_launch<10, S, PURE, false, 17>(A, nrec, total, stream, rmin, prim_bias, 0);
+        else if (qcap == 9)
+            e = ww_launch<18, S, PURE, false, 9>(A, nrec, total, stream, rmin, prim_bias, 0);
+        else if (qcap == 5)
+            e = ww_launch<22, S, PURE, false, 5>(A, nrec, total, stream, rmin, prim_bias, 0);
         else
-            hipLaunchKernelGGL((dev::secondary_ww_kernel<kBlockSecondary, kStackSize, S, PURE>), dim3((unsigned)grid),
-                               dim3(kBlockSecondary), 0, stream, A, nrec, total, rmin, prim_bias);
+            e = ww_launch<kShallowStack, S, PURE, false, 4>(A, nrec, total, stream, rmin, prim_bias, 0);
+        if (e != hipSuccess) return e;
     } else {  // one ray per thread
         uint64_t blocks = (total + kBlockSecondary - 1) / kBlockSecondary;
         if (blocks > 65536ull * 16ull) blocks = 65536ull * 16ull;
@@ -1113,7 +1236,10 @@ hipError_t gauss_secondary(const RenderArgs& A, uint32_t nrec, hipStream_t strea
     // canonical, non-speculative work of a near-first BVH traversal per secondary ray, which is
     // what the roofline's algorithmic flops are defined on (the persistent kernel's postponed
     // leaves make it do a little more, speculatively).
-    const int v = stats ? 0 : variant;
+    // VR_WW_COUNT=1: instrument the persistent kernel itself instead (diagnostics; list-member
+    // tests are then counted in the kCtrMu slot).
+    static const bool ww_count = getenv("VR_WW_COUNT") && getenv("VR_WW_COUNT")[0] == '1';
+    const int v = stats ? (ww_count ? 2 : 0) : variant;
     if (A.pure) {
         if (stats) return secondary_launch<true, true, true>(A, nrec, total, stream, v);
         return secondary_launch<false, true, true>(A, nrec, total, stream, v);

@@ -118,6 +118,8 @@ struct RenderArgs {
     uint32_t* slowq;                // light rays needing the exact stopping event: [0] count, [1..] ray ids
     uint32_t slowq_cap;
     unsigned long long* ray_next;   // persistent secondary kernel: next unclaimed ray id
+    int32_t* stack_ovf;             // persistent secondary kernel: traversal-stack entries past its LDS stack
+    uint32_t stack_ovf_lanes;       // lanes (grid x block) the overflow buffer holds
     int32_t* rec_list;              // per record kListCap slots: central members from the front, others from the back
     uint32_t* rec_nlist;            // per record: central count | others << 16; 0xffffffff = no list (overflow)
     int32_t list_ok;                // scene allows neighbour lists (all covariances positive definite)
