@@ -34,6 +34,8 @@ struct vr_ctx {
     int32_t num_prims = 0;
     GaussianRecord* d_gauss = nullptr;
     BVHNode* d_nodes = nullptr;
+    HNode* d_hnodes = nullptr;
+    float hn_center[3] = {0, 0, 0}, hn_scale = 1.0f;
     SphereRecord* d_spheres = nullptr;
     std::vector<LightRecord> lights;
     float env[3] = {0, 0, 0};
@@ -87,11 +89,84 @@ vr_status hip_fail(hipError_t e, const char* what) {
 void free_scene(vr_ctx* c) {
     if (c->d_gauss) (void)hipFree(c->d_gauss);
     if (c->d_nodes) (void)hipFree(c->d_nodes);
+    if (c->d_hnodes) (void)hipFree(c->d_hnodes);
+    c->d_hnodes = nullptr;
     if (c->d_spheres) (void)hipFree(c->d_spheres);
     c->d_gauss = nullptr;
     c->d_nodes = nullptr;
     c->d_spheres = nullptr;
     c->has_scene = false;
+}
+
+// ---- half-precision node copy for the secondary rays ----
+uint16_t f16_bits(_Float16 h) {
+    uint16_t b;
+    std::memcpy(&b, &h, 2);
+    return b;
+}
+double f16_to_double(uint16_t b) {
+    _Float16 h;
+    std::memcpy(&h, &b, 2);
+    return (double)h;
+}
+uint16_t f16_step(uint16_t h, bool up) {  // next representable half toward +inf (up) or -inf
+    const bool neg = h & 0x8000u;
+    if ((h & 0x7fffu) == 0) return up ? 0x0001u : 0x8001u;
+    return (uint16_t)((neg != up) ? h + 1 : h - 1);
+}
+uint16_t f16_directed(double v, bool up) {  // smallest half >= v (up) / largest half <= v
+    if (std::isinf(v)) return v > 0 ? 0x7c00u : 0xfc00u;
+    uint16_t h = f16_bits((_Float16)v);  // nearest, then stepped outward
+    if (up) {
+        while (f16_to_double(h) < v) h = f16_step(h, true);
+    } else {
+        while (f16_to_double(h) > v) h = f16_step(h, false);
+    }
+    return h;
+}
+
+// Builds the 32-B half-precision node copy (HNode) when the scene suits it: f16 keeps ~11 bits,
+// so boxes widen by up to ~1e-3 of the scene's half extent; scenes whose leaf boxes are small
+// against that (median leaf box under 3 % of the half extent) keep the f32 nodes only.
+vr_status upload_half_nodes(vr_ctx* c, const std::vector<BVHNode>& nodes) {
+    if (c->d_hnodes) (void)hipFree(c->d_hnodes);
+    c->d_hnodes = nullptr;
+    if (getenv("VR_NO_HALF_NODES")) return VR_OK;
+    double half = 0.0;
+    for (int k = 0; k < 3; ++k) {
+        c->hn_center[k] = 0.5f * (c->bmin[k] + c->bmax[k]);
+        half = std::max(half, 0.5 * ((double)c->bmax[k] - (double)c->bmin[k]));
+    }
+    if (!(half > 0.0) || !std::isfinite(half)) return VR_OK;
+    c->hn_scale = (float)(1.0 / half);
+    std::vector<float> leaf_ext;
+    for (const BVHNode& n : nodes)
+        for (int side = 0; side < 2; ++side)
+            if (n.c[side] < 0) {
+                float e = 0.0f;
+                for (int k = 0; k < 3; ++k) e = std::max(e, n.f[6 * side + 3 + k] - n.f[6 * side + k]);
+                leaf_ext.push_back(e);
+            }
+    if (!leaf_ext.empty()) {
+        std::nth_element(leaf_ext.begin(), leaf_ext.begin() + leaf_ext.size() / 2, leaf_ext.end());
+        if (!(leaf_ext[leaf_ext.size() / 2] >= 0.03 * half)) return VR_OK;
+    }
+    std::vector<HNode> hn(nodes.size());
+    for (size_t i = 0; i < nodes.size(); ++i) {
+        for (int side = 0; side < 2; ++side) {
+            for (int k = 0; k < 3; ++k) {
+                const float lo = nodes[i].f[6 * side + k], hi = nodes[i].f[6 * side + 3 + k];
+                const double ulo = std::isinf(lo) ? (double)lo : ((double)lo - c->hn_center[k]) * (double)c->hn_scale;
+                const double uhi = std::isinf(hi) ? (double)hi : ((double)hi - c->hn_center[k]) * (double)c->hn_scale;
+                hn[i].h[6 * side + k] = f16_directed(ulo, false);
+                hn[i].h[6 * side + 3 + k] = f16_directed(uhi, true);
+            }
+            hn[i].c[side] = nodes[i].c[side];
+        }
+    }
+    HIP_TRY(hipMalloc(&c->d_hnodes, hn.size() * sizeof(HNode)), "hipMalloc(half nodes)");
+    HIP_TRY(hipMemcpy(c->d_hnodes, hn.data(), hn.size() * sizeof(HNode), hipMemcpyHostToDevice), "hipMemcpy(half nodes)");
+    return VR_OK;
 }
 
 // Farthest distance any ray can travel before leaving the scene box: the rays of both camera
@@ -183,6 +258,9 @@ vr_status fill_args(vr_ctx* c, const vr_camera* cam, const vr_render_params* p, 
     A.tiles_x = (W + kTile - 1) / kTile;
     A.gauss = c->d_gauss;
     A.nodes = c->d_nodes;
+    A.hnodes = c->d_hnodes;
+    for (int k = 0; k < 3; ++k) A.hn_center[k] = c->hn_center[k];
+    A.hn_scale = c->hn_scale;
     A.spheres = c->d_spheres;
     A.num_prims = c->num_prims;
     A.bvh_depth = c->bvh_depth;
@@ -446,6 +524,7 @@ vr_status vr_upload_scene(vr_ctx* c, const vr_scene* sc) {
         HIP_TRY(hipMemcpy(c->d_nodes, b.nodes.data(), b.nodes.size() * sizeof(BVHNode), hipMemcpyHostToDevice), "hipMemcpy(nodes)");
         c->num_prims = (int32_t)N;
         c->bvh_depth = b.max_depth;
+        if (vr_status hs = upload_half_nodes(c, b.nodes); hs != VR_OK) return hs;
         // neighbour lists rely on the 3.15-sigma boxes bounding {q <= kListR2}: true for positive
         // definite covariances with a finite inverse
         c->list_ok = true;

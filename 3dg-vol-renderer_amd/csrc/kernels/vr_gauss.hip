@@ -433,7 +433,8 @@ __device__ __forceinline__ bool ray_slot(uint32_t t, uint32_t nrec, uint32_t ns,
     return r < nrec;
 }
 
-__device__ __forceinline__ bool sec_init(const RenderArgs& A, uint32_t nrec, uint64_t t, SecRay& R) {
+// norm: slab-test terms in the half nodes' scene-normalised coordinates (HNode).
+__device__ __forceinline__ bool sec_init(const RenderArgs& A, uint32_t nrec, uint64_t t, SecRay& R, bool norm = false) {
     uint32_t s, r;
     if (!ray_slot((uint32_t)t, nrec, (uint32_t)(A.num_lights + A.env_samples), s, r)) return false;  // padding id
     R.slot = s * nrec + r;
@@ -467,12 +468,20 @@ __device__ __forceinline__ bool sec_init(const RenderArgs& A, uint32_t nrec, uin
         R.lim = 0.0f;  // last event so far
     }
     // |d| clamped away from 0: the fma slab form b/d - o/d must never see inf - inf
-    R.ix = __frcp_rn(fabsf(R.ray.dx) > 1e-30f ? R.ray.dx : copysignf(1e-30f, R.ray.dx));
-    R.iy = __frcp_rn(fabsf(R.ray.dy) > 1e-30f ? R.ray.dy : copysignf(1e-30f, R.ray.dy));
-    R.iz = __frcp_rn(fabsf(R.ray.dz) > 1e-30f ? R.ray.dz : copysignf(1e-30f, R.ray.dz));
-    R.oxi = R.ray.ox * R.ix;
-    R.oyi = R.ray.oy * R.iy;
-    R.ozi = R.ray.oz * R.iz;
+    const float sc = norm ? A.hn_scale : 1.0f;
+    const float dx = R.ray.dx * sc, dy = R.ray.dy * sc, dz = R.ray.dz * sc;
+    R.ix = __frcp_rn(fabsf(dx) > 1e-30f ? dx : copysignf(1e-30f, dx));
+    R.iy = __frcp_rn(fabsf(dy) > 1e-30f ? dy : copysignf(1e-30f, dy));
+    R.iz = __frcp_rn(fabsf(dz) > 1e-30f ? dz : copysignf(1e-30f, dz));
+    if (norm) {
+        R.oxi = (R.ray.ox - A.hn_center[0]) * sc * R.ix;
+        R.oyi = (R.ray.oy - A.hn_center[1]) * sc * R.iy;
+        R.ozi = (R.ray.oz - A.hn_center[2]) * sc * R.iz;
+    } else {
+        R.oxi = R.ray.ox * R.ix;
+        R.oyi = R.ray.oy * R.iy;
+        R.ozi = R.ray.oz * R.iz;
+    }
     return true;
 }
 
@@ -717,24 +726,41 @@ __device__ __forceinline__ uint32_t ovf_slot(int sp) {
 // One child-pair step of the postponed-leaf traversal: leaf children go to the queue (nearer
 // first); node < 0 afterwards means the traversal is finished. Written branch-free (bitwise
 // predicates, selects) so a wave does not split inside the step.
-template <int BLOCK, bool S, int QCAP, int STACK>
+template <int BLOCK, bool S, int QCAP, int STACK, bool H>
 __device__ __forceinline__ void sec_node(const RenderArgs& A, SecRay& R, int* stack, int& sp, int& node, LeafQueue& Q,
                                          Ctr& c) {
     if constexpr (S) {
         c.v[kCtrNodes]++;
         ++R.nsteps;
     }
-    const float4* np = reinterpret_cast<const float4*>(A.nodes + node);
-    const float4 n0 = np[0], n1 = np[1], n2 = np[2];
-    const int4 nc = reinterpret_cast<const int4*>(A.nodes + node)[3];
-    const float tx1 = fmaf(n0.x, R.ix, -R.oxi), tx2 = fmaf(n0.w, R.ix, -R.oxi);
-    const float ty1 = fmaf(n0.y, R.iy, -R.oyi), ty2 = fmaf(n1.x, R.iy, -R.oyi);
-    const float tz1 = fmaf(n0.z, R.iz, -R.ozi), tz2 = fmaf(n1.y, R.iz, -R.ozi);
+    float f[12];  // left min xyz, left max xyz, right min xyz, right max xyz
+    int2 nc;
+    if constexpr (H) {  // 32-B half node, scene-normalised coordinates (R.ix.. are normalised too)
+        const uint4* np = reinterpret_cast<const uint4*>(A.hnodes + node);
+        const uint4 a = np[0], b = np[1];
+        const uint32_t w[6] = {a.x, a.y, a.z, a.w, b.x, b.y};
+#pragma unroll
+        for (int i = 0; i < 6; ++i) {
+            f[2 * i] = (float)__builtin_bit_cast(_Float16, (uint16_t)(w[i] & 0xffffu));
+            f[2 * i + 1] = (float)__builtin_bit_cast(_Float16, (uint16_t)(w[i] >> 16));
+        }
+        nc = make_int2((int)b.z, (int)b.w);
+    } else {
+        const float4* np = reinterpret_cast<const float4*>(A.nodes + node);
+        const float4 n0 = np[0], n1 = np[1], n2 = np[2];
+        const int4 c4 = reinterpret_cast<const int4*>(A.nodes + node)[3];
+        f[0] = n0.x, f[1] = n0.y, f[2] = n0.z, f[3] = n0.w, f[4] = n1.x, f[5] = n1.y;
+        f[6] = n1.z, f[7] = n1.w, f[8] = n2.x, f[9] = n2.y, f[10] = n2.z, f[11] = n2.w;
+        nc = make_int2(c4.x, c4.y);
+    }
+    const float tx1 = fmaf(f[0], R.ix, -R.oxi), tx2 = fmaf(f[3], R.ix, -R.oxi);
+    const float ty1 = fmaf(f[1], R.iy, -R.oyi), ty2 = fmaf(f[4], R.iy, -R.oyi);
+    const float tz1 = fmaf(f[2], R.iz, -R.ozi), tz2 = fmaf(f[5], R.iz, -R.ozi);
     const float lmin = fmaxf(fmaxf(fminf(tx1, tx2), fminf(ty1, ty2)), fminf(tz1, tz2));
     const float lmax = fminf(fminf(fmaxf(tx1, tx2), fmaxf(ty1, ty2)), fmaxf(tz1, tz2));
-    const float ux1 = fmaf(n1.z, R.ix, -R.oxi), ux2 = fmaf(n2.y, R.ix, -R.oxi);
-    const float uy1 = fmaf(n1.w, R.iy, -R.oyi), uy2 = fmaf(n2.z, R.iy, -R.oyi);
-    const float uz1 = fmaf(n2.x, R.iz, -R.ozi), uz2 = fmaf(n2.w, R.iz, -R.ozi);
+    const float ux1 = fmaf(f[6], R.ix, -R.oxi), ux2 = fmaf(f[9], R.ix, -R.oxi);
+    const float uy1 = fmaf(f[7], R.iy, -R.oyi), uy2 = fmaf(f[10], R.iy, -R.oyi);
+    const float uz1 = fmaf(f[8], R.iz, -R.ozi), uz2 = fmaf(f[11], R.iz, -R.ozi);
     const float rmin = fmaxf(fmaxf(fminf(ux1, ux2), fminf(uy1, uy2)), fminf(uz1, uz2));
     const float rmax = fminf(fminf(fmaxf(ux1, ux2), fmaxf(uy1, uy2)), fmaxf(uz1, uz2));
     const float lim = R.light ? R.lim + kTPad * (1.0f + R.lim) : INFINITY;
@@ -889,7 +915,7 @@ __device__ __forceinline__ uint64_t clock_after(float a, int b) {
 // iterations). VR_WW_PROF=2: [4] NODE, [5] PRIM, [6] refill + finish shader-clock cycles instead.
 // 6 waves/SIMD = 80 VGPRs: the ray state is kept small enough for that without scratch spills (a
 // spilling 6-wave build measured 9 % slower than 5 waves; this one is 5 % faster than 5 waves).
-template <int BLOCK, int STACK, bool S, bool PURE, int WAVES = 6, bool P = false, int QCAP = 2>
+template <int BLOCK, int STACK, bool S, bool PURE, int WAVES = 6, bool P = false, int QCAP = 2, bool H = false>
 __global__ __launch_bounds__(BLOCK, WAVES) void secondary_ww_kernel(RenderArgs A, uint32_t nrec, uint64_t total,
                                                                     int refill_min, int prim_bias, int prof_clock, int node_steps,
                                                                     int prim_steps) {
@@ -927,7 +953,7 @@ __global__ __launch_bounds__(BLOCK, WAVES) void secondary_ww_kernel(RenderArgs A
             if (!live && pool + rank < pool_end) {
                 t = (uint32_t)(pool + rank);
                 if constexpr (S) c.v[kCtrSecRays]++;
-                live = sec_init(A, nrec, t, R);  // false: padding id, or complete already (Tr written)
+                live = sec_init(A, nrec, t, R, H);  // false: padding id, or complete already (Tr written)
                 sp = 0;
                 node = -1;
                 Q.n = 0;
@@ -983,7 +1009,7 @@ __global__ __launch_bounds__(BLOCK, WAVES) void secondary_ww_kernel(RenderArgs A
         } else {  // NODE iteration: up to `node_steps` child-pair steps per lane
             bool go = can_node;
             for (int k = 0; k < node_steps; ++k) {
-                if (go) sec_node<BLOCK, S, QCAP, STACK>(A, R, stack, sp, node, Q, c);
+                if (go) sec_node<BLOCK, S, QCAP, STACK, H>(A, R, stack, sp, node, Q, c);
                 go = go && node >= 0 && Q.n <= QCAP - 2;
             }
         }
@@ -1141,13 +1167,13 @@ hipError_t gauss_march(const RenderArgs& A, hipStream_t stream, bool stats) {
 }
 
 // One launch of the persistent kernel: one resident grid (every CU filled to the kernel's occupancy).
-template <int STACK, bool S, bool PURE, bool P, int QCAP, int WAVES = 6>
+template <int STACK, bool S, bool PURE, bool P, int QCAP, int WAVES = 6, bool H = false>
 static hipError_t ww_launch(const RenderArgs& A, uint32_t nrec, uint64_t total, hipStream_t stream, int refill_min,
                             int prim_bias, int prof_clock) {
     static const int node_steps = getenv("VR_WW_NK") ? atoi(getenv("VR_WW_NK")) : 6;
     static const int prim_steps = getenv("VR_WW_PK") ? atoi(getenv("VR_WW_PK")) : 6;
     constexpr int kWaves = PURE ? 5 : WAVES;  // PureRayMarching's marched depth does not fit 80 VGPRs without spills
-    const void* fn = (const void*)dev::secondary_ww_kernel<kBlockSecondary, STACK, S, PURE, kWaves, P, QCAP>;
+    const void* fn = (const void*)dev::secondary_ww_kernel<kBlockSecondary, STACK, S, PURE, kWaves, P, QCAP, H>;
     int dv = 0, cus = 0, per_cu = 0;
     if (hipGetDevice(&dv) != hipSuccess) return hipErrorUnknown;
     if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dv) != hipSuccess) return hipErrorUnknown;
@@ -1158,7 +1184,7 @@ static hipError_t ww_launch(const RenderArgs& A, uint32_t nrec, uint64_t total, 
     if (grid > need) grid = need;
     if (grid * kBlockSecondary > A.stack_ovf_lanes) grid = A.stack_ovf_lanes / kBlockSecondary;  // overflow slots
     if (grid == 0) return hipErrorInvalidValue;
-    hipLaunchKernelGGL((dev::secondary_ww_kernel<kBlockSecondary, STACK, S, PURE, kWaves, P, QCAP>), dim3((unsigned)grid),
+    hipLaunchKernelGGL((dev::secondary_ww_kernel<kBlockSecondary, STACK, S, PURE, kWaves, P, QCAP, H>), dim3((unsigned)grid),
                        dim3(kBlockSecondary), 0, stream, A, nrec, total, refill_min, prim_bias, prof_clock,
                        node_steps < 1 ? 1 : node_steps, prim_steps < 1 ? 1 : prim_steps);
     return hipGetLastError();
@@ -1169,29 +1195,20 @@ static hipError_t secondary_launch(const RenderArgs& A, uint32_t nrec, uint64_t 
     if (variant == 2) {  // persistent while-while kernel (default)
         static const int refill_min = getenv("VR_WW_REFILL") ? atoi(getenv("VR_WW_REFILL")) : 24;
         static const int prim_bias = getenv("VR_WW_BIAS") ? atoi(getenv("VR_WW_BIAS")) : 0;
-        static const int qcap = getenv("VR_WW_QCAP") ? atoi(getenv("VR_WW_QCAP")) : 9;
-        static const int waves = getenv("VR_WW_WAVES") ? atoi(getenv("VR_WW_WAVES")) : 6;
         const int rmin = refill_min < 1 ? 1 : (refill_min > 64 ? 64 : refill_min);
         hipError_t e = hipMemsetAsync(A.ray_next, 0, sizeof(unsigned long long), stream);
         if (e != hipSuccess) return e;
         static const int prof = getenv("VR_WW_PROF") ? atoi(getenv("VR_WW_PROF")) : 0;
-        // LDS words per lane: STACK traversal entries + the leaf queue's LDS part (QCAP 4: 2, ring: QCAP - 1)
+        // LDS words per lane: 18 traversal-stack entries (deeper ones overflow to global memory) +
+        // the 8-entry LDS ring of the 9-entry leaf queue = 26 (6 blocks of 256 lanes per CU).
+        const bool half = A.hnodes != nullptr;
         if (S && prof)  // diagnostics in place of the work counts (S selects the counting run)
-            e = ww_launch<kShallowStack, false, PURE, true, 4>(A, nrec, total, stream, rmin, prim_bias, prof == 2);
-        else if (qcap == 4 && waves == 5)
-            e = ww_launch<kShallowStack, S, PURE, false, 4, 5>(A, nrec, total, stream, rmin, prim_bias, 0);
-        else if (qcap == 9 && waves == 5)
-            e = ww_launch<22, S, PURE, false, 9, 5>(A, nrec, total, stream, rmin, prim_bias, 0);
-        else if (qcap == 17 && waves == 5)
-            e = ww_launch<14, S, PURE, false, 17, 5>(A, nrec, total, stream, rmin, prim_bias, 0);
-        else if (qcap == 17)
-            e = ww_launch<10, S, PURE, false, 17>(A, nrec, total, stream, rmin, prim_bias, 0);
-        else if (qcap == 9)
-            e = ww_launch<18, S, PURE, false, 9>(A, nrec, total, stream, rmin, prim_bias, 0);
-        else if (qcap == 5)
-            e = ww_launch<22, S, PURE, false, 5>(A, nrec, total, stream, rmin, prim_bias, 0);
+            e = half ? ww_launch<18, false, PURE, true, 9, 6, true>(A, nrec, total, stream, rmin, prim_bias, prof == 2)
+                     : ww_launch<18, false, PURE, true, 9, 6, false>(A, nrec, total, stream, rmin, prim_bias, prof == 2);
+        else if (half)
+            e = ww_launch<18, S, PURE, false, 9, 6, true>(A, nrec, total, stream, rmin, prim_bias, 0);
         else
-            e = ww_launch<kShallowStack, S, PURE, false, 4>(A, nrec, total, stream, rmin, prim_bias, 0);
+            e = ww_launch<18, S, PURE, false, 9, 6, false>(A, nrec, total, stream, rmin, prim_bias, 0);
         if (e != hipSuccess) return e;
     } else {  // one ray per thread
         uint64_t blocks = (total + kBlockSecondary - 1) / kBlockSecondary;

@@ -35,6 +35,16 @@ struct BVHNode {
 };
 static_assert(sizeof(BVHNode) == 64, "node must be 64 B");
 
+// The same child-pair node at half precision (secondary rays): the two children's boxes in
+// scene-normalised coordinates u = (x - hn_center) * hn_scale, rounded outward to f16 (min down,
+// max up), so every box still contains the f32 one. Ray parameters t are unchanged by the
+// normalisation (o' + t d' = (o + t d - c) s), so the slab test is the f32 one on a wider box.
+struct HNode {
+    uint16_t h[12];  // [6 side + k]: min xyz, [6 side + 3 + k]: max xyz, side 0 = left
+    int32_t c[2];
+};
+static_assert(sizeof(HNode) == 32, "half node must be 32 B");
+
 constexpr int kLeafMax = 4;          // primitives per leaf
 constexpr int kMaxDepth = 30;        // builder guarantees node depth <= kMaxDepth
 constexpr int kStackSize = 32;       // traversal stack entries (>= kMaxDepth + 1)
@@ -83,6 +93,8 @@ struct RenderArgs {
     // scene
     const GaussianRecord* gauss;
     const BVHNode* nodes;
+    const HNode* hnodes;      // nullptr: the scene is not suited to half-precision boxes (see vr_device.cpp)
+    float hn_center[3], hn_scale;
     const SphereRecord* spheres;
     int32_t num_prims;
     int32_t bvh_depth;  // deepest node level of the uploaded BVH (root = 1)

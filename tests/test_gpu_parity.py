@@ -238,6 +238,18 @@ def test_render_is_bitwise_deterministic():
     assert np.array_equal(a, b)
 
 
+@pytest.mark.parametrize("name", ["50_random.txt", "1000_random.txt"])
+def test_half_precision_nodes_match_f32_nodes(name, monkeypatch):
+    """The secondary kernel's 32-B half-precision BVH nodes (boxes rounded outward in scene-
+    normalised coordinates) visit a superset of the f32 tree's boxes: the same Gaussians are hit,
+    so the frames agree up to summation order. VR_NO_HALF_NODES is read at every scene upload."""
+    path = scene_path(name)
+    a, _ = _render_gpu_gmm(path, 96, 96)
+    monkeypatch.setenv("VR_NO_HALF_NODES", "1")
+    b, _ = _render_gpu_gmm(path, 96, 96)
+    assert float(np.max(np.abs(a - b))) < 2e-6
+
+
 def test_empty_scene_renders_env():
     scene = vr.Scene.from_gaussians(np.zeros((0, 3)), np.zeros((0, 6)), [], [], [vr.Light([0, 1, 0], [1, 1, 1])])
     img = vr.Image(20, 20)
