@@ -67,7 +67,7 @@ struct vr_ctx {
         size_t bytes = 0;
     };
     Buf px_first, px_T, rec_pos, rec_meta, rec_next, rec_act, tr, rec_alloc, rec_bloom, slowq;
-    Buf pcg_jump, ray_next, rec_list, rec_nlist, stack_ovf;
+    Buf pcg_jump, ray_next, rec_list, rec_nlist, stack_ovf, env_order;
     bool list_ok = false;  // all covariances positive definite: neighbour lists are exact
     int pcg_jump_n = -1;
     uint32_t* h_totals = nullptr;  // pinned copy of rec_alloc: [0] records, [1] overflow-pool entries, [2] exceeded
@@ -271,6 +271,9 @@ vr_status fill_args(vr_ctx* c, const vr_camera* cam, const vr_render_params* p, 
     A.env_samples = p->env_samples;
     A.t_eps = p->t_eps;
     A.pure = p->integrator == VR_PURE_RAYMARCH ? 1 : 0;
+    A.env_order = nullptr;  // set per frame by gauss_pipeline
+    A.chunk_rec = 64u;
+    A.chunk_shift = 6u;
     // Secondary-ray optical-depth cut-off. Exact mode (t_eps = 0): 104, where expf(-tau) is already
     // 0 in f32, so stopping is bit-neutral. With an early-out budget t_eps > 0 the cut-off is
     // ln(1/t_eps) + ln(1000): a dropped transmittance is <= 1e-3 * t_eps, a thousandth of the error
@@ -394,6 +397,24 @@ vr_status gauss_pipeline(vr_ctx* c, RenderArgs& A, hipStream_t s, bool stats) {
     HIP_TRY(hipEventRecord(c->ev_stage[1], s), "hipEventRecord");
     HIP_TRY(gauss_lists(A, nrec, s), "neighbour lists");
     HIP_TRY(hipEventRecord(c->ev_stage[2], s), "hipEventRecord");
+    {  // environment rays traced in direction order within chunks of 256 records (see ray_slot)
+        static const bool no_order = getenv("VR_NO_ENV_ORDER") && getenv("VR_NO_ENV_ORDER")[0] == '1';
+        static const uint32_t order_cr = getenv("VR_ENV_CHUNK") ? (uint32_t)atoi(getenv("VR_ENV_CHUNK")) : 64u;
+        uint32_t cr = 64u, shift = 6u;  // power of 2 in [64, 256] (entries hold record-in-chunk in 8 bits)
+        while (cr < order_cr && cr < 256u) cr <<= 1, ++shift;
+        A.env_order = nullptr;
+        A.chunk_rec = 64u;
+        A.chunk_shift = 6u;
+        if (!no_order && A.env_samples > 0 && A.env_samples <= 256) {
+            const uint64_t nch = ((uint64_t)nrec + cr - 1) / cr;
+            if ((st = grow(c->env_order, std::max<uint64_t>(nch, 1) * cr * (uint64_t)A.env_samples * 2ull,
+                           "hipMalloc(environment-ray order)")) != VR_OK)
+                return st;
+            A.env_order = (uint16_t*)c->env_order.p;
+            A.chunk_rec = cr;
+            A.chunk_shift = shift;
+        }
+    }
     HIP_TRY(gauss_secondary(A, nrec, s, stats), "secondary rays");
     HIP_TRY(hipEventRecord(c->ev_stage[3], s), "hipEventRecord");
     HIP_TRY(gauss_accumulate(A, nrec, s), "accumulate");
@@ -472,7 +493,7 @@ void vr_destroy(vr_ctx* c) {
     if (c->h_totals) (void)hipHostFree(c->h_totals);
     for (vr_ctx::Buf* b : {&c->px_first, &c->px_T, &c->rec_pos, &c->rec_meta, &c->rec_next, &c->rec_act, &c->tr,
                            &c->rec_alloc, &c->rec_bloom, &c->slowq, &c->pcg_jump, &c->ray_next, &c->rec_list, &c->rec_nlist,
-                           &c->stack_ovf})
+                           &c->stack_ovf, &c->env_order})
         if (b->p) (void)hipFree(b->p);
     if (c->d_frame) (void)hipFree(c->d_frame);
     if (c->ev_start) (void)hipEventDestroy(c->ev_start);

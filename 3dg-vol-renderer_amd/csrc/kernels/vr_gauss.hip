@@ -375,8 +375,9 @@ struct SecRay {
     float tau, lim;                   // optical depth so far; light: dist, env: +inf
     // `lim`: a light ray's distance to the light; an environment ray's last event so far (the
     // reference's t_env_end, test_integrators.h:258-271), which bounds nothing during traversal
-    uint64_t hitmask, bloom;
-    uint32_t act_off, act_n;
+    uint64_t hitmask;  // which of the record's active Gaussians the ray has met
+    uint64_t bloom;    // membership mask of the record's active list (act_find)
+    uint32_t act_off, act_n;  // the record's active list
     bool light, needs_stop;
     uint32_t nsteps;  // instrumented build only: node steps taken by this ray
     uint32_t rec;     // record index
@@ -403,8 +404,10 @@ __device__ __forceinline__ void env_sample_dir(const RenderArgs& A, const uint4&
     env_dir(xi1, xi2, wx, wy, wz);
 }
 
-// Octahedral direction cell (8 x 8) used to group environment rays for coherent traversal.
-__device__ __forceinline__ uint32_t dir_cell(float x, float y, float z) {
+// Direction key of an environment ray: octahedral map of the unit sphere onto [-1, 1]^2, 16 x 16
+// cells numbered in Morton order (neighbouring keys = neighbouring directions).
+constexpr int kEnvCells = 256;
+__device__ __forceinline__ uint32_t dir_key(float x, float y, float z) {
     const float n = fabsf(x) + fabsf(y) + fabsf(z);
     float u = x / n, v = y / n;
     if (z < 0.0f) {
@@ -413,30 +416,83 @@ __device__ __forceinline__ uint32_t dir_cell(float x, float y, float z) {
         u = uu;
         v = vv;
     }
-    const int cu = min(7, max(0, (int)((u + 1.0f) * 4.0f)));
-    const int cv = min(7, max(0, (int)((v + 1.0f) * 4.0f)));
-    return (uint32_t)(cu * 8 + cv);
+    const uint32_t cu = (uint32_t)min(15, max(0, (int)((u + 1.0f) * 8.0f)));
+    const uint32_t cv = (uint32_t)min(15, max(0, (int)((v + 1.0f) * 8.0f)));
+    uint32_t k = 0;
+#pragma unroll
+    for (int b = 0; b < 4; ++b) k |= (((cu >> b) & 1u) << (2 * b)) | (((cv >> b) & 1u) << (2 * b + 1));
+    return k;
 }
 
-// Start ray t = s * nrec + r. Returns false if the ray is already complete (Tr written).
-// Ray ids are scheduled record-chunk-major: id t covers record r = 64 * chunk + (t mod 64) and
-// sample s (light, then environment), where chunk = t / (64 * NS) and s = (t mod 64 NS) / 64. The
-// 64 * NS rays of a chunk share 64 records' data (position, active list, neighbour list), so a
-// wave that takes consecutive ids reads each record from its cache instead of once per sample.
-// The result slot stays sample-major: tr[s * nrec + r].
-__device__ __forceinline__ bool ray_slot(uint32_t t, uint32_t nrec, uint32_t ns, uint32_t& s, uint32_t& r) {
-    const uint32_t per = 64u * ns;
-    const uint32_t chunk = t / per;
-    const uint32_t rem = t - chunk * per;
-    s = rem >> 6;
-    r = chunk * 64u + (rem & 63u);
+// One workgroup per record chunk: counting sort of the chunk's environment rays by direction key
+// (order inside a key is arbitrary: every ray's result is independent of when it is traced).
+template <int BLOCK>
+__global__ __launch_bounds__(BLOCK) void env_order_kernel(RenderArgs A, uint32_t nrec) {
+    __shared__ uint32_t hist[kEnvCells];
+    const uint32_t cr = A.chunk_rec, ne = (uint32_t)A.env_samples;
+    const uint32_t n = cr * ne, r0 = blockIdx.x * cr;
+    for (uint32_t i = threadIdx.x; i < kEnvCells; i += BLOCK) hist[i] = 0;
+    __syncthreads();
+    auto key = [&](uint32_t i) -> uint32_t {
+        const uint32_t rl = i / ne, r = r0 + rl;
+        if (r >= nrec) return kEnvCells - 1;  // padding records
+        float wx, wy, wz;
+        env_sample_dir(A, A.rec_meta[r], i - rl * ne, wx, wy, wz);
+        return dir_key(wx, wy, wz);
+    };
+    for (uint32_t i = threadIdx.x; i < n; i += BLOCK) atomicAdd(&hist[key(i)], 1u);
+    __syncthreads();
+    if (threadIdx.x < 64) {  // exclusive scan of the 256 counts by one wave (4 per lane)
+        const uint32_t l = threadIdx.x;
+        const uint32_t a = hist[4 * l], b = hist[4 * l + 1], c = hist[4 * l + 2], d = hist[4 * l + 3];
+        uint32_t sum = a + b + c + d, incl = sum;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t y = __shfl_up(incl, o, 64);
+            if (l >= (uint32_t)o) incl += y;
+        }
+        const uint32_t ex = incl - sum;
+        hist[4 * l] = ex;
+        hist[4 * l + 1] = ex + a;
+        hist[4 * l + 2] = ex + a + b;
+        hist[4 * l + 3] = ex + a + b + c;
+    }
+    __syncthreads();
+    uint16_t* out = A.env_order + (size_t)blockIdx.x * n;
+    for (uint32_t i = threadIdx.x; i < n; i += BLOCK) {
+        const uint32_t rl = i / ne;
+        out[atomicAdd(&hist[key(i)], 1u)] = (uint16_t)((rl << 8) | (i - rl * ne));
+    }
+}
+
+// Ray ids are scheduled record-chunk-major: a chunk is A.chunk_rec consecutive records x all
+// their samples (light rays first, then environment rays), so a wave that takes consecutive ids
+// reads each record's data (position, active list, neighbour list) from its cache instead of
+// once per sample. Light rays of a chunk go sample-major (neighbouring records towards the same
+// light: coherent). Environment rays are random directions; with A.env_order they are handed
+// out in the direction order env_order_kernel computed for the chunk, so a wave traces similar
+// directions from nearby records. The result slot stays sample-major: tr[s * nrec + r].
+__device__ __forceinline__ bool ray_slot(const RenderArgs& A, uint32_t chunk, uint32_t rem, uint32_t nrec, uint32_t& s,
+                                         uint32_t& r) {
+    const uint32_t cr = A.chunk_rec, lights = cr * (uint32_t)A.num_lights;
+    if (A.env_order == nullptr || rem < lights) {
+        s = rem >> A.chunk_shift;
+        r = chunk * cr + (rem & (cr - 1u));
+    } else {  // entry = record-in-chunk << 8 | environment sample
+        const uint32_t v = A.env_order[(size_t)chunk * (cr * (uint32_t)A.env_samples) + (rem - lights)];
+        s = (uint32_t)A.num_lights + (v & 0xffu);
+        r = chunk * cr + (v >> 8);
+    }
     return r < nrec;
 }
 
-// norm: slab-test terms in the half nodes' scene-normalised coordinates (HNode).
-__device__ __forceinline__ bool sec_init(const RenderArgs& A, uint32_t nrec, uint64_t t, SecRay& R, bool norm = false) {
+// Start ray `rem` of record chunk `chunk`. Returns false if the ray is already complete (Tr
+// written) or a padding id. norm: slab-test terms in the half nodes' scene-normalised
+// coordinates (HNode).
+__device__ __forceinline__ bool sec_init(const RenderArgs& A, uint32_t nrec, uint32_t chunk, uint32_t rem, SecRay& R,
+                                         bool norm = false) {
     uint32_t s, r;
-    if (!ray_slot((uint32_t)t, nrec, (uint32_t)(A.num_lights + A.env_samples), s, r)) return false;  // padding id
+    if (!ray_slot(A, chunk, rem, nrec, s, r)) return false;  // padding id
     R.slot = s * nrec + r;
     const float4 pos = A.rec_pos[r];
     const uint4 meta = A.rec_meta[r];
@@ -916,7 +972,7 @@ __device__ __forceinline__ uint64_t clock_after(float a, int b) {
 // 6 waves/SIMD = 80 VGPRs: the ray state is kept small enough for that without scratch spills (a
 // spilling 6-wave build measured 9 % slower than 5 waves; this one is 5 % faster than 5 waves).
 template <int BLOCK, int STACK, bool S, bool PURE, int WAVES = 6, bool P = false, int QCAP = 2, bool H = false>
-__global__ __launch_bounds__(BLOCK, WAVES) void secondary_ww_kernel(RenderArgs A, uint32_t nrec, uint64_t total,
+__global__ __launch_bounds__(BLOCK, WAVES) void secondary_ww_kernel(RenderArgs A, uint32_t nrec, uint32_t nchunks,
                                                                     int refill_min, int prim_bias, int prof_clock, int node_steps,
                                                                     int prim_steps) {
     __shared__ int s_stack[(STACK + kQueueLds<QCAP>) * BLOCK];
@@ -928,8 +984,10 @@ __global__ __launch_bounds__(BLOCK, WAVES) void secondary_ww_kernel(RenderArgs A
     uint32_t t = 0;
     int sp = 0, node = -1;
     bool live = false;
-    uint64_t pool = 0, pool_end = 0;  // wave-uniform: ray ids fetched but not yet handed out
-    bool counter_done = false;        // wave-uniform: the global ray counter has passed `total`
+    // wave-uniform: the record chunk being handed out and its rays [pool, pool_end) not yet handed out
+    uint32_t chunk = 0, pool = 0, pool_end = 0;
+    bool counter_done = false;  // wave-uniform: the global chunk counter has passed nchunks
+    const uint32_t per = A.chunk_rec * (uint32_t)(A.num_lights + A.env_samples);
     uint64_t pc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     uint64_t tA = 0, tB = 0;
     for (;;) {
@@ -938,30 +996,30 @@ __global__ __launch_bounds__(BLOCK, WAVES) void secondary_ww_kernel(RenderArgs A
         const uint64_t idle = __ballot(!live);
         if (__popcll(idle) >= refill_min) {
             if constexpr (P) pc[7]++;  // refill once enough lanes are idle (amortises sec_init)
-            if (pool == pool_end && !counter_done) {
-                uint64_t base = 0;
-                // a whole record chunk (64 records x all their samples, see ray_slot) per fetch
-                const uint64_t fetch = 64ull * (uint64_t)(A.num_lights + A.env_samples);
-                if (lane == 0) base = atomicAdd(A.ray_next, fetch);
-                const uint32_t lo = __shfl((uint32_t)base, 0, 64), hi = __shfl((uint32_t)(base >> 32), 0, 64);
-                base = ((uint64_t)hi << 32) | lo;
-                pool = base < total ? base : total;
-                pool_end = base + fetch < total ? base + fetch : total;
-                counter_done = base + fetch >= total;
+            if (pool == pool_end && !counter_done) {  // next record chunk (all samples of its records)
+                uint32_t cnext = 0;
+                if (lane == 0) cnext = (uint32_t)atomicAdd(A.ray_next, 1ull);
+                cnext = __shfl(cnext, 0, 64);
+                if (cnext < nchunks) {
+                    chunk = cnext;
+                    pool = 0;
+                    pool_end = per;
+                }
+                counter_done = cnext + 1u >= nchunks;
             }
             const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(idle >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)idle, 0u));
             if (!live && pool + rank < pool_end) {
-                t = (uint32_t)(pool + rank);
+                t = pool + rank;
                 if constexpr (S) c.v[kCtrSecRays]++;
-                live = sec_init(A, nrec, t, R, H);  // false: padding id, or complete already (Tr written)
+                live = sec_init(A, nrec, chunk, t, R, H);  // false: padding id, or complete already (Tr written)
                 sp = 0;
                 node = -1;
                 Q.n = 0;
                 Q.j = Q.end = 0;
                 if (live) list_begin(A, R, Q, node);
             }
-            const uint64_t handed = (uint64_t)__popcll(idle);
-            pool = pool + handed < pool_end ? pool + handed : pool_end;
+            const uint32_t handed = (uint32_t)__popcll(idle);
+            pool = pool_end - pool > handed ? pool + handed : pool_end;
         }
         if (!__any(live)) {
             if (counter_done && pool == pool_end) break;
@@ -1047,7 +1105,9 @@ __global__ __launch_bounds__(BLOCK) void secondary_simple_kernel(RenderArgs A, u
     for (uint64_t t = t_begin + (uint64_t)blockIdx.x * BLOCK + threadIdx.x; t < t_end; t += stride_t) {
         SecRay R;
         if constexpr (S) c.v[kCtrSecRays]++;
-        if (!sec_init(A, nrec, t, R)) continue;
+        const uint32_t per = A.chunk_rec * (uint32_t)(A.num_lights + A.env_samples);
+        const uint32_t ch = (uint32_t)t / per;
+        if (!sec_init(A, nrec, ch, (uint32_t)t - ch * per, R)) continue;
         int sp = 0, node = 0;
         while (!sec_step<BLOCK, S, FAST, PURE>(A, R, stack, sp, node, c)) {
         }
@@ -1168,7 +1228,8 @@ hipError_t gauss_march(const RenderArgs& A, hipStream_t stream, bool stats) {
 
 // One launch of the persistent kernel: one resident grid (every CU filled to the kernel's occupancy).
 template <int STACK, bool S, bool PURE, bool P, int QCAP, int WAVES = 6, bool H = false>
-static hipError_t ww_launch(const RenderArgs& A, uint32_t nrec, uint64_t total, hipStream_t stream, int refill_min,
+static hipError_t ww_launch(const RenderArgs& A, uint32_t nrec, uint64_t total, uint32_t nchunks, hipStream_t stream,
+                            int refill_min,
                             int prim_bias, int prof_clock) {
     static const int node_steps = getenv("VR_WW_NK") ? atoi(getenv("VR_WW_NK")) : 6;
     static const int prim_steps = getenv("VR_WW_PK") ? atoi(getenv("VR_WW_PK")) : 6;
@@ -1185,13 +1246,14 @@ static hipError_t ww_launch(const RenderArgs& A, uint32_t nrec, uint64_t total, 
     if (grid * kBlockSecondary > A.stack_ovf_lanes) grid = A.stack_ovf_lanes / kBlockSecondary;  // overflow slots
     if (grid == 0) return hipErrorInvalidValue;
     hipLaunchKernelGGL((dev::secondary_ww_kernel<kBlockSecondary, STACK, S, PURE, kWaves, P, QCAP, H>), dim3((unsigned)grid),
-                       dim3(kBlockSecondary), 0, stream, A, nrec, total, refill_min, prim_bias, prof_clock,
+                       dim3(kBlockSecondary), 0, stream, A, nrec, nchunks, refill_min, prim_bias, prof_clock,
                        node_steps < 1 ? 1 : node_steps, prim_steps < 1 ? 1 : prim_steps);
     return hipGetLastError();
 }
 
 template <bool S, bool FAST, bool PURE>
-static hipError_t secondary_launch(const RenderArgs& A, uint32_t nrec, uint64_t total, hipStream_t stream, int variant) {
+static hipError_t secondary_launch(const RenderArgs& A, uint32_t nrec, uint64_t total, uint32_t nchunks, hipStream_t stream,
+                                   int variant) {
     if (variant == 2) {  // persistent while-while kernel (default)
         static const int refill_min = getenv("VR_WW_REFILL") ? atoi(getenv("VR_WW_REFILL")) : 24;
         static const int prim_bias = getenv("VR_WW_BIAS") ? atoi(getenv("VR_WW_BIAS")) : 0;
@@ -1203,12 +1265,12 @@ static hipError_t secondary_launch(const RenderArgs& A, uint32_t nrec, uint64_t 
         // the 8-entry LDS ring of the 9-entry leaf queue = 26 (6 blocks of 256 lanes per CU).
         const bool half = A.hnodes != nullptr;
         if (S && prof)  // diagnostics in place of the work counts (S selects the counting run)
-            e = half ? ww_launch<18, false, PURE, true, 9, 6, true>(A, nrec, total, stream, rmin, prim_bias, prof == 2)
-                     : ww_launch<18, false, PURE, true, 9, 6, false>(A, nrec, total, stream, rmin, prim_bias, prof == 2);
+            e = half ? ww_launch<18, false, PURE, true, 9, 6, true>(A, nrec, total, nchunks, stream, rmin, prim_bias, prof == 2)
+                     : ww_launch<18, false, PURE, true, 9, 6, false>(A, nrec, total, nchunks, stream, rmin, prim_bias, prof == 2);
         else if (half)
-            e = ww_launch<18, S, PURE, false, 9, 6, true>(A, nrec, total, stream, rmin, prim_bias, 0);
+            e = ww_launch<18, S, PURE, false, 9, 6, true>(A, nrec, total, nchunks, stream, rmin, prim_bias, 0);
         else
-            e = ww_launch<18, S, PURE, false, 9, 6, false>(A, nrec, total, stream, rmin, prim_bias, 0);
+            e = ww_launch<18, S, PURE, false, 9, 6, false>(A, nrec, total, nchunks, stream, rmin, prim_bias, 0);
         if (e != hipSuccess) return e;
     } else {  // one ray per thread
         uint64_t blocks = (total + kBlockSecondary - 1) / kBlockSecondary;
@@ -1236,9 +1298,16 @@ hipError_t gauss_lists(const RenderArgs& A, uint32_t nrec, hipStream_t stream) {
 
 hipError_t gauss_secondary(const RenderArgs& A, uint32_t nrec, hipStream_t stream, bool stats) {
     // padded ray-id space of the record-chunk schedule (see ray_slot)
-    const uint64_t total = ((uint64_t)nrec + 63u) / 64u * 64u * (uint64_t)(A.num_lights + A.env_samples);
+    const uint64_t cr = A.chunk_rec;
+    const uint64_t nchunks = ((uint64_t)nrec + cr - 1) / cr;
+    const uint64_t total = nchunks * cr * (uint64_t)(A.num_lights + A.env_samples);
     if (total == 0) return hipSuccess;
     if (total >= 0xffffffffull) return hipErrorInvalidValue;
+    if (A.env_order != nullptr) {
+        hipLaunchKernelGGL(dev::env_order_kernel<256>, dim3((unsigned)nchunks), dim3(256), 0, stream, A, nrec);
+        hipError_t e = hipGetLastError();
+        if (e != hipSuccess) return e;
+    }
     // A/B switches (read once): VR_SECONDARY=s one ray per thread, =p refill-only persistent kernel; VR_SEC_EXACT=1 correctly rounded
     // secondary-ray arithmetic (the fast form is the default).
     static const int variant = [] {  // 2: while-while persistent (default), 0: one ray per thread
@@ -1258,13 +1327,13 @@ hipError_t gauss_secondary(const RenderArgs& A, uint32_t nrec, hipStream_t strea
     static const bool ww_count = getenv("VR_WW_COUNT") && getenv("VR_WW_COUNT")[0] == '1';
     const int v = stats ? (ww_count ? 2 : 0) : variant;
     if (A.pure) {
-        if (stats) return secondary_launch<true, true, true>(A, nrec, total, stream, v);
-        return secondary_launch<false, true, true>(A, nrec, total, stream, v);
+        if (stats) return secondary_launch<true, true, true>(A, nrec, total, (uint32_t)nchunks, stream, v);
+        return secondary_launch<false, true, true>(A, nrec, total, (uint32_t)nchunks, stream, v);
     }
-    if (stats) return exact ? secondary_launch<true, false, false>(A, nrec, total, stream, v)
-                            : secondary_launch<true, true, false>(A, nrec, total, stream, v);
-    return exact ? secondary_launch<false, false, false>(A, nrec, total, stream, v)
-                 : secondary_launch<false, true, false>(A, nrec, total, stream, v);
+    if (stats) return exact ? secondary_launch<true, false, false>(A, nrec, total, (uint32_t)nchunks, stream, v)
+                            : secondary_launch<true, true, false>(A, nrec, total, (uint32_t)nchunks, stream, v);
+    return exact ? secondary_launch<false, false, false>(A, nrec, total, (uint32_t)nchunks, stream, v)
+                 : secondary_launch<false, true, false>(A, nrec, total, (uint32_t)nchunks, stream, v);
 }
 
 hipError_t gauss_accumulate(const RenderArgs& A, uint32_t nrec, hipStream_t stream) {

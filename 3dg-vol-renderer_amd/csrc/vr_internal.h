@@ -134,6 +134,9 @@ struct RenderArgs {
     uint32_t stack_ovf_lanes;       // lanes (grid x block) the overflow buffer holds
     int32_t* rec_list;              // per record kListCap slots: central members from the front, others from the back
     uint32_t* rec_nlist;            // per record: central count | others << 16; 0xffffffff = no list (overflow)
+    uint16_t* env_order;            // per record chunk: its environment rays (record-in-chunk << 8 | sample), direction order
+    uint32_t chunk_rec;             // records per secondary-ray chunk (power of 2; 64 without env_order)
+    uint32_t chunk_shift;           // log2(chunk_rec)
     int32_t list_ok;                // scene allows neighbour lists (all covariances positive definite)
     const unsigned long long* pcg_jump;  // [2k] = A^k, [2k+1] = inc (A^(k-1) + ... + 1): PCG32 state after k draws
 };
