@@ -58,8 +58,8 @@ __device__ float light_transmittance(const RenderArgs& A, const Ray& sr, float d
     float tau = 0.0f;
     bool needs_stop = false;
     uint64_t hitmask = 0;
-    traverse(
-        A.nodes, sr, stack, stride, [&](float tmin, float) { return tmin <= dist + kTPad * (1.0f + dist); },
+    traverse<false>(
+        A, sr, stack, stride, [&](float tmin, float) { return tmin <= dist + kTPad * (1.0f + dist); },
         [&](uint32_t first, uint32_t count) {
             for (uint32_t j = first; j < first + count; ++j) {
                 if constexpr (S) c.v[kCtrPrims]++;
@@ -88,8 +88,8 @@ __device__ float light_transmittance(const RenderArgs& A, const Ray& sr, float d
     if (tau >= kTauCut) return 0.0f;   // exp(-tau) == 0 exactly; later terms are >= 0
     if (needs_stop || missed) {
         float tstop = INFINITY;  // first event at or beyond the light
-        traverse(
-            A.nodes, sr, stack, stride,
+        traverse<false>(
+            A, sr, stack, stride,
             [&](float tmin, float tmax) {
                 return tmax >= dist - kTPad * (1.0f + dist) && tmin <= tstop + kTPad * (1.0f + tstop);
             },
@@ -107,8 +107,8 @@ __device__ float light_transmittance(const RenderArgs& A, const Ray& sr, float d
             NodeCount<S>{&c});
         if (tstop == INFINITY) tstop = dist;
         if (needs_stop) {
-            traverse(
-                A.nodes, sr, stack, stride,
+            traverse<false>(
+                A, sr, stack, stride,
                 [&](float tmin, float tmax) {
                     return tmin <= dist + kTPad * (1.0f + dist) && tmax >= dist - kTPad * (1.0f + dist);
                 },
@@ -148,7 +148,7 @@ __device__ float light_transmittance(const RenderArgs& A, const Ray& sr, float d
 // to the pixel's previous record (px_first / rec_next), so a pixel's records are visited in step
 // order by accumulate_kernel wherever they landed in memory. Records that do not fit the
 // capacity raise rec_alloc[2]; the host then grows the buffers and re-runs the march.
-template <int ACT, bool S>
+template <int ACT, bool S, bool H>
 __device__ int march(const RenderArgs& A, uint32_t p, int px, int py, int* act_base, int* stack, int stride, Ctr& c) {
     const Ray ray = primary_ray(A, px, py);
     const GaussianRecord* __restrict__ G = A.gauss;
@@ -167,8 +167,8 @@ __device__ int march(const RenderArgs& A, uint32_t p, int px, int py, int* act_b
             if (act.n == 0) {  // closest entry strictly after t_lo
                 if constexpr (S) c.v[kCtrPrimQueries]++;
                 float best = INFINITY;
-                traverse(
-                    A.nodes, ray, stack, stride,
+                traverse<H>(
+                    A, ray, stack, stride,
                     [&](float tmin, float tmax) {
                         return tmax >= t_lo - kTPad * (1.0f + fabsf(t_lo)) && tmin <= best + kTPad * (1.0f + best);
                     },
@@ -193,8 +193,8 @@ __device__ int march(const RenderArgs& A, uint32_t p, int px, int py, int* act_b
             // entrants: t_lo < a <= t_k and still inside at t_k (b > t_k)
             if constexpr (S) c.v[kCtrPrimQueries]++;
             bool ovf = false;
-            traverse(
-                A.nodes, ray, stack, stride,
+            traverse<H>(
+                A, ray, stack, stride,
                 [&](float tmin, float tmax) {
                     return tmax >= t_lo - kTPad * (1.0f + fabsf(t_lo)) && tmin <= t_k + kTPad * (1.0f + t_k);
                 },
@@ -311,7 +311,7 @@ __device__ __forceinline__ void mark_error(const RenderArgs& A, uint32_t p) {
     A.px_T[p] = __builtin_nanf("");
 }
 
-template <int ACT, int BLOCK, bool S, int STACK = kStackSize>
+template <int ACT, int BLOCK, bool S, int STACK, bool H>
 __global__ __launch_bounds__(BLOCK) void march_kernel(RenderArgs A) {
     __shared__ int s_act[ACT * BLOCK];
     __shared__ int s_stack[STACK * BLOCK];
@@ -323,7 +323,7 @@ __global__ __launch_bounds__(BLOCK) void march_kernel(RenderArgs A) {
     Ctr c{};
     int st = kOK;
     if (x < (int)A.width && y < (int)A.height) {
-        st = march<ACT, S>(A, p, x, y, s_act + tid, s_stack + tid, BLOCK, c);
+        st = march<ACT, S, H>(A, p, x, y, s_act + tid, s_stack + tid, BLOCK, c);
     } else {
         A.px_first[p] = kNoRecord;
         A.px_T[p] = 0.0f;
@@ -338,7 +338,7 @@ __global__ __launch_bounds__(BLOCK) void march_kernel(RenderArgs A) {
     }
 }
 
-template <int ACT, int BLOCK, bool S>
+template <int ACT, int BLOCK, bool S, bool H>
 __global__ __launch_bounds__(BLOCK) void march_fallback_kernel(RenderArgs A) {
     __shared__ int s_act[ACT * BLOCK];
     __shared__ int s_stack[kStackSize * BLOCK];
@@ -349,7 +349,7 @@ __global__ __launch_bounds__(BLOCK) void march_fallback_kernel(RenderArgs A) {
         int lx, ly, x, y;
         tile_pixel(A, p >> 8, (int)(p & 255u), lx, ly, x, y);
         Ctr c{};
-        int st = march<ACT, S>(A, p, x, y, s_act + tid, s_stack + tid, BLOCK, c);  // re-links px_first
+        int st = march<ACT, S, H>(A, p, x, y, s_act + tid, s_stack + tid, BLOCK, c);  // re-links px_first
         if constexpr (S)
             for (int i = 0; i < kNumCtr; ++i) atomicAdd(A.work + i, (unsigned long long)c.v[i]);
         if (st != kOK) mark_error(A, p);
@@ -428,9 +428,12 @@ __device__ __forceinline__ uint32_t dir_key(float x, float y, float z) {
 // (order inside a key is arbitrary: every ray's result is independent of when it is traced).
 template <int BLOCK>
 __global__ __launch_bounds__(BLOCK) void env_order_kernel(RenderArgs A, uint32_t nrec) {
+    constexpr uint32_t kKeyCap = 16384;  // keys kept in LDS (one byte each); larger chunks recompute them
     __shared__ uint32_t hist[kEnvCells];
+    __shared__ uint8_t keys[kKeyCap];
     const uint32_t cr = A.chunk_rec, ne = (uint32_t)A.env_samples;
     const uint32_t n = cr * ne, r0 = blockIdx.x * cr;
+    const bool cached = n <= kKeyCap;
     for (uint32_t i = threadIdx.x; i < kEnvCells; i += BLOCK) hist[i] = 0;
     __syncthreads();
     auto key = [&](uint32_t i) -> uint32_t {
@@ -440,7 +443,11 @@ __global__ __launch_bounds__(BLOCK) void env_order_kernel(RenderArgs A, uint32_t
         env_sample_dir(A, A.rec_meta[r], i - rl * ne, wx, wy, wz);
         return dir_key(wx, wy, wz);
     };
-    for (uint32_t i = threadIdx.x; i < n; i += BLOCK) atomicAdd(&hist[key(i)], 1u);
+    for (uint32_t i = threadIdx.x; i < n; i += BLOCK) {
+        const uint32_t k = key(i);
+        if (cached) keys[i] = (uint8_t)k;
+        atomicAdd(&hist[k], 1u);
+    }
     __syncthreads();
     if (threadIdx.x < 64) {  // exclusive scan of the 256 counts by one wave (4 per lane)
         const uint32_t l = threadIdx.x;
@@ -461,7 +468,7 @@ __global__ __launch_bounds__(BLOCK) void env_order_kernel(RenderArgs A, uint32_t
     uint16_t* out = A.env_order + (size_t)blockIdx.x * n;
     for (uint32_t i = threadIdx.x; i < n; i += BLOCK) {
         const uint32_t rl = i / ne;
-        out[atomicAdd(&hist[key(i)], 1u)] = (uint16_t)((rl << 8) | (i - rl * ne));
+        out[atomicAdd(&hist[cached ? (uint32_t)keys[i] : key(i)], 1u)] = (uint16_t)((rl << 8) | (i - rl * ne));
     }
 }
 
@@ -791,24 +798,7 @@ __device__ __forceinline__ void sec_node(const RenderArgs& A, SecRay& R, int* st
     }
     float f[12];  // left min xyz, left max xyz, right min xyz, right max xyz
     int2 nc;
-    if constexpr (H) {  // 32-B half node, scene-normalised coordinates (R.ix.. are normalised too)
-        const uint4* np = reinterpret_cast<const uint4*>(A.hnodes + node);
-        const uint4 a = np[0], b = np[1];
-        const uint32_t w[6] = {a.x, a.y, a.z, a.w, b.x, b.y};
-#pragma unroll
-        for (int i = 0; i < 6; ++i) {
-            f[2 * i] = (float)__builtin_bit_cast(_Float16, (uint16_t)(w[i] & 0xffffu));
-            f[2 * i + 1] = (float)__builtin_bit_cast(_Float16, (uint16_t)(w[i] >> 16));
-        }
-        nc = make_int2((int)b.z, (int)b.w);
-    } else {
-        const float4* np = reinterpret_cast<const float4*>(A.nodes + node);
-        const float4 n0 = np[0], n1 = np[1], n2 = np[2];
-        const int4 c4 = reinterpret_cast<const int4*>(A.nodes + node)[3];
-        f[0] = n0.x, f[1] = n0.y, f[2] = n0.z, f[3] = n0.w, f[4] = n1.x, f[5] = n1.y;
-        f[6] = n1.z, f[7] = n1.w, f[8] = n2.x, f[9] = n2.y, f[10] = n2.z, f[11] = n2.w;
-        nc = make_int2(c4.x, c4.y);
-    }
+    load_pair<H>(A, node, f, nc);  // H: scene-normalised coordinates (R.ix.. are normalised too)
     const float tx1 = fmaf(f[0], R.ix, -R.oxi), tx2 = fmaf(f[3], R.ix, -R.oxi);
     const float ty1 = fmaf(f[1], R.iy, -R.oyi), ty2 = fmaf(f[4], R.iy, -R.oyi);
     const float tz1 = fmaf(f[2], R.iz, -R.ozi), tz2 = fmaf(f[5], R.iz, -R.ozi);
@@ -852,30 +842,33 @@ __device__ __forceinline__ void sec_node(const RenderArgs& A, SecRay& R, int* st
 // depths from pos) at the front of the record's slots, the others at the back. All secondary rays
 // of the record test this list first — most of them become opaque right there, without touching
 // the tree — and the tree walk that follows skips exactly these members (same q, bit for bit).
-template <int BLOCK>
+template <int BLOCK, bool H>
 __global__ __launch_bounds__(BLOCK) void record_list_kernel(RenderArgs A, uint32_t nrec) {
     __shared__ int s_stack[kStackSize * BLOCK];
     int* stack = s_stack + threadIdx.x;
     for (uint32_t r = blockIdx.x * BLOCK + threadIdx.x; r < nrec; r += gridDim.x * BLOCK) {
         const float4 pos = A.rec_pos[r];
+        float bx = pos.x, by = pos.y, bz = pos.z;  // the point in the node boxes' coordinates
+        node_space<H>(A, bx, by, bz);
         int32_t* slot = A.rec_list + (size_t)r * kListCap;
         uint32_t nc = 0, nb = 0;
         bool ovf = false;
         int sp = 0, node = 0;
         for (;;) {
-            const float4* np = reinterpret_cast<const float4*>(A.nodes + node);
-            const float4 n0 = np[0], n1 = np[1], n2 = np[2];
-            const int4 ncr = reinterpret_cast<const int4*>(A.nodes + node)[3];
-            const bool inl = (ncr.x != 0) & (n0.x <= pos.x) & (pos.x <= n0.w) & (n0.y <= pos.y) & (pos.y <= n1.x) &
-                             (n0.z <= pos.z) & (pos.z <= n1.y);
-            const bool inr = (ncr.y != 0) & (n1.z <= pos.x) & (pos.x <= n2.y) & (n1.w <= pos.y) & (pos.y <= n2.z) &
-                             (n2.x <= pos.z) & (pos.z <= n2.w);
-            int32_t leaves[2];
-            int nleaf = 0;
-            if (inl && ncr.x < 0) leaves[nleaf++] = ncr.x;
-            if (inr && ncr.y < 0) leaves[nleaf++] = ncr.y;
-            for (int li = 0; li < nleaf; ++li) {
-                const uint32_t first = leaf_first(leaves[li]), count = leaf_count(leaves[li]);
+            float f[12];
+            int2 ncr;
+            load_pair<H>(A, node, f, ncr);
+            const bool inl = (ncr.x != 0) & (f[0] <= bx) & (bx <= f[3]) & (f[1] <= by) & (by <= f[4]) & (f[2] <= bz) &
+                             (bz <= f[5]);
+            const bool inr = (ncr.y != 0) & (f[6] <= bx) & (bx <= f[9]) & (f[7] <= by) & (by <= f[10]) & (f[8] <= bz) &
+                             (bz <= f[11]);
+            // leaf children: one contiguous primitive range each (left first)
+            const bool ll = inl && ncr.x < 0, lr = inr && ncr.y < 0;
+            for (int li = 0; li < 2; ++li) {
+                const bool use = li == 0 ? ll : lr;
+                if (!use) continue;
+                const int32_t ref = li == 0 ? ncr.x : ncr.y;
+                const uint32_t first = leaf_first(ref), count = leaf_count(ref);
                 for (uint32_t j = first; j < first + count; ++j) {
                     const GRec g = load_rec(A.gauss, (int)j);
                     const float q = cq_fast(g, pos.x - g.mx, pos.y - g.my, pos.z - g.mz);
@@ -1202,28 +1195,29 @@ constexpr int kActFast = 16, kBlockFast = 256;
 constexpr int kActFallback = 64, kBlockFallback = 64;
 constexpr int kBlockSecondary = 256;
 
-template <bool S>
+template <bool S, bool H>
 static hipError_t march_pass(const RenderArgs& A, hipStream_t stream) {
     // LDS per 256-lane workgroup = (active-list slots + stack entries) * 1 KiB. Shallow trees use a
-    // 24-entry stack; the 16-slot active list overflows to the 64-slot fallback kernel.
-    static const int act_env = getenv("VR_MARCH_ACT") ? atoi(getenv("VR_MARCH_ACT")) : 16;  // A/B
+    // 24-entry stack; the 16-slot active list overflows to the 64-slot fallback kernel. H: the
+    // half-precision node copy (boxes only propose candidates; every decision is the exact quadratic).
     const bool shallow = A.bvh_depth <= kShallowStack + 1;
-    if (act_env == 32)
-        hipLaunchKernelGGL((dev::march_kernel<32, kBlockFast, S>), dim3(A.num_tiles), dim3(kBlockFast), 0, stream, A);
-    else if (shallow)
-        hipLaunchKernelGGL((dev::march_kernel<kActFast, kBlockFast, S, kShallowStack>), dim3(A.num_tiles),
+    if (shallow)
+        hipLaunchKernelGGL((dev::march_kernel<kActFast, kBlockFast, S, kShallowStack, H>), dim3(A.num_tiles),
                            dim3(kBlockFast), 0, stream, A);
     else
-        hipLaunchKernelGGL((dev::march_kernel<kActFast, kBlockFast, S>), dim3(A.num_tiles), dim3(kBlockFast), 0, stream, A);
+        hipLaunchKernelGGL((dev::march_kernel<kActFast, kBlockFast, S, kStackSize, H>), dim3(A.num_tiles), dim3(kBlockFast),
+                           0, stream, A);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL((dev::march_fallback_kernel<kActFallback, kBlockFallback, S>), dim3(1024), dim3(kBlockFallback), 0,
+    hipLaunchKernelGGL((dev::march_fallback_kernel<kActFallback, kBlockFallback, S, H>), dim3(1024), dim3(kBlockFallback), 0,
                        stream, A);
     return hipGetLastError();
 }
 
 hipError_t gauss_march(const RenderArgs& A, hipStream_t stream, bool stats) {
-    return stats ? march_pass<true>(A, stream) : march_pass<false>(A, stream);
+    static const bool f32_march = getenv("VR_MARCH_F32") && getenv("VR_MARCH_F32")[0] == '1';  // A/B
+    if (A.hnodes != nullptr && !f32_march) return stats ? march_pass<true, true>(A, stream) : march_pass<false, true>(A, stream);
+    return stats ? march_pass<true, false>(A, stream) : march_pass<false, false>(A, stream);
 }
 
 // One launch of the persistent kernel: one resident grid (every CU filled to the kernel's occupancy).
@@ -1291,8 +1285,12 @@ hipError_t gauss_lists(const RenderArgs& A, uint32_t nrec, hipStream_t stream) {
     if (!A.list_ok || nrec == 0) return hipSuccess;
     uint64_t lb = ((uint64_t)nrec + kBlockSecondary - 1) / kBlockSecondary;
     if (lb > 65536ull * 4ull) lb = 65536ull * 4ull;
-    hipLaunchKernelGGL((dev::record_list_kernel<kBlockSecondary>), dim3((unsigned)lb), dim3(kBlockSecondary), 0, stream, A,
-                       nrec);
+    if (A.hnodes != nullptr)
+        hipLaunchKernelGGL((dev::record_list_kernel<kBlockSecondary, true>), dim3((unsigned)lb), dim3(kBlockSecondary), 0,
+                           stream, A, nrec);
+    else
+        hipLaunchKernelGGL((dev::record_list_kernel<kBlockSecondary, false>), dim3((unsigned)lb), dim3(kBlockSecondary), 0,
+                           stream, A, nrec);
     return hipGetLastError();
 }
 

@@ -271,22 +271,62 @@ struct NoCount {
     __device__ __forceinline__ void operator()() const {}
 };
 
-template <class Prune, class Leaf, class OnNode = NoCount>
-__device__ __forceinline__ void traverse(const BVHNode* __restrict__ nodes, const Ray& r, int* stack, int stride,
-                                         Prune prune, Leaf leaf, OnNode on_node = OnNode()) {
+// Child-pair node `node` as 12 box floats (left min xyz, left max xyz, right min xyz, right max
+// xyz) + the two child refs. H: the 32-B half node (HNode, scene-normalised coordinates).
+template <bool H>
+__device__ __forceinline__ void load_pair(const RenderArgs& A, int node, float* f, int2& nc) {
+    if constexpr (H) {
+        const uint4* np = reinterpret_cast<const uint4*>(A.hnodes + node);
+        const uint4 a = np[0], b = np[1];
+        const uint32_t w[6] = {a.x, a.y, a.z, a.w, b.x, b.y};
+#pragma unroll
+        for (int i = 0; i < 6; ++i) {
+            f[2 * i] = (float)__builtin_bit_cast(_Float16, (uint16_t)(w[i] & 0xffffu));
+            f[2 * i + 1] = (float)__builtin_bit_cast(_Float16, (uint16_t)(w[i] >> 16));
+        }
+        nc = make_int2((int)b.z, (int)b.w);
+    } else {
+        const float4* np = reinterpret_cast<const float4*>(A.nodes + node);
+        const float4 n0 = np[0], n1 = np[1], n2 = np[2];
+        const int4 c4 = reinterpret_cast<const int4*>(A.nodes + node)[3];
+        f[0] = n0.x, f[1] = n0.y, f[2] = n0.z, f[3] = n0.w, f[4] = n1.x, f[5] = n1.y;
+        f[6] = n1.z, f[7] = n1.w, f[8] = n2.x, f[9] = n2.y, f[10] = n2.z, f[11] = n2.w;
+        nc = make_int2(c4.x, c4.y);
+    }
+}
+
+// A point in the coordinates of the H = true / false node boxes.
+template <bool H>
+__device__ __forceinline__ void node_space(const RenderArgs& A, float& x, float& y, float& z) {
+    if constexpr (H) {
+        x = (x - A.hn_center[0]) * A.hn_scale;
+        y = (y - A.hn_center[1]) * A.hn_scale;
+        z = (z - A.hn_center[2]) * A.hn_scale;
+    }
+}
+
+template <bool H, typename Prune, typename Leaf, typename OnNode = NoCount>
+__device__ __forceinline__ void traverse(const RenderArgs& A, const Ray& r0, int* stack, int stride, Prune prune, Leaf leaf,
+                                         OnNode on_node = OnNode()) {
+    // H: the ray in the half nodes' normalised coordinates (same parameter t along it)
+    Ray r = r0;
+    if constexpr (H) {
+        node_space<true>(A, r.ox, r.oy, r.oz);
+        r.dx *= A.hn_scale;
+        r.dy *= A.hn_scale;
+        r.dz *= A.hn_scale;
+    }
     const float ix = __frcp_rn(r.dx), iy = __frcp_rn(r.dy), iz = __frcp_rn(r.dz);
     int sp = 0;
     int node = 0;
     for (;;) {
-        const float4* np = reinterpret_cast<const float4*>(nodes + node);
-        float4 n0 = np[0], n1 = np[1], n2 = np[2];
-        int4 nc = reinterpret_cast<const int4*>(nodes + node)[3];
+        float f[12];
+        int2 nc;
+        load_pair<H>(A, node, f, nc);
         on_node();
-        float bl[6] = {n0.x, n0.y, n0.z, n0.w, n1.x, n1.y};
-        float br[6] = {n1.z, n1.w, n2.x, n2.y, n2.z, n2.w};
         float lmin, lmax, rmin, rmax;
-        slab(bl, r, ix, iy, iz, lmin, lmax);
-        slab(br, r, ix, iy, iz, rmin, rmax);
+        slab(f, r, ix, iy, iz, lmin, lmax);
+        slab(f + 6, r, ix, iy, iz, rmin, rmax);
         bool hl = nc.x != 0 && lmax >= fmaxf(lmin, 0.0f) && prune(lmin, lmax);
         bool hr = nc.y != 0 && rmax >= fmaxf(rmin, 0.0f) && prune(rmin, rmax);
         // leaf children are handled at once, nearer first; a leaf callback returning false ends

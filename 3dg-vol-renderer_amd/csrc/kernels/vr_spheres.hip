@@ -191,7 +191,7 @@ __global__ __launch_bounds__(BLOCK) void hitmask_kernel(RenderArgs A, int sphere
                 any = sphere_hit(A.spheres[i], ray, te, tx);
             }
         } else if (A.num_prims > 0) {
-            traverse(A.nodes, ray, s_stack + threadIdx.x, BLOCK, [&](float, float) { return !any; },
+            traverse<false>(A, ray, s_stack + threadIdx.x, BLOCK, [&](float, float) { return !any; },
                      [&](uint32_t first, uint32_t count) {
                          for (uint32_t j = first; j < first + count; ++j) {
                              GRec gg = load_rec(A.gauss, j);
