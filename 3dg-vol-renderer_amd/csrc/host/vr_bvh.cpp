@@ -94,14 +94,14 @@ BVHBuild build_bvh(const std::vector<float>& boxes) {
     };
     static const int kBins = std::min(64, std::max(4, (int)env_or("VR_BVH_BINS", 16)));
     static const float vol_w = (float)env_or("VR_BVH_VOL", 0.0);
-    static const uint32_t leaf_max = (uint32_t)std::min(kLeafMax, std::max(1, (int)env_or("VR_BVH_LEAF", kLeafMax)));
+    static const uint32_t leaf_max = (uint32_t)std::min(16, std::max(1, (int)env_or("VR_BVH_LEAF", kLeafMax)));
     // Depth budget: SAH may go kSlack levels deeper than a perfectly balanced tree, but never past
     // kMaxDepth. Shallow trees let the secondary-ray kernel use a 24-entry LDS stack (more waves per
     // CU); very large scenes fall back to the 32-entry stack.
     constexpr int kSlack = 6;
     static const int depth_env = getenv("VR_BVH_DEPTH") ? atoi(getenv("VR_BVH_DEPTH")) : 0;  // A/B override
     const int depth_cap = depth_env > 0 ? std::min(kMaxDepth, depth_env)
-                                        : std::min(kMaxDepth, std::max(kShallowDepth, ceil_log2((N + kLeafMax - 1) / kLeafMax + 1) + kSlack));
+                                        : std::min(kMaxDepth, std::max(kShallowDepth, ceil_log2((N + leaf_max - 1) / leaf_max + 1) + kSlack));
     while (!work.empty()) {
         Work w = work.back();
         work.pop_back();
@@ -120,7 +120,7 @@ BVHBuild build_bvh(const std::vector<float>& boxes) {
         if (ext[1] > ext[axis]) axis = 1;
         if (ext[2] > ext[axis]) axis = 2;
         uint32_t mid = 0;
-        const bool balanced = w.depth + ceil_log2((count + kLeafMax - 1) / kLeafMax) >= depth_cap - 1;
+        const bool balanced = w.depth + ceil_log2((count + leaf_max - 1) / leaf_max) >= depth_cap - 1;
         if (!balanced && ext[axis] > 0.0f) {
             // binned SAH over all three axes
             float best_cost = INFINITY;

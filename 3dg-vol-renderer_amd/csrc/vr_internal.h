@@ -45,7 +45,7 @@ struct HNode {
 };
 static_assert(sizeof(HNode) == 32, "half node must be 32 B");
 
-constexpr int kLeafMax = 4;          // primitives per leaf
+constexpr int kLeafMax = 3;          // primitives per leaf (<= 16: leaf refs hold count - 1 in 4 bits)
 constexpr int kMaxDepth = 30;        // builder guarantees node depth <= kMaxDepth
 constexpr int kStackSize = 32;       // traversal stack entries (>= kMaxDepth + 1)
 constexpr int kShallowDepth = 24;    // trees this shallow use the 24-entry stack variant
