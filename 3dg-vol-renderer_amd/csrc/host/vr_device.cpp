@@ -35,6 +35,7 @@ struct vr_ctx {
     GaussianRecord* d_gauss = nullptr;
     BVHNode* d_nodes = nullptr;
     HNode* d_hnodes = nullptr;
+    HNode4* d_hnodes4 = nullptr;
     float hn_center[3] = {0, 0, 0}, hn_scale = 1.0f;
     SphereRecord* d_spheres = nullptr;
     std::vector<LightRecord> lights;
@@ -91,6 +92,8 @@ void free_scene(vr_ctx* c) {
     if (c->d_nodes) (void)hipFree(c->d_nodes);
     if (c->d_hnodes) (void)hipFree(c->d_hnodes);
     c->d_hnodes = nullptr;
+    if (c->d_hnodes4) (void)hipFree(c->d_hnodes4);
+    c->d_hnodes4 = nullptr;
     if (c->d_spheres) (void)hipFree(c->d_spheres);
     c->d_gauss = nullptr;
     c->d_nodes = nullptr;
@@ -131,6 +134,8 @@ uint16_t f16_directed(double v, bool up) {  // smallest half >= v (up) / largest
 vr_status upload_half_nodes(vr_ctx* c, const std::vector<BVHNode>& nodes) {
     if (c->d_hnodes) (void)hipFree(c->d_hnodes);
     c->d_hnodes = nullptr;
+    if (c->d_hnodes4) (void)hipFree(c->d_hnodes4);
+    c->d_hnodes4 = nullptr;
     if (getenv("VR_NO_HALF_NODES")) return VR_OK;
     double half = 0.0;
     for (int k = 0; k < 3; ++k) {
@@ -166,6 +171,74 @@ vr_status upload_half_nodes(vr_ctx* c, const std::vector<BVHNode>& nodes) {
     }
     HIP_TRY(hipMalloc(&c->d_hnodes, hn.size() * sizeof(HNode)), "hipMalloc(half nodes)");
     HIP_TRY(hipMemcpy(c->d_hnodes, hn.data(), hn.size() * sizeof(HNode), hipMemcpyHostToDevice), "hipMemcpy(half nodes)");
+
+    // 4-wide collapse for the secondary rays: a pair node's two children, then repeatedly the
+    // inner child with the largest box surface replaced by its own two children, up to 4.
+    if (getenv("VR_NO_WIDE_NODES")) return VR_OK;
+    struct Kid {
+        int side;      // box source: nodes[pair].f[6 side ..]
+        int32_t pair;  // pair node holding this child's box
+        int32_t ref;   // the child's ref in the pair tree
+    };
+    auto area = [&](const Kid& k) {
+        const float* f = &nodes[k.pair].f[6 * k.side];
+        const float d0 = f[3] - f[0], d1 = f[4] - f[1], d2 = f[5] - f[2];
+        return d0 * d1 + d0 * d2 + d1 * d2;
+    };
+    std::vector<HNode4> w4;
+    std::vector<std::pair<int32_t, int32_t>> todo{{0, 0}};  // (pair node, HNode4 slot)
+    w4.emplace_back();
+    while (!todo.empty()) {
+        const auto [pn, slot] = todo.back();
+        todo.pop_back();
+        Kid kids[4];
+        int nk = 0;
+        for (int side = 0; side < 2; ++side)
+            if (nodes[pn].c[side] != 0) kids[nk++] = Kid{side, pn, nodes[pn].c[side]};
+        for (;;) {
+            int best = -1;
+            float best_a = -1.0f;
+            for (int i = 0; i < nk; ++i)
+                if (kids[i].ref > 0) {
+                    const int extra = (nodes[kids[i].ref].c[0] != 0) + (nodes[kids[i].ref].c[1] != 0) - 1;
+                    if (nk + extra <= 4 && area(kids[i]) > best_a) {
+                        best_a = area(kids[i]);
+                        best = i;
+                    }
+                }
+            if (best < 0) break;
+            const int32_t inner = kids[best].ref;
+            Kid repl[2];
+            int nr = 0;
+            for (int side = 0; side < 2; ++side)
+                if (nodes[inner].c[side] != 0) repl[nr++] = Kid{side, inner, nodes[inner].c[side]};
+            kids[best] = repl[0];
+            if (nr == 2) kids[nk++] = repl[1];
+        }
+        HNode4 h{};
+        for (int i = 0; i < 4; ++i) {
+            if (i >= nk) {
+                for (int k = 0; k < 3; ++k) {
+                    h.h[i][k] = 0x7c00u;      // +inf
+                    h.h[i][3 + k] = 0xfc00u;  // -inf
+                }
+                h.c[i] = 0;
+                continue;
+            }
+            for (int k = 0; k < 6; ++k) h.h[i][k] = hn[kids[i].pair].h[6 * kids[i].side + k];
+            if (kids[i].ref < 0) {
+                h.c[i] = kids[i].ref;
+            } else {
+                h.c[i] = (int32_t)w4.size();
+                w4.emplace_back();
+                todo.push_back({kids[i].ref, h.c[i]});
+            }
+        }
+        w4[slot] = h;
+    }
+    HIP_TRY(hipMalloc(&c->d_hnodes4, w4.size() * sizeof(HNode4)), "hipMalloc(wide nodes)");
+    HIP_TRY(hipMemcpy(c->d_hnodes4, w4.data(), w4.size() * sizeof(HNode4), hipMemcpyHostToDevice), "hipMemcpy(wide nodes)");
+    if (getenv("VR_DEBUG")) fprintf(stderr, "[vr] wide BVH: %zu nodes\n", w4.size());
     return VR_OK;
 }
 
@@ -259,6 +332,7 @@ vr_status fill_args(vr_ctx* c, const vr_camera* cam, const vr_render_params* p, 
     A.gauss = c->d_gauss;
     A.nodes = c->d_nodes;
     A.hnodes = c->d_hnodes;
+    A.hnodes4 = c->d_hnodes4;
     for (int k = 0; k < 3; ++k) A.hn_center[k] = c->hn_center[k];
     A.hn_scale = c->hn_scale;
     A.spheres = c->d_spheres;
@@ -377,11 +451,11 @@ vr_status gauss_pipeline(vr_ctx* c, RenderArgs& A, hipStream_t s, bool stats) {
     HIP_TRY(hipMemsetAsync(A.slowq, 0, sizeof(uint32_t), s), "hipMemsetAsync(slow queue)");
     if ((st = grow(c->ray_next, 8, "hipMalloc(ray counter)")) != VR_OK) return st;
     A.ray_next = (unsigned long long*)c->ray_next.p;
-    {  // traversal-stack overflow of the persistent kernel: kMaxDepth entries for every lane it can keep resident
+    {  // traversal-stack overflow of the persistent kernel: kWideStackMax entries for every lane it can keep resident
         int cus = 0;
         HIP_TRY(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, c->device), "hipDeviceGetAttribute");
         const uint64_t lanes = (uint64_t)std::max(cus, 1) * 2048ull;  // 32 waves of 64 lanes per CU at most
-        if ((st = grow(c->stack_ovf, lanes * kMaxDepth * 4ull, "hipMalloc(stack overflow)")) != VR_OK) return st;
+        if ((st = grow(c->stack_ovf, lanes * kWideStackMax * 4ull, "hipMalloc(stack overflow)")) != VR_OK) return st;
         A.stack_ovf = (int32_t*)c->stack_ovf.p;
         A.stack_ovf_lanes = (uint32_t)lanes;
     }

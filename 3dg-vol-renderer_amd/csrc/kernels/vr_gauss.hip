@@ -780,10 +780,92 @@ struct LeafQueue {
 
 // Traversal-stack entries past the STACK held in LDS spill to this lane's slots of the global
 // overflow buffer (kMaxDepth - STACK entries per lane of the resident grid; rarely touched).
-template <int BLOCK, int STACK>
+template <int BLOCK, int STACK, int PER = kMaxDepth>
 __device__ __forceinline__ uint32_t ovf_slot(int sp) {
     const uint32_t lane_id = blockIdx.x * BLOCK + threadIdx.x;
-    return lane_id * (uint32_t)(kMaxDepth - STACK) + (uint32_t)(sp - STACK);
+    return lane_id * (uint32_t)(PER - STACK) + (uint32_t)(sp - STACK);
+}
+
+
+// Sorts (key, ref) pairs ascending by key (compare-exchange).
+__device__ __forceinline__ void cswap(float& ka, int32_t& ra, float& kb, int32_t& rb) {
+    const bool sw = kb < ka;
+    const float k = sw ? kb : ka;
+    kb = sw ? ka : kb;
+    ka = k;
+    const int32_t r = sw ? rb : ra;
+    rb = sw ? ra : rb;
+    ra = r;
+}
+
+// One step of the 4-wide traversal: the four children of HNode4 `node` are tested, sorted near to
+// far (misses last); leaf children go to the leaf queue in that order, the nearest inner child
+// is walked next and the other inner ones are pushed far-first (so the nearer pop first).
+template <int BLOCK, bool S, int QCAP, int STACK>
+__device__ __forceinline__ void sec_node4(const RenderArgs& A, SecRay& R, int* stack, int& sp, int& node, LeafQueue& Q,
+                                          Ctr& c) {
+    if constexpr (S) {
+        c.v[kCtrNodes]++;
+        ++R.nsteps;
+    }
+    const uint4* np = reinterpret_cast<const uint4*>(A.hnodes4 + node);
+    const uint4 q0 = np[0], q1 = np[1], q2 = np[2], rf = np[3];
+    const uint32_t w[12] = {q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, q1.z, q1.w, q2.x, q2.y, q2.z, q2.w};
+    const int32_t ref[4] = {(int32_t)rf.x, (int32_t)rf.y, (int32_t)rf.z, (int32_t)rf.w};
+    const float lim = R.light ? R.lim + kTPad * (1.0f + R.lim) : INFINITY;
+    float key[4];
+    int32_t kr[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        float f[6];
+#pragma unroll
+        for (int k = 0; k < 6; ++k) {
+            const uint32_t word = w[(6 * i + k) >> 1];
+            f[k] = (float)__builtin_bit_cast(_Float16, (uint16_t)(((6 * i + k) & 1) ? (word >> 16) : (word & 0xffffu)));
+        }
+        const float tx1 = fmaf(f[0], R.ix, -R.oxi), tx2 = fmaf(f[3], R.ix, -R.oxi);
+        const float ty1 = fmaf(f[1], R.iy, -R.oyi), ty2 = fmaf(f[4], R.iy, -R.oyi);
+        const float tz1 = fmaf(f[2], R.iz, -R.ozi), tz2 = fmaf(f[5], R.iz, -R.ozi);
+        const float tmin = fmaxf(fmaxf(fminf(tx1, tx2), fminf(ty1, ty2)), fminf(tz1, tz2));
+        const float tmax = fminf(fminf(fmaxf(tx1, tx2), fmaxf(ty1, ty2)), fmaxf(tz1, tz2));
+        const bool hit = (ref[i] != 0) & (tmax >= fmaxf(tmin, 0.0f)) & (tmin <= lim);
+        key[i] = hit ? tmin : INFINITY;
+        kr[i] = hit ? ref[i] : 0;
+    }
+    // 4-input sorting network (5 compare-exchanges)
+    cswap(key[0], kr[0], key[1], kr[1]);
+    cswap(key[2], kr[2], key[3], kr[3]);
+    cswap(key[0], kr[0], key[2], kr[2]);
+    cswap(key[1], kr[1], key[3], kr[3]);
+    cswap(key[1], kr[1], key[2], kr[2]);
+    // leaves -> queue, nearest first
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const bool leaf = kr[i] < 0;
+        Q.put<QCAP, BLOCK>(leaf ? Q.n : -1, kr[i], stack + STACK * BLOCK);
+        Q.n += (int)leaf;
+    }
+    // inner children: the nearest continues, the others are pushed far-first
+    int first = -1;
+#pragma unroll
+    for (int i = 3; i >= 0; --i)
+        if (kr[i] > 0) first = i;
+#pragma unroll
+    for (int i = 3; i >= 0; --i) {
+        if (kr[i] > 0 && i != first) {
+            if (sp < STACK) stack[sp * BLOCK] = kr[i];
+            else A.stack_ovf[ovf_slot<BLOCK, STACK, kWideStackMax>(sp)] = kr[i];
+            ++sp;
+        }
+    }
+    if (first >= 0) {
+        node = kr[first];
+    } else if (sp > 0) {
+        --sp;
+        node = sp < STACK ? stack[sp * BLOCK] : A.stack_ovf[ovf_slot<BLOCK, STACK, kWideStackMax>(sp)];
+    } else {
+        node = -1;
+    }
 }
 
 // One child-pair step of the postponed-leaf traversal: leaf children go to the queue (nearer
@@ -964,7 +1046,8 @@ __device__ __forceinline__ uint64_t clock_after(float a, int b) {
 // iterations). VR_WW_PROF=2: [4] NODE, [5] PRIM, [6] refill + finish shader-clock cycles instead.
 // 6 waves/SIMD = 80 VGPRs: the ray state is kept small enough for that without scratch spills (a
 // spilling 6-wave build measured 9 % slower than 5 waves; this one is 5 % faster than 5 waves).
-template <int BLOCK, int STACK, bool S, bool PURE, int WAVES = 6, bool P = false, int QCAP = 2, bool H = false>
+template <int BLOCK, int STACK, bool S, bool PURE, int WAVES = 6, bool P = false, int QCAP = 2, bool H = false,
+          bool W = false>
 __global__ __launch_bounds__(BLOCK, WAVES) void secondary_ww_kernel(RenderArgs A, uint32_t nrec, uint32_t nchunks,
                                                                     int refill_min, int prim_bias, int prof_clock, int node_steps,
                                                                     int prim_steps) {
@@ -1029,7 +1112,8 @@ __global__ __launch_bounds__(BLOCK, WAVES) void secondary_ww_kernel(RenderArgs A
             }
         }
         const bool has_prim = live && Q.has_prim();
-        const bool can_node = live && node >= 0 && (QCAP == 2 ? Q.n == 0 : Q.n <= QCAP - 2);  // room for the 2 leaves a step can queue
+        constexpr int kRoom = W ? 4 : 2;  // leaves one NODE step can queue
+        const bool can_node = live && node >= 0 && (QCAP == 2 ? Q.n == 0 : Q.n <= QCAP - kRoom);
         const int np = __popcll(__ballot(has_prim)), nn = __popcll(__ballot(can_node));
         // whichever kind more lanes can use; never a kind no lane can use (that would not progress)
         const bool prim_iter = nn == 0 || (np > 0 && np + prim_bias >= nn);
@@ -1060,8 +1144,11 @@ __global__ __launch_bounds__(BLOCK, WAVES) void secondary_ww_kernel(RenderArgs A
         } else {  // NODE iteration: up to `node_steps` child-pair steps per lane
             bool go = can_node;
             for (int k = 0; k < node_steps; ++k) {
-                if (go) sec_node<BLOCK, S, QCAP, STACK, H>(A, R, stack, sp, node, Q, c);
-                go = go && node >= 0 && Q.n <= QCAP - 2;
+                if (go) {
+                    if constexpr (W) sec_node4<BLOCK, S, QCAP, STACK>(A, R, stack, sp, node, Q, c);
+                    else sec_node<BLOCK, S, QCAP, STACK, H>(A, R, stack, sp, node, Q, c);
+                }
+                go = go && node >= 0 && Q.n <= QCAP - kRoom;
             }
         }
         if constexpr (P) {
@@ -1221,14 +1308,14 @@ hipError_t gauss_march(const RenderArgs& A, hipStream_t stream, bool stats) {
 }
 
 // One launch of the persistent kernel: one resident grid (every CU filled to the kernel's occupancy).
-template <int STACK, bool S, bool PURE, bool P, int QCAP, int WAVES = 6, bool H = false>
+template <int STACK, bool S, bool PURE, bool P, int QCAP, int WAVES = 6, bool H = false, bool W = false>
 static hipError_t ww_launch(const RenderArgs& A, uint32_t nrec, uint64_t total, uint32_t nchunks, hipStream_t stream,
                             int refill_min,
                             int prim_bias, int prof_clock) {
     static const int node_steps = getenv("VR_WW_NK") ? atoi(getenv("VR_WW_NK")) : 6;
     static const int prim_steps = getenv("VR_WW_PK") ? atoi(getenv("VR_WW_PK")) : 6;
     constexpr int kWaves = PURE ? 5 : WAVES;  // PureRayMarching's marched depth does not fit 80 VGPRs without spills
-    const void* fn = (const void*)dev::secondary_ww_kernel<kBlockSecondary, STACK, S, PURE, kWaves, P, QCAP, H>;
+    const void* fn = (const void*)dev::secondary_ww_kernel<kBlockSecondary, STACK, S, PURE, kWaves, P, QCAP, H, W>;
     int dv = 0, cus = 0, per_cu = 0;
     if (hipGetDevice(&dv) != hipSuccess) return hipErrorUnknown;
     if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dv) != hipSuccess) return hipErrorUnknown;
@@ -1239,7 +1326,7 @@ static hipError_t ww_launch(const RenderArgs& A, uint32_t nrec, uint64_t total, 
     if (grid > need) grid = need;
     if (grid * kBlockSecondary > A.stack_ovf_lanes) grid = A.stack_ovf_lanes / kBlockSecondary;  // overflow slots
     if (grid == 0) return hipErrorInvalidValue;
-    hipLaunchKernelGGL((dev::secondary_ww_kernel<kBlockSecondary, STACK, S, PURE, kWaves, P, QCAP, H>), dim3((unsigned)grid),
+    hipLaunchKernelGGL((dev::secondary_ww_kernel<kBlockSecondary, STACK, S, PURE, kWaves, P, QCAP, H, W>), dim3((unsigned)grid),
                        dim3(kBlockSecondary), 0, stream, A, nrec, nchunks, refill_min, prim_bias, prof_clock,
                        node_steps < 1 ? 1 : node_steps, prim_steps < 1 ? 1 : prim_steps);
     return hipGetLastError();
@@ -1261,6 +1348,8 @@ static hipError_t secondary_launch(const RenderArgs& A, uint32_t nrec, uint64_t 
         if (S && prof)  // diagnostics in place of the work counts (S selects the counting run)
             e = half ? ww_launch<18, false, PURE, true, 9, 6, true>(A, nrec, total, nchunks, stream, rmin, prim_bias, prof == 2)
                      : ww_launch<18, false, PURE, true, 9, 6, false>(A, nrec, total, nchunks, stream, rmin, prim_bias, prof == 2);
+        else if (half && A.hnodes4 != nullptr)
+            e = ww_launch<18, S, PURE, false, 9, 6, true, true>(A, nrec, total, nchunks, stream, rmin, prim_bias, 0);
         else if (half)
             e = ww_launch<18, S, PURE, false, 9, 6, true>(A, nrec, total, nchunks, stream, rmin, prim_bias, 0);
         else

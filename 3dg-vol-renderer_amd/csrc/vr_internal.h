@@ -45,8 +45,19 @@ struct HNode {
 };
 static_assert(sizeof(HNode) == 32, "half node must be 32 B");
 
+// 4-wide half-precision node for the secondary rays: up to 4 children (boxes as in HNode, same
+// normalisation and outward rounding), collapsed from the child-pair tree. c == 0: empty slot.
+struct HNode4 {
+    uint16_t h[4][6];  // child i: min xyz, max xyz
+    int32_t c[4];      // > 0: HNode4 index, < 0: leaf ref, 0: empty
+};
+static_assert(sizeof(HNode4) == 64, "4-wide half node must be 64 B");
+
 constexpr int kLeafMax = 3;          // primitives per leaf (<= 16: leaf refs hold count - 1 in 4 bits)
 constexpr int kMaxDepth = 30;        // builder guarantees node depth <= kMaxDepth
+// Per-lane traversal-stack capacity of the 4-wide walk (up to 3 pushes per level; the collapsed
+// tree is no deeper than the pair tree): sizes the persistent kernel's global stack overflow.
+constexpr int kWideStackMax = 3 * kMaxDepth + 1;
 constexpr int kStackSize = 32;       // traversal stack entries (>= kMaxDepth + 1)
 constexpr int kShallowDepth = 24;    // trees this shallow use the 24-entry stack variant
 constexpr int kShallowStack = 24;    // (a child-pair traversal pushes at most depth - 1 entries)
@@ -94,6 +105,7 @@ struct RenderArgs {
     const GaussianRecord* gauss;
     const BVHNode* nodes;
     const HNode* hnodes;      // nullptr: the scene is not suited to half-precision boxes (see vr_device.cpp)
+    const HNode4* hnodes4;    // 4-wide collapse of the same tree (secondary rays); nullptr with hnodes
     float hn_center[3], hn_scale;
     const SphereRecord* spheres;
     int32_t num_prims;
