@@ -1346,7 +1346,8 @@ static hipError_t secondary_launch(const RenderArgs& A, uint32_t nrec, uint64_t 
         // the 8-entry LDS ring of the 9-entry leaf queue = 26 (6 blocks of 256 lanes per CU).
         const bool half = A.hnodes != nullptr;
         if (S && prof)  // diagnostics in place of the work counts (S selects the counting run)
-            e = half ? ww_launch<18, false, PURE, true, 9, 6, true>(A, nrec, total, nchunks, stream, rmin, prim_bias, prof == 2)
+            e = half ? ww_launch<18, false, PURE, true, 9, 6, true, true>(A, nrec, total, nchunks, stream, rmin, prim_bias,
+                                                                          prof == 2)
                      : ww_launch<18, false, PURE, true, 9, 6, false>(A, nrec, total, nchunks, stream, rmin, prim_bias, prof == 2);
         else if (half && A.hnodes4 != nullptr)
             e = ww_launch<18, S, PURE, false, 9, 6, true, true>(A, nrec, total, nchunks, stream, rmin, prim_bias, 0);
