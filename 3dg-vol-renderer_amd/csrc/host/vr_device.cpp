@@ -19,6 +19,7 @@ hipError_t gauss_march(const RenderArgs& A, hipStream_t stream, bool stats);
 hipError_t gauss_lists(const RenderArgs& A, uint32_t nrec, hipStream_t stream);
 hipError_t gauss_secondary(const RenderArgs& A, uint32_t nrec, hipStream_t stream, bool stats);
 hipError_t gauss_accumulate(const RenderArgs& A, uint32_t nrec, hipStream_t stream);
+hipError_t gauss_record_cut(const RenderArgs& A, float budget, hipStream_t stream);
 hipError_t launch_unshuffle(const float* slabs, uint32_t nslabs, uint32_t tiles_per_slab, uint32_t tiles_x, uint32_t W,
                             uint32_t H, float* img, hipStream_t stream);
 }  // namespace vr
@@ -68,7 +69,7 @@ struct vr_ctx {
         size_t bytes = 0;
     };
     Buf px_first, px_T, rec_pos, rec_meta, rec_next, rec_act, tr, rec_alloc, rec_bloom, slowq;
-    Buf pcg_jump, ray_next, rec_list, rec_nlist, stack_ovf, env_order;
+    Buf pcg_jump, ray_next, rec_list, rec_nlist, stack_ovf, env_order, rec_cut;
     bool list_ok = false;  // all covariances positive definite: neighbour lists are exact
     int pcg_jump_n = -1;
     uint32_t* h_totals = nullptr;  // pinned copy of rec_alloc: [0] records, [1] overflow-pool entries, [2] exceeded
@@ -346,6 +347,7 @@ vr_status fill_args(vr_ctx* c, const vr_camera* cam, const vr_render_params* p, 
     A.t_eps = p->t_eps;
     A.pure = p->integrator == VR_PURE_RAYMARCH ? 1 : 0;
     A.env_order = nullptr;  // set per frame by gauss_pipeline
+    A.rec_cut = nullptr;
     A.chunk_rec = 64u;
     A.chunk_shift = 6u;
     // Secondary-ray optical-depth cut-off. Exact mode (t_eps = 0): 104, where expf(-tau) is already
@@ -353,6 +355,7 @@ vr_status fill_args(vr_ctx* c, const vr_camera* cam, const vr_render_params* p, 
     // ln(1/t_eps) + ln(1000): a dropped transmittance is <= 1e-3 * t_eps, a thousandth of the error
     // the primary early-out itself is allowed (DESIGN.md §Error budget).
     A.tau_cut = p->t_eps > 0.0f ? std::min(104.0f, (float)(std::log(1.0 / p->t_eps) + std::log(1000.0))) : 104.0f;
+    if (getenv("VR_DBG_TAUCUT")) A.tau_cut = (float)atof(getenv("VR_DBG_TAUCUT"));  // EXPERIMENT
     if (p->integrator != VR_TEST_HITMASK) {
         const float* d;
         int n;
@@ -458,6 +461,18 @@ vr_status gauss_pipeline(vr_ctx* c, RenderArgs& A, hipStream_t s, bool stats) {
         if ((st = grow(c->stack_ovf, lanes * kWideStackMax * 4ull, "hipMalloc(stack overflow)")) != VR_OK) return st;
         A.stack_ovf = (int32_t*)c->stack_ovf.p;
         A.stack_ovf_lanes = (uint32_t)lanes;
+    }
+    {  // per-pixel error budget of the secondary cut-off (record_cut_kernel): budget = t_eps, so the
+       // secondary rays' truncation moves a pixel by at most t_eps, the same bound as the primary
+       // early-out (error budget). t_eps = 0 (exact mode) keeps the bit-neutral 104.
+        const bool no_cut = getenv("VR_NO_REC_CUT") && getenv("VR_NO_REC_CUT")[0] == '1';  // read per frame (tests)
+        static const float budget_scale = getenv("VR_CUT_BUDGET") ? (float)atof(getenv("VR_CUT_BUDGET")) : 1.0f;
+        A.rec_cut = nullptr;
+        if (!no_cut && A.t_eps > 0.0f && nrec > 0) {
+            if ((st = grow(c->rec_cut, (uint64_t)nrec * 4ull, "hipMalloc(record cut-offs)")) != VR_OK) return st;
+            A.rec_cut = (float*)c->rec_cut.p;
+            HIP_TRY(gauss_record_cut(A, A.t_eps * budget_scale, s), "record cut-offs");
+        }
     }
     static const bool no_list = getenv("VR_NOLIST") && getenv("VR_NOLIST")[0] == '1';
     A.list_ok = c->list_ok && !no_list && (uint64_t)nrec * kListCap < 0xffffffffull;
@@ -567,7 +582,7 @@ void vr_destroy(vr_ctx* c) {
     if (c->h_totals) (void)hipHostFree(c->h_totals);
     for (vr_ctx::Buf* b : {&c->px_first, &c->px_T, &c->rec_pos, &c->rec_meta, &c->rec_next, &c->rec_act, &c->tr,
                            &c->rec_alloc, &c->rec_bloom, &c->slowq, &c->pcg_jump, &c->ray_next, &c->rec_list, &c->rec_nlist,
-                           &c->stack_ovf, &c->env_order})
+                           &c->stack_ovf, &c->env_order, &c->rec_cut})
         if (b->p) (void)hipFree(b->p);
     if (c->d_frame) (void)hipFree(c->d_frame);
     if (c->ev_start) (void)hipEventDestroy(c->ev_start);

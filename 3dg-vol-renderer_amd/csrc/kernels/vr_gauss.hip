@@ -375,6 +375,7 @@ struct SecRay {
     float tau, lim;                   // optical depth so far; light: dist, env: +inf
     // `lim`: a light ray's distance to the light; an environment ray's last event so far (the
     // reference's t_env_end, test_integrators.h:258-271), which bounds nothing during traversal
+    float cut;         // optical depth at which the ray's transmittance counts as 0 (error budget)
     uint64_t hitmask;  // which of the record's active Gaussians the ray has met
     uint64_t bloom;    // membership mask of the record's active list (act_find)
     uint32_t act_off, act_n;  // the record's active list
@@ -504,6 +505,7 @@ __device__ __forceinline__ bool sec_init(const RenderArgs& A, uint32_t nrec, uin
     const float4 pos = A.rec_pos[r];
     const uint4 meta = A.rec_meta[r];
     R.rec = r;
+    R.cut = A.rec_cut != nullptr ? A.rec_cut[r] : A.tau_cut;
     R.act_off = meta.z;
     R.act_n = meta.w;
     R.bloom = A.rec_bloom[r];
@@ -612,14 +614,14 @@ __device__ __forceinline__ void sec_leaf(const RenderArgs& A, SecRay& R, int32_t
 template <bool S, bool FAST, bool PURE>
 __device__ __forceinline__ void sec_finish(const RenderArgs& A, SecRay& R, Ctr& c) {
     if constexpr (S) {  // secondary-stage diagnostics in otherwise unused counter slots
-        if (R.tau >= A.tau_cut) {
+        if (R.tau >= R.cut) {
             c.v[kCtrSteps]++;                 // rays ended by the optical-depth cut-off
             c.v[kCtrPrimQueries] += R.nsteps;  // ... and their node steps
         } else {
             c.v[kCtrPixels] += R.nsteps;       // node steps of rays that ran to the end of the tree
         }
     }
-    if (R.tau >= A.tau_cut) {
+    if (R.tau >= R.cut) {
         A.tr[R.slot] = 0.0f;
         return;
     }
@@ -683,11 +685,11 @@ __device__ __forceinline__ bool sec_step(const RenderArgs& A, SecRay& R, int* st
     if (ll || lr) {
         const bool r_first = lr && (!ll || rmin < lmin);
         sec_leaf<S, FAST, PURE>(A, R, r_first ? nc.y : nc.x, c);
-        if (ll && lr && R.tau < A.tau_cut) sec_leaf<S, FAST, PURE>(A, R, r_first ? nc.x : nc.y, c);
+        if (ll && lr && R.tau < R.cut) sec_leaf<S, FAST, PURE>(A, R, r_first ? nc.x : nc.y, c);
         if (ll) hl = false;
         if (lr) hr = false;
     }
-    bool done = R.tau >= A.tau_cut;
+    bool done = R.tau >= R.cut;
     if (!done) {
         if (hl && hr) {
             int nearer = nc.x, farther = nc.y;
@@ -1139,7 +1141,7 @@ __global__ __launch_bounds__(BLOCK, WAVES) void secondary_ww_kernel(RenderArgs A
                     }
                     list_advance(Q, node);
                 }
-                go = go && Q.has_prim() && R.tau < A.tau_cut;
+                go = go && Q.has_prim() && R.tau < R.cut;
             }
         } else {  // NODE iteration: up to `node_steps` child-pair steps per lane
             bool go = can_node;
@@ -1160,7 +1162,7 @@ __global__ __launch_bounds__(BLOCK, WAVES) void secondary_ww_kernel(RenderArgs A
                 tA = tC;
             }
         }
-        if (live && (R.tau >= A.tau_cut || (node == -1 && !Q.has_prim()))) {
+        if (live && (R.tau >= R.cut || (node == -1 && !Q.has_prim()))) {
             sec_finish<S, true, PURE>(A, R, c);
             live = false;
         }
@@ -1228,6 +1230,36 @@ __global__ __launch_bounds__(BLOCK) void secondary_slow_kernel(RenderArgs A, uin
 // ---------------------------------------------------------------------------------------------
 // Stage 3: per-pixel accumulation in step order (test_integrators.h:237, 272-277, 292).
 // ---------------------------------------------------------------------------------------------
+// Per-pixel error budget of the secondary optical-depth cut-off. accumulate_kernel weighs a light
+// ray's Tr by C = Ts dt I_l / (4 pi d_l^2) and an environment ray's by Ts dt env / NE, so a ray
+// stopped at optical depth >= cut (true Tr <= e^-cut, output 0) moves the pixel by at most
+// C e^-cut. With W = max over channels of the sum of C over all of the pixel's rays (= its
+// radiance if every Tr were 1) and cut = ln(W / budget), the pixel moves by at most `budget` in
+// total, whatever the rays do. cut is capped by A.tau_cut (the frame-wide cut-off).
+__device__ __forceinline__ float record_weight(const RenderArgs& A, const float4& pos) {
+    float w[3] = {A.env[0], A.env[1], A.env[2]};  // sum over the NE env rays of env / NE
+    for (int l = 0; l < A.num_lights; ++l) {
+        const LightRecord& lr = A.lights[l];
+        const float dx = lr.px - pos.x, dy = lr.py - pos.y, dz = lr.pz - pos.z;
+        const float d2 = dx * dx + dy * dy + dz * dz;
+        const float s = kInv4Pi / d2;
+        w[0] += lr.ix * s;
+        w[1] += lr.iy * s;
+        w[2] += lr.iz * s;
+    }
+    return pos.w * A.step_size * fmaxf(fmaxf(fabsf(w[0]), fabsf(w[1])), fabsf(w[2]));
+}
+
+__global__ __launch_bounds__(256) void record_cut_kernel(RenderArgs A, float budget) {
+    const uint32_t p = blockIdx.x * 256u + threadIdx.x;
+    if (p >= A.num_tiles * 256u) return;
+    float W = 0.0f;
+    for (uint32_t r = A.px_first[p]; r != kNoRecord; r = A.rec_next[r]) W += record_weight(A, A.rec_pos[r]);
+    // 1.001: headroom for the f32 rounding of W and of the optical depths themselves
+    const float cut = fminf(A.tau_cut, fmaxf(0.0f, logf(1.001f * W / budget)));
+    for (uint32_t r = A.px_first[p]; r != kNoRecord; r = A.rec_next[r]) A.rec_cut[r] = cut;
+}
+
 __global__ __launch_bounds__(256) void accumulate_kernel(RenderArgs A, uint32_t nrec) {
     const uint32_t tile_local = blockIdx.x;
     const int tid = threadIdx.x;
@@ -1422,6 +1454,12 @@ hipError_t gauss_secondary(const RenderArgs& A, uint32_t nrec, hipStream_t strea
                             : secondary_launch<true, true, false>(A, nrec, total, (uint32_t)nchunks, stream, v);
     return exact ? secondary_launch<false, false, false>(A, nrec, total, (uint32_t)nchunks, stream, v)
                  : secondary_launch<false, true, false>(A, nrec, total, (uint32_t)nchunks, stream, v);
+}
+
+hipError_t gauss_record_cut(const RenderArgs& A, float budget, hipStream_t stream) {
+    if (A.rec_cut == nullptr) return hipSuccess;
+    hipLaunchKernelGGL(dev::record_cut_kernel, dim3(A.num_tiles), dim3(256), 0, stream, A, budget);
+    return hipGetLastError();
 }
 
 hipError_t gauss_accumulate(const RenderArgs& A, uint32_t nrec, hipStream_t stream) {

@@ -370,6 +370,23 @@ def test_full_size_benchmark_settings_match_exact_oracle(W, H, n, npix):
     err, nm = _linf(img.pixels[pix[:, 1], pix[:, 0]], ref)
     print(f"{W}x{H}/{n} t_eps=1e-6: L-inf {err:.3e}")
     assert nm == 0 and err < TOL, f"{W}x{H}/{n}: L-inf {err:.3e}"
+    assert err < 1e-5, f"{W}x{H}/{n}: L-inf {err:.3e} above the stated error budget"
+
+
+@pytest.mark.parametrize("name,W", [("1000_random.txt", 192), ("many_gaussians.txt", 96)])
+def test_secondary_cut_off_stays_within_its_pixel_budget(name, W, monkeypatch):
+    """With t_eps > 0 each pixel's secondary rays stop at cut = ln(W_p / t_eps) (W_p: the pixel's
+    radiance if every Tr were 1), which bounds the frame change the cut can cause by t_eps per
+    pixel. Compare against the same render with only the frame-wide cut-off."""
+    path = scene_path(name)
+    cam = vr.Pinhole_Camera(CAM_POS, main_view_dir(), FOV)
+    a, b = vr.Image(W, W), vr.Image(W, W)
+    vr.RayMarchingGaussians(cam, t_eps=1e-6).render(vr.Scene.load_GMM(path), a)
+    monkeypatch.setenv("VR_NO_REC_CUT", "1")
+    vr.RayMarchingGaussians(cam, t_eps=1e-6).render(vr.Scene.load_GMM(path), b)
+    d = float(np.max(np.abs(a.pixels.astype(np.float64) - b.pixels)))
+    print(f"{name}: max |cut - no cut| = {d:.3e}")
+    assert d <= 1.2e-6, d
 
 
 # ---- PureRayMarching (integrator.h:100-267): marched primary and secondary transmittance -------
