@@ -1235,7 +1235,7 @@ __global__ __launch_bounds__(BLOCK) void secondary_slow_kernel(RenderArgs A, uin
 // stopped at optical depth >= cut (true Tr <= e^-cut, output 0) moves the pixel by at most
 // C e^-cut. With W = max over channels of the sum of C over all of the pixel's rays (= its
 // radiance if every Tr were 1) and cut = ln(W / budget), the pixel moves by at most `budget` in
-// total, whatever the rays do. cut is capped by A.tau_cut (the frame-wide cut-off).
+// total, whatever the rays do (capped at kTauCut, where expf is 0 anyway).
 __device__ __forceinline__ float record_weight(const RenderArgs& A, const float4& pos) {
     float w[3] = {A.env[0], A.env[1], A.env[2]};  // sum over the NE env rays of env / NE
     for (int l = 0; l < A.num_lights; ++l) {
@@ -1256,7 +1256,7 @@ __global__ __launch_bounds__(256) void record_cut_kernel(RenderArgs A, float bud
     float W = 0.0f;
     for (uint32_t r = A.px_first[p]; r != kNoRecord; r = A.rec_next[r]) W += record_weight(A, A.rec_pos[r]);
     // 1.001: headroom for the f32 rounding of W and of the optical depths themselves
-    const float cut = fminf(A.tau_cut, fmaxf(0.0f, logf(1.001f * W / budget)));
+    const float cut = fminf(kTauCut, fmaxf(0.0f, logf(1.001f * W / budget)));
     for (uint32_t r = A.px_first[p]; r != kNoRecord; r = A.rec_next[r]) A.rec_cut[r] = cut;
 }
 
