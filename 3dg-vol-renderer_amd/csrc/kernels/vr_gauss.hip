@@ -148,7 +148,9 @@ __device__ float light_transmittance(const RenderArgs& A, const Ray& sr, float d
 // to the pixel's previous record (px_first / rec_next), so a pixel's records are visited in step
 // order by accumulate_kernel wherever they landed in memory. Records that do not fit the
 // capacity raise rec_alloc[2]; the host then grows the buffers and re-runs the march.
-template <int ACT, bool S, bool H>
+// W: BVH window queries on the 4-wide half-precision tree (CAP-entry stack; a query that could
+// overflow it sends the pixel to the fallback kernel, which walks the pair tree).
+template <int ACT, bool S, bool H, bool W = false, int CAP = kStackSize>
 __device__ int march(const RenderArgs& A, uint32_t p, int px, int py, int* act_base, int* stack, int stride, Ctr& c) {
     const Ray ray = primary_ray(A, px, py);
     const GaussianRecord* __restrict__ G = A.gauss;
@@ -159,6 +161,14 @@ __device__ int march(const RenderArgs& A, uint32_t p, int px, int py, int* act_b
     uint32_t prev = kNoRecord;  // this pixel's last record
     A.px_first[p] = kNoRecord;
     ActList act{act_base, stride, 0, 0};
+    auto walk = [&](auto prune, auto leaf) -> bool {
+        if constexpr (W) {
+            return traverse_wide<CAP>(A, ray, stack, stride, prune, leaf, NodeCount<S>{&c});
+        } else {
+            traverse<H>(A, ray, stack, stride, prune, leaf, NodeCount<S>{&c});
+            return true;
+        }
+    };
     int kq = 0;
     if (A.num_prims > 0) {
         for (;;) {
@@ -167,8 +177,7 @@ __device__ int march(const RenderArgs& A, uint32_t p, int px, int py, int* act_b
             if (act.n == 0) {  // closest entry strictly after t_lo
                 if constexpr (S) c.v[kCtrPrimQueries]++;
                 float best = INFINITY;
-                traverse<H>(
-                    A, ray, stack, stride,
+                const bool ok = walk(
                     [&](float tmin, float tmax) {
                         return tmax >= t_lo - kTPad * (1.0f + fabsf(t_lo)) && tmin <= best + kTPad * (1.0f + best);
                     },
@@ -181,8 +190,8 @@ __device__ int march(const RenderArgs& A, uint32_t p, int px, int py, int* act_b
                             if (intersect(q, a, b) && a > t_lo && a < best) best = a;
                         }
                         return true;
-                    },
-                    NodeCount<S>{&c});
+                    });
+                if (!ok) return kOverflow;
                 if (best == INFINITY) break;
                 k = kfirst(ts, nts, step, best);
             } else {
@@ -193,8 +202,7 @@ __device__ int march(const RenderArgs& A, uint32_t p, int px, int py, int* act_b
             // entrants: t_lo < a <= t_k and still inside at t_k (b > t_k)
             if constexpr (S) c.v[kCtrPrimQueries]++;
             bool ovf = false;
-            traverse<H>(
-                A, ray, stack, stride,
+            const bool ok = walk(
                 [&](float tmin, float tmax) {
                     return tmax >= t_lo - kTPad * (1.0f + fabsf(t_lo)) && tmin <= t_k + kTPad * (1.0f + t_k);
                 },
@@ -218,9 +226,8 @@ __device__ int march(const RenderArgs& A, uint32_t p, int px, int py, int* act_b
                         act.n++;
                     }
                     return true;
-                },
-                NodeCount<S>{&c});
-            if (ovf) return kOverflow;
+                });
+            if (ovf || !ok) return kOverflow;
             kq = k + 1;
             // retire (b <= t_k); sigma at pos (gmm.h:98-126); the step's optical depth (:146-157)
             const float px_ = ray.ox + t_k * ray.dx;
@@ -311,7 +318,7 @@ __device__ __forceinline__ void mark_error(const RenderArgs& A, uint32_t p) {
     A.px_T[p] = __builtin_nanf("");
 }
 
-template <int ACT, int BLOCK, bool S, int STACK, bool H>
+template <int ACT, int BLOCK, bool S, int STACK, bool H, bool W = false>
 __global__ __launch_bounds__(BLOCK) void march_kernel(RenderArgs A) {
     __shared__ int s_act[ACT * BLOCK];
     __shared__ int s_stack[STACK * BLOCK];
@@ -323,7 +330,7 @@ __global__ __launch_bounds__(BLOCK) void march_kernel(RenderArgs A) {
     Ctr c{};
     int st = kOK;
     if (x < (int)A.width && y < (int)A.height) {
-        st = march<ACT, S, H>(A, p, x, y, s_act + tid, s_stack + tid, BLOCK, c);
+        st = march<ACT, S, H, W, STACK>(A, p, x, y, s_act + tid, s_stack + tid, BLOCK, c);
     } else {
         A.px_first[p] = kNoRecord;
         A.px_T[p] = 0.0f;
@@ -789,17 +796,6 @@ __device__ __forceinline__ uint32_t ovf_slot(int sp) {
 }
 
 
-// Sorts (key, ref) pairs ascending by key (compare-exchange).
-__device__ __forceinline__ void cswap(float& ka, int32_t& ra, float& kb, int32_t& rb) {
-    const bool sw = kb < ka;
-    const float k = sw ? kb : ka;
-    kb = sw ? ka : kb;
-    ka = k;
-    const int32_t r = sw ? rb : ra;
-    rb = sw ? ra : rb;
-    ra = r;
-}
-
 // One step of the 4-wide traversal: the four children of HNode4 `node` are tested, sorted near to
 // far (misses last); leaf children go to the leaf queue in that order, the nearest inner child
 // is walked next and the other inner ones are pushed far-first (so the nearer pop first).
@@ -849,9 +845,12 @@ __device__ __forceinline__ void sec_node4(const RenderArgs& A, SecRay& R, int* s
     }
     // inner children: the nearest continues, the others are pushed far-first
     int first = -1;
+    int32_t next = 0;  // the nearest inner child (selects only: no dynamic register indexing)
 #pragma unroll
-    for (int i = 3; i >= 0; --i)
-        if (kr[i] > 0) first = i;
+    for (int i = 3; i >= 0; --i) {
+        first = kr[i] > 0 ? i : first;
+        next = kr[i] > 0 ? kr[i] : next;
+    }
 #pragma unroll
     for (int i = 3; i >= 0; --i) {
         if (kr[i] > 0 && i != first) {
@@ -861,7 +860,7 @@ __device__ __forceinline__ void sec_node4(const RenderArgs& A, SecRay& R, int* s
         }
     }
     if (first >= 0) {
-        node = kr[first];
+        node = next;
     } else if (sp > 0) {
         --sp;
         node = sp < STACK ? stack[sp * BLOCK] : A.stack_ovf[ovf_slot<BLOCK, STACK, kWideStackMax>(sp)];
@@ -1320,7 +1319,11 @@ static hipError_t march_pass(const RenderArgs& A, hipStream_t stream) {
     // 24-entry stack; the 16-slot active list overflows to the 64-slot fallback kernel. H: the
     // half-precision node copy (boxes only propose candidates; every decision is the exact quadratic).
     const bool shallow = A.bvh_depth <= kShallowStack + 1;
-    if (shallow)
+    static const bool pair_march = getenv("VR_MARCH_PAIR") && getenv("VR_MARCH_PAIR")[0] == '1';  // A/B
+    if (H && A.hnodes4 != nullptr && !pair_march)  // 4-wide tree; a query that could overflow the stack goes to the fallback
+        hipLaunchKernelGGL((dev::march_kernel<kActFast, kBlockFast, S, kShallowStack, true, true>), dim3(A.num_tiles),
+                           dim3(kBlockFast), 0, stream, A);
+    else if (shallow)
         hipLaunchKernelGGL((dev::march_kernel<kActFast, kBlockFast, S, kShallowStack, H>), dim3(A.num_tiles),
                            dim3(kBlockFast), 0, stream, A);
     else

@@ -364,6 +364,92 @@ __device__ __forceinline__ void traverse(const RenderArgs& A, const Ray& r0, int
     }
 }
 
+// Compare-exchange of (key, ref) pairs: afterwards ka <= kb.
+__device__ __forceinline__ void cswap(float& ka, int32_t& ra, float& kb, int32_t& rb) {
+    const bool sw = kb < ka;
+    const float k = sw ? kb : ka;
+    kb = sw ? ka : kb;
+    ka = k;
+    const int32_t r = sw ? rb : ra;
+    rb = sw ? ra : rb;
+    ra = r;
+}
+
+// Slab tests of the four children of 4-wide half node `node` (HNode4) for a ray already in the
+// nodes' normalised coordinates, sorted near to far; misses (and empty slots) get key +inf, ref 0.
+template <typename Hit>
+__device__ __forceinline__ void wide_children(const RenderArgs& A, int node, float ix, float iy, float iz, float oxi,
+                                              float oyi, float ozi, Hit hit, float* key, int32_t* kr) {
+    const uint4* np = reinterpret_cast<const uint4*>(A.hnodes4 + node);
+    const uint4 q0 = np[0], q1 = np[1], q2 = np[2], rf = np[3];
+    const uint32_t w[12] = {q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, q1.z, q1.w, q2.x, q2.y, q2.z, q2.w};
+    const int32_t ref[4] = {(int32_t)rf.x, (int32_t)rf.y, (int32_t)rf.z, (int32_t)rf.w};
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        float f[6];
+#pragma unroll
+        for (int k = 0; k < 6; ++k) {
+            const uint32_t word = w[(6 * i + k) >> 1];
+            f[k] = (float)__builtin_bit_cast(_Float16, (uint16_t)(((6 * i + k) & 1) ? (word >> 16) : (word & 0xffffu)));
+        }
+        const float tx1 = fmaf(f[0], ix, -oxi), tx2 = fmaf(f[3], ix, -oxi);
+        const float ty1 = fmaf(f[1], iy, -oyi), ty2 = fmaf(f[4], iy, -oyi);
+        const float tz1 = fmaf(f[2], iz, -ozi), tz2 = fmaf(f[5], iz, -ozi);
+        const float tmin = fmaxf(fmaxf(fminf(tx1, tx2), fminf(ty1, ty2)), fminf(tz1, tz2));
+        const float tmax = fminf(fminf(fmaxf(tx1, tx2), fmaxf(ty1, ty2)), fmaxf(tz1, tz2));
+        const bool h = (ref[i] != 0) && (tmax >= fmaxf(tmin, 0.0f)) && hit(tmin, tmax);
+        key[i] = h ? tmin : INFINITY;
+        kr[i] = h ? ref[i] : 0;
+    }
+    cswap(key[0], kr[0], key[1], kr[1]);  // 4-input sorting network
+    cswap(key[2], kr[2], key[3], kr[3]);
+    cswap(key[0], kr[0], key[2], kr[2]);
+    cswap(key[1], kr[1], key[3], kr[3]);
+    cswap(key[1], kr[1], key[2], kr[2]);
+}
+
+// Stack traversal of the 4-wide half-precision tree (HNode4) with the generic traverse's
+// contract (prune / leaf / on_node); leaves are handled near-first as a node's children are
+// reached, the nearest inner child is walked next and the others pushed far-first. Returns false
+// if the LDS stack (cap entries) could overflow — the caller then re-runs the work on the pair tree.
+template <int CAP, typename Prune, typename Leaf, typename OnNode = NoCount>
+__device__ __forceinline__ bool traverse_wide(const RenderArgs& A, const Ray& r0, int* stack, int stride, Prune prune,
+                                              Leaf leaf, OnNode on_node = OnNode()) {
+    float ox = r0.ox, oy = r0.oy, oz = r0.oz;
+    node_space<true>(A, ox, oy, oz);
+    const float ix = __frcp_rn(r0.dx * A.hn_scale), iy = __frcp_rn(r0.dy * A.hn_scale), iz = __frcp_rn(r0.dz * A.hn_scale);
+    const float oxi = ox * ix, oyi = oy * iy, ozi = oz * iz;
+    int sp = 0;
+    int node = 0;
+    for (;;) {
+        on_node();
+        float key[4];
+        int32_t kr[4];
+        wide_children(A, node, ix, iy, iz, oxi, oyi, ozi, prune, key, kr);
+#pragma unroll
+        for (int i = 0; i < 4; ++i)  // leaves, near first
+            if (kr[i] < 0 && !leaf(leaf_first(kr[i]), leaf_count(kr[i]))) return true;
+        int first = -1;
+        int32_t next = 0;  // the nearest inner child (selects only: no dynamic register indexing)
+#pragma unroll
+        for (int i = 3; i >= 0; --i) {
+            first = kr[i] > 0 ? i : first;
+            next = kr[i] > 0 ? kr[i] : next;
+        }
+        if (sp + 3 > CAP) return false;
+#pragma unroll
+        for (int i = 3; i >= 0; --i)
+            if (kr[i] > 0 && i != first) stack[(sp++) * stride] = kr[i];
+        if (first >= 0) {
+            node = next;
+        } else {
+            if (sp == 0) return true;
+            --sp;
+            node = stack[sp * stride];
+        }
+    }
+}
+
 // First index k with t_k >= a in the iterated step table (returns n if beyond the table).
 __device__ __forceinline__ int kfirst(const float* __restrict__ ts, int n, float step, float a) {
     int k = (int)(a / step);
