@@ -925,60 +925,95 @@ __device__ __forceinline__ void sec_node(const RenderArgs& A, SecRay& R, int* st
 // depths from pos) at the front of the record's slots, the others at the back. All secondary rays
 // of the record test this list first — most of them become opaque right there, without touching
 // the tree — and the tree walk that follows skips exactly these members (same q, bit for bit).
-template <int BLOCK, bool H>
+template <int BLOCK, bool H, bool W = false>
 __global__ __launch_bounds__(BLOCK) void record_list_kernel(RenderArgs A, uint32_t nrec) {
     __shared__ int s_stack[kStackSize * BLOCK];
     int* stack = s_stack + threadIdx.x;
     for (uint32_t r = blockIdx.x * BLOCK + threadIdx.x; r < nrec; r += gridDim.x * BLOCK) {
         const float4 pos = A.rec_pos[r];
         float bx = pos.x, by = pos.y, bz = pos.z;  // the point in the node boxes' coordinates
-        node_space<H>(A, bx, by, bz);
+        node_space<H || W>(A, bx, by, bz);
         int32_t* slot = A.rec_list + (size_t)r * kListCap;
         uint32_t nc = 0, nb = 0;
         bool ovf = false;
-        int sp = 0, node = 0;
-        for (;;) {
-            float f[12];
-            int2 ncr;
-            load_pair<H>(A, node, f, ncr);
-            const bool inl = (ncr.x != 0) & (f[0] <= bx) & (bx <= f[3]) & (f[1] <= by) & (by <= f[4]) & (f[2] <= bz) &
-                             (bz <= f[5]);
-            const bool inr = (ncr.y != 0) & (f[6] <= bx) & (bx <= f[9]) & (f[7] <= by) & (by <= f[10]) & (f[8] <= bz) &
-                             (bz <= f[11]);
-            // leaf children: one contiguous primitive range each (left first)
-            const bool ll = inl && ncr.x < 0, lr = inr && ncr.y < 0;
-            for (int li = 0; li < 2; ++li) {
-                const bool use = li == 0 ? ll : lr;
-                if (!use) continue;
-                const int32_t ref = li == 0 ? ncr.x : ncr.y;
-                const uint32_t first = leaf_first(ref), count = leaf_count(ref);
-                for (uint32_t j = first; j < first + count; ++j) {
-                    const GRec g = load_rec(A.gauss, (int)j);
-                    const float q = cq_fast(g, pos.x - g.mx, pos.y - g.my, pos.z - g.mz);
-                    if (!(q <= kListR2)) continue;
-                    if (nc + nb >= (uint32_t)kListCap) {
-                        ovf = true;
-                    } else if (q <= kListCentral) {
-                        slot[nc++] = (int32_t)j;
-                    } else {
-                        slot[kListCap - 1 - nb++] = (int32_t)j;
-                    }
+        auto leaf = [&](int32_t ref) {  // a leaf's members with q(pos) <= kListR2
+            const uint32_t first = leaf_first(ref), count = leaf_count(ref);
+            for (uint32_t j = first; j < first + count; ++j) {
+                const GRec g = load_rec(A.gauss, (int)j);
+                const float q = cq_fast(g, pos.x - g.mx, pos.y - g.my, pos.z - g.mz);
+                if (!(q <= kListR2)) continue;
+                if (nc + nb >= (uint32_t)kListCap) {
+                    ovf = true;
+                } else if (q <= kListCentral) {
+                    slot[nc++] = (int32_t)j;
+                } else {
+                    slot[kListCap - 1 - nb++] = (int32_t)j;
                 }
             }
-            const bool il = inl && ncr.x > 0, ir = inr && ncr.y > 0;
-            if (il && ir) {
-                stack[sp * BLOCK] = ncr.y;
-                ++sp;
-                node = ncr.x;
-            } else if (il) {
-                node = ncr.x;
-            } else if (ir) {
-                node = ncr.y;
-            } else if (sp > 0) {
-                --sp;
-                node = stack[sp * BLOCK];
+        };
+        int sp = 0, node = 0;
+        for (;;) {
+            if constexpr (W) {  // 4-wide tree: every child box holding the point
+                const uint4* np = reinterpret_cast<const uint4*>(A.hnodes4 + node);
+                const uint4 q0 = np[0], q1 = np[1], q2 = np[2], rf = np[3];
+                const uint32_t w[12] = {q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, q1.z, q1.w, q2.x, q2.y, q2.z, q2.w};
+                const int32_t ref[4] = {(int32_t)rf.x, (int32_t)rf.y, (int32_t)rf.z, (int32_t)rf.w};
+                int32_t next = 0;
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    float f[6];
+#pragma unroll
+                    for (int k = 0; k < 6; ++k) {
+                        const uint32_t word = w[(6 * i + k) >> 1];
+                        f[k] = (float)__builtin_bit_cast(_Float16,
+                                                         (uint16_t)(((6 * i + k) & 1) ? (word >> 16) : (word & 0xffffu)));
+                    }
+                    const bool in = (ref[i] != 0) & (f[0] <= bx) & (bx <= f[3]) & (f[1] <= by) & (by <= f[4]) &
+                                    (f[2] <= bz) & (bz <= f[5]);
+                    if (in && ref[i] < 0) leaf(ref[i]);
+                    if (in && ref[i] > 0) {
+                        if (next == 0) {
+                            next = ref[i];
+                        } else if (sp < kStackSize) {
+                            stack[(sp++) * BLOCK] = ref[i];
+                        } else {
+                            ovf = true;  // no list for this record: its rays walk the whole tree (still exact)
+                        }
+                    }
+                }
+                if (next != 0) {
+                    node = next;
+                } else if (sp > 0) {
+                    --sp;
+                    node = stack[sp * BLOCK];
+                } else {
+                    break;
+                }
             } else {
-                break;
+                float f[12];
+                int2 ncr;
+                load_pair<H>(A, node, f, ncr);
+                const bool inl = (ncr.x != 0) & (f[0] <= bx) & (bx <= f[3]) & (f[1] <= by) & (by <= f[4]) &
+                                 (f[2] <= bz) & (bz <= f[5]);
+                const bool inr = (ncr.y != 0) & (f[6] <= bx) & (bx <= f[9]) & (f[7] <= by) & (by <= f[10]) &
+                                 (f[8] <= bz) & (bz <= f[11]);
+                if (inl && ncr.x < 0) leaf(ncr.x);  // leaf children: one contiguous primitive range each
+                if (inr && ncr.y < 0) leaf(ncr.y);
+                const bool il = inl && ncr.x > 0, ir = inr && ncr.y > 0;
+                if (il && ir) {
+                    stack[sp * BLOCK] = ncr.y;
+                    ++sp;
+                    node = ncr.x;
+                } else if (il) {
+                    node = ncr.x;
+                } else if (ir) {
+                    node = ncr.y;
+                } else if (sp > 0) {
+                    --sp;
+                    node = stack[sp * BLOCK];
+                } else {
+                    break;
+                }
             }
         }
         A.rec_nlist[r] = ovf ? 0xffffffffu : (nc | (nb << 16));
@@ -1410,7 +1445,11 @@ hipError_t gauss_lists(const RenderArgs& A, uint32_t nrec, hipStream_t stream) {
     if (!A.list_ok || nrec == 0) return hipSuccess;
     uint64_t lb = ((uint64_t)nrec + kBlockSecondary - 1) / kBlockSecondary;
     if (lb > 65536ull * 4ull) lb = 65536ull * 4ull;
-    if (A.hnodes != nullptr)
+    static const bool pair_lists = getenv("VR_LISTS_PAIR") && getenv("VR_LISTS_PAIR")[0] == '1';  // A/B
+    if (A.hnodes4 != nullptr && !pair_lists)
+        hipLaunchKernelGGL((dev::record_list_kernel<kBlockSecondary, true, true>), dim3((unsigned)lb), dim3(kBlockSecondary),
+                           0, stream, A, nrec);
+    else if (A.hnodes != nullptr)
         hipLaunchKernelGGL((dev::record_list_kernel<kBlockSecondary, true>), dim3((unsigned)lb), dim3(kBlockSecondary), 0,
                            stream, A, nrec);
     else
