@@ -1265,33 +1265,33 @@ __global__ __launch_bounds__(BLOCK) void secondary_slow_kernel(RenderArgs A, uin
 // Stage 3: per-pixel accumulation in step order (test_integrators.h:237, 272-277, 292).
 // ---------------------------------------------------------------------------------------------
 // Per-pixel error budget of the secondary optical-depth cut-off. accumulate_kernel weighs a light
-// ray's Tr by C = Ts dt I_l / (4 pi d_l^2) and an environment ray's by Ts dt env / NE, so a ray
-// stopped at optical depth >= cut (true Tr <= e^-cut, output 0) moves the pixel by at most
-// C e^-cut. With W = max over channels of the sum of C over all of the pixel's rays (= its
-// radiance if every Tr were 1) and cut = ln(W / budget), the pixel moves by at most `budget` in
-// total, whatever the rays do (capped at kTauCut, where expf is 0 anyway).
+// ray's Tr by C = Ts dt I_l / (4 pi d_l^2) and an environment ray's by Ts dt env / NE (per
+// channel), so a ray stopped at optical depth >= cut (its true Tr <= e^-cut, output 0) moves the
+// pixel by at most C e^-cut. Every ray of the pixel gets an equal share budget / N_p of the
+// budget (N_p: the pixel's secondary rays): a record's rays stop at
+//   cut_r = ln(Cmax_r * N_p / budget),   Cmax_r = the largest C of the record's rays,
+// so the pixel moves by at most sum C e^-cut <= N_p * budget / N_p = budget in every channel.
+// (Equal shares minimise the work: dim records deep in a pixel get small cut-offs.)
 __device__ __forceinline__ float record_weight(const RenderArgs& A, const float4& pos) {
-    float w[3] = {A.env[0], A.env[1], A.env[2]};  // sum over the NE env rays of env / NE
+    float w = fmaxf(fmaxf(fabsf(A.env[0]), fabsf(A.env[1])), fabsf(A.env[2])) / (float)max(A.env_samples, 1);
     for (int l = 0; l < A.num_lights; ++l) {
         const LightRecord& lr = A.lights[l];
         const float dx = lr.px - pos.x, dy = lr.py - pos.y, dz = lr.pz - pos.z;
-        const float d2 = dx * dx + dy * dy + dz * dz;
-        const float s = kInv4Pi / d2;
-        w[0] += lr.ix * s;
-        w[1] += lr.iy * s;
-        w[2] += lr.iz * s;
+        const float s = kInv4Pi / (dx * dx + dy * dy + dz * dz);
+        w = fmaxf(w, fmaxf(fmaxf(fabsf(lr.ix), fabsf(lr.iy)), fabsf(lr.iz)) * s);
     }
-    return pos.w * A.step_size * fmaxf(fmaxf(fabsf(w[0]), fabsf(w[1])), fabsf(w[2]));
+    return pos.w * A.step_size * w;
 }
 
 __global__ __launch_bounds__(256) void record_cut_kernel(RenderArgs A, float budget) {
     const uint32_t p = blockIdx.x * 256u + threadIdx.x;
     if (p >= A.num_tiles * 256u) return;
-    float W = 0.0f;
-    for (uint32_t r = A.px_first[p]; r != kNoRecord; r = A.rec_next[r]) W += record_weight(A, A.rec_pos[r]);
-    // 1.001: headroom for the f32 rounding of W and of the optical depths themselves
-    const float cut = fminf(kTauCut, fmaxf(0.0f, logf(1.001f * W / budget)));
-    for (uint32_t r = A.px_first[p]; r != kNoRecord; r = A.rec_next[r]) A.rec_cut[r] = cut;
+    uint32_t n = 0;
+    for (uint32_t r = A.px_first[p]; r != kNoRecord; r = A.rec_next[r]) ++n;
+    const float rays = (float)n * (float)(A.num_lights + A.env_samples);
+    // 1.001: headroom for the f32 rounding of the weights and of the optical depths themselves
+    for (uint32_t r = A.px_first[p]; r != kNoRecord; r = A.rec_next[r])
+        A.rec_cut[r] = fminf(kTauCut, fmaxf(0.0f, logf(1.001f * record_weight(A, A.rec_pos[r]) * rays / budget)));
 }
 
 __global__ __launch_bounds__(256) void accumulate_kernel(RenderArgs A, uint32_t nrec) {
