@@ -38,6 +38,7 @@ struct vr_ctx {
     HNode* d_hnodes = nullptr;
     HNode4* d_hnodes4 = nullptr;
     float hn_center[3] = {0, 0, 0}, hn_scale = 1.0f;
+    float sig_max[3] = {0, 0, 0};  // largest per-axis standard deviation of any Gaussian
     SphereRecord* d_spheres = nullptr;
     std::vector<LightRecord> lights;
     float env[3] = {0, 0, 0};
@@ -476,6 +477,16 @@ vr_status gauss_pipeline(vr_ctx* c, RenderArgs& A, hipStream_t s, bool stats) {
     }
     static const bool no_list = getenv("VR_NOLIST") && getenv("VR_NOLIST")[0] == '1';
     A.list_ok = c->list_ok && !no_list && (uint64_t)nrec * kListCap < 0xffffffffull;
+    {  // list radius; beyond the 3.15-sigma BVH boxes the query box grows by the excess radius of the
+       // widest Gaussian on each axis (conservative: every member's box meets the query box)
+        static const float r2 = getenv("VR_LIST_R2") ? (float)atof(getenv("VR_LIST_R2")) : kListR2;
+        A.list_r2 = r2;
+        const double excess = std::max(0.0, std::sqrt((double)r2) - 3.0 * 1.05);
+        for (int k = 0; k < 3; ++k) {
+            const double h = excess * c->sig_max[k];
+            A.list_h[k] = h > 0.0 ? (float)(h * (A.hnodes != nullptr ? c->hn_scale : 1.0f) * 1.001 + 1e-6) : 0.0f;
+        }
+    }
     if (A.list_ok) {
         if ((st = grow(c->rec_list, std::max<uint64_t>(nrec, 1) * kListCap * 4ull, "hipMalloc(record lists)")) != VR_OK)
             return st;
@@ -613,7 +624,10 @@ vr_status vr_upload_scene(vr_ctx* c, const vr_scene* sc) {
         const size_t N = s.pre.size();
         if (N >= (1u << 27)) return fail(VR_ERR_UNSUPPORTED, "more than 2^27 Gaussians");
         std::vector<float> boxes(6 * N);
+        for (int k = 0; k < 3; ++k) c->sig_max[k] = 0.0f;
         for (size_t i = 0; i < N; ++i) {
+            const float dg[3] = {s.pre[i].cov[0], s.pre[i].cov[3], s.pre[i].cov[5]};
+            for (int k = 0; k < 3; ++k) c->sig_max[k] = std::max(c->sig_max[k], std::sqrt(std::max(dg[k], 0.0f)));
             gaussian_bounds(s.pre[i], &boxes[6 * i], &boxes[6 * i + 3]);
             for (int k = 0; k < 3; ++k) {
                 c->bmin[k] = std::min(c->bmin[k], boxes[6 * i + k]);

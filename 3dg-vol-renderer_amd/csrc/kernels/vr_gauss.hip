@@ -936,12 +936,13 @@ __global__ __launch_bounds__(BLOCK) void record_list_kernel(RenderArgs A, uint32
         int32_t* slot = A.rec_list + (size_t)r * kListCap;
         uint32_t nc = 0, nb = 0;
         bool ovf = false;
-        auto leaf = [&](int32_t ref) {  // a leaf's members with q(pos) <= kListR2
+        const float hx = A.list_h[0], hy = A.list_h[1], hz = A.list_h[2], r2 = A.list_r2;
+        auto leaf = [&](int32_t ref) {  // a leaf's members with q(pos) <= list_r2
             const uint32_t first = leaf_first(ref), count = leaf_count(ref);
             for (uint32_t j = first; j < first + count; ++j) {
                 const GRec g = load_rec(A.gauss, (int)j);
                 const float q = cq_fast(g, pos.x - g.mx, pos.y - g.my, pos.z - g.mz);
-                if (!(q <= kListR2)) continue;
+                if (!(q <= r2)) continue;
                 if (nc + nb >= (uint32_t)kListCap) {
                     ovf = true;
                 } else if (q <= kListCentral) {
@@ -968,8 +969,9 @@ __global__ __launch_bounds__(BLOCK) void record_list_kernel(RenderArgs A, uint32
                         f[k] = (float)__builtin_bit_cast(_Float16,
                                                          (uint16_t)(((6 * i + k) & 1) ? (word >> 16) : (word & 0xffffu)));
                     }
-                    const bool in = (ref[i] != 0) & (f[0] <= bx) & (bx <= f[3]) & (f[1] <= by) & (by <= f[4]) &
-                                    (f[2] <= bz) & (bz <= f[5]);
+                    // the query box [pos - h, pos + h] meets the child box (h = 0 for the 3.08-sigma radius)
+                    const bool in = (ref[i] != 0) & (f[0] <= bx + hx) & (bx - hx <= f[3]) & (f[1] <= by + hy) &
+                                    (by - hy <= f[4]) & (f[2] <= bz + hz) & (bz - hz <= f[5]);
                     if (in && ref[i] < 0) leaf(ref[i]);
                     if (in && ref[i] > 0) {
                         if (next == 0) {
@@ -993,10 +995,10 @@ __global__ __launch_bounds__(BLOCK) void record_list_kernel(RenderArgs A, uint32
                 float f[12];
                 int2 ncr;
                 load_pair<H>(A, node, f, ncr);
-                const bool inl = (ncr.x != 0) & (f[0] <= bx) & (bx <= f[3]) & (f[1] <= by) & (by <= f[4]) &
-                                 (f[2] <= bz) & (bz <= f[5]);
-                const bool inr = (ncr.y != 0) & (f[6] <= bx) & (bx <= f[9]) & (f[7] <= by) & (by <= f[10]) &
-                                 (f[8] <= bz) & (bz <= f[11]);
+                const bool inl = (ncr.x != 0) & (f[0] <= bx + hx) & (bx - hx <= f[3]) & (f[1] <= by + hy) &
+                                 (by - hy <= f[4]) & (f[2] <= bz + hz) & (bz - hz <= f[5]);
+                const bool inr = (ncr.y != 0) & (f[6] <= bx + hx) & (bx - hx <= f[9]) & (f[7] <= by + hy) &
+                                 (by - hy <= f[10]) & (f[8] <= bz + hz) & (bz - hz <= f[11]);
                 if (inl && ncr.x < 0) leaf(ncr.x);  // leaf children: one contiguous primitive range each
                 if (inr && ncr.y < 0) leaf(ncr.y);
                 const bool il = inl && ncr.x > 0, ir = inr && ncr.y > 0;
@@ -1164,7 +1166,7 @@ __global__ __launch_bounds__(BLOCK, WAVES) void secondary_ww_kernel(RenderArgs A
                     const Quad q = quad_fast(g, R.ray);
                     float a, b;
                     // a tree leaf skips the record's list members (already summed)
-                    if (!(R.listed && !from_list && q.Cq <= kListR2) && intersect_fast(q, a, b)) {
+                    if (!(R.listed && !from_list && q.Cq <= A.list_r2) && intersect_fast(q, a, b)) {
                         const int slot = act_find(A, R, (int)j);
                         float lo = a;
                         if (slot >= 0) {

@@ -150,6 +150,8 @@ struct RenderArgs {
     uint32_t chunk_rec;             // records per secondary-ray chunk (power of 2; 64 without env_order)
     uint32_t chunk_shift;           // log2(chunk_rec)
     float* rec_cut;                 // per record: optical-depth cut-off of its secondary rays (nullptr: tau_cut)
+    float list_r2;                  // neighbour-list radius: members are the Gaussians with q(pos) <= list_r2
+    float list_h[3];                // half-size of the list query box around pos, in node coordinates
     int32_t list_ok;                // scene allows neighbour lists (all covariances positive definite)
     const unsigned long long* pcg_jump;  // [2k] = A^k, [2k+1] = inc (A^(k-1) + ... + 1): PCG32 state after k draws
 };
