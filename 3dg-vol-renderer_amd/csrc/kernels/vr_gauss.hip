@@ -1113,7 +1113,7 @@ __global__ __launch_bounds__(BLOCK, WAVES) void secondary_ww_kernel(RenderArgs A
             if (pool == pool_end && !counter_done) {  // next record chunk (all samples of its records)
                 uint32_t cnext = 0;
                 if (lane == 0) cnext = (uint32_t)atomicAdd(A.ray_next, 1ull);
-                cnext = __shfl(cnext, 0, 64);
+                cnext = (uint32_t)__builtin_amdgcn_readfirstlane((int)cnext);  // wave-uniform: scalar register
                 if (cnext < nchunks) {
                     chunk = cnext;
                     pool = 0;
@@ -1414,6 +1414,7 @@ static hipError_t secondary_launch(const RenderArgs& A, uint32_t nrec, uint64_t 
         hipError_t e = hipMemsetAsync(A.ray_next, 0, sizeof(unsigned long long), stream);
         if (e != hipSuccess) return e;
         static const int prof = getenv("VR_WW_PROF") ? atoi(getenv("VR_WW_PROF")) : 0;
+        static const bool waves7 = getenv("VR_WW_WAVES") && atoi(getenv("VR_WW_WAVES")) == 7;
         // LDS words per lane: 18 traversal-stack entries (deeper ones overflow to global memory) +
         // the 8-entry LDS ring of the 9-entry leaf queue = 26 (6 blocks of 256 lanes per CU).
         const bool half = A.hnodes != nullptr;
@@ -1421,6 +1422,8 @@ static hipError_t secondary_launch(const RenderArgs& A, uint32_t nrec, uint64_t 
             e = half ? ww_launch<18, false, PURE, true, 9, 6, true, true>(A, nrec, total, nchunks, stream, rmin, prim_bias,
                                                                           prof == 2)
                      : ww_launch<18, false, PURE, true, 9, 6, false>(A, nrec, total, nchunks, stream, rmin, prim_bias, prof == 2);
+        else if (half && A.hnodes4 != nullptr && waves7)  // EXPERIMENT
+            e = ww_launch<14, S, PURE, false, 9, 7, true, true>(A, nrec, total, nchunks, stream, rmin, prim_bias, 0);
         else if (half && A.hnodes4 != nullptr)
             e = ww_launch<18, S, PURE, false, 9, 6, true, true>(A, nrec, total, nchunks, stream, rmin, prim_bias, 0);
         else if (half)
