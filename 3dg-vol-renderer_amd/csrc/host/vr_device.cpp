@@ -19,6 +19,7 @@ hipError_t gauss_march(const RenderArgs& A, hipStream_t stream, bool stats);
 hipError_t gauss_lists(const RenderArgs& A, uint32_t nrec, hipStream_t stream);
 hipError_t gauss_secondary(const RenderArgs& A, uint32_t nrec, hipStream_t stream, bool stats);
 hipError_t gauss_accumulate(const RenderArgs& A, uint32_t nrec, hipStream_t stream);
+hipError_t launch_free_flight(const RenderArgs& A, uint32_t chunk_tiles, hipStream_t stream);
 hipError_t gauss_record_cut(const RenderArgs& A, float budget, hipStream_t stream);
 hipError_t launch_unshuffle(const float* slabs, uint32_t nslabs, uint32_t tiles_per_slab, uint32_t tiles_x, uint32_t W,
                             uint32_t H, float* img, hipStream_t stream);
@@ -71,6 +72,7 @@ struct vr_ctx {
     };
     Buf px_first, px_T, rec_pos, rec_meta, rec_next, rec_act, tr, rec_alloc, rec_bloom, slowq;
     Buf pcg_jump, ray_next, rec_list, rec_nlist, stack_ovf, env_order, rec_cut;
+    Buf ff_scratch, ff_path, ff_sum;  // free-flight integrators (vr_freeflight.hip)
     bool list_ok = false;  // all covariances positive definite: neighbour lists are exact
     int pcg_jump_n = -1;
     uint32_t* h_totals = nullptr;  // pinned copy of rec_alloc: [0] records, [1] overflow-pool entries, [2] exceeded
@@ -314,10 +316,15 @@ vr_status fill_args(vr_ctx* c, const vr_camera* cam, const vr_render_params* p, 
         return fail(VR_ERR_INVALID, "RayMarchingGaussians needs a Gaussian scene");
     if (p->integrator == VR_RAYMARCH_SPHERES && c->type != VR_VOLUME_SPHERES)
         return fail(VR_ERR_INVALID, "RayMarchingSpheres needs a sphere scene");
+    const bool ff = p->integrator == VR_FREE_FLIGHT || p->integrator == VR_MULTI_SCATTER;
     if (p->integrator != VR_RAYMARCH_GAUSSIANS && p->integrator != VR_RAYMARCH_SPHERES && p->integrator != VR_TEST_HITMASK &&
-        p->integrator != VR_PURE_RAYMARCH)
+        p->integrator != VR_PURE_RAYMARCH && !ff)
         return fail(VR_ERR_UNSUPPORTED, "integrator has no device implementation");
-    if (p->integrator != VR_TEST_HITMASK && p->env_samples < 0) return fail(VR_ERR_INVALID, "env_samples must be >= 0");
+    if (ff && c->type != VR_VOLUME_GAUSSIANS)
+        return fail(VR_ERR_INVALID, "free-flight integrators need a Gaussian scene (integrator.h:327 reads scene.gmm)");
+    if (ff && p->num_samples <= 0) return fail(VR_ERR_INVALID, "num_samples must be > 0");
+    if (ff && p->min_bounces < 0) return fail(VR_ERR_INVALID, "min_bounces must be >= 0");
+    if (!ff && p->integrator != VR_TEST_HITMASK && p->env_samples < 0) return fail(VR_ERR_INVALID, "env_samples must be >= 0");
     if (!(p->t_eps >= 0.0f) || p->t_eps >= 1.0f) return fail(VR_ERR_INVALID, "t_eps must be in [0, 1)");
     std::memset(&A, 0, sizeof(A));
     A.cam_type = cam->type;
@@ -357,7 +364,13 @@ vr_status fill_args(vr_ctx* c, const vr_camera* cam, const vr_render_params* p, 
     // the primary early-out itself is allowed (DESIGN.md §Error budget).
     A.tau_cut = p->t_eps > 0.0f ? std::min(104.0f, (float)(std::log(1.0 / p->t_eps) + std::log(1000.0))) : 104.0f;
     if (getenv("VR_DBG_TAUCUT")) A.tau_cut = (float)atof(getenv("VR_DBG_TAUCUT"));  // EXPERIMENT
-    if (p->integrator != VR_TEST_HITMASK) {
+    if (ff) {
+        A.ff_multi = p->integrator == VR_MULTI_SCATTER ? 1 : 0;
+        A.ff_samples = p->num_samples;
+        A.ff_n = (int32_t)std::sqrt((double)p->num_samples);  // int(std::sqrt(num_samples)), integrator.h:564
+        A.ff_min_bounces = p->min_bounces;
+        A.ff_max_bounces = 1 << 16;
+    } else if (p->integrator != VR_TEST_HITMASK) {
         const float* d;
         int n;
         vr_status st = get_table(c, p->step_size, scene_tmax(c, cam), &d, &n);
@@ -524,6 +537,61 @@ vr_status gauss_pipeline(vr_ctx* c, RenderArgs& A, hipStream_t s, bool stats) {
     return VR_OK;
 }
 
+// Free-flight integrators: the frame's tiles x samples are cut into steps of at most kFFThreads
+// paths (a tile chunk x a sample batch); each step runs the path kernel and adds its radiance to
+// the per-pixel running sums in sample order (vr_freeflight.hip).
+constexpr uint32_t kFFThreads = 1u << 20;
+constexpr int32_t kFFHitCap = 64, kFFActCap = 32;
+vr_status free_flight_pipeline(vr_ctx* c, RenderArgs& A, hipStream_t s) {
+    const uint32_t spp = (uint32_t)A.ff_samples;
+    const uint32_t tiles_fit = std::max(1u, kFFThreads / 256u);
+    const uint32_t nsb = std::min(spp, std::max(1u, tiles_fit / std::max(1u, A.num_tiles)));
+    const uint32_t chunk = std::min(A.num_tiles, std::max(1u, tiles_fit / nsb));
+    const uint32_t threads = chunk * nsb * 256u;
+    vr_status st = grow(c->ff_scratch, (size_t)threads * (3 * kFFHitCap + kFFActCap) * 4, "free-flight scratch");
+    if (st != VR_OK) return st;
+    if ((st = grow(c->ff_path, (size_t)threads * 3 * sizeof(float), "free-flight paths")) != VR_OK) return st;
+    if ((st = grow(c->ff_sum, (size_t)A.num_tiles * 256 * 3 * sizeof(float), "free-flight sums")) != VR_OK) return st;
+    float* base = (float*)c->ff_scratch.p;
+    A.ff_threads = threads;
+    A.ff_hit_cap = kFFHitCap;
+    A.ff_act_cap = kFFActCap;
+    A.ff_key = base;
+    A.ff_t1 = base + (size_t)kFFHitCap * threads;
+    A.ff_gid = (int32_t*)(base + (size_t)2 * kFFHitCap * threads);
+    A.ff_act = (int32_t*)(base + (size_t)3 * kFFHitCap * threads);
+    A.ff_path = (float*)c->ff_path.p;
+    A.ff_sum = (float*)c->ff_sum.p;
+    const char* dbg = getenv("VR_FF_DEBUG");  // EXPERIMENT: first-bounce dump of a one-step render
+    vr_ctx::Buf dbuf;
+    if (dbg) {
+        if ((st = grow(dbuf, (size_t)threads * 8 * sizeof(float), "dbg")) != VR_OK) return st;
+        HIP_TRY(hipMemsetAsync(dbuf.p, 0, (size_t)threads * 8 * sizeof(float), s), "memset");
+        A.ff_dbg = (float*)dbuf.p;
+    }
+    for (uint32_t t0 = 0; t0 < A.num_tiles; t0 += chunk) {
+        const uint32_t nt = std::min(chunk, A.num_tiles - t0);
+        for (uint32_t si = 0; si < spp; si += nsb) {
+            A.ff_tile_base = t0;
+            A.ff_si0 = si;
+            A.ff_nsb = std::min(nsb, spp - si);
+            HIP_TRY(launch_free_flight(A, nt, s), "free-flight launch");
+        }
+    }
+    if (dbg) {
+        std::vector<float> h((size_t)threads * 8);
+        HIP_TRY(hipMemcpyAsync(h.data(), dbuf.p, h.size() * 4, hipMemcpyDeviceToHost, s), "dbg copy");
+        HIP_TRY(hipStreamSynchronize(s), "dbg sync");
+        FILE* fp = fopen(dbg, "wb");
+        if (fp) {
+            fwrite(h.data(), 4, h.size(), fp);
+            fclose(fp);
+        }
+        (void)hipFree(dbuf.p);
+    }
+    return VR_OK;
+}
+
 vr_status launch(vr_ctx* c, RenderArgs& A, const vr_render_params* p, hipStream_t s, bool stats = false) {
     vr_status st = ensure_queue(c, (uint64_t)A.num_tiles * 256u);
     if (st != VR_OK) return st;
@@ -541,6 +609,9 @@ vr_status launch(vr_ctx* c, RenderArgs& A, const vr_render_params* p, hipStream_
     c->last_secondary = 0;
     if (c->type == VR_VOLUME_GAUSSIANS && (p->integrator == VR_RAYMARCH_GAUSSIANS || p->integrator == VR_PURE_RAYMARCH)) {
         st = gauss_pipeline(c, A, s, stats);
+        if (st != VR_OK) return st;
+    } else if (p->integrator == VR_FREE_FLIGHT || p->integrator == VR_MULTI_SCATTER) {
+        st = free_flight_pipeline(c, A, s);
         if (st != VR_OK) return st;
     } else {
         HIP_TRY(launch_render(A, s, c->type, p->integrator), "kernel launch");
@@ -593,7 +664,7 @@ void vr_destroy(vr_ctx* c) {
     if (c->h_totals) (void)hipHostFree(c->h_totals);
     for (vr_ctx::Buf* b : {&c->px_first, &c->px_T, &c->rec_pos, &c->rec_meta, &c->rec_next, &c->rec_act, &c->tr,
                            &c->rec_alloc, &c->rec_bloom, &c->slowq, &c->pcg_jump, &c->ray_next, &c->rec_list, &c->rec_nlist,
-                           &c->stack_ovf, &c->env_order, &c->rec_cut})
+                           &c->stack_ovf, &c->env_order, &c->rec_cut, &c->ff_scratch, &c->ff_path, &c->ff_sum})
         if (b->p) (void)hipFree(b->p);
     if (c->d_frame) (void)hipFree(c->d_frame);
     if (c->ev_start) (void)hipEventDestroy(c->ev_start);

@@ -287,6 +287,8 @@ extern "C" vr_status vr_scene_load_xml(const char* path, vr_scene** out, vr_came
         params->env_samples = sc->s.type == VR_VOLUME_SPHERES ? 5 : 20;
         params->t_eps = 0.0f;
         params->flags = 0;
+        params->num_samples = 1;  // sample_count (the ray-march integrators take one sample per pixel)
+        params->min_bounces = 5;
     }
     *out = sc.release();
     return VR_OK;

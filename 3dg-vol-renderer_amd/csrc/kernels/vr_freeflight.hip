@@ -1,0 +1,477 @@
+// Free-flight integrators on the device:
+//   FreeFlightGaussians    include/integrator.h:300-408  (single scattering, float optical-depth sum)
+//   MultiScatterGaussians  include/integrator.h:532-717  (free-flight bounces, NEE, Russian roulette)
+// with the ANALYTIC_PLUS_NEWTON distance solver (distance_solvers.h:25-187, gaussian.h:10-25,
+// 235-297) and the unsorted shadow transmittance transmittance_up_to_BVH (gmm.h:517-578).
+//
+// One thread = one path (pixel, sample index si). A 256-thread workgroup is one 16x16 tile at one
+// sample index, so a wave's 64 paths start from an 8x8 pixel block with the same stratum.
+//
+// Sortless event sweep. The reference builds every ray's full sorted event list (gmm.h:457-515)
+// and walks it segment by segment. Here a ray collects, in one BVH walk, the hits overlapping the
+// window [W0, inf) into a bounded per-thread buffer (kHitCap entries, keyed by entry distance
+// max(t0, W0)); when the buffer is full the largest key is evicted and the window is cut at the
+// smallest evicted key t_cut, so the buffer holds EVERY hit that enters before t_cut. The buffer
+// is sorted by key, and the sweep merges those entries with the exits of the active list
+// (swap-remove order, integrator.h:470-492), producing exactly the reference's segments up to
+// t_cut (t_cut itself is an event of the reference: the evicted entry). The next window starts
+// at t_cut. Usual scenes need a single window.
+//
+// Floating point: ray generation, intersection distances and every discrete decision use the
+// exact (correctly rounded, uncontracted) forms of vr_march.h. libm functions (log, erf, acos,
+// sin, cos) come from the device library, so individual paths can diverge from the oracle when a
+// comparison lands within an ulp; parity is per pixel on most pixels and on the image mean.
+#include <type_traits>
+
+#include "vr_dev_common.h"
+
+namespace vr {
+namespace dev {
+
+constexpr int kFFBlock = 256;
+
+// Per-thread scratch rows (global memory, [slot][thread] so a wave's lanes touch one cache line).
+struct FFScratch {
+    float* key;   // entry distance max(t0, W0)
+    float* t1;    // exit distance
+    int* gid;     // record id (leaf order)
+    int* act;     // active list: slots into the hit buffer
+    uint32_t stride;
+    __device__ __forceinline__ float& K(int i) const { return key[(size_t)i * stride]; }
+    __device__ __forceinline__ float& T1(int i) const { return t1[(size_t)i * stride]; }
+    __device__ __forceinline__ int& G(int i) const { return gid[(size_t)i * stride]; }
+    __device__ __forceinline__ int& Act(int i) const { return act[(size_t)i * stride]; }
+};
+
+// camera.h:45-53 / :64-73 for a float (u, v) (the stratified sample of integrator.h:564-568).
+__device__ __forceinline__ Ray camera_ray(const RenderArgs& A, float uvx, float uvy) {
+    float u, v;
+    if (A.cam_type == 0) {
+        u = 1.0f - uvx * 2.0f;
+        v = uvy * 2.0f - 1.0f;
+    } else {
+        u = uvx * 2.0f - 1.0f;
+        v = 1.0f - uvy * 2.0f;
+    }
+    float o0 = (A.cam_pos[0] + u * A.cam_right[0]) + v * A.cam_up[0];
+    float o1 = (A.cam_pos[1] + u * A.cam_right[1]) + v * A.cam_up[1];
+    float o2 = (A.cam_pos[2] + u * A.cam_right[2]) + v * A.cam_up[2];
+    float d0, d1, d2;
+    if (A.cam_type == 0) {
+        d0 = A.cam_pinhole[0] - o0;
+        d1 = A.cam_pinhole[1] - o1;
+        d2 = A.cam_pinhole[2] - o2;
+    } else {
+        d0 = A.cam_view[0];
+        d1 = A.cam_view[1];
+        d2 = A.cam_view[2];
+    }
+    normalize3(d0, d1, d2);
+    return make_ray(o0, o1, o2, d0, d1, d2);
+}
+
+// integrator.h:32-44: theta = 2.0f * pi (double) * xi1 rounded to float; phi = acos(1 - 2 xi2).
+__device__ __forceinline__ void sample_uniform_direction(PCG32& rng, float& x, float& y, float& z) {
+    float xi1 = rng.uniform();
+    float xi2 = rng.uniform();
+    float theta = (float)(6.283185307179586 * (double)xi1);
+    float phi = acosf(1.0f - 2.0f * xi2);
+    float sp = sinf(phi);
+    x = sp * cosf(theta);
+    y = sp * sinf(theta);
+    z = cosf(phi);
+}
+
+// Optical depth of active entry i on [a, b] (gaussian.h:208-231).
+__device__ __forceinline__ float act_od(const RenderArgs& A, const FFScratch& S, int i, const Ray& r, float a, float b) {
+    GRec g = load_rec(A.gauss, S.G(S.Act(i)));
+    return optical_depth(g, quad(g, r), a, b);
+}
+
+// gaussian.h:10-25
+__device__ __forceinline__ double erfinv_approx(double x) {
+    if (isnan(x)) return __builtin_nan("");
+    if (x <= -1.0) return -__builtin_inf();
+    if (x >= 1.0) return __builtin_inf();
+    const double a = 0.14;
+    double sign = (x < 0.0) ? -1.0 : 1.0;
+    double ln_term = log(1.0 - x * x);
+    double first = 2.0 / (3.14159265358979323846 * a) + ln_term / 2.0;
+    double inside = first * first - ln_term / a;
+    if (inside < 0.0) inside = 0.0;
+    return sign * sqrt(sqrt(inside) - first);
+}
+
+// gaussian.h:235-297 (double)
+__device__ bool solve_for_t_given_tau(const GRec& g, const Ray& r, float t0, float tb, float target_tau, float& t_out) {
+    Quad q = quad(g, r);
+    double Ad = (double)q.A;
+    if (!(Ad > 0.0) || !isfinite(Ad)) return false;
+    double B = 2.0 * (double)(q.B * 0.5f);  // q.B = 2 p.Md exactly (power-of-two scaling)
+    double C = (double)q.Cq;
+    double sqrtA = sqrt(Ad);
+    double pref = (double)g.density * (double)g.norm * sqrt(3.14159265358979323846 / (2.0 * Ad));
+    double exp_factor = exp(-0.5 * (C - (B * B) / (4.0 * Ad)));
+    double denom = pref * exp_factor;
+    if (!(denom > 0.0) || !isfinite(denom)) return false;
+    double two_sqrt2_sqrtA = 2.0 * sqrt(2.0) * sqrtA;
+    double erf_t0 = erf((B + 2.0 * Ad * (double)t0) / two_sqrt2_sqrtA);
+    double target_erf = (double)target_tau / denom + erf_t0;
+    const double one_eps = 1.0 - 1e-14;
+    if (target_erf >= one_eps) {
+        t_out = tb;
+        return true;
+    }
+    if (target_erf <= -one_eps) {
+        t_out = t0;
+        return true;
+    }
+    if (!isfinite(target_erf)) return false;
+    if (target_erf <= -1.0 || target_erf >= 1.0) return false;
+    double arg_t = erfinv_approx(target_erf);
+    double t_candidate = (two_sqrt2_sqrtA * arg_t - B) / (2.0 * Ad);
+    if (!isfinite(t_candidate)) return false;
+    if (t_candidate < (double)t0 - 1e-6) t_candidate = t0;
+    if (t_candidate > (double)tb + 1e-6) t_candidate = tb;
+    t_out = (float)t_candidate;
+    return true;
+}
+
+// sum_i tau_i(ta, t) over the active list, in list order (distance_solvers.h:38-40, 72-78)
+__device__ __forceinline__ float act_tau(const RenderArgs& A, const FFScratch& S, int m, const Ray& r, float ta, float t) {
+    float s = 0.0f;
+    for (int i = 0; i < m; ++i) s += act_od(A, S, i, r, ta, t);
+    return s;
+}
+
+// distance_solvers.h:25-57
+__device__ float solve_bisection(const RenderArgs& A, const FFScratch& S, int m, const Ray& r, float ta, float tb, float target) {
+    float a = ta, b = tb;
+    for (int i = 0; i < 15; ++i) {
+        float mid = 0.5f * (a + b);
+        float f = act_tau(A, S, m, r, ta, mid) - target;
+        if (fabsf(f) <= 1e-6f) return mid;
+        if (f < 0.0f) a = mid;
+        else b = mid;
+    }
+    return 0.5f * (a + b);
+}
+
+// distance_solvers.h:62-127
+__device__ float solve_newton(const RenderArgs& A, const FFScratch& S, int m, const Ray& r, float ta, float tb, float target) {
+    const float a = ta, b = tb, tol = 1e-6f;
+    float t = 0.5f * (a + b);
+    for (int iter = 0; iter < 8; ++iter) {
+        float f = act_tau(A, S, m, r, ta, fminf(t, b)) - target;
+        if (fabsf(f) <= tol) return fminf(fmaxf(t, a), b);
+        float h = fmaxf(1e-5f, (b - a) * 1e-6f);
+        float tp = fminf(b, t + h);
+        float fp = act_tau(A, S, m, r, ta, fminf(tp, b)) - target;
+        float deriv = __fdiv_rn(fp - f, tp - t);
+        if (!(deriv > 0.0f) || !isfinite(deriv) || fabsf(deriv) < 1e-12f) return solve_bisection(A, S, m, r, ta, tb, target);
+        float t_next = t - __fdiv_rn(f, deriv);
+        if (!isfinite(t_next) || t_next < a || t_next > b) return solve_bisection(A, S, m, r, ta, tb, target);
+        if (fabsf(t_next - t) <= tol * fmaxf(1.0f, fabsf(t))) return fminf(fmaxf(t_next, a), b);
+        t = t_next;
+    }
+    return solve_bisection(A, S, m, r, ta, tb, target);
+}
+
+// distance_solvers.h:150-187, ANALYTIC_PLUS_NEWTON
+__device__ float solve_distance(const RenderArgs& A, const FFScratch& S, int m, const Ray& r, float ta, float tb, float rem) {
+    if (m == 1) {
+        float t_an = 0.0f;
+        if (solve_for_t_given_tau(load_rec(A.gauss, S.G(S.Act(0))), r, ta, tb, rem, t_an)) return fminf(fmaxf(t_an, ta), tb);
+    }
+    return solve_newton(A, S, m, r, ta, tb, rem);
+}
+
+// gmm.h:128-143
+__device__ float evaluate_albedo(const RenderArgs& A, const FFScratch& S, int m, float x, float y, float z) {
+    float sum = 0.0f, sum_alb = 0.0f;
+    for (int i = 0; i < m; ++i) {
+        GRec g = load_rec(A.gauss, S.G(S.Act(i)));
+        float mt = mu_t(g, x, y, z);
+        sum += mt;
+        sum_alb += mt * g.albedo;
+    }
+    float a = __fdiv_rn(sum_alb, sum);
+    return a < 0.0f ? 0.0f : (1.0f < a ? 1.0f : a);  // std::clamp: a NaN (0/0) passes through
+}
+
+// gmm.h:517-578: exp(-sum tau_i(max(0,t0_i), min(tmax,t1_i))), unsorted, double accumulation.
+__device__ float transmittance_up_to(const RenderArgs& A, const Ray& r, float tmax, int* stack, int stride) {
+    if (!(tmax > 0.0f)) return 1.0f;
+    double sum = 0.0;
+    traverse<false>(
+        A, r, stack, stride, [&](float tmin, float) { return tmin <= tmax + kTPad * (1.0f + fminf(tmax, 1e30f)); },
+        [&](uint32_t first, uint32_t count) {
+            for (uint32_t j = first; j < first + count; ++j) {
+                GRec g = load_rec(A.gauss, (int)j);
+                Quad q = quad(g, r);
+                float t0, t1;
+                if (!intersect(q, t0, t1)) continue;
+                float a = fmaxf(0.0f, t0);
+                float b = fminf(tmax, t1);
+                if (b > a) sum += (double)optical_depth(g, q, a, b);
+            }
+            return true;
+        });
+    return expf(-(float)sum);
+}
+
+// Free-flight distance along r for target optical depth `target` (integrator.h:330-360 for
+// MULTI = false with a float sum, :422-498 for MULTI = true with a double sum). Returns t >= 0,
+// -1 (no scatter before the last event) or -2 (a per-thread capacity was exceeded). On return
+// with t >= 0 the active list holds the critical segment's Gaussians (count in m).
+template <bool MULTI>
+__device__ float free_flight_distance(const RenderArgs& A, const FFScratch& S, const Ray& r, float target, int& m, int* stack,
+                                      int stride) {
+    using Acc = typename std::conditional<MULTI, double, float>::type;
+    Acc acc = 0;
+    float t_prev = 0.0f;
+    float W0 = 0.0f;
+    const int cap = A.ff_hit_cap;
+    for (;;) {
+        // ---- collect the hits overlapping [W0, inf), keeping the cap smallest entry keys ----
+        int n = 0;
+        float t_cut = INFINITY;
+        traverse<false>(
+            A, r, stack, stride, [&](float, float tmax) { return tmax >= W0 - kTPad * (1.0f + W0); },
+            [&](uint32_t first, uint32_t count) {
+                for (uint32_t j = first; j < first + count; ++j) {
+                    GRec g = load_rec(A.gauss, (int)j);
+                    float t0, t1;
+                    if (!intersect(quad(g, r), t0, t1)) continue;
+                    if (!(t0 <= t1)) continue;  // NaN distances (degenerate covariance): no event
+                    if (W0 > 0.0f && !(t1 > W0)) continue;
+                    float key = fmaxf(t0, W0);
+                    if (key >= t_cut) continue;
+                    if (n < cap) {
+                        S.K(n) = key;
+                        S.T1(n) = t1;
+                        S.G(n) = (int)j;
+                        ++n;
+                    } else {
+                        int imax = 0;
+                        float kmax = S.K(0);
+                        for (int i = 1; i < n; ++i) {
+                            float k = S.K(i);
+                            if (k > kmax) kmax = k, imax = i;
+                        }
+                        if (key < kmax) {
+                            t_cut = fminf(t_cut, kmax);
+                            S.K(imax) = key;
+                            S.T1(imax) = t1;
+                            S.G(imax) = (int)j;
+                        } else {
+                            t_cut = fminf(t_cut, key);
+                        }
+                    }
+                }
+                return true;
+            });
+        // ---- sort the buffer by key (insertion sort; stable, so equal keys keep walk order) ----
+        for (int i = 1; i < n; ++i) {
+            float k = S.K(i), e = S.T1(i);
+            int gi = S.G(i);
+            int j = i - 1;
+            while (j >= 0 && S.K(j) > k) {
+                S.K(j + 1) = S.K(j);
+                S.T1(j + 1) = S.T1(j);
+                S.G(j + 1) = S.G(j);
+                --j;
+            }
+            S.K(j + 1) = k;
+            S.T1(j + 1) = e;
+            S.G(j + 1) = gi;
+        }
+        while (n > 0 && S.K(n - 1) >= t_cut) --n;  // entries past the window (t_cut fell after they were kept)
+        if (t_cut <= W0) return -2.0f;  // more than cap Gaussians overlap at W0: no progress possible
+        if (n == 0 && t_cut == INFINITY) return -1.0f;
+        // ---- sweep the window's events (integrator.h:438-495) ----
+        int i = 0;
+        m = 0;
+        for (;;) {
+            float next_entry = i < n ? S.K(i) : INFINITY;
+            float next_exit = INFINITY;
+            int exit_pos = -1;
+            for (int a = 0; a < m; ++a) {
+                float e = S.T1(S.Act(a));
+                if (e < next_exit) next_exit = e, exit_pos = a;
+            }
+            float t_evt = fminf(next_entry, next_exit);
+            const bool window_end = t_cut <= t_evt;
+            if (window_end) t_evt = t_cut;
+            if (t_evt == INFINITY) return -1.0f;  // past the last event: no scatter (integrator.h:362-366)
+            Acc seg = 0;
+            for (int a = 0; a < m; ++a) seg += (Acc)act_od(A, S, a, r, t_prev, t_evt);
+            if (acc + seg > (Acc)target) {
+                float rem = (float)((Acc)target - acc);
+                if (A.ff_dbg) {
+                    float* d = A.ff_dbg + (size_t)(blockIdx.x * kFFBlock + threadIdx.x) * 8;
+                    d[2] = t_prev, d[3] = t_evt, d[4] = (float)m, d[5] = (float)n, d[6] = rem, d[7] = (float)seg;
+                }
+                return solve_distance(A, S, m, r, t_prev, t_evt, rem);
+            }
+            acc += seg;
+            t_prev = t_evt;
+            if (window_end) break;
+            if (next_entry <= next_exit) {
+                if (m >= A.ff_act_cap) return -2.0f;
+                S.Act(m++) = i++;
+            } else {
+                S.Act(exit_pos) = S.Act(m - 1);
+                --m;
+            }
+        }
+        W0 = t_cut;
+    }
+}
+
+// One path per thread: block b = (tile b / nsb, sample si0 + b % nsb).
+template <bool MULTI>
+__global__ void __launch_bounds__(kFFBlock) ff_path_kernel(RenderArgs A) {
+    __shared__ int s_stack[kStackSize * kFFBlock];
+    int* stack = s_stack + threadIdx.x;
+    const uint32_t b = blockIdx.x;
+    const uint32_t tile_local = A.ff_tile_base + b / A.ff_nsb;
+    const int si = (int)(A.ff_si0 + b % A.ff_nsb);
+    const uint32_t gt = b * kFFBlock + threadIdx.x;
+    FFScratch S{A.ff_key + gt, A.ff_t1 + gt, A.ff_gid + gt, A.ff_act + gt, A.ff_threads};
+    int lx, ly, x, y;
+    tile_pixel(A, tile_local, threadIdx.x, lx, ly, x, y);
+    float L0 = 0.0f, L1 = 0.0f, L2 = 0.0f;
+    if (x < (int)A.width && y < (int)A.height) {
+        PCG32 rng(derive_path_seed(x, y, si), 1);
+        const int n = A.ff_n;
+        const int sx = si % n, sy = si / n;
+        float xi = rng.uniform();
+        float u = __fdiv_rn((float)x + __fdiv_rn((float)sx + xi, (float)n), (float)A.width);
+        xi = rng.uniform();
+        float v = __fdiv_rn((float)y + __fdiv_rn((float)sy + xi, (float)n), (float)A.height);
+        Ray ray = camera_ray(A, u, v);
+        float tp0 = 1.0f, tp1 = 1.0f, tp2 = 1.0f;
+        const int nl = A.num_lights;
+        const float w_ne = (float)(nl + 1);
+        const float p_env = __fdiv_rn(1.0f, (float)(nl + 1));
+        for (int bounce = 0;; ++bounce) {
+            int m = 0;
+            const float target = -logf(1.0f - rng.uniform());
+            const float ts = free_flight_distance<MULTI>(A, S, ray, target, m, stack, kFFBlock);
+            if (ts == -2.0f || bounce >= A.ff_max_bounces) {
+                L0 = L1 = L2 = __builtin_nanf("");
+                atomicAdd(A.counters, 1u);
+                break;
+            }
+            if (ts < 0.0f) {  // no event, or no scatter before the last event: environment
+                L0 += tp0 * A.env[0];
+                L1 += tp1 * A.env[1];
+                L2 += tp2 * A.env[2];
+                break;
+            }
+            const float px = ray.ox + ts * ray.dx, py = ray.oy + ts * ray.dy, pz = ray.oz + ts * ray.dz;
+            const float albedo = evaluate_albedo(A, S, m, px, py, pz);
+            const bool is_env = rng.uniform() < p_env;
+            float Li0, Li1, Li2;
+            if (!is_env) {
+                int li = (int)(rng.uniform() * (float)nl);
+                const LightRecord& Lt = A.lights[li];
+                float wx = Lt.px - px, wy = Lt.py - py, wz = Lt.pz - pz;
+                float dist = sqrtf(dot3(wx, wy, wz, wx, wy, wz));
+                normalize3(wx, wy, wz);
+                Ray sr = make_ray(px, py, pz, wx, wy, wz);
+                float Tr = transmittance_up_to(A, sr, dist, stack, kFFBlock);
+                float d2 = dist * dist;
+                Li0 = __fdiv_rn(Tr * Lt.ix, d2);
+                Li1 = __fdiv_rn(Tr * Lt.iy, d2);
+                Li2 = __fdiv_rn(Tr * Lt.iz, d2);
+            } else {
+                float wx, wy, wz;
+                sample_uniform_direction(rng, wx, wy, wz);
+                Ray er = make_ray(px, py, pz, wx, wy, wz);
+                float Tr = transmittance_up_to(A, er, INFINITY, stack, kFFBlock);
+                Li0 = (Tr * A.env[0]) * k4Pi;
+                Li1 = (Tr * A.env[1]) * k4Pi;
+                Li2 = (Tr * A.env[2]) * k4Pi;
+            }
+            const float w = (albedo * kInv4Pi) * w_ne;
+            if (A.ff_dbg && bounce == 0) {
+                float* d = A.ff_dbg + (size_t)gt * 8;
+                d[0] = target, d[1] = ts;
+            }
+            if constexpr (!MULTI) {  // integrator.h:396-399
+                L0 = w * Li0;
+                L1 = w * Li1;
+                L2 = w * Li2;
+                break;
+            }
+            L0 += (tp0 * w) * Li0;  // integrator.h:681-687
+            L1 += (tp1 * w) * Li1;
+            L2 += (tp2 * w) * Li2;
+            tp0 *= albedo;
+            tp1 *= albedo;
+            tp2 *= albedo;
+            if (bounce >= A.ff_min_bounces) {  // integrator.h:691-695
+                float rr = fminf(fmaxf(tp0, fmaxf(tp1, tp2)), 0.9f);
+                if (rng.uniform() > rr) break;
+                tp0 = __fdiv_rn(tp0, rr);
+                tp1 = __fdiv_rn(tp1, rr);
+                tp2 = __fdiv_rn(tp2, rr);
+            }
+            float nx, ny, nz;
+            sample_uniform_direction(rng, nx, ny, nz);
+            ray = make_ray(px, py, pz, nx, ny, nz);
+        }
+    }
+    A.ff_path[(size_t)gt * 3 + 0] = L0;
+    A.ff_path[(size_t)gt * 3 + 1] = L1;
+    A.ff_path[(size_t)gt * 3 + 2] = L2;
+}
+
+// pixel_L += L_accum in sample order (integrator.h:706), then pixel_L / num_samples on the last batch.
+__global__ void __launch_bounds__(kFFBlock) ff_accumulate_kernel(RenderArgs A, uint32_t chunk_tiles) {
+    const uint32_t tl = blockIdx.x;  // tile within the chunk
+    if (tl >= chunk_tiles) return;
+    const uint32_t tile_local = A.ff_tile_base + tl;
+    const size_t p = (size_t)tile_local * kFFBlock + threadIdx.x;
+    float s0 = 0.0f, s1 = 0.0f, s2 = 0.0f;
+    if (A.ff_si0 != 0) {
+        s0 = A.ff_sum[p * 3 + 0];
+        s1 = A.ff_sum[p * 3 + 1];
+        s2 = A.ff_sum[p * 3 + 2];
+    }
+    for (uint32_t s = 0; s < A.ff_nsb; ++s) {
+        const size_t q = ((size_t)(tl * A.ff_nsb + s) * kFFBlock + threadIdx.x) * 3;
+        s0 += A.ff_path[q + 0];
+        s1 += A.ff_path[q + 1];
+        s2 += A.ff_path[q + 2];
+    }
+    if (A.ff_si0 + A.ff_nsb < (uint32_t)A.ff_samples) {
+        A.ff_sum[p * 3 + 0] = s0;
+        A.ff_sum[p * 3 + 1] = s1;
+        A.ff_sum[p * 3 + 2] = s2;
+        return;
+    }
+    int lx, ly, x, y;
+    tile_pixel(A, tile_local, threadIdx.x, lx, ly, x, y);
+    const float fs = (float)A.ff_samples;
+    store_px(A, tile_local, lx, ly, x, y, __fdiv_rn(s0, fs), __fdiv_rn(s1, fs), __fdiv_rn(s2, fs));
+}
+
+}  // namespace dev
+
+// Host launcher: one (tile chunk, sample batch) step. A.ff_* describe the step.
+hipError_t launch_free_flight(const RenderArgs& A, uint32_t chunk_tiles, hipStream_t stream) {
+    dim3 grid(chunk_tiles * A.ff_nsb);
+    if (A.ff_multi)
+        hipLaunchKernelGGL(dev::ff_path_kernel<true>, grid, dim3(dev::kFFBlock), 0, stream, A);
+    else
+        hipLaunchKernelGGL(dev::ff_path_kernel<false>, grid, dim3(dev::kFFBlock), 0, stream, A);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(dev::ff_accumulate_kernel, dim3(chunk_tiles), dim3(dev::kFFBlock), 0, stream, A, chunk_tiles);
+    return hipGetLastError();
+}
+
+}  // namespace vr

@@ -153,6 +153,23 @@ struct RenderArgs {
     float list_r2;                  // neighbour-list radius: members are the Gaussians with q(pos) <= list_r2
     float list_h[3];                // half-size of the list query box around pos, in node coordinates
     int32_t list_ok;                // scene allows neighbour lists (all covariances positive definite)
+    // ---- free-flight integrators (vr_freeflight.hip): one (tile chunk, sample batch) step ----
+    int32_t ff_multi;        // 0 FreeFlightGaussians, 1 MultiScatterGaussians
+    int32_t ff_samples;      // samples per pixel (integrator num_samples)
+    int32_t ff_n;            // int(sqrt(num_samples)): strata per axis (integrator.h:564)
+    int32_t ff_min_bounces;  // MultiScatterGaussians min_scatter (Russian roulette after it)
+    int32_t ff_max_bounces;  // safety bound on a path's bounces (exceeded: error path)
+    uint32_t ff_si0, ff_nsb; // first sample index of the batch, samples in the batch
+    uint32_t ff_tile_base;   // first tile (tile-local index) of the chunk
+    uint32_t ff_threads;     // threads of one step = row stride of the scratch arrays
+    int32_t ff_hit_cap, ff_act_cap;  // per-thread hit-buffer / active-list capacities
+    float* ff_key;           // scratch [hit_cap][threads]
+    float* ff_t1;            // scratch [hit_cap][threads]
+    int32_t* ff_gid;         // scratch [hit_cap][threads]
+    int32_t* ff_act;         // scratch [act_cap][threads]
+    float* ff_path;          // [threads][3] path radiance of the step
+    float* ff_sum;           // [tile-local pixel][3] running sum over sample batches
+    float* ff_dbg;           // debug (VR_FF_DEBUG): per path of the step, 8 floats of its first bounce
     const unsigned long long* pcg_jump;  // [2k] = A^k, [2k+1] = inc (A^(k-1) + ... + 1): PCG32 state after k draws
 };
 

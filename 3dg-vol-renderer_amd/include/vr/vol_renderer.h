@@ -428,6 +428,26 @@ public:
         : HipIntegrator(camera, VR_RAYMARCH_SPHERES, step_size, env_samples, dev) {}
 };
 
+// integrator.h:273-408 — FreeFlightGaussians(camera, num_samples = 256)
+class FreeFlightGaussians : public HipIntegrator {
+public:
+    FreeFlightGaussians(const std::shared_ptr<Camera>& camera, int num_samples = 256, int dev = 0)
+        : HipIntegrator(camera, VR_FREE_FLIGHT, 0.01f, 0, dev) {
+        params_.num_samples = num_samples;
+    }
+};
+
+// integrator.h:416-720 — MultiScatterGaussians(camera, samples = 16, min_bounces = 5)
+class MultiScatterGaussians : public HipIntegrator {
+public:
+    MultiScatterGaussians(const std::shared_ptr<Camera>& camera, int samples = 16, int min_bounces = 5, int dev = 0)
+        : HipIntegrator(camera, VR_MULTI_SCATTER, 0.01f, 0, dev) {
+        params_.num_samples = samples;
+        params_.min_bounces = min_bounces;
+    }
+    void set_num_samples(int n) { params_.num_samples = n; }  // integrator.h:719
+};
+
 // integrator.h:65-94 — TestIntegrator(camera)
 class TestIntegrator : public HipIntegrator {
 public:

@@ -21,7 +21,8 @@ from ._lib import VRError, check, fptr, lib
 
 __all__ = [
     "VRError", "Light", "Scene", "Camera", "Pinhole_Camera", "Orthographic_Camera", "Ray", "Image",
-    "Integrator", "RayMarchingGaussians", "PureRayMarching", "RayMarchingSpheres", "TestIntegrator", "Device",
+    "Integrator", "RayMarchingGaussians", "PureRayMarching", "RayMarchingSpheres", "FreeFlightGaussians",
+    "MultiScatterGaussians", "TestIntegrator", "Device",
     "load_xml",
     "num_tiles",
 ]
@@ -424,6 +425,35 @@ class PureRayMarching(Integrator):
 
     def __init__(self, camera, step_size=0.01, env_samples=20, t_eps=0.0, device=0):
         super().__init__(camera, step_size, env_samples, t_eps, device)
+
+
+class FreeFlightGaussians(Integrator):
+    """integrator.h:273-408: FreeFlightGaussians(camera, num_samples=256) — single scattering by
+    free-flight sampling, one NEE sample (a light or the environment) per path."""
+
+    integrator_id = L.VR_FREE_FLIGHT
+
+    def __init__(self, camera, num_samples=256, device=0):
+        super().__init__(camera, 0.01, 0, 0.0, device)
+        self.params.num_samples = int(num_samples)
+
+    def set_num_samples(self, n):
+        self.params.num_samples = int(n)
+
+
+class MultiScatterGaussians(Integrator):
+    """integrator.h:416-720: MultiScatterGaussians(camera, samples=16, min_bounces=5) — free-flight
+    paths with NEE at every scattering event and Russian roulette after min_bounces."""
+
+    integrator_id = L.VR_MULTI_SCATTER
+
+    def __init__(self, camera, samples=16, min_bounces=5, device=0):
+        super().__init__(camera, 0.01, 0, 0.0, device)
+        self.params.num_samples = int(samples)
+        self.params.min_bounces = int(min_bounces)
+
+    def set_num_samples(self, n):  # integrator.h:719
+        self.params.num_samples = int(n)
 
 
 class RayMarchingSpheres(Integrator):

@@ -17,6 +17,7 @@ STATUS_NAMES = {
 VR_VOLUME_GAUSSIANS, VR_VOLUME_SPHERES = 0, 1
 VR_CAMERA_PINHOLE, VR_CAMERA_ORTHOGRAPHIC = 0, 1
 VR_RAYMARCH_GAUSSIANS, VR_RAYMARCH_SPHERES, VR_TEST_HITMASK, VR_PURE_RAYMARCH = 0, 1, 2, 3
+VR_FREE_FLIGHT, VR_MULTI_SCATTER = 4, 5
 
 f3 = ctypes.c_float * 3
 
@@ -42,7 +43,8 @@ class vr_camera(ctypes.Structure):
 
 class vr_render_params(ctypes.Structure):
     _fields_ = [("integrator", ctypes.c_int32), ("step_size", ctypes.c_float), ("env_samples", ctypes.c_int32),
-                ("t_eps", ctypes.c_float), ("flags", ctypes.c_uint32)]
+                ("t_eps", ctypes.c_float), ("flags", ctypes.c_uint32), ("num_samples", ctypes.c_int32),
+                ("min_bounces", ctypes.c_int32)]
 
 
 class vr_scene_info(ctypes.Structure):

@@ -23,7 +23,7 @@
 extern "C" {
 #endif
 
-#define VR_ABI_VERSION 1
+#define VR_ABI_VERSION 2
 
 typedef enum vr_status {
     VR_OK = 0,
@@ -47,7 +47,9 @@ typedef enum vr_integrator {
     VR_RAYMARCH_GAUSSIANS = 0, /* RayMarchingGaussians  test_integrators.h:143-297 */
     VR_RAYMARCH_SPHERES = 1,   /* RayMarchingSpheres    test_integrators.h:11-136  */
     VR_TEST_HITMASK = 2,       /* TestIntegrator        integrator.h:65-94         */
-    VR_PURE_RAYMARCH = 3       /* PureRayMarching       integrator.h:100-267       */
+    VR_PURE_RAYMARCH = 3,      /* PureRayMarching       integrator.h:100-267       */
+    VR_FREE_FLIGHT = 4,        /* FreeFlightGaussians   integrator.h:273-408 (single scattering) */
+    VR_MULTI_SCATTER = 5       /* MultiScatterGaussians integrator.h:416-720 (ANALYTIC_PLUS_NEWTON) */
 } vr_integrator;
 
 /* Light (scene.h:12-15). */
@@ -87,13 +89,17 @@ typedef struct vr_camera {
     float focal_length;  /* 1 / tan(fov / 2) */
 } vr_camera;
 
-/* Render parameters = the integrator constructor arguments (test_integrators.h:17,149-153). */
+/* Render parameters = the integrator constructor arguments (test_integrators.h:17,149-153;
+ * integrator.h:278-281, 501-505). */
 typedef struct vr_render_params {
     int32_t integrator;   /* vr_integrator */
     float step_size;      /* ray-march step (reference default 0.01) */
     int32_t env_samples;  /* environment directions per scattering step (20 Gaussians, 5 spheres) */
     float t_eps;          /* stop a ray once T <= t_eps; 0 = exact (stop only when T == 0) */
     uint32_t flags;       /* reserved, must be 0 */
+    int32_t num_samples;  /* free-flight integrators: paths per pixel (FreeFlightGaussians 256,
+                             MultiScatterGaussians 16; set_num_samples, integrator.h:719) */
+    int32_t min_bounces;  /* MultiScatterGaussians min_scatter (default 5): Russian roulette after it */
 } vr_render_params;
 
 typedef struct vr_scene_info {

@@ -60,6 +60,9 @@ def lib():
     L.orc_pcg32.argtypes = [ctypes.c_uint64, ctypes.c_uint64, ctypes.c_int, ctypes.POINTER(ctypes.c_uint32)]
     L.orc_env_dir.argtypes = [ctypes.c_float, ctypes.c_float, fp]
     L.orc_render.restype = ctypes.c_int
+    L.orc_render_ff.argtypes = [P, ctypes.c_int, fp, fp, ctypes.c_float, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_int), ctypes.c_int64, fp,
+                                ctypes.c_int]
     L.orc_render.argtypes = [P, ctypes.c_int, fp, fp, ctypes.c_float, ctypes.c_int, ctypes.c_float,
                              ctypes.c_int, ctypes.c_int, ctypes.c_int, ip, ctypes.c_int64, fp, ctypes.c_int]
     _lib = L
@@ -163,6 +166,28 @@ def render(scene, cam_type, pos, view_dir, fov, W, H, integrator=RAYMARCH_GAUSSI
     rc = lib().orc_render(scene.h, cam_type, pp, pv, float(fov), integrator, float(step_size), int(env_samples),
                           int(W), int(H), pix_p, npix, out.ctypes.data_as(ctypes.POINTER(ctypes.c_float)),
                           int(nthreads))
+    if rc != 0:
+        raise RuntimeError("oracle render failed: " + lib().orc_last_error().decode())
+    return out
+
+
+def render_ff(scene, cam_type, pos, view_dir, fov, W, H, multi=True, num_samples=16, min_bounces=5, pixels=None,
+              nthreads=0):
+    """FreeFlightGaussians (multi=False) / MultiScatterGaussians (multi=True); output as render()."""
+    pos, pp = _f(pos)
+    vd, pv = _f(view_dir)
+    if pixels is not None:
+        pix = np.ascontiguousarray(np.asarray(pixels, dtype=np.int32).reshape(-1, 2))
+        out = np.zeros((pix.shape[0], 3), np.float32)
+        pix_p = pix.ctypes.data_as(ctypes.POINTER(ctypes.c_int))
+        npix = pix.shape[0]
+    else:
+        out = np.zeros((H, W, 3), np.float32)
+        pix_p = None
+        npix = 0
+    rc = lib().orc_render_ff(scene.h, cam_type, pp, pv, float(fov), int(bool(multi)), int(num_samples),
+                             int(min_bounces), int(W), int(H), pix_p, npix,
+                             out.ctypes.data_as(ctypes.POINTER(ctypes.c_float)), int(nthreads))
     if rc != 0:
         raise RuntimeError("oracle render failed: " + lib().orc_last_error().decode())
     return out

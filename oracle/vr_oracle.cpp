@@ -951,6 +951,322 @@ static V3 rm_spheres_pixel(const Scene& scene, const Camera& cam, int i, int j, 
     return radiance;
 }
 
+// =============================================================================================
+// Free-flight integrators. The reference's paths are deterministic per
+// (x, y, sample) through PCG32(derive_path_seed(x, y, si), 1) (rng.h:20-57), so these are
+// restated as written, incl. sample_uniform_direction's libm trigonometry (integrator.h:32-44).
+// =============================================================================================
+
+// integrator.h:32-44. theta: 2.0f * pi (double) * xi1 -> double product rounded to float.
+static V3 sample_uniform_direction(PCG32& rng) {
+    float xi1 = rng.uniform();
+    float xi2 = rng.uniform();
+    float theta = 2.0f * std::numbers::pi * xi1;
+    float phi = std::acos(1.0f - 2.0f * xi2);
+    float x = std::sin(phi) * std::cos(theta);
+    float y = std::sin(phi) * std::sin(theta);
+    float z = std::cos(phi);
+    return {x, y, z};
+}
+
+// gaussian.h:10-25 (Winitzki, a = 0.14, double).
+static double erfinv_approx(double x) {
+    if (std::isnan(x)) return std::numeric_limits<double>::quiet_NaN();
+    if (x <= -1.0) return -std::numeric_limits<double>::infinity();
+    if (x >= 1.0) return std::numeric_limits<double>::infinity();
+    const double a = 0.14;
+    double sign = (x < 0.0) ? -1.0 : 1.0;
+    double ln_term = std::log(1.0 - x * x);
+    double first = 2.0 / (std::numbers::pi * a) + ln_term / 2.0;
+    double inside = first * first - ln_term / a;
+    if (inside < 0.0) inside = 0.0;
+    return sign * std::sqrt(std::sqrt(inside) - first);
+}
+
+// gaussian.h:235-297 — analytic inverse of one Gaussian's optical depth (double).
+static bool solve_for_t_given_tau(const Gaussian& g, const Ray& ray, float t0, float tb, float target_tau, float& t_out) {
+    V3 p = ray.origin - g.mean;
+    V3 Md = mul(g.inv_cov, ray.direction);
+    V3 Mp = mul(g.inv_cov, p);
+    double A = double(dot(ray.direction, Md));
+    if (!(A > 0.0) || !std::isfinite(A)) return false;
+    double B = 2.0 * double(dot(p, Md));
+    double C = double(dot(p, Mp));
+    double sqrtA = std::sqrt(A);
+    double pref = double(g.density) * double(g.norm) * std::sqrt(std::numbers::pi / (2.0 * A));
+    double exp_factor = std::exp(-0.5 * (C - (B * B) / (4.0 * A)));
+    double denom = pref * exp_factor;
+    if (!(denom > 0.0) || !std::isfinite(denom)) return false;
+    double two_sqrt2_sqrtA = 2.0 * std::sqrt(2.0) * sqrtA;
+    double erf_t0 = std::erf((B + 2.0 * A * double(t0)) / two_sqrt2_sqrtA);
+    double target_erf = double(target_tau) / denom + erf_t0;
+    constexpr double one_eps = 1.0 - 1e-14;
+    if (target_erf >= one_eps) { t_out = tb; return true; }
+    if (target_erf <= -one_eps) { t_out = t0; return true; }
+    if (!std::isfinite(target_erf)) return false;
+    if (target_erf <= -1.0 || target_erf >= 1.0) return false;
+    double arg_t = erfinv_approx(target_erf);
+    double t_candidate = (two_sqrt2_sqrtA * arg_t - B) / (2.0 * A);
+    if (!std::isfinite(t_candidate)) return false;
+    if (t_candidate < double(t0) - 1e-6) t_candidate = t0;
+    if (t_candidate > double(tb) + 1e-6) t_candidate = tb;
+    t_out = float(t_candidate);
+    return true;
+}
+
+// distance_solvers.h:25-57
+static float solve_distance_bisection(const Ray& ray, float ta, float tb, const std::vector<size_t>& act, float target,
+                                      const GMM& gmm, int max_iters = 15, float tol = 1e-6f) {
+    float a = ta, b = tb;
+    for (int i = 0; i < max_iters; ++i) {
+        float m = 0.5f * (a + b);
+        float tau = 0.0f;
+        for (auto idx : act) tau += gmm.gaussians[idx].optical_depth(ray, ta, m);
+        float f = tau - target;
+        if (std::fabs(f) <= tol) return m;
+        if (f < 0.0f) a = m;
+        else b = m;
+    }
+    return 0.5f * (a + b);
+}
+
+// distance_solvers.h:62-127
+static float solve_distance_newton_raphson(const Ray& ray, float ta, float tb, const std::vector<size_t>& act,
+                                           float target_tau, const GMM& gmm, int max_iters = 8, float tol = 1e-6f) {
+    float a = ta, b = tb;
+    float t = 0.5f * (a + b);
+    auto compute_f = [&](float tt) -> float {
+        float sum_tau = 0.0f;
+        float tt_clamped = std::min(tt, b);
+        for (auto idx : act) sum_tau += gmm.gaussians[idx].optical_depth(ray, ta, tt_clamped);
+        return sum_tau - target_tau;
+    };
+    for (int iter = 0; iter < max_iters; ++iter) {
+        float f = compute_f(t);
+        if (std::fabs(f) <= tol) return std::clamp(t, a, b);
+        float h = std::max(1e-5f, (b - a) * 1e-6f);
+        float tp = std::min(b, t + h);
+        float fp = compute_f(tp);
+        float deriv = (fp - f) / (tp - t);
+        if (!(deriv > 0.0f) || !std::isfinite(deriv) || std::fabs(deriv) < 1e-12f)
+            return solve_distance_bisection(ray, ta, tb, act, target_tau, gmm);
+        float t_next = t - f / deriv;
+        if (!std::isfinite(t_next) || t_next < a || t_next > b)
+            return solve_distance_bisection(ray, ta, tb, act, target_tau, gmm);
+        if (std::fabs(t_next - t) <= tol * std::max(1.0f, std::fabs(t))) {
+            t = t_next;
+            return std::clamp(t, a, b);
+        }
+        t = t_next;
+    }
+    return solve_distance_bisection(ray, ta, tb, act, target_tau, gmm);
+}
+
+// distance_solvers.h:150-187, ANALYTIC_PLUS_NEWTON (the compiled-in mode, :146).
+static float solve_distance(const Ray& ray, float ta, float tb, const std::vector<size_t>& act, float remaining_tau,
+                            const GMM& gmm) {
+    if (act.size() == 1) {
+        float t_analytic = 0.0f;
+        if (solve_for_t_given_tau(gmm.gaussians[act[0]], ray, ta, tb, remaining_tau, t_analytic))
+            return std::clamp(t_analytic, ta, tb);
+    }
+    return solve_distance_newton_raphson(ray, ta, tb, act, remaining_tau, gmm);
+}
+
+// gmm.h:128-143
+static float evaluate_albedo(const GMM& gmm, const std::vector<size_t>& act, V3 pos) {
+    float sum_mu_t = 0.0f, sum_mu_t_alb = 0.0f;
+    for (size_t idx : act) {
+        float mu_t_i = gmm.gaussians[idx].mu_t(pos);
+        sum_mu_t += mu_t_i;
+        sum_mu_t_alb += mu_t_i * gmm.gaussians[idx].albedo;
+    }
+    float a = sum_mu_t_alb / sum_mu_t;
+    return std::clamp(a, 0.0f, 1.0f);
+}
+
+// gmm.h:517-578 — unsorted, clipped, double-accumulated shadow optical depth on [0, tmax].
+static float transmittance_up_to(const GMM& gmm, const Ray& ray, float tmax) {
+    if (tmax <= 0.0f) return 1.0f;
+    if (gmm.gaussians.empty() || gmm.nodes.empty()) return 1.0f;
+    const float inf = std::numeric_limits<float>::infinity();
+    double sum = 0.0;
+    std::vector<int> stack{0};
+    while (!stack.empty()) {
+        int ni = stack.back();
+        stack.pop_back();
+        const GMM::Node& node = gmm.nodes[ni];
+        float tmin = GMM::IntersectAABB(ray, node.bmin, node.bmax);
+        if (tmin == inf || tmin > tmax) continue;
+        if (node.isLeaf()) {
+            for (int ii = 0; ii < (int)node.count; ++ii) {
+                uint32_t gidx = gmm.indices[node.leftFirst + ii];
+                float g_t0, g_t1;
+                if (!gmm.gaussians[gidx].intersect_direct(ray, g_t0, g_t1)) continue;
+                float a = std::max(0.0f, g_t0);
+                float b = std::min(tmax, g_t1);
+                if (b > a) sum += gmm.gaussians[gidx].optical_depth(ray, a, b);
+            }
+        } else {
+            int li = (int)node.leftFirst, ri = li + 1;
+            float dl = GMM::IntersectAABB(ray, gmm.nodes[li].bmin, gmm.nodes[li].bmax);
+            float dr = GMM::IntersectAABB(ray, gmm.nodes[ri].bmin, gmm.nodes[ri].bmax);
+            if (dl == inf || dl > tmax) dl = inf;
+            if (dr == inf || dr > tmax) dr = inf;
+            if (dl > dr) {
+                if (dl != inf) stack.push_back(li);
+                if (dr != inf) stack.push_back(ri);
+            } else {
+                if (dr != inf) stack.push_back(ri);
+                if (dl != inf) stack.push_back(li);
+            }
+        }
+    }
+    return std::exp(-float(sum));
+}
+
+// integrator.h:422-498 — MultiScatterGaussians::get_free_flight_distance (double accumulation,
+// swap-remove active list). `pos_of` is the index -> list-position map (-1 = absent).
+static float free_flight_distance_ms(const Ray& ray, const std::vector<PrimitiveHitEvent>& events, float target_tau,
+                                     const GMM& gmm, std::vector<size_t>& act, std::vector<int>& pos_of) {
+    double acc_tau = 0.0;
+    float t_prev = 0.0f;
+    float result = -1.0f;
+    for (size_t ev = 0; ev < events.size(); ++ev) {
+        float t_evt = events[ev].t;
+        double seg_tau = 0.0;
+        for (size_t idx : act) seg_tau += gmm.gaussians[idx].optical_depth(ray, t_prev, t_evt);
+        if (acc_tau + seg_tau > double(target_tau)) {
+            float remaining_tau = float(double(target_tau) - acc_tau);
+            result = solve_distance(ray, t_prev, t_evt, act, remaining_tau, gmm);
+            break;
+        }
+        acc_tau += seg_tau;
+        size_t g = events[ev].index;
+        if (events[ev].entering) {
+            if (pos_of[g] < 0) {
+                pos_of[g] = (int)act.size();
+                act.push_back(g);
+            }
+        } else if (pos_of[g] >= 0) {
+            int p = pos_of[g];
+            size_t last = act.back();
+            act[p] = last;
+            pos_of[last] = p;
+            act.pop_back();
+            pos_of[g] = -1;
+        }
+        t_prev = t_evt;
+    }
+    for (size_t idx : act) pos_of[idx] = -1;  // leave the map clean for the next call
+    return result;
+}
+
+static float* g_ff_dbg = nullptr;  // debug: first-bounce values of sample 0 per pixel (8 floats)
+
+// integrator.h:300-408 (single scatter, float accumulation, index-ordered active list) when
+// multi == false; integrator.h:532-717 (multi-scatter, min_bounces, Russian roulette) otherwise.
+static V3 free_flight_pixel(const Scene& scene, const Camera& cam, int x, int y, int W, int H, int num_samples,
+                            int min_scatter, bool multi) {
+    const GMM& gmm = scene.gmm;
+    const size_t N = gmm.gaussians.size();
+    const float phase_pdf = kInv4Pi;
+    const float w_light = float(scene.lights.size() + 1);
+    std::vector<PrimitiveHitEvent> events;
+    std::vector<size_t> act;
+    std::vector<int> pos_of(N, -1);
+    std::vector<bool> active(N, false);
+    V3 pixel_L{0, 0, 0};
+    const int n = int(std::sqrt(num_samples));
+    for (int si = 0; si < num_samples; ++si) {
+        PCG32 rng(derive_path_seed(x, y, si), 1);
+        int sx = si % n, sy = si / n;
+        float u = (x + (sx + rng.uniform()) / n) / W;
+        float v = (y + (sy + rng.uniform()) / n) / H;
+        Ray ray = cam.sample_ray(u, v);
+        V3 throughput{1, 1, 1}, L_accum{0, 0, 0};
+        for (int bounce = 0;; ++bounce) {
+            gmm.intersect_events(ray, events);
+            if (events.empty()) {
+                L_accum = L_accum + V3{throughput.x * scene.env_color.x, throughput.y * scene.env_color.y,
+                                       throughput.z * scene.env_color.z};
+                break;
+            }
+            float target_tau = -std::log(1.0f - rng.uniform());
+            float t_scatter = -1.0f;
+            act.clear();
+            if (multi) {
+                t_scatter = free_flight_distance_ms(ray, events, target_tau, gmm, act, pos_of);
+            } else {  // integrator.h:330-360
+                std::fill(active.begin(), active.end(), false);
+                float acc_tau = 0.0f, t_prev = 0.0f;
+                for (size_t ev = 0; ev < events.size(); ++ev) {
+                    float t_evt = events[ev].t;
+                    act.clear();
+                    for (size_t i = 0; i < N; ++i)
+                        if (active[i]) act.push_back(i);
+                    float seg_tau = 0.0f;
+                    for (auto idx : act) seg_tau += gmm.gaussians[idx].optical_depth(ray, t_prev, t_evt);
+                    if (acc_tau + seg_tau > target_tau) {
+                        t_scatter = solve_distance(ray, t_prev, t_evt, act, target_tau - acc_tau, gmm);
+                        break;
+                    }
+                    acc_tau += seg_tau;
+                    active[events[ev].index] = events[ev].entering;
+                    t_prev = t_evt;
+                }
+            }
+            if (t_scatter < 0.0f) {
+                L_accum = L_accum + V3{throughput.x * scene.env_color.x, throughput.y * scene.env_color.y,
+                                       throughput.z * scene.env_color.z};
+                break;
+            }
+            V3 pos = ray.origin + t_scatter * ray.direction;
+            float albedo = evaluate_albedo(gmm, act, pos);
+            bool is_env = (rng.uniform() < 1.0f / (scene.lights.size() + 1));
+            V3 Li{0, 0, 0};
+            if (!is_env) {
+                int li = int(rng.uniform() * scene.lights.size());
+                const Light& Lt = scene.lights[li];
+                V3 wi = normalized(Lt.position - pos);
+                float dist = norm(Lt.position - pos);
+                Ray shadow(pos, wi);
+                float Tr = transmittance_up_to(gmm, shadow, dist);
+                float d2 = dist * dist;
+                Li = V3{(Tr * Lt.intensity.x) / d2, (Tr * Lt.intensity.y) / d2, (Tr * Lt.intensity.z) / d2};
+            } else {
+                V3 wi = sample_uniform_direction(rng);
+                Ray eray(pos, wi);
+                float Tr = transmittance_up_to(gmm, eray, std::numeric_limits<float>::infinity());
+                Li = V3{(Tr * scene.env_color.x) * k4Pi, (Tr * scene.env_color.y) * k4Pi, (Tr * scene.env_color.z) * k4Pi};
+            }
+            if (g_ff_dbg && si == 0 && bounce == 0) {
+                float* d = g_ff_dbg + ((size_t)y * W + x) * 8;
+                d[0] = target_tau, d[1] = t_scatter, d[2] = albedo, d[3] = is_env ? 0.0f : Li.x, d[4] = pos.x, d[5] = pos.y,
+                d[6] = pos.z, d[7] = is_env ? 1.0f : 0.0f;
+            }
+            if (!multi) {  // integrator.h:396-399
+                float w = (albedo * phase_pdf) * w_light;
+                L_accum = V3{w * Li.x, w * Li.y, w * Li.z};
+                break;
+            }
+            float w = (albedo * phase_pdf) * w_light;  // integrator.h:682-687
+            L_accum = L_accum + V3{(throughput.x * w) * Li.x, (throughput.y * w) * Li.y, (throughput.z * w) * Li.z};
+            throughput = V3{throughput.x * albedo, throughput.y * albedo, throughput.z * albedo};
+            if (bounce >= min_scatter) {  // integrator.h:691-695
+                float rr = std::min(std::max(throughput.x, std::max(throughput.y, throughput.z)), 0.9f);
+                if (rng.uniform() > rr) break;
+                throughput = V3{throughput.x / rr, throughput.y / rr, throughput.z / rr};
+            }
+            V3 new_dir = sample_uniform_direction(rng);
+            ray = Ray(pos, new_dir);
+        }
+        pixel_L = pixel_L + L_accum;
+    }
+    float fs = float(num_samples);
+    return V3{pixel_L.x / fs, pixel_L.y / fs, pixel_L.z / fs};
+}
+
 }  // namespace orc
 
 // =============================================================================================
@@ -1179,6 +1495,34 @@ int orc_render(void* sp, int cam_type, const float* pos, const float* vd, float 
                    : integrator == 2 ? rm_gaussians_pixel_lists(*s, c, x, y, W, H, step_size, env_samples)
                    : integrator == 3 ? rm_pure_pixel(*s, c, x, y, W, H, step_size, env_samples)
                                      : rm_spheres_pixel(*s, c, x, y, W, H, step_size, env_samples);
+            out[3 * q] = L.x; out[3 * q + 1] = L.y; out[3 * q + 2] = L.z;
+        }
+        return 0;
+    } catch (const std::exception& e) {
+        g_err = e.what();
+        return 2;
+    }
+}
+
+void orc_ff_debug(float* buf) { g_ff_dbg = buf; }
+
+// FreeFlightGaussians (multi = 0, integrator.h:300-408) / MultiScatterGaussians (multi = 1,
+// integrator.h:532-717). Same pixel selection and output convention as orc_render.
+int orc_render_ff(void* sp, int cam_type, const float* pos, const float* vd, float fov, int multi, int num_samples,
+                  int min_bounces, int W, int H, const int* pix, int64_t npix, float* out, int nthreads) {
+    try {
+        Scene* s = (Scene*)sp;
+        if (s->volume_type != 0) { g_err = "free-flight integrators need a Gaussian scene"; return 1; }
+        if (num_samples <= 0) { g_err = "num_samples must be > 0"; return 1; }
+        Camera c = cam_type == 0 ? Camera::make_pinhole({pos[0], pos[1], pos[2]}, {vd[0], vd[1], vd[2]}, fov)
+                                 : Camera::make_ortho({pos[0], pos[1], pos[2]}, {vd[0], vd[1], vd[2]});
+        int64_t total = pix ? npix : (int64_t)W * H;
+        if (nthreads > 0) omp_set_num_threads(nthreads);
+#pragma omp parallel for schedule(dynamic, 1)
+        for (int64_t q = 0; q < total; ++q) {
+            int x = pix ? pix[2 * q] : (int)(q % W);
+            int y = pix ? pix[2 * q + 1] : (int)(q / W);
+            V3 L = free_flight_pixel(*s, c, x, y, W, H, num_samples, min_bounces, multi != 0);
             out[3 * q] = L.x; out[3 * q + 1] = L.y; out[3 * q + 2] = L.z;
         }
         return 0;

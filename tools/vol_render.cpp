@@ -2,7 +2,8 @@
 // tests/main.cpp, which hard-codes scene, camera and integrator; here they are arguments).
 //
 //   vol_render --scene scenes/many_gaussians.txt [--spheres] [--xml] [--size 512x512]
-//              [--integrator gaussians|pure|spheres|test] [--step 0.01] [--env 20]
+//              [--integrator gaussians|pure|spheres|test|freeflight|multiscatter] [--step 0.01] [--env 20]
+//              [--spp N] (free-flight paths per pixel; main.cpp:42 renders MultiScatterGaussians at 256)
 //              [--camera pinhole|ortho] [--pos 0,1,6] [--lookat 0,1,0] [--fov 0.785398]
 //              [--out output.ppm] [--dump-rays N]
 //
@@ -28,7 +29,7 @@ int main(int argc, char** argv) try {
     bool spheres = false, xml = false;
     unsigned W = 512, H = 512;
     float step = 0.01f, fov = 0.25f * std::numbers::pi_v<float>;
-    int env = -1, dump = 0;
+    int env = -1, dump = 0, spp = -1;
     Eigen::Vector3f pos(0, 1, 6), lookat(0, 1, 0);
     for (int i = 1; i < argc; ++i) {
         std::string a = argv[i];
@@ -41,6 +42,7 @@ int main(int argc, char** argv) try {
         else if (a == "--xml") xml = true;
         else if (a == "--size") { if (std::sscanf(next(), "%ux%u", &W, &H) != 2) throw std::runtime_error("bad --size"); }
         else if (a == "--integrator") integ = next();
+        else if (a == "--spp") spp = std::stoi(next());
         else if (a == "--step") step = std::strtof(next(), nullptr);
         else if (a == "--env") env = std::atoi(next());
         else if (a == "--camera") cam_type = next();
@@ -90,6 +92,8 @@ int main(int argc, char** argv) try {
     else if (integ == "spheres") integrator = std::make_unique<RayMarchingSpheres>(camera, step, env < 0 ? 5 : env);
     else if (integ == "pure") integrator = std::make_unique<PureRayMarching>(camera, step, env < 0 ? 20 : env);
     else if (integ == "test") integrator = std::make_unique<TestIntegrator>(camera);
+    else if (integ == "freeflight") integrator = std::make_unique<FreeFlightGaussians>(camera, spp < 0 ? 256 : spp);
+    else if (integ == "multiscatter") integrator = std::make_unique<MultiScatterGaussians>(camera, spp < 0 ? 16 : spp);
     else throw std::runtime_error("unknown integrator " + integ);
 
     Image image(W, H);
