@@ -541,7 +541,9 @@ vr_status gauss_pipeline(vr_ctx* c, RenderArgs& A, hipStream_t s, bool stats) {
 // paths (a tile chunk x a sample batch); each step runs the path kernel and adds its radiance to
 // the per-pixel running sums in sample order (vr_freeflight.hip).
 constexpr uint32_t kFFThreads = 1u << 20;
-constexpr int32_t kFFHitCap = 64, kFFActCap = 32;
+// The active list indexes the hit buffer, so it never holds more than kFFHitCap entries: the only
+// capacity a path can exceed is kFFHitCap Gaussians overlapping one point (error path, NaN).
+constexpr int32_t kFFHitCap = 128, kFFActCap = kFFHitCap;
 vr_status free_flight_pipeline(vr_ctx* c, RenderArgs& A, hipStream_t s) {
     const uint32_t spp = (uint32_t)A.ff_samples;
     const uint32_t tiles_fit = std::max(1u, kFFThreads / 256u);
@@ -556,6 +558,7 @@ vr_status free_flight_pipeline(vr_ctx* c, RenderArgs& A, hipStream_t s) {
     A.ff_threads = threads;
     A.ff_hit_cap = kFFHitCap;
     A.ff_act_cap = kFFActCap;
+    A.ff_hit_cap0 = getenv("VR_FF_CAP0") ? std::max(1, std::min(kFFHitCap, atoi(getenv("VR_FF_CAP0")))) : 8;
     A.ff_key = base;
     A.ff_t1 = base + (size_t)kFFHitCap * threads;
     A.ff_gid = (int32_t*)(base + (size_t)2 * kFFHitCap * threads);

@@ -9,7 +9,7 @@
 //
 // Sortless event sweep. The reference builds every ray's full sorted event list (gmm.h:457-515)
 // and walks it segment by segment. Here a ray collects, in one BVH walk, the hits overlapping the
-// window [W0, inf) into a bounded per-thread buffer (kHitCap entries, keyed by entry distance
+// window [W0, inf) into a bounded per-thread buffer (ff_hit_cap entries, keyed by entry distance
 // max(t0, W0)); when the buffer is full the largest key is evicted and the window is cut at the
 // smallest evicted key t_cut, so the buffer holds EVERY hit that enters before t_cut. The buffer
 // is sorted by key, and the sweep merges those entries with the exits of the active list
@@ -80,6 +80,16 @@ __device__ __forceinline__ void sample_uniform_direction(PCG32& rng, float& x, f
     x = sp * cosf(theta);
     y = sp * sinf(theta);
     z = cosf(phi);
+}
+
+// BVH walk over the 32-B half-precision child-pair nodes when the scene has them (boxes rounded
+// outward: the same hit set, since every candidate gets the exact ellipsoid test), else the f32 nodes.
+template <typename Prune, typename Leaf>
+__device__ __forceinline__ void walk(const RenderArgs& A, const Ray& r, int* stack, int stride, Prune prune, Leaf leaf) {
+    if (A.hnodes)
+        traverse<true>(A, r, stack, stride, prune, leaf);
+    else
+        traverse<false>(A, r, stack, stride, prune, leaf);
 }
 
 // Optical depth of active entry i on [a, b] (gaussian.h:208-231).
@@ -203,7 +213,7 @@ __device__ float evaluate_albedo(const RenderArgs& A, const FFScratch& S, int m,
 __device__ float transmittance_up_to(const RenderArgs& A, const Ray& r, float tmax, int* stack, int stride) {
     if (!(tmax > 0.0f)) return 1.0f;
     double sum = 0.0;
-    traverse<false>(
+    walk(
         A, r, stack, stride, [&](float tmin, float) { return tmin <= tmax + kTPad * (1.0f + fminf(tmax, 1e30f)); },
         [&](uint32_t first, uint32_t count) {
             for (uint32_t j = first; j < first + count; ++j) {
@@ -215,7 +225,7 @@ __device__ float transmittance_up_to(const RenderArgs& A, const Ray& r, float tm
                 float b = fminf(tmax, t1);
                 if (b > a) sum += (double)optical_depth(g, q, a, b);
             }
-            return true;
+            return sum < 104.0;  // expf(-x) == 0 in f32 for x >= 104: later terms cannot change Tr
         });
     return expf(-(float)sum);
 }
@@ -231,13 +241,28 @@ __device__ float free_flight_distance(const RenderArgs& A, const FFScratch& S, c
     Acc acc = 0;
     float t_prev = 0.0f;
     float W0 = 0.0f;
-    const int cap = A.ff_hit_cap;
+    // Window capacity starts small (most scatters happen within the first few events) and doubles
+    // after every window without a scatter, or when the overlap at W0 does not fit, up to ff_hit_cap.
+    int cap = A.ff_hit_cap0;
     for (;;) {
-        // ---- collect the hits overlapping [W0, inf), keeping the cap smallest entry keys ----
+        // ---- collect the hits overlapping [W0, inf): the cap smallest entry keys, kept sorted ----
+        // The walk is near-first; once the buffer is full, subtrees starting beyond its largest key
+        // are skipped (their hits could only be evicted), and the window is then cut at that key.
         int n = 0;
         float t_cut = INFINITY;
-        traverse<false>(
-            A, r, stack, stride, [&](float, float tmax) { return tmax >= W0 - kTPad * (1.0f + W0); },
+        float kfull = INFINITY;  // largest kept key while the buffer is full
+        bool pruned_full = false;
+        walk(
+            A, r, stack, stride,
+            [&](float tmin, float tmax) {
+                if (tmax < W0 - kTPad * (1.0f + W0)) return false;
+                const float lim = fminf(t_cut, kfull);
+                if (tmin > lim + kTPad * (1.0f + fminf(lim, 1e30f))) {
+                    pruned_full |= n == cap;
+                    return false;
+                }
+                return true;
+            },
             [&](uint32_t first, uint32_t count) {
                 for (uint32_t j = first; j < first + count; ++j) {
                     GRec g = load_rec(A.gauss, (int)j);
@@ -245,49 +270,39 @@ __device__ float free_flight_distance(const RenderArgs& A, const FFScratch& S, c
                     if (!intersect(quad(g, r), t0, t1)) continue;
                     if (!(t0 <= t1)) continue;  // NaN distances (degenerate covariance): no event
                     if (W0 > 0.0f && !(t1 > W0)) continue;
-                    float key = fmaxf(t0, W0);
+                    const float key = fmaxf(t0, W0);
                     if (key >= t_cut) continue;
-                    if (n < cap) {
-                        S.K(n) = key;
-                        S.T1(n) = t1;
-                        S.G(n) = (int)j;
-                        ++n;
-                    } else {
-                        int imax = 0;
-                        float kmax = S.K(0);
-                        for (int i = 1; i < n; ++i) {
-                            float k = S.K(i);
-                            if (k > kmax) kmax = k, imax = i;
-                        }
-                        if (key < kmax) {
-                            t_cut = fminf(t_cut, kmax);
-                            S.K(imax) = key;
-                            S.T1(imax) = t1;
-                            S.G(imax) = (int)j;
-                        } else {
+                    if (n == cap) {
+                        if (key >= kfull) {  // would be the largest: not kept
                             t_cut = fminf(t_cut, key);
+                            continue;
                         }
+                        t_cut = fminf(t_cut, kfull);  // evict the largest
+                        --n;
                     }
+                    int p = n;  // sorted insert after equal keys (walk order among ties)
+                    while (p > 0 && S.K(p - 1) > key) {
+                        S.K(p) = S.K(p - 1);
+                        S.T1(p) = S.T1(p - 1);
+                        S.G(p) = S.G(p - 1);
+                        --p;
+                    }
+                    S.K(p) = key;
+                    S.T1(p) = t1;
+                    S.G(p) = (int)j;
+                    ++n;
+                    if (n == cap) kfull = S.K(n - 1);
                 }
                 return true;
             });
-        // ---- sort the buffer by key (insertion sort; stable, so equal keys keep walk order) ----
-        for (int i = 1; i < n; ++i) {
-            float k = S.K(i), e = S.T1(i);
-            int gi = S.G(i);
-            int j = i - 1;
-            while (j >= 0 && S.K(j) > k) {
-                S.K(j + 1) = S.K(j);
-                S.T1(j + 1) = S.T1(j);
-                S.G(j + 1) = S.G(j);
-                --j;
-            }
-            S.K(j + 1) = k;
-            S.T1(j + 1) = e;
-            S.G(j + 1) = gi;
-        }
+        // skipped subtrees only hold keys beyond the (final) largest kept key
+        if (pruned_full && n > 0) t_cut = fminf(t_cut, S.K(n - 1));
         while (n > 0 && S.K(n - 1) >= t_cut) --n;  // entries past the window (t_cut fell after they were kept)
-        if (t_cut <= W0) return -2.0f;  // more than cap Gaussians overlap at W0: no progress possible
+        if (t_cut <= W0) {  // more than cap Gaussians overlap at W0: no progress possible at this cap
+            if (cap >= A.ff_hit_cap) return -2.0f;
+            cap = min(2 * cap, A.ff_hit_cap);
+            continue;
+        }
         if (n == 0 && t_cut == INFINITY) return -1.0f;
         // ---- sweep the window's events (integrator.h:438-495) ----
         int i = 0;
@@ -326,6 +341,7 @@ __device__ float free_flight_distance(const RenderArgs& A, const FFScratch& S, c
             }
         }
         W0 = t_cut;
+        cap = min(2 * cap, A.ff_hit_cap);
     }
 }
 

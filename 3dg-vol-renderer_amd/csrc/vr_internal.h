@@ -163,6 +163,7 @@ struct RenderArgs {
     uint32_t ff_tile_base;   // first tile (tile-local index) of the chunk
     uint32_t ff_threads;     // threads of one step = row stride of the scratch arrays
     int32_t ff_hit_cap, ff_act_cap;  // per-thread hit-buffer / active-list capacities
+    int32_t ff_hit_cap0;     // first window's capacity (doubles per window up to ff_hit_cap)
     float* ff_key;           // scratch [hit_cap][threads]
     float* ff_t1;            // scratch [hit_cap][threads]
     int32_t* ff_gid;         // scratch [hit_cap][threads]

@@ -93,6 +93,33 @@ def cpu_baseline(scene, W, H, env_samples, budget_s, threads, log):
                       f"faithful O(N)-mask restatement)"}
 
 
+def cpu_baseline_ff(scene, W, H, multi, spp, budget_s, threads, log):
+    """Free-flight lines: the oracle's restatement of FreeFlightGaussians / MultiScatterGaussians
+    timed on this host on a bounded random pixel sample (all spp paths of each pixel)."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import pyoracle as O
+    g = scene.gaussians()
+    lights = scene.lights
+    osc = O.OracleScene.from_gaussians(g[:, 0:3], g[:, 3:9], g[:, 9], g[:, 10],
+                                       np.array([l.position for l in lights], np.float32),
+                                       np.array([l.intensity for l in lights], np.float32))
+    rng = np.random.default_rng(1234)
+    done, t_total = 0, 0.0
+    batch = 4 * max(1, threads)
+    while t_total < budget_s and done < W * H:
+        idx = rng.choice(W * H, size=batch, replace=False)
+        pix = np.stack([idx % W, idx // W], 1).astype(np.int32)
+        t0 = time.perf_counter()
+        O.render_ff(osc, O.PINHOLE, CAM_POS, CAM_VIEW, FOV, W, H, multi=multi, num_samples=spp, pixels=pix,
+                    nthreads=threads)
+        t_total += time.perf_counter() - t0
+        done += batch
+        log(f"cpu baseline: {done} px in {t_total:.1f} s")
+    return {"value": done * spp / t_total / 1e6, "unit": "Mpaths/s", "cores": threads, "kind": "port",
+            "sample": f"{done} uniformly random pixels x {spp} paths of the {W}x{H} frame ({t_total:.1f} s on "
+                      f"{threads} OpenMP threads); oracle restatement of the reference integrator"}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -106,6 +133,10 @@ def main():
     ap.add_argument("--cpu-budget", type=float, default=20.0, help="seconds of CPU-baseline work (0 = skip)")
     ap.add_argument("--cpu-threads", type=int, default=min(16, os.cpu_count() or 1))
     ap.add_argument("--flops", type=int, default=1, help="run one instrumented frame to count algorithmic work")
+    ap.add_argument("--integrator", default="raymarch", choices=["raymarch", "freeflight", "multiscatter"],
+                    help="raymarch = RayMarchingGaussians (the headline); the free-flight integrators are "
+                         "secondary lines (unit Mpaths/s = pixel samples per second)")
+    ap.add_argument("--spp", type=int, default=16, help="free-flight paths per pixel")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -128,8 +159,14 @@ def main():
     t_setup = time.perf_counter()
     scene, W, H = build_scene(args.config, args.seed)
     camera = vr.Pinhole_Camera(CAM_POS, CAM_VIEW, FOV)
-    integ = vr.RayMarchingGaussians(camera, step_size=0.01, env_samples=args.env_samples, t_eps=args.t_eps,
-                                    device=local)
+    ff = args.integrator != "raymarch"
+    if args.integrator == "freeflight":
+        integ = vr.FreeFlightGaussians(camera, args.spp, device=local)
+    elif args.integrator == "multiscatter":
+        integ = vr.MultiScatterGaussians(camera, args.spp, 5, device=local)
+    else:
+        integ = vr.RayMarchingGaussians(camera, step_size=0.01, env_samples=args.env_samples, t_eps=args.t_eps,
+                                        device=local)
     dev = vr.Device.get(local)
     dev.upload(scene)
     t_setup = time.perf_counter() - t_setup
@@ -188,6 +225,26 @@ def main():
     ms_per_step = elapsed / args.steps * 1e3
     rays = W * H  # whole frame per step, all ranks together (1 primary ray per pixel)
     value = rays / (ms_per_step * 1e-3) / 1e6
+    if ff:
+        if rank == 0:
+            paths = W * H * args.spp
+            cpu = None
+            if world == 1 and args.cpu_budget > 0:
+                cpu = cpu_baseline_ff(scene, W, H, args.integrator == "multiscatter", args.spp, args.cpu_budget,
+                                      args.cpu_threads, log)
+            print(json.dumps({
+                "metric": f"Mpaths/s, {args.integrator} render", "value": paths / (ms_per_step * 1e-3) / 1e6,
+                "unit": "Mpaths/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+                "ms_per_step": ms_per_step, "higher_is_better": True, "scaling": "strong", "vs_baseline": None,
+                "dtype": "f32", "data": "synthetic (seeded make_random.py distribution)",
+                "config": {"workload": CONFIGS[args.config][3], "width": W, "height": H,
+                           "gaussians": scene.get_num_primitives(), "integrator": type(integ).__name__,
+                           "spp": args.spp, "min_bounces": 5, "parallelism": f"tiles{world}",
+                           "frame_kernel_ms": kernel_ms},
+                "cpu_baseline": cpu}), flush=True)
+        if world > 1:
+            dist.destroy_process_group()
+        return
 
     # ---- algorithmic work of this rank's share of one frame (instrumented kernels, untimed) ----
     work = None

@@ -68,7 +68,7 @@ def test_multi_scatter_orthographic_and_min_bounces():
 
 
 def test_many_overlapping_hits_use_several_windows():
-    # 400 Gaussians strung along the central ray: > 64 hits per ray forces the bounded hit buffer to
+    # 400 Gaussians strung along the central ray: > 128 hits per ray forces the bounded hit buffer to
     # cut the event sweep into windows; results must still follow the sorted-event reference.
     rng = np.random.default_rng(7)
     n = 400
@@ -111,3 +111,27 @@ def test_empty_scene_free_flight_is_env():
     for _ in range(4):
         s = np.float32(s + np.float32(0.25))
     assert np.all(g[..., 0] == np.float32(s / np.float32(4)))
+
+
+def test_overlap_beyond_capacity_fails_loudly():
+    # 200 coincident Gaussians: more than the 128-entry per-path hit buffer overlap at one point, so
+    # the sweep cannot make progress; the render must fail (VR_ERR_OVERFLOW), not return garbage.
+    n = 200
+    mean = np.tile(np.float32([0.0, 1.0, 0.0]), (n, 1))
+    cov6 = np.tile(np.float32([0.04, 0, 0, 0.04, 0, 0.04]), (n, 1))
+    scene = vr.Scene.from_gaussians(mean, cov6, np.full(n, 0.01, np.float32), np.full(n, 0.8, np.float32),
+                                    lights=[vr.Light((0.0, 4.0, 0.0), (30.0, 30.0, 30.0))])
+    with pytest.raises(vr.VRError):
+        _gpu(scene, 16, 16, True, 1)
+
+
+@pytest.mark.parametrize("cap0", ["1", "128"])
+def test_window_capacity_does_not_change_results(cap0, monkeypatch):
+    # first-window capacity 1 (a window per event) vs 128 (one window): the event sweep must be the
+    # reference's either way
+    monkeypatch.setenv("VR_FF_CAP0", cap0)
+    path = scene_path("50_random.txt")
+    g = _gpu(vr.Scene.load_GMM(path), 32, 32, True, 4)
+    r = O.render_ff(O.OracleScene.load_gmm(path), O.PINHOLE, CAM_POS, main_view_dir(), FOV, 32, 32, multi=True,
+                    num_samples=4)
+    _check(g, r)
