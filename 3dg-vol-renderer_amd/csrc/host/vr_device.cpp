@@ -550,7 +550,7 @@ vr_status free_flight_pipeline(vr_ctx* c, RenderArgs& A, hipStream_t s) {
     const uint32_t nsb = std::min(spp, std::max(1u, tiles_fit / std::max(1u, A.num_tiles)));
     const uint32_t chunk = std::min(A.num_tiles, std::max(1u, tiles_fit / nsb));
     const uint32_t threads = chunk * nsb * 256u;
-    vr_status st = grow(c->ff_scratch, (size_t)threads * (3 * kFFHitCap + kFFActCap) * 4, "free-flight scratch");
+    vr_status st = grow(c->ff_scratch, (size_t)threads * (3 * kFFHitCap + 8 * kFFActCap) * 4, "free-flight scratch");
     if (st != VR_OK) return st;
     if ((st = grow(c->ff_path, (size_t)threads * 3 * sizeof(float), "free-flight paths")) != VR_OK) return st;
     if ((st = grow(c->ff_sum, (size_t)A.num_tiles * 256 * 3 * sizeof(float), "free-flight sums")) != VR_OK) return st;
@@ -563,6 +563,7 @@ vr_status free_flight_pipeline(vr_ctx* c, RenderArgs& A, hipStream_t s) {
     A.ff_t1 = base + (size_t)kFFHitCap * threads;
     A.ff_gid = (int32_t*)(base + (size_t)2 * kFFHitCap * threads);
     A.ff_act = (int32_t*)(base + (size_t)3 * kFFHitCap * threads);
+    A.ff_cache = base + (size_t)(3 * kFFHitCap + kFFActCap) * threads;
     A.ff_path = (float*)c->ff_path.p;
     A.ff_sum = (float*)c->ff_sum.p;
     const char* dbg = getenv("VR_FF_DEBUG");  // EXPERIMENT: first-bounce dump of a one-step render

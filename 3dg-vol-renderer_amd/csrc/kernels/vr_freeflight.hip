@@ -36,11 +36,52 @@ struct FFScratch {
     float* t1;    // exit distance
     int* gid;     // record id (leaf order)
     int* act;     // active list: slots into the hit buffer
+    // per active entry, cached for the bounce's ray when it enters (optical_depth's factors,
+    // gaussian.h:208-231): od(t_prev, t) = P * (erf((B + 2A t) / den) - F) with F = erf(.. t_prev ..),
+    // the same float operations as optical_depth(), so the values are bit-identical
+    float* aP;    // pref * exp(-0.5 (C - B^2 / 4A))
+    float* aB;    // B
+    float* a2A;   // 2A
+    float* aDen;  // 2 sqrt(2A)
+    float* aF;    // erf argument value at t_prev
+    float* aFn;   // erf value at the segment end (committed when the segment is passed)
+    float* aT1;   // exit distance
     uint32_t stride;
     __device__ __forceinline__ float& K(int i) const { return key[(size_t)i * stride]; }
     __device__ __forceinline__ float& T1(int i) const { return t1[(size_t)i * stride]; }
     __device__ __forceinline__ int& G(int i) const { return gid[(size_t)i * stride]; }
     __device__ __forceinline__ int& Act(int i) const { return act[(size_t)i * stride]; }
+    __device__ __forceinline__ float& P(int i) const { return aP[(size_t)i * stride]; }
+    __device__ __forceinline__ float& Bq(int i) const { return aB[(size_t)i * stride]; }
+    __device__ __forceinline__ float& TwoA(int i) const { return a2A[(size_t)i * stride]; }
+    __device__ __forceinline__ float& Den(int i) const { return aDen[(size_t)i * stride]; }
+    __device__ __forceinline__ float& F(int i) const { return aF[(size_t)i * stride]; }
+    __device__ __forceinline__ float& Fn(int i) const { return aFn[(size_t)i * stride]; }
+    __device__ __forceinline__ float& AT1(int i) const { return aT1[(size_t)i * stride]; }
+    // entry i (hit slot `slot`) becomes active at t: cache its factors (optical_depth's own ops)
+    __device__ __forceinline__ void enter(const RenderArgs& A, int i, int slot, const Ray& r, float t) const {
+        Act(i) = slot;
+        AT1(i) = T1(slot);
+        GRec g = load_rec(A.gauss, G(slot));
+        Quad q = quad(g, r);
+        float twoA = 2.0f * q.A;
+        float pref = (g.density * g.norm) * sqrtf(__fdiv_rn(3.14159265358979323846f, twoA));
+        float den = 2.0f * sqrtf(twoA);
+        float e = expf(-0.5f * (q.Cq - __fdiv_rn(q.B * q.B, 4.0f * q.A)));
+        P(i) = pref * e;
+        Bq(i) = q.B;
+        TwoA(i) = twoA;
+        Den(i) = den;
+        F(i) = erff(__fdiv_rn(q.B + twoA * t, den));
+    }
+    __device__ __forceinline__ void move(int dst, int src) const {
+        Act(dst) = Act(src), AT1(dst) = AT1(src), P(dst) = P(src), Bq(dst) = Bq(src);
+        TwoA(dst) = TwoA(src), Den(dst) = Den(src), F(dst) = F(src);
+    }
+    // optical depth of active entry i on [t_prev, t]
+    __device__ __forceinline__ float od_to(int i, float t) const {
+        return P(i) * (erff(__fdiv_rn(Bq(i) + TwoA(i) * t, Den(i))) - F(i));
+    }
 };
 
 // camera.h:45-53 / :64-73 for a float (u, v) (the stratified sample of integrator.h:564-568).
@@ -90,12 +131,6 @@ __device__ __forceinline__ void walk(const RenderArgs& A, const Ray& r, int* sta
         traverse<true>(A, r, stack, stride, prune, leaf);
     else
         traverse<false>(A, r, stack, stride, prune, leaf);
-}
-
-// Optical depth of active entry i on [a, b] (gaussian.h:208-231).
-__device__ __forceinline__ float act_od(const RenderArgs& A, const FFScratch& S, int i, const Ray& r, float a, float b) {
-    GRec g = load_rec(A.gauss, S.G(S.Act(i)));
-    return optical_depth(g, quad(g, r), a, b);
 }
 
 // gaussian.h:10-25
@@ -149,8 +184,8 @@ __device__ bool solve_for_t_given_tau(const GRec& g, const Ray& r, float t0, flo
 
 // sum_i tau_i(ta, t) over the active list, in list order (distance_solvers.h:38-40, 72-78)
 __device__ __forceinline__ float act_tau(const RenderArgs& A, const FFScratch& S, int m, const Ray& r, float ta, float t) {
-    float s = 0.0f;
-    for (int i = 0; i < m; ++i) s += act_od(A, S, i, r, ta, t);
+    float s = 0.0f;  // ta is the segment start t_prev, where the cached F values were taken
+    for (int i = 0; i < m; ++i) s += S.od_to(i, t);
     return s;
 }
 
@@ -312,7 +347,7 @@ __device__ float free_flight_distance(const RenderArgs& A, const FFScratch& S, c
             float next_exit = INFINITY;
             int exit_pos = -1;
             for (int a = 0; a < m; ++a) {
-                float e = S.T1(S.Act(a));
+                float e = S.AT1(a);
                 if (e < next_exit) next_exit = e, exit_pos = a;
             }
             float t_evt = fminf(next_entry, next_exit);
@@ -320,7 +355,11 @@ __device__ float free_flight_distance(const RenderArgs& A, const FFScratch& S, c
             if (window_end) t_evt = t_cut;
             if (t_evt == INFINITY) return -1.0f;  // past the last event: no scatter (integrator.h:362-366)
             Acc seg = 0;
-            for (int a = 0; a < m; ++a) seg += (Acc)act_od(A, S, a, r, t_prev, t_evt);
+            for (int a = 0; a < m; ++a) {
+                const float f1 = erff(__fdiv_rn(S.Bq(a) + S.TwoA(a) * t_evt, S.Den(a)));
+                S.Fn(a) = f1;
+                seg += (Acc)(S.P(a) * (f1 - S.F(a)));
+            }
             if (acc + seg > (Acc)target) {
                 float rem = (float)((Acc)target - acc);
                 if (A.ff_dbg) {
@@ -331,12 +370,13 @@ __device__ float free_flight_distance(const RenderArgs& A, const FFScratch& S, c
             }
             acc += seg;
             t_prev = t_evt;
+            for (int a = 0; a < m; ++a) S.F(a) = S.Fn(a);
             if (window_end) break;
             if (next_entry <= next_exit) {
                 if (m >= A.ff_act_cap) return -2.0f;
-                S.Act(m++) = i++;
+                S.enter(A, m++, i++, r, t_evt);
             } else {
-                S.Act(exit_pos) = S.Act(m - 1);
+                S.move(exit_pos, m - 1);
                 --m;
             }
         }
@@ -354,7 +394,11 @@ __global__ void __launch_bounds__(kFFBlock) ff_path_kernel(RenderArgs A) {
     const uint32_t tile_local = A.ff_tile_base + b / A.ff_nsb;
     const int si = (int)(A.ff_si0 + b % A.ff_nsb);
     const uint32_t gt = b * kFFBlock + threadIdx.x;
-    FFScratch S{A.ff_key + gt, A.ff_t1 + gt, A.ff_gid + gt, A.ff_act + gt, A.ff_threads};
+    const size_t AC = (size_t)A.ff_act_cap * A.ff_threads;
+    float* cache = A.ff_cache + gt;
+    FFScratch S{A.ff_key + gt, A.ff_t1 + gt, A.ff_gid + gt, A.ff_act + gt,
+                cache, cache + AC, cache + 2 * AC, cache + 3 * AC, cache + 4 * AC, cache + 5 * AC, cache + 6 * AC,
+                A.ff_threads};
     int lx, ly, x, y;
     tile_pixel(A, tile_local, threadIdx.x, lx, ly, x, y);
     float L0 = 0.0f, L1 = 0.0f, L2 = 0.0f;
