@@ -20,6 +20,8 @@ hipError_t gauss_lists(const RenderArgs& A, uint32_t nrec, hipStream_t stream);
 hipError_t gauss_secondary(const RenderArgs& A, uint32_t nrec, hipStream_t stream, bool stats);
 hipError_t gauss_accumulate(const RenderArgs& A, uint32_t nrec, hipStream_t stream);
 hipError_t launch_free_flight(const RenderArgs& A, uint32_t chunk_tiles, hipStream_t stream);
+hipError_t launch_sfd_loss_diff(const uint32_t* bits0, const uint32_t* bits1, const float* lb, const float* lp, uint32_t npix,
+                                uint32_t n, double* out, hipStream_t stream);
 hipError_t gauss_record_cut(const RenderArgs& A, float budget, hipStream_t stream);
 hipError_t launch_unshuffle(const float* slabs, uint32_t nslabs, uint32_t tiles_per_slab, uint32_t tiles_x, uint32_t W,
                             uint32_t H, float* img, hipStream_t stream);
@@ -73,6 +75,10 @@ struct vr_ctx {
     Buf px_first, px_T, rec_pos, rec_meta, rec_next, rec_act, tr, rec_alloc, rec_bloom, slowq;
     Buf pcg_jump, ray_next, rec_list, rec_nlist, stack_ovf, env_order, rec_cut;
     Buf ff_scratch, ff_path, ff_sum;  // free-flight integrators (vr_freeflight.hip)
+    uint32_t* d_order = nullptr;      // record (leaf order) -> scene index
+    Buf rec_bits[2];                  // RECORD_PIXEL_GAUSSIANS bitsets (vr_render_record slots)
+    uint32_t rec_npix[2] = {0, 0}, rec_n[2] = {0, 0};
+    Buf sfd_tmp;                      // vr_sfd_loss_diff: losses + output
     bool list_ok = false;  // all covariances positive definite: neighbour lists are exact
     int pcg_jump_n = -1;
     uint32_t* h_totals = nullptr;  // pinned copy of rec_alloc: [0] records, [1] overflow-pool entries, [2] exceeded
@@ -92,6 +98,8 @@ vr_status hip_fail(hipError_t e, const char* what) {
     } while (0)
 
 void free_scene(vr_ctx* c) {
+    if (c->d_order) (void)hipFree(c->d_order);
+    c->d_order = nullptr;
     if (c->d_gauss) (void)hipFree(c->d_gauss);
     if (c->d_nodes) (void)hipFree(c->d_nodes);
     if (c->d_hnodes) (void)hipFree(c->d_hnodes);
@@ -379,6 +387,7 @@ vr_status fill_args(vr_ctx* c, const vr_camera* cam, const vr_render_params* p, 
         A.num_tsteps = n;
     }
     A.counters = c->d_counters;
+    A.gauss_order = c->d_order;
     return VR_OK;
 }
 
@@ -668,7 +677,7 @@ void vr_destroy(vr_ctx* c) {
     if (c->h_totals) (void)hipHostFree(c->h_totals);
     for (vr_ctx::Buf* b : {&c->px_first, &c->px_T, &c->rec_pos, &c->rec_meta, &c->rec_next, &c->rec_act, &c->tr,
                            &c->rec_alloc, &c->rec_bloom, &c->slowq, &c->pcg_jump, &c->ray_next, &c->rec_list, &c->rec_nlist,
-                           &c->stack_ovf, &c->env_order, &c->rec_cut, &c->ff_scratch, &c->ff_path, &c->ff_sum})
+                           &c->stack_ovf, &c->env_order, &c->rec_cut, &c->ff_scratch, &c->ff_path, &c->ff_sum, &c->rec_bits[0], &c->rec_bits[1], &c->sfd_tmp})
         if (b->p) (void)hipFree(b->p);
     if (c->d_frame) (void)hipFree(c->d_frame);
     if (c->ev_start) (void)hipEventDestroy(c->ev_start);
@@ -719,6 +728,12 @@ vr_status vr_upload_scene(vr_ctx* c, const vr_scene* sc) {
         }
         HIP_TRY(hipMalloc(&c->d_gauss, rec.size() * sizeof(GaussianRecord)), "hipMalloc(records)");
         HIP_TRY(hipMemcpy(c->d_gauss, rec.data(), rec.size() * sizeof(GaussianRecord), hipMemcpyHostToDevice), "hipMemcpy(records)");
+        {
+            std::vector<uint32_t> order(std::max<size_t>(N, 1), 0u);
+            for (size_t j = 0; j < N; ++j) order[j] = (uint32_t)b.order[j];
+            HIP_TRY(hipMalloc(&c->d_order, order.size() * sizeof(uint32_t)), "hipMalloc(order)");
+            HIP_TRY(hipMemcpy(c->d_order, order.data(), order.size() * sizeof(uint32_t), hipMemcpyHostToDevice), "hipMemcpy(order)");
+        }
         HIP_TRY(hipMalloc(&c->d_nodes, b.nodes.size() * sizeof(BVHNode)), "hipMalloc(nodes)");
         HIP_TRY(hipMemcpy(c->d_nodes, b.nodes.data(), b.nodes.size() * sizeof(BVHNode), hipMemcpyHostToDevice), "hipMemcpy(nodes)");
         c->num_prims = (int32_t)N;
@@ -858,6 +873,79 @@ vr_status vr_unshuffle_tiles_device(vr_ctx* c, const float* d_slabs, uint32_t ns
     HIP_TRY(hipSetDevice(c->device), "hipSetDevice");
     HIP_TRY(launch_unshuffle(d_slabs, nslabs, tiles_per_slab, (W + kTile - 1) / kTile, W, H, d_image, (hipStream_t)stream),
             "unshuffle launch");
+    return VR_OK;
+}
+
+vr_status vr_render_record(vr_ctx* c, const vr_camera* cam, const vr_render_params* p, uint32_t W, uint32_t H, float* rgb,
+                           int32_t slot) {
+    if (!c || !rgb || !p) return fail(VR_ERR_INVALID, "vr_render_record: NULL argument");
+    if (slot != 0 && slot != 1) return fail(VR_ERR_INVALID, "vr_render_record: slot must be 0 or 1");
+    if (p->integrator != VR_MULTI_SCATTER)
+        return fail(VR_ERR_INVALID, "vr_render_record: MultiScatterGaussians only (integrator.h:532-536)");
+    HIP_TRY(hipSetDevice(c->device), "hipSetDevice");
+    RenderArgs A;
+    vr_status st = fill_args(c, cam, p, W, H, A);
+    if (st != VR_OK) return st;
+    const uint64_t npix = (uint64_t)W * H, words = ((uint64_t)c->num_prims + 31) / 32;
+    const size_t bytes = std::max<size_t>((size_t)(words * npix * 4), 4);
+    if ((st = grow(c->rec_bits[slot], bytes, "hipMalloc(pixel Gaussian bits)")) != VR_OK) return st;
+    HIP_TRY(hipMemsetAsync(c->rec_bits[slot].p, 0, bytes, c->stream), "hipMemsetAsync(bits)");
+    c->rec_npix[slot] = (uint32_t)npix;
+    c->rec_n[slot] = (uint32_t)c->num_prims;
+    A.rec_bits = (uint32_t*)c->rec_bits[slot].p;
+    A.rec_npix = (uint32_t)npix;
+    size_t fb = npix * 3 * sizeof(float);
+    if (fb > c->frame_cap) {
+        if (c->d_frame) (void)hipFree(c->d_frame);
+        c->d_frame = nullptr;
+        HIP_TRY(hipMalloc(&c->d_frame, fb), "hipMalloc(frame)");
+        c->frame_cap = fb;
+    }
+    A.first_tile = 0;
+    A.tile_stride = 1;
+    A.num_tiles = vr_num_tiles(W, H);
+    A.packed = 0;
+    A.out = c->d_frame;
+    st = launch(c, A, p, c->stream);
+    if (st != VR_OK) return st;
+    HIP_TRY(hipMemcpyAsync(rgb, c->d_frame, fb, hipMemcpyDeviceToHost, c->stream), "hipMemcpyAsync(frame)");
+    HIP_TRY(hipStreamSynchronize(c->stream), "render");
+    c->stats_pending = false;
+    if (c->h_counters[1] != 0)
+        return fail(VR_ERR_OVERFLOW, std::to_string(c->h_counters[1]) + " paths exceeded the per-path capacity (NaN)");
+    return VR_OK;
+}
+
+vr_status vr_get_pixel_gaussians(vr_ctx* c, int32_t slot, uint32_t* bits, size_t n_words) {
+    if (!c || !bits || (slot != 0 && slot != 1)) return fail(VR_ERR_INVALID, "vr_get_pixel_gaussians: bad argument");
+    const size_t need = (size_t)((c->rec_n[slot] + 31) / 32) * c->rec_npix[slot];
+    if (!c->rec_bits[slot].p || c->rec_npix[slot] == 0) return fail(VR_ERR_INVALID, "slot holds no recording");
+    if (n_words != need) return fail(VR_ERR_INVALID, "n_words must be ceil(N/32) * W * H = " + std::to_string(need));
+    HIP_TRY(hipSetDevice(c->device), "hipSetDevice");
+    HIP_TRY(hipMemcpy(bits, c->rec_bits[slot].p, need * 4, hipMemcpyDeviceToHost), "hipMemcpy(bits)");
+    return VR_OK;
+}
+
+vr_status vr_sfd_loss_diff(vr_ctx* c, const float* loss_base, const float* loss_plus, uint32_t W, uint32_t H, double* out,
+                           size_t n) {
+    if (!c || !loss_base || !loss_plus || !out) return fail(VR_ERR_INVALID, "vr_sfd_loss_diff: NULL argument");
+    const uint32_t npix = W * H;
+    if (c->rec_npix[0] != npix || c->rec_npix[1] != npix || c->rec_n[0] != c->rec_n[1] || n != c->rec_n[0])
+        return fail(VR_ERR_INVALID, "vr_sfd_loss_diff: slots 0 and 1 must hold recordings of this frame size and n Gaussians");
+    HIP_TRY(hipSetDevice(c->device), "hipSetDevice");
+    vr_status st = grow(c->sfd_tmp, (size_t)npix * 8 + n * 8 + 16, "hipMalloc(sfd)");
+    if (st != VR_OK) return st;
+    float* lb = (float*)c->sfd_tmp.p;
+    float* lp = lb + npix;
+    double* d_out = (double*)((char*)c->sfd_tmp.p + (((size_t)npix * 8 + 15) & ~(size_t)15));
+    HIP_TRY(hipMemcpyAsync(lb, loss_base, (size_t)npix * 4, hipMemcpyHostToDevice, c->stream), "hipMemcpyAsync");
+    HIP_TRY(hipMemcpyAsync(lp, loss_plus, (size_t)npix * 4, hipMemcpyHostToDevice, c->stream), "hipMemcpyAsync");
+    HIP_TRY(hipMemsetAsync(d_out, 0, n * 8, c->stream), "hipMemsetAsync");
+    if (n > 0)
+        HIP_TRY(launch_sfd_loss_diff((const uint32_t*)c->rec_bits[0].p, (const uint32_t*)c->rec_bits[1].p, lb, lp, npix,
+                                     (uint32_t)n, d_out, c->stream), "sfd launch");
+    HIP_TRY(hipMemcpyAsync(out, d_out, n * 8, hipMemcpyDeviceToHost, c->stream), "hipMemcpyAsync");
+    HIP_TRY(hipStreamSynchronize(c->stream), "sfd");
     return VR_OK;
 }
 

@@ -265,6 +265,25 @@ __device__ float transmittance_up_to(const RenderArgs& A, const Ray& r, float tm
     return expf(-(float)sum);
 }
 
+// RECORD_PIXEL_GAUSSIANS (integrator.h:616-644): mark, for pixel p, every Gaussian whose events on
+// this ray lie at or before t_scatter + 1e-6 (entries t0 <= lim), or every Gaussian the ray hits
+// when it did not scatter. Bits are per original scene index: word (g >> 5) of pixel p.
+__device__ void record_hits(const RenderArgs& A, const Ray& r, float lim, uint32_t p, int* stack, int stride) {
+    walk(
+        A, r, stack, stride, [&](float tmin, float) { return tmin <= lim + kTPad * (1.0f + fminf(lim, 1e30f)); },
+        [&](uint32_t first, uint32_t count) {
+            for (uint32_t j = first; j < first + count; ++j) {
+                GRec g = load_rec(A.gauss, (int)j);
+                float t0, t1;
+                if (!intersect(quad(g, r), t0, t1)) continue;
+                if (!(t0 <= lim)) continue;
+                const uint32_t o = A.gauss_order[j];
+                atomicOr(A.rec_bits + (size_t)(o >> 5) * A.rec_npix + p, 1u << (o & 31u));
+            }
+            return true;
+        });
+}
+
 // Free-flight distance along r for target optical depth `target` (integrator.h:330-360 for
 // MULTI = false with a float sum, :422-498 for MULTI = true with a double sum). Returns t >= 0,
 // -1 (no scatter before the last event) or -2 (a per-thread capacity was exceeded). On return
@@ -419,6 +438,8 @@ __global__ void __launch_bounds__(kFFBlock) ff_path_kernel(RenderArgs A) {
             int m = 0;
             const float target = -logf(1.0f - rng.uniform());
             const float ts = free_flight_distance<MULTI>(A, S, ray, target, m, stack, kFFBlock);
+            if (MULTI && A.rec_bits && ts != -2.0f)
+                record_hits(A, ray, ts >= 0.0f ? ts + 1e-6f : INFINITY, (uint32_t)y * A.width + (uint32_t)x, stack, kFFBlock);
             if (ts == -2.0f || bounce >= A.ff_max_bounces) {
                 L0 = L1 = L2 = __builtin_nanf("");
                 atomicAdd(A.counters, 1u);
@@ -519,7 +540,43 @@ __global__ void __launch_bounds__(kFFBlock) ff_accumulate_kernel(RenderArgs A, u
     store_px(A, tile_local, lx, ly, x, y, __fdiv_rn(s0, fs), __fdiv_rn(s1, fs), __fdiv_rn(s2, fs));
 }
 
+// inverse_integrator.h:166-182: out[g] += sum over pixels p whose bit g is set in bits0 or bits1 of
+// (loss_plus[p] - loss_base[p]) (double). Grid: (words, pixel chunks); each thread keeps the 32
+// Gaussians of its word in registers, a wave reduces them, lane 0 adds them atomically.
+__global__ void __launch_bounds__(256) sfd_loss_diff_kernel(const uint32_t* __restrict__ bits0, const uint32_t* __restrict__ bits1,
+                                                            const float* __restrict__ loss_base, const float* __restrict__ loss_plus,
+                                                            uint32_t npix, uint32_t chunk, uint32_t n, double* out) {
+    const uint32_t w = blockIdx.x;
+    const uint32_t p0 = blockIdx.y * chunk, p1 = min(npix, p0 + chunk);
+    double acc[32];
+#pragma unroll
+    for (int b = 0; b < 32; ++b) acc[b] = 0.0;
+    for (uint32_t p = p0 + threadIdx.x; p < p1; p += blockDim.x) {
+        const uint32_t word = bits0[(size_t)w * npix + p] | bits1[(size_t)w * npix + p];
+        if (!word) continue;
+        const double d = (double)loss_plus[p] - (double)loss_base[p];
+#pragma unroll
+        for (int b = 0; b < 32; ++b)
+            if ((word >> b) & 1u) acc[b] += d;
+    }
+#pragma unroll
+    for (int b = 0; b < 32; ++b) {
+        double v = acc[b];
+        for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+        const uint32_t g = w * 32u + (uint32_t)b;
+        if ((threadIdx.x & 63) == 0 && v != 0.0 && g < n) atomicAdd(out + g, v);
+    }
+}
+
 }  // namespace dev
+
+hipError_t launch_sfd_loss_diff(const uint32_t* bits0, const uint32_t* bits1, const float* lb, const float* lp, uint32_t npix,
+                                uint32_t n, double* out, hipStream_t stream) {
+    const uint32_t words = (n + 31) / 32, chunk = 4096;
+    dim3 grid(words, (npix + chunk - 1) / chunk);
+    hipLaunchKernelGGL(dev::sfd_loss_diff_kernel, grid, dim3(256), 0, stream, bits0, bits1, lb, lp, npix, chunk, n, out);
+    return hipGetLastError();
+}
 
 // Host launcher: one (tile chunk, sample batch) step. A.ff_* describe the step.
 hipError_t launch_free_flight(const RenderArgs& A, uint32_t chunk_tiles, hipStream_t stream) {

@@ -171,6 +171,9 @@ struct RenderArgs {
     float* ff_cache;         // scratch [7][act_cap][threads]: per active entry P, B, 2A, den, F, F_next, t1
     float* ff_path;          // [threads][3] path radiance of the step
     float* ff_sum;           // [tile-local pixel][3] running sum over sample batches
+    const uint32_t* gauss_order;  // record (leaf order) -> scene index
+    uint32_t* rec_bits;      // RECORD_PIXEL_GAUSSIANS bitset [word][pixel] (nullptr: not recording)
+    uint32_t rec_npix;       // W * H
     float* ff_dbg;           // debug (VR_FF_DEBUG): per path of the step, 8 floats of its first bounce
     const unsigned long long* pcg_jump;  // [2k] = A^k, [2k+1] = inc (A^(k-1) + ... + 1): PCG32 state after k draws
 };

@@ -22,7 +22,7 @@ from ._lib import VRError, check, fptr, lib
 __all__ = [
     "VRError", "Light", "Scene", "Camera", "Pinhole_Camera", "Orthographic_Camera", "Ray", "Image",
     "Integrator", "RayMarchingGaussians", "PureRayMarching", "RayMarchingSpheres", "FreeFlightGaussians",
-    "MultiScatterGaussians", "TestIntegrator", "Device",
+    "MultiScatterGaussians", "bits_to_lists", "TestIntegrator", "Device",
     "load_xml",
     "num_tiles",
 ]
@@ -454,6 +454,45 @@ class MultiScatterGaussians(Integrator):
 
     def set_num_samples(self, n):  # integrator.h:719
         self.params.num_samples = int(n)
+
+    def render(self, scene, image, per_pixel_gaussians=None, slot=0):
+        """render(scene, image[, per_pixel_gaussians]) (integrator.h:525-536). With RECORD_PIXEL_GAUSSIANS
+        semantics when `per_pixel_gaussians` is a list: it is filled with one sorted list of Gaussian
+        indices per row-major pixel (integrator.h:616-644, 700-705). The device keeps the recording
+        in `slot` (0/1) for vr_sfd_loss_diff; record() skips the host decode."""
+        if per_pixel_gaussians is None:
+            return super().render(scene, image)
+        self.record(scene, image, slot)
+        bits = self.pixel_gaussian_bits(slot)
+        per_pixel_gaussians[:] = bits_to_lists(bits, scene.get_num_primitives())
+        return image
+
+    def record(self, scene, image, slot=0):
+        dev = Device.get(self.device)
+        dev.upload(scene)
+        W, H = image.get_width(), image.get_height()
+        out = np.empty((H, W, 3), np.float32)
+        check(lib().vr_render_record(dev._h, ctypes.byref(self.camera.struct), ctypes.byref(self.params), W, H,
+                                     fptr(out), int(slot)))
+        image.pixels[...] = out
+        self._rec_shape = (scene.get_num_primitives(), W * H)
+        self.last_stats = dev.stats()
+        return image
+
+    def pixel_gaussian_bits(self, slot=0):
+        """(ceil(N/32), W*H) uint32: bit b of word w at pixel p <=> Gaussian 32w+b recorded at p."""
+        n, npix = self._rec_shape
+        bits = np.zeros(((n + 31) // 32, npix), np.uint32)
+        check(lib().vr_get_pixel_gaussians(Device.get(self.device)._h, int(slot),
+                                          bits.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32)), bits.size))
+        return bits
+
+
+def bits_to_lists(bits, n):
+    """Decode a (words, npix) recording bitset into per-pixel sorted Gaussian index lists."""
+    words, npix = bits.shape
+    unpacked = np.unpackbits(bits.T.copy().view(np.uint8), axis=1, bitorder="little")[:, :n]
+    return [np.nonzero(row)[0].astype(np.uint32).tolist() for row in unpacked]
 
 
 class RayMarchingSpheres(Integrator):

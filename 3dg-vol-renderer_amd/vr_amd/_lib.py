@@ -101,6 +101,11 @@ SIGNATURES = {
     "vr_count_work": (ST, [P, ctypes.POINTER(vr_camera), ctypes.POINTER(vr_render_params), ctypes.c_uint32,
                            ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,
                            ctypes.POINTER(ctypes.c_uint64)]),
+    "vr_render_record": (ST, [P, ctypes.POINTER(vr_camera), ctypes.POINTER(vr_render_params), ctypes.c_uint32,
+                              ctypes.c_uint32, ctypes.POINTER(ctypes.c_float), ctypes.c_int32]),
+    "vr_get_pixel_gaussians": (ST, [P, ctypes.c_int32, ctypes.POINTER(ctypes.c_uint32), ctypes.c_size_t]),
+    "vr_sfd_loss_diff": (ST, [P, ctypes.POINTER(ctypes.c_float), ctypes.POINTER(ctypes.c_float), ctypes.c_uint32,
+                              ctypes.c_uint32, ctypes.POINTER(ctypes.c_double), ctypes.c_size_t]),
     "vr_num_tiles": (ctypes.c_uint32, [ctypes.c_uint32, ctypes.c_uint32]),
     "vr_synchronize": (ST, [P]),
     "vr_get_stats": (ST, [P, ctypes.POINTER(vr_render_stats)]),

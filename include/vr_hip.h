@@ -213,6 +213,22 @@ vr_status vr_unshuffle_tiles_device(vr_ctx* ctx, const float* d_slabs, uint32_t 
 vr_status vr_count_work(vr_ctx* ctx, const vr_camera* cam, const vr_render_params* p, uint32_t width,
                         uint32_t height, uint32_t first_tile, uint32_t tile_stride, uint32_t num_tiles,
                         uint64_t counts[16]);
+/* MultiScatterGaussians::render(scene, image, &per_pixel_gaussians) under RECORD_PIXEL_GAUSSIANS
+ * (integrator.h:532-536, 616-644): renders like vr_render (params->integrator must be
+ * VR_MULTI_SCATTER) and records, per pixel, the Gaussians (scene order) with an event at or before
+ * a path's scattering point (t <= t_scatter + 1e-6), or every Gaussian hit by a path segment that did
+ * not scatter, as a bitset in the context's recording `slot` (0 or 1). Synchronous. */
+vr_status vr_render_record(vr_ctx* ctx, const vr_camera* cam, const vr_render_params* p, uint32_t width,
+                           uint32_t height, float* rgb_host, int32_t slot);
+/* Copy a recording to the host: bits[w * W*H + p] bit b set <=> Gaussian 32w + b was recorded at
+ * row-major pixel p. n_words must be ceil(N/32) * W * H. */
+vr_status vr_get_pixel_gaussians(vr_ctx* ctx, int32_t slot, uint32_t* bits, size_t n_words);
+/* Stochastic finite-difference statistic of StochasticFiniteDiffInverseIntegrator::optimize
+ * (inverse_integrator.h:166-182): out[g] = sum over the union of the pixels recorded for Gaussian g
+ * in slot 0 (base render) and slot 1 (perturbed render) of loss_plus[p] - loss_base[p] (double).
+ * loss_* are host arrays of W*H per-pixel L1 losses (compute_pixel_losses, :21-30); n = N. */
+vr_status vr_sfd_loss_diff(vr_ctx* ctx, const float* loss_base, const float* loss_plus, uint32_t width,
+                           uint32_t height, double* out, size_t n);
 /* Number of 16x16 tiles of a W x H frame. */
 uint32_t vr_num_tiles(uint32_t width, uint32_t height);
 vr_status vr_synchronize(vr_ctx* ctx);

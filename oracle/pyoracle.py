@@ -63,6 +63,8 @@ def lib():
     L.orc_render_ff.argtypes = [P, ctypes.c_int, fp, fp, ctypes.c_float, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                 ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_int), ctypes.c_int64, fp,
                                 ctypes.c_int]
+    L.orc_render_ms_record.argtypes = [P, ctypes.c_int, fp, fp, ctypes.c_float, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                       ctypes.c_int, fp, ctypes.POINTER(ctypes.c_uint32), ctypes.c_int]
     L.orc_render.argtypes = [P, ctypes.c_int, fp, fp, ctypes.c_float, ctypes.c_int, ctypes.c_float,
                              ctypes.c_int, ctypes.c_int, ctypes.c_int, ip, ctypes.c_int64, fp, ctypes.c_int]
     _lib = L
@@ -191,6 +193,20 @@ def render_ff(scene, cam_type, pos, view_dir, fov, W, H, multi=True, num_samples
     if rc != 0:
         raise RuntimeError("oracle render failed: " + lib().orc_last_error().decode())
     return out
+
+
+def render_ms_record(scene, cam_type, pos, view_dir, fov, W, H, num_samples=16, min_bounces=5, nthreads=0):
+    """MultiScatterGaussians with RECORD_PIXEL_GAUSSIANS: (image H x W x 3, bits (ceil(N/32), W*H))."""
+    pos, pp = _f(pos)
+    vd, pv = _f(view_dir)
+    out = np.zeros((H, W, 3), np.float32)
+    bits = np.zeros(((scene.num + 31) // 32, W * H), np.uint32)
+    rc = lib().orc_render_ms_record(scene.h, cam_type, pp, pv, float(fov), int(num_samples), int(min_bounces), int(W),
+                                    int(H), out.ctypes.data_as(ctypes.POINTER(ctypes.c_float)),
+                                    bits.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32)), int(nthreads))
+    if rc != 0:
+        raise RuntimeError("oracle render failed: " + lib().orc_last_error().decode())
+    return out, bits
 
 
 def derive_path_seed(x, y, si):

@@ -1167,7 +1167,7 @@ static float* g_ff_dbg = nullptr;  // debug: first-bounce values of sample 0 per
 // integrator.h:300-408 (single scatter, float accumulation, index-ordered active list) when
 // multi == false; integrator.h:532-717 (multi-scatter, min_bounces, Russian roulette) otherwise.
 static V3 free_flight_pixel(const Scene& scene, const Camera& cam, int x, int y, int W, int H, int num_samples,
-                            int min_scatter, bool multi) {
+                            int min_scatter, bool multi, std::vector<uint32_t>* pixel_list = nullptr) {
     const GMM& gmm = scene.gmm;
     const size_t N = gmm.gaussians.size();
     const float phase_pdf = kInv4Pi;
@@ -1214,6 +1214,21 @@ static V3 free_flight_pixel(const Scene& scene, const Camera& cam, int x, int y,
                     acc_tau += seg_tau;
                     active[events[ev].index] = events[ev].entering;
                     t_prev = t_evt;
+                }
+            }
+            if (pixel_list && multi) {  // RECORD_PIXEL_GAUSSIANS, integrator.h:616-644
+                auto add = [&](uint32_t g) {
+                    if (std::find(pixel_list->begin(), pixel_list->end(), g) == pixel_list->end()) pixel_list->push_back(g);
+                };
+                const float tol = 1e-6f;
+                if (t_scatter >= 0.0f) {
+                    for (const auto& ev : events) {
+                        if (ev.t <= t_scatter + tol) add((uint32_t)ev.index);
+                        else break;
+                    }
+                } else {
+                    for (const auto& ev : events)
+                        if (!(ev.t < 0.0f)) add((uint32_t)ev.index);
                 }
             }
             if (t_scatter < 0.0f) {
@@ -1505,6 +1520,32 @@ int orc_render(void* sp, int cam_type, const float* pos, const float* vd, float 
 }
 
 void orc_ff_debug(float* buf) { g_ff_dbg = buf; }
+
+// MultiScatterGaussians::render with RECORD_PIXEL_GAUSSIANS (integrator.h:532-536, 616-644): the
+// frame into out[3*W*H] and the per-pixel Gaussian sets into bits[(g >> 5) * W*H + p] (bit g & 31).
+int orc_render_ms_record(void* sp, int cam_type, const float* pos, const float* vd, float fov, int num_samples,
+                         int min_bounces, int W, int H, float* out, uint32_t* bits, int nthreads) {
+    try {
+        Scene* s = (Scene*)sp;
+        if (s->volume_type != 0) { g_err = "free-flight integrators need a Gaussian scene"; return 1; }
+        Camera c = cam_type == 0 ? Camera::make_pinhole({pos[0], pos[1], pos[2]}, {vd[0], vd[1], vd[2]}, fov)
+                                 : Camera::make_ortho({pos[0], pos[1], pos[2]}, {vd[0], vd[1], vd[2]});
+        const int64_t total = (int64_t)W * H;
+        if (nthreads > 0) omp_set_num_threads(nthreads);
+#pragma omp parallel for schedule(dynamic, 1)
+        for (int64_t q = 0; q < total; ++q) {
+            int x = (int)(q % W), y = (int)(q / W);
+            std::vector<uint32_t> list;
+            V3 L = free_flight_pixel(*s, c, x, y, W, H, num_samples, min_bounces, true, &list);
+            out[3 * q] = L.x; out[3 * q + 1] = L.y; out[3 * q + 2] = L.z;
+            for (uint32_t g : list) bits[(size_t)(g >> 5) * total + q] |= 1u << (g & 31u);
+        }
+        return 0;
+    } catch (const std::exception& e) {
+        g_err = e.what();
+        return 2;
+    }
+}
 
 // FreeFlightGaussians (multi = 0, integrator.h:300-408) / MultiScatterGaussians (multi = 1,
 // integrator.h:532-717). Same pixel selection and output convention as orc_render.
