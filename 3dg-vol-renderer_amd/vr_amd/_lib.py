@@ -7,7 +7,7 @@ import ctypes
 import os
 
 _PKG_ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-LIB_PATH = os.path.join(_PKG_ROOT, "libvr_hip.so")
+LIB_PATH = os.environ.get("VR_LIB_PATH") or os.path.join(_PKG_ROOT, "libvr_hip.so")  # override: A/B builds
 
 VR_OK = 0
 STATUS_NAMES = {

@@ -112,12 +112,17 @@ def apply_params(params, lights, env_color):
     covariance R S S^T R^T; returns a new Scene (the device BVH is rebuilt at upload, gmm.h:673)."""
     p = np.asarray(params, np.float32).reshape(-1, PER)
     n = p.shape[0]
-    cov6 = np.zeros((n, 6), np.float32)
-    for i in range(n):
-        R = _rotation_from_rodrigues(p[i, 3:6].astype(np.float64))
-        S = np.diag(np.exp(p[i, 6:9].astype(np.float32)).astype(np.float64))
-        C = R @ S @ S.T @ R.T
-        cov6[i] = [C[0, 0], C[0, 1], C[0, 2], C[1, 1], C[1, 2], C[2, 2]]
+    rod = p[:, 3:6].astype(np.float64)
+    angle = np.linalg.norm(rod, axis=1)
+    ok = angle > 1e-12
+    ax = np.where(ok[:, None], rod / np.where(ok, angle, 1.0)[:, None], 0.0)
+    K = np.zeros((n, 3, 3))
+    K[:, 0, 1], K[:, 0, 2], K[:, 1, 2] = -ax[:, 2], ax[:, 1], -ax[:, 0]
+    K[:, 1, 0], K[:, 2, 0], K[:, 2, 1] = ax[:, 2], -ax[:, 1], ax[:, 0]
+    R = np.eye(3)[None] + np.sin(angle)[:, None, None] * K + (1 - np.cos(angle))[:, None, None] * np.einsum("nij,njk->nik", K, K)
+    s2 = np.exp(p[:, 6:9].astype(np.float32)).astype(np.float64) ** 2
+    C = np.einsum("nij,nj,nkj->nik", R, s2, R)  # R S S^T R^T (AngleAxis::toRotationMatrix)
+    cov6 = np.stack([C[:, 0, 0], C[:, 0, 1], C[:, 0, 2], C[:, 1, 1], C[:, 1, 2], C[:, 2, 2]], 1).astype(np.float32)
     density = np.exp(p[:, 9]).astype(np.float32)
     albedo = np.clip(sigmoidf_safe(p[:, 10]), 0.0, 1.0)
     return Scene.from_gaussians(p[:, 0:3], cov6, density, albedo, lights=lights, env_color=env_color)

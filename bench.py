@@ -40,6 +40,7 @@ CONFIGS = {
     "c4": (4096, 4096, 1_000_000, "4096x4096, 1M Gaussians (make_random distribution)"),
     "c3": (1920, 1080, 100_000, "1920x1080, 100k Gaussians (make_random distribution)"),
     "c2": (512, 512, "1000_random.txt", "512x512, scenes/gaussians/1000_random.txt"),
+    "c5": (512, 512, 10_000, "512x512, 10k Gaussians (make_random distribution; 10k_random.txt's generator)"),
 }
 LIGHTS = [((0.0, 5.0, 0.1), (50.0, 0.0, 0.0)), ((-3.0, 3.0, 0.3), (0.0, 30.0, 0.0)),
           ((3.0, 3.0, -0.2), (0.0, 0.0, 30.0))]  # scenes/gaussians/1000_random.txt:1-3
@@ -120,6 +121,47 @@ def cpu_baseline_ff(scene, W, H, multi, spp, budget_s, threads, log):
                       f"{threads} OpenMP threads); oracle restatement of the reference integrator"}
 
 
+def bench_sfd(args, scene, camera, W, H, t_setup):
+    """Config 5: one step = one StochasticFiniteDiffInverseIntegrator iteration (inverse_integrator.h:
+    115-200): a recorded base render + num_stoch_samples (4) recorded perturbed renders of
+    MultiScatterGaussians at --spp paths/pixel, the device union-of-pixels loss statistic, Adam, and
+    the scene re-uploads (host BVH builds). Target image: the scene itself rendered at --spp; start:
+    densities scaled by 0.5. One GPU (the loop is sequential)."""
+    from vr_amd import inverse as inv
+    I_ref = vr.Image(W, H)
+    vr.MultiScatterGaussians(camera, args.spp).render(scene, I_ref)
+    p = inv.pack_parameters(scene.gaussians())
+    p[9::11] += np.float32(np.log(0.5))
+    start = inv.apply_params(p, scene.lights, scene.env_color)
+
+    def one_iter():
+        opt = inv.StochasticFiniteDiffInverseIntegrator(camera, vr.MultiScatterGaussians(camera, args.spp),
+                                                        inv.SFDConfig(max_iters=1, num_stoch_samples=4, lr=1e-2))
+        if not opt.optimize(start, I_ref):
+            raise SystemExit("SFD iteration failed")
+        return opt
+
+    for _ in range(args.warmup):
+        one_iter()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        opt = one_iter()
+    torch.cuda.synchronize()
+    ms = (time.perf_counter() - t0) / args.steps * 1e3
+    paths = 5 * W * H * args.spp
+    print(json.dumps({
+        "metric": "SFD inverse iterations/s (5 recorded multi-scatter renders each)", "value": 1e3 / ms,
+        "unit": "iter/s", "n_gpus": 1, "steps": args.steps, "warmup": args.warmup, "ms_per_step": ms,
+        "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "f32",
+        "data": "synthetic (seeded make_random.py distribution)",
+        "config": {"workload": CONFIGS[args.config][3], "width": W, "height": H,
+                   "gaussians": scene.get_num_primitives(), "integrator": "StochasticFiniteDiffInverseIntegrator",
+                   "forward": "MultiScatterGaussians", "spp": args.spp, "num_stoch_samples": 4,
+                   "paths_per_iter": paths, "mpaths_per_s": paths / (ms * 1e-3) / 1e6, "setup_s": t_setup,
+                   "mean_l1_loss": opt.history[-1]}}), flush=True)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -133,7 +175,7 @@ def main():
     ap.add_argument("--cpu-budget", type=float, default=20.0, help="seconds of CPU-baseline work (0 = skip)")
     ap.add_argument("--cpu-threads", type=int, default=min(16, os.cpu_count() or 1))
     ap.add_argument("--flops", type=int, default=1, help="run one instrumented frame to count algorithmic work")
-    ap.add_argument("--integrator", default="raymarch", choices=["raymarch", "freeflight", "multiscatter"],
+    ap.add_argument("--integrator", default="raymarch", choices=["raymarch", "freeflight", "multiscatter", "sfd"],
                     help="raymarch = RayMarchingGaussians (the headline); the free-flight integrators are "
                          "secondary lines (unit Mpaths/s = pixel samples per second)")
     ap.add_argument("--spp", type=int, default=16, help="free-flight paths per pixel")
@@ -160,6 +202,8 @@ def main():
     scene, W, H = build_scene(args.config, args.seed)
     camera = vr.Pinhole_Camera(CAM_POS, CAM_VIEW, FOV)
     ff = args.integrator != "raymarch"
+    if args.integrator == "sfd":
+        return bench_sfd(args, scene, camera, W, H, time.perf_counter() - t_setup)
     if args.integrator == "freeflight":
         integ = vr.FreeFlightGaussians(camera, args.spp, device=local)
     elif args.integrator == "multiscatter":
