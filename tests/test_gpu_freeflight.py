@@ -97,6 +97,35 @@ def test_free_flight_is_deterministic_and_tiles_agree():
     assert np.array_equal(a, b)
 
 
+@pytest.mark.parametrize("multi", [False, True])
+def test_free_flight_tile_slabs_unshuffle_bitwise(multi):
+    """The multi-GPU building block with the free-flight integrators: rank r of 3 renders tiles
+    r, r+3, ... into a packed slab (its own sample batches and running sums); the unshuffled frame
+    equals the single-call frame bit for bit (paths depend only on (x, y, si))."""
+    torch = pytest.importorskip("torch")
+    path = scene_path("50_random.txt")
+    W, H = 70, 50
+    scene = vr.Scene.load_GMM(path)
+    cam = vr.Pinhole_Camera(CAM_POS, main_view_dir(), FOV)
+    integ = vr.MultiScatterGaussians(cam, 4) if multi else vr.FreeFlightGaussians(cam, 4)
+    full = vr.Image(W, H)
+    integ.render(scene, full)
+    dev = vr.Device.get(0)
+    dev.upload(scene)
+    nt = vr.num_tiles(W, H)
+    R = 3
+    per = (nt + R - 1) // R
+    slabs = torch.zeros((R, per * 256 * 3), dtype=torch.float32, device="cuda")
+    stream = torch.cuda.current_stream().cuda_stream
+    for r in range(R):
+        cnt = len(range(r, nt, R))
+        dev.render_tiles_device(cam, integ.params, W, H, r, R, cnt, True, slabs[r].data_ptr(), stream)
+    img = torch.zeros((H, W, 3), dtype=torch.float32, device="cuda")
+    dev.unshuffle_tiles_device(slabs.data_ptr(), R, per, W, H, img.data_ptr(), stream)
+    torch.cuda.synchronize()
+    assert np.array_equal(img.cpu().numpy(), full.pixels)
+
+
 def test_free_flight_needs_a_gaussian_scene():
     scene = vr.Scene.load_SMM(scene_path("sph_1_spheres.txt"))
     with pytest.raises(vr.VRError):
