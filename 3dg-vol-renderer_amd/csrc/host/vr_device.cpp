@@ -546,23 +546,25 @@ vr_status gauss_pipeline(vr_ctx* c, RenderArgs& A, hipStream_t s, bool stats) {
     return VR_OK;
 }
 
-// Free-flight integrators: the frame's tiles x samples are cut into steps of at most kFFThreads
-// paths (a tile chunk x a sample batch); each step runs the path kernel and adds its radiance to
-// the per-pixel running sums in sample order (vr_freeflight.hip).
-constexpr uint32_t kFFThreads = 1u << 20;
+// Free-flight integrators: one persistent launch per chunk of tiles (all samples of those tiles,
+// at most kFFMaxPaths paths) on a grid of resident waves that claim 64-path groups from a counter;
+// then the chunk's path radiance is added to the pixels in sample order (vr_freeflight.hip).
+constexpr uint64_t kFFMaxPaths = 1ull << 27;
 // The active list indexes the hit buffer, so it never holds more than kFFHitCap entries: the only
 // capacity a path can exceed is kFFHitCap Gaussians overlapping one point (error path, NaN).
 constexpr int32_t kFFHitCap = 128, kFFActCap = kFFHitCap;
 vr_status free_flight_pipeline(vr_ctx* c, RenderArgs& A, hipStream_t s) {
     const uint32_t spp = (uint32_t)A.ff_samples;
-    const uint32_t tiles_fit = std::max(1u, kFFThreads / 256u);
-    const uint32_t nsb = std::min(spp, std::max(1u, tiles_fit / std::max(1u, A.num_tiles)));
-    const uint32_t chunk = std::min(A.num_tiles, std::max(1u, tiles_fit / nsb));
-    const uint32_t threads = chunk * nsb * 256u;
-    vr_status st = grow(c->ff_scratch, (size_t)threads * (3 * kFFHitCap + 8 * kFFActCap) * 4, "free-flight scratch");
+    if ((uint64_t)spp * 256u > kFFMaxPaths) return fail(VR_ERR_INVALID, "num_samples too large");
+    int cus = 0;
+    HIP_TRY(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, c->device), "hipDeviceGetAttribute");
+    const uint32_t threads = (uint32_t)std::max(1, cus) * 4u * 256u;  // 4 waves/SIMD x 4 SIMDs = 4 blocks per CU
+    const uint32_t chunk = (uint32_t)std::min<uint64_t>(A.num_tiles, kFFMaxPaths / ((uint64_t)spp * 256u));
+    vr_status st = grow(c->ff_scratch, (size_t)threads * (3 * kFFHitCap + 8 * kFFActCap) * 4 + 64, "free-flight scratch");
     if (st != VR_OK) return st;
-    if ((st = grow(c->ff_path, (size_t)threads * 3 * sizeof(float), "free-flight paths")) != VR_OK) return st;
+    if ((st = grow(c->ff_path, (size_t)chunk * spp * 256 * 3 * sizeof(float), "free-flight paths")) != VR_OK) return st;
     if ((st = grow(c->ff_sum, (size_t)A.num_tiles * 256 * 3 * sizeof(float), "free-flight sums")) != VR_OK) return st;
+    const uint32_t nsb = spp;
     float* base = (float*)c->ff_scratch.p;
     A.ff_threads = threads;
     A.ff_hit_cap = kFFHitCap;
@@ -573,6 +575,7 @@ vr_status free_flight_pipeline(vr_ctx* c, RenderArgs& A, hipStream_t s) {
     A.ff_gid = (int32_t*)(base + (size_t)2 * kFFHitCap * threads);
     A.ff_act = (int32_t*)(base + (size_t)3 * kFFHitCap * threads);
     A.ff_cache = base + (size_t)(3 * kFFHitCap + kFFActCap) * threads;
+    A.ff_next = (unsigned long long*)(base + (size_t)(3 * kFFHitCap + 8 * kFFActCap) * threads);
     A.ff_path = (float*)c->ff_path.p;
     A.ff_sum = (float*)c->ff_sum.p;
     const char* dbg = getenv("VR_FF_DEBUG");  // EXPERIMENT: first-bounce dump of a one-step render
@@ -588,6 +591,7 @@ vr_status free_flight_pipeline(vr_ctx* c, RenderArgs& A, hipStream_t s) {
             A.ff_tile_base = t0;
             A.ff_si0 = si;
             A.ff_nsb = std::min(nsb, spp - si);
+            A.ff_total = (unsigned long long)nt * A.ff_nsb * 256ull;
             HIP_TRY(launch_free_flight(A, nt, s), "free-flight launch");
         }
     }

@@ -404,24 +404,14 @@ __device__ float free_flight_distance(const RenderArgs& A, const FFScratch& S, c
     }
 }
 
-// One path per thread: block b = (tile b / nsb, sample si0 + b % nsb). Launch bounds: 4 waves/SIMD
-// (128 VGPRs, a few spills) measured 1.14-1.44x faster than the unconstrained 2 waves/SIMD (203
-// VGPRs) on C2/C4/C5; 5 waves/SIMD (the LDS-stack limit) is slower again.
+// One path: path group b = (tile b / nsb, sample si0 + b % nsb), lane_id = pixel of the tile.
 template <bool MULTI>
-__global__ void __launch_bounds__(kFFBlock, 4) ff_path_kernel(RenderArgs A) {
-    __shared__ int s_stack[kStackSize * kFFBlock];
-    int* stack = s_stack + threadIdx.x;
-    const uint32_t b = blockIdx.x;
+__device__ __forceinline__ void ff_one_path(const RenderArgs& A, const FFScratch& S, int* stack, uint32_t b,
+                                            uint32_t lane_id, size_t out) {
     const uint32_t tile_local = A.ff_tile_base + b / A.ff_nsb;
     const int si = (int)(A.ff_si0 + b % A.ff_nsb);
-    const uint32_t gt = b * kFFBlock + threadIdx.x;
-    const size_t AC = (size_t)A.ff_act_cap * A.ff_threads;
-    float* cache = A.ff_cache + gt;
-    FFScratch S{A.ff_key + gt, A.ff_t1 + gt, A.ff_gid + gt, A.ff_act + gt,
-                cache, cache + AC, cache + 2 * AC, cache + 3 * AC, cache + 4 * AC, cache + 5 * AC, cache + 6 * AC,
-                A.ff_threads};
     int lx, ly, x, y;
-    tile_pixel(A, tile_local, threadIdx.x, lx, ly, x, y);
+    tile_pixel(A, tile_local, (int)lane_id, lx, ly, x, y);
     float L0 = 0.0f, L1 = 0.0f, L2 = 0.0f;
     if (x < (int)A.width && y < (int)A.height) {
         PCG32 rng(derive_path_seed(x, y, si), 1);
@@ -480,7 +470,7 @@ __global__ void __launch_bounds__(kFFBlock, 4) ff_path_kernel(RenderArgs A) {
             }
             const float w = (albedo * kInv4Pi) * w_ne;
             if (A.ff_dbg && bounce == 0) {
-                float* d = A.ff_dbg + (size_t)gt * 8;
+                float* d = A.ff_dbg + (size_t)(blockIdx.x * kFFBlock + threadIdx.x) * 8;
                 d[0] = target, d[1] = ts;
             }
             if constexpr (!MULTI) {  // integrator.h:396-399
@@ -507,9 +497,35 @@ __global__ void __launch_bounds__(kFFBlock, 4) ff_path_kernel(RenderArgs A) {
             ray = make_ray(px, py, pz, nx, ny, nz);
         }
     }
-    A.ff_path[(size_t)gt * 3 + 0] = L0;
-    A.ff_path[(size_t)gt * 3 + 1] = L1;
-    A.ff_path[(size_t)gt * 3 + 2] = L2;
+    A.ff_path[out * 3 + 0] = L0;
+    A.ff_path[out * 3 + 1] = L1;
+    A.ff_path[out * 3 + 2] = L2;
+}
+
+// Persistent: a grid of resident waves; each wave claims the next 64 paths (one 8x8 pixel block
+// of one tile at one sample index) from a global counter until all ff_total paths are taken, so a
+// wave that drew short paths moves on instead of idling until the launch's longest path ends.
+// Launch bounds: 4 waves/SIMD (128 VGPRs, a few spills) measured 1.14-1.44x faster than the
+// unconstrained 2 waves/SIMD (203 VGPRs) on C2/C4/C5; 5 waves/SIMD (the LDS-stack limit) is slower.
+template <bool MULTI>
+__global__ void __launch_bounds__(kFFBlock, 4) ff_path_kernel(RenderArgs A) {
+    __shared__ int s_stack[kStackSize * kFFBlock];
+    int* stack = s_stack + threadIdx.x;
+    const uint32_t gt = blockIdx.x * kFFBlock + threadIdx.x;
+    const size_t AC = (size_t)A.ff_act_cap * A.ff_threads;
+    float* cache = A.ff_cache + gt;
+    const FFScratch S{A.ff_key + gt, A.ff_t1 + gt, A.ff_gid + gt, A.ff_act + gt,
+                      cache, cache + AC, cache + 2 * AC, cache + 3 * AC, cache + 4 * AC, cache + 5 * AC, cache + 6 * AC,
+                      A.ff_threads};
+    const uint32_t lane = threadIdx.x & 63u;
+    for (;;) {
+        unsigned long long base = 0;
+        if (lane == 0) base = atomicAdd(A.ff_next, 64ull);
+        base = __shfl(base, 0, 64);
+        if (base >= A.ff_total) break;  // wave-uniform: every wave leaves once the work is handed out
+        const unsigned long long pid = base + lane;
+        if (pid < A.ff_total) ff_one_path<MULTI>(A, S, stack, (uint32_t)(pid / kFFBlock), (uint32_t)(pid % kFFBlock), pid);
+    }
 }
 
 // pixel_L += L_accum in sample order (integrator.h:706), then pixel_L / num_samples on the last batch.
@@ -582,7 +598,9 @@ hipError_t launch_sfd_loss_diff(const uint32_t* bits0, const uint32_t* bits1, co
 
 // Host launcher: one (tile chunk, sample batch) step. A.ff_* describe the step.
 hipError_t launch_free_flight(const RenderArgs& A, uint32_t chunk_tiles, hipStream_t stream) {
-    dim3 grid(chunk_tiles * A.ff_nsb);
+    hipError_t e0 = hipMemsetAsync(A.ff_next, 0, sizeof(unsigned long long), stream);
+    if (e0 != hipSuccess) return e0;
+    dim3 grid(A.ff_threads / dev::kFFBlock);
     if (A.ff_multi)
         hipLaunchKernelGGL(dev::ff_path_kernel<true>, grid, dim3(dev::kFFBlock), 0, stream, A);
     else
