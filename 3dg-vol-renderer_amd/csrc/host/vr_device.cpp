@@ -578,6 +578,7 @@ vr_status free_flight_pipeline(vr_ctx* c, RenderArgs& A, hipStream_t s) {
     A.ff_next = (unsigned long long*)(base + (size_t)(3 * kFFHitCap + 8 * kFFActCap) * threads);
     A.ff_path = (float*)c->ff_path.p;
     A.ff_sum = (float*)c->ff_sum.p;
+    A.ff_refill = getenv("VR_FF_REFILL") ? atoi(getenv("VR_FF_REFILL")) : 0;
     const char* dbg = getenv("VR_FF_DEBUG");  // EXPERIMENT: first-bounce dump of a one-step render
     vr_ctx::Buf dbuf;
     if (dbg) {

@@ -169,7 +169,8 @@ struct RenderArgs {
     int32_t* ff_gid;         // scratch [hit_cap][threads]
     int32_t* ff_act;         // scratch [act_cap][threads]
     unsigned long long* ff_next;  // persistent path kernel: next unclaimed path of the launch
-    unsigned long long ff_total;  // paths of the launch (tiles of the chunk x samples x 256)
+    unsigned long long ff_total;
+    int32_t ff_refill;            // per-lane path refill kernel (A/B: VR_FF_REFILL)  // paths of the launch (tiles of the chunk x samples x 256)
     float* ff_cache;         // scratch [7][act_cap][threads]: per active entry P, B, 2A, den, F, F_next, t1
     float* ff_path;          // [threads][3] path radiance of the step
     float* ff_sum;           // [tile-local pixel][3] running sum over sample batches
