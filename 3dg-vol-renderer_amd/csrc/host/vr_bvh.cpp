@@ -43,13 +43,6 @@ struct Box {
         if (!(d0 >= 0.0f) || !(d1 >= 0.0f) || !(d2 >= 0.0f)) return 0.0f;
         return 2.0f * (d0 * d1 + d0 * d2 + d1 * d2);
     }
-    // Probability-of-visit metric: surface area (long rays) + vol_w * volume (rays that start
-    // inside the volume: a short ray of length l hits a box with probability ~ V + S l / 4).
-    float metric(float vol_w) const {
-        float d0 = mx[0] - mn[0], d1 = mx[1] - mn[1], d2 = mx[2] - mn[2];
-        if (!(d0 >= 0.0f) || !(d1 >= 0.0f) || !(d2 >= 0.0f)) return 0.0f;
-        return 2.0f * (d0 * d1 + d0 * d2 + d1 * d2) + vol_w * (d0 * d1 * d2);
-    }
 };
 
 struct TNode {
@@ -88,20 +81,13 @@ BVHBuild build_bvh(const std::vector<float>& boxes) {
         work.push_back({0, 1});
     }
     uint32_t* ord = out.order.data();
-    auto env_or = [](const char* name, double def) {
-        const char* v = getenv(name);
-        return v ? atof(v) : def;
-    };
-    static const int kBins = std::min(64, std::max(4, (int)env_or("VR_BVH_BINS", 16)));
-    static const float vol_w = (float)env_or("VR_BVH_VOL", 0.0);
-    static const uint32_t leaf_max = (uint32_t)std::min(16, std::max(1, (int)env_or("VR_BVH_LEAF", kLeafMax)));
+    constexpr int kBins = 16;            // SAH bins per axis
+    constexpr uint32_t leaf_max = kLeafMax;
     // Depth budget: SAH may go kSlack levels deeper than a perfectly balanced tree, but never past
-    // kMaxDepth. Shallow trees let the secondary-ray kernel use a 24-entry LDS stack (more waves per
-    // CU); very large scenes fall back to the 32-entry stack.
+    // kMaxDepth. Shallow trees let the march kernel use a 24-entry LDS stack (more waves per CU);
+    // very large scenes fall back to the 32-entry stack.
     constexpr int kSlack = 6;
-    static const int depth_env = getenv("VR_BVH_DEPTH") ? atoi(getenv("VR_BVH_DEPTH")) : 0;  // A/B override
-    const int depth_cap = depth_env > 0 ? std::min(kMaxDepth, depth_env)
-                                        : std::min(kMaxDepth, std::max(kShallowDepth, ceil_log2((N + leaf_max - 1) / leaf_max + 1) + kSlack));
+    const int depth_cap = std::min(kMaxDepth, std::max(kShallowDepth, ceil_log2((N + leaf_max - 1) / leaf_max + 1) + kSlack));
     while (!work.empty()) {
         Work w = work.back();
         work.pop_back();
@@ -144,7 +130,7 @@ BVHBuild build_bvh(const std::vector<float>& boxes) {
                 for (int b = kBins - 1; b > 0; --b) {
                     acc.grow(bb[b]);
                     n += bn[b];
-                    ra[b] = acc.metric(vol_w);
+                    ra[b] = acc.area();
                     rn[b] = n;
                 }
                 Box lacc;
@@ -153,7 +139,7 @@ BVHBuild build_bvh(const std::vector<float>& boxes) {
                     lacc.grow(bb[b]);
                     ln += bn[b];
                     if (ln == 0 || rn[b + 1] == 0) continue;
-                    float c = lacc.metric(vol_w) * ln + ra[b + 1] * rn[b + 1];
+                    float c = lacc.area() * ln + ra[b + 1] * rn[b + 1];
                     if (c < best_cost) {
                         best_cost = c;
                         best_axis = a;

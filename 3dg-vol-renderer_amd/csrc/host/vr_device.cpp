@@ -16,9 +16,9 @@
 namespace vr {
 hipError_t launch_render(const RenderArgs& A, hipStream_t stream, int volume_type, int integrator);
 hipError_t gauss_march(const RenderArgs& A, hipStream_t stream, bool stats);
-hipError_t gauss_lists(const RenderArgs& A, uint32_t nrec, hipStream_t stream);
-hipError_t gauss_secondary(const RenderArgs& A, uint32_t nrec, hipStream_t stream, bool stats);
-hipError_t gauss_accumulate(const RenderArgs& A, uint32_t nrec, hipStream_t stream);
+hipError_t gauss_lists(const RenderArgs& A, hipStream_t stream);
+hipError_t gauss_secondary(const RenderArgs& A, hipStream_t stream, bool stats);
+hipError_t gauss_accumulate(const RenderArgs& A, hipStream_t stream);
 hipError_t launch_free_flight(const RenderArgs& A, uint32_t chunk_tiles, hipStream_t stream);
 hipError_t launch_sfd_loss_diff(const uint32_t* bits0, const uint32_t* bits1, const float* lb, const float* lp, uint32_t npix,
                                 uint32_t n, double* out, hipStream_t stream);
@@ -58,15 +58,21 @@ struct vr_ctx {
     // workspaces
     uint32_t* d_queue = nullptr;
     uint32_t queue_cap = 0;
-    uint32_t* d_counters = nullptr;  // [0] errors
-    uint32_t* h_counters = nullptr;  // pinned: [0] queue count, [1] errors
+    uint32_t* d_counters = nullptr;  // [0] error pixels / paths of the frame
+    // Pinned report of the last frame, copied on the render stream after its last kernel:
+    // [0] fallback-queue length, [1] error pixels, [2] scatter records, [3] overflow-pool entries,
+    // [4] record capacity exceeded (the frame is invalid and must be rendered again)
+    uint32_t* h_report = nullptr;
+    bool report_gauss = false;  // the last frame ran the RayMarchingGaussians pipeline (fields [2..4])
     float* d_frame = nullptr;
     size_t frame_cap = 0;
     hipEvent_t ev_start = nullptr, ev_stop = nullptr;
+    hipEvent_t ev_report = nullptr;  // after the frame report's copies (collect() waits for it)
     hipEvent_t ev_stage[4] = {nullptr, nullptr, nullptr, nullptr};  // stage boundaries of gauss_pipeline
     bool staged = false;                                            // last launch recorded ev_stage
-    bool stats_pending = false;
+    bool stats_pending = false;  // h_report of the last frame has not been collected yet
     int64_t last_pixels = 0;
+    uint32_t last_secondary_per_record = 0;
     // wavefront pipeline buffers (grown on demand, never shrunk)
     struct Buf {
         void* p = nullptr;
@@ -81,9 +87,12 @@ struct vr_ctx {
     Buf sfd_tmp;                      // vr_sfd_loss_diff: losses + output
     bool list_ok = false;  // all covariances positive definite: neighbour lists are exact
     int pcg_jump_n = -1;
-    uint32_t* h_totals = nullptr;  // pinned copy of rec_alloc: [0] records, [1] overflow-pool entries, [2] exceeded
-    int64_t last_records = 0, last_secondary = 0;
-    uint64_t rec_hint = 0, ovf_hint = 0;  // record / overflow-pool capacities that sufficed last time
+    uint32_t* h_sizing = nullptr;  // pinned copy of rec_alloc for the sizing march of a context's first frame
+    uint64_t rec_hint = 0, ovf_hint = 0;  // record / overflow-pool capacities (0: not known yet)
+    // vr_set_option values (explicit per-context tuning; no environment variables are read)
+    int64_t opt_half_nodes = 1;        // VR_OPT_HALF_NODES
+    int64_t opt_secondary_budget = 1;  // VR_OPT_SECONDARY_BUDGET
+    int64_t opt_ff_window0 = 8;        // VR_OPT_FF_WINDOW0
 };
 
 namespace {
@@ -148,7 +157,7 @@ vr_status upload_half_nodes(vr_ctx* c, const std::vector<BVHNode>& nodes) {
     c->d_hnodes = nullptr;
     if (c->d_hnodes4) (void)hipFree(c->d_hnodes4);
     c->d_hnodes4 = nullptr;
-    if (getenv("VR_NO_HALF_NODES")) return VR_OK;
+    if (!c->opt_half_nodes) return VR_OK;
     double half = 0.0;
     for (int k = 0; k < 3; ++k) {
         c->hn_center[k] = 0.5f * (c->bmin[k] + c->bmax[k]);
@@ -186,7 +195,6 @@ vr_status upload_half_nodes(vr_ctx* c, const std::vector<BVHNode>& nodes) {
 
     // 4-wide collapse for the secondary rays: a pair node's two children, then repeatedly the
     // inner child with the largest box surface replaced by its own two children, up to 4.
-    if (getenv("VR_NO_WIDE_NODES")) return VR_OK;
     struct Kid {
         int side;      // box source: nodes[pair].f[6 side ..]
         int32_t pair;  // pair node holding this child's box
@@ -250,7 +258,6 @@ vr_status upload_half_nodes(vr_ctx* c, const std::vector<BVHNode>& nodes) {
     }
     HIP_TRY(hipMalloc(&c->d_hnodes4, w4.size() * sizeof(HNode4)), "hipMalloc(wide nodes)");
     HIP_TRY(hipMemcpy(c->d_hnodes4, w4.data(), w4.size() * sizeof(HNode4), hipMemcpyHostToDevice), "hipMemcpy(wide nodes)");
-    if (getenv("VR_DEBUG")) fprintf(stderr, "[vr] wide BVH: %zu nodes\n", w4.size());
     return VR_OK;
 }
 
@@ -371,7 +378,6 @@ vr_status fill_args(vr_ctx* c, const vr_camera* cam, const vr_render_params* p, 
     // ln(1/t_eps) + ln(1000): a dropped transmittance is <= 1e-3 * t_eps, a thousandth of the error
     // the primary early-out itself is allowed (DESIGN.md §Error budget).
     A.tau_cut = p->t_eps > 0.0f ? std::min(104.0f, (float)(std::log(1.0 / p->t_eps) + std::log(1000.0))) : 104.0f;
-    if (getenv("VR_DBG_TAUCUT")) A.tau_cut = (float)atof(getenv("VR_DBG_TAUCUT"));  // EXPERIMENT
     if (ff) {
         A.ff_multi = p->integrator == VR_MULTI_SCATTER ? 1 : 0;
         A.ff_samples = p->num_samples;
@@ -430,12 +436,16 @@ vr_status gauss_pipeline(vr_ctx* c, RenderArgs& A, hipStream_t s, bool stats) {
     }
     A.pcg_jump = (const unsigned long long*)c->pcg_jump.p;
 
-    // One march pass; record capacity from the last frame (re-run with the exact need on overflow).
+    // Record capacity: from earlier frames of this context (hints), so the host never waits for
+    // the march. A context's first frame sizes it: one host sync after the march, re-run with the
+    // exact need if it did not fit. A later frame that outgrows the buffers is reported
+    // (h_report[4]) and the synchronous entry points render it again with grown buffers.
+    const bool sized = c->rec_hint != 0;
     uint64_t cap = std::max<uint64_t>({c->rec_hint, 2ull * npix, 4096ull});
     uint64_t ovf = std::max<uint64_t>({c->ovf_hint, cap, 4096ull});
-    uint32_t nrec = 0;
+    const uint32_t S = (uint32_t)(A.num_lights + A.env_samples);
     for (int attempt = 0;; ++attempt) {
-        if (cap > 0xffffffffull / kActInline || ovf > 0xffffffffull - cap * kActInline)
+        if (cap > 0xffffffffull / kActInline || ovf > 0xffffffffull - cap * kActInline || cap * std::max(S, 1u) >= 0xffffffffull)
             return fail(VR_ERR_UNSUPPORTED, "too many scatter records in one call (split the frame)");
         if ((st = grow(c->rec_pos, cap * 16ull, "hipMalloc(records)")) != VR_OK) return st;
         if ((st = grow(c->rec_meta, cap * 16ull, "hipMalloc(records)")) != VR_OK) return st;
@@ -453,24 +463,23 @@ vr_status gauss_pipeline(vr_ctx* c, RenderArgs& A, hipStream_t s, bool stats) {
         HIP_TRY(hipMemsetAsync(c->d_queue, 0, sizeof(uint32_t), s), "hipMemsetAsync(queue)");
         HIP_TRY(gauss_march(A, s, stats), "march");
         if (attempt == 0) HIP_TRY(hipEventRecord(c->ev_stage[0], s), "hipEventRecord");
-        HIP_TRY(hipMemcpyAsync(c->h_totals, A.rec_alloc, 3 * sizeof(uint32_t), hipMemcpyDeviceToHost, s), "rec_alloc D2H");
+        if (sized) break;
+        HIP_TRY(hipMemcpyAsync(c->h_sizing, A.rec_alloc, 3 * sizeof(uint32_t), hipMemcpyDeviceToHost, s), "rec_alloc D2H");
         HIP_TRY(hipStreamSynchronize(s), "march");
-        if (c->h_totals[2] == 0) {
-            nrec = c->h_totals[0];
+        if (c->h_sizing[2] == 0) {
+            c->rec_hint = std::max<uint64_t>(4096, (uint64_t)c->h_sizing[0] + c->h_sizing[0] / 8);
+            c->ovf_hint = std::max<uint64_t>(c->ovf_hint, (uint64_t)c->h_sizing[1] + c->h_sizing[1] / 8);
             break;
         }
         if (attempt >= 3) return fail(VR_ERR_OVERFLOW, "scatter-record capacity could not be sized");
-        cap = std::max<uint64_t>(2 * cap, (uint64_t)c->h_totals[0] + c->h_totals[0] / 4 + 1024);
-        ovf = std::max<uint64_t>(2 * ovf, (uint64_t)c->h_totals[1] + c->h_totals[1] / 4 + 1024);
+        cap = std::max<uint64_t>(2 * cap, (uint64_t)c->h_sizing[0] + c->h_sizing[0] / 4 + 1024);
+        ovf = std::max<uint64_t>(2 * ovf, (uint64_t)c->h_sizing[1] + c->h_sizing[1] / 4 + 1024);
     }
-    c->rec_hint = (uint64_t)nrec + nrec / 8;
-    c->ovf_hint = std::max<uint64_t>(c->ovf_hint, (uint64_t)c->h_totals[1] + c->h_totals[1] / 8);
 
-    const uint64_t nsec = (uint64_t)nrec * (uint64_t)(A.num_lights + A.env_samples);
-    if (nsec >= 0xffffffffull) return fail(VR_ERR_UNSUPPORTED, "more than 2^32 secondary rays in one call (split the frame)");
-    if ((st = grow(c->tr, std::max<uint64_t>(nsec, 1) * 4ull, "hipMalloc(secondary)")) != VR_OK) return st;
+    // Everything below is sized by the capacity; the kernels read the live record count on the device.
+    if ((st = grow(c->tr, std::max<uint64_t>(cap * S, 1) * 4ull, "hipMalloc(secondary)")) != VR_OK) return st;
     A.tr = (float*)c->tr.p;
-    const uint64_t nslow = (uint64_t)nrec * (uint64_t)A.num_lights;
+    const uint64_t nslow = cap * (uint64_t)A.num_lights;
     if ((st = grow(c->slowq, (nslow + 1) * 4ull, "hipMalloc(slow queue)")) != VR_OK) return st;
     A.slowq = (uint32_t*)c->slowq.p;
     A.slowq_cap = (uint32_t)nslow;
@@ -488,61 +497,51 @@ vr_status gauss_pipeline(vr_ctx* c, RenderArgs& A, hipStream_t s, bool stats) {
     {  // per-pixel error budget of the secondary cut-off (record_cut_kernel): budget = t_eps, so the
        // secondary rays' truncation moves a pixel by at most t_eps, the same bound as the primary
        // early-out (error budget). t_eps = 0 (exact mode) keeps the bit-neutral 104.
-        const bool no_cut = getenv("VR_NO_REC_CUT") && getenv("VR_NO_REC_CUT")[0] == '1';  // read per frame (tests)
-        static const float budget_scale = getenv("VR_CUT_BUDGET") ? (float)atof(getenv("VR_CUT_BUDGET")) : 1.0f;
         A.rec_cut = nullptr;
-        if (!no_cut && A.t_eps > 0.0f && nrec > 0) {
-            if ((st = grow(c->rec_cut, (uint64_t)nrec * 4ull, "hipMalloc(record cut-offs)")) != VR_OK) return st;
+        if (c->opt_secondary_budget && A.t_eps > 0.0f) {
+            if ((st = grow(c->rec_cut, cap * 4ull, "hipMalloc(record cut-offs)")) != VR_OK) return st;
             A.rec_cut = (float*)c->rec_cut.p;
-            HIP_TRY(gauss_record_cut(A, A.t_eps * budget_scale, s), "record cut-offs");
+            HIP_TRY(gauss_record_cut(A, A.t_eps, s), "record cut-offs");
         }
     }
-    static const bool no_list = getenv("VR_NOLIST") && getenv("VR_NOLIST")[0] == '1';
-    A.list_ok = c->list_ok && !no_list && (uint64_t)nrec * kListCap < 0xffffffffull;
+    A.list_ok = c->list_ok && cap * kListCap < 0xffffffffull;
     {  // list radius; beyond the 3.15-sigma BVH boxes the query box grows by the excess radius of the
        // widest Gaussian on each axis (conservative: every member's box meets the query box)
-        static const float r2 = getenv("VR_LIST_R2") ? (float)atof(getenv("VR_LIST_R2")) : kListR2;
-        A.list_r2 = r2;
-        const double excess = std::max(0.0, std::sqrt((double)r2) - 3.0 * 1.05);
+        A.list_r2 = kListR2;
+        const double excess = std::max(0.0, std::sqrt((double)kListR2) - 3.0 * 1.05);
         for (int k = 0; k < 3; ++k) {
             const double h = excess * c->sig_max[k];
             A.list_h[k] = h > 0.0 ? (float)(h * (A.hnodes != nullptr ? c->hn_scale : 1.0f) * 1.001 + 1e-6) : 0.0f;
         }
     }
     if (A.list_ok) {
-        if ((st = grow(c->rec_list, std::max<uint64_t>(nrec, 1) * kListCap * 4ull, "hipMalloc(record lists)")) != VR_OK)
-            return st;
-        if ((st = grow(c->rec_nlist, std::max<uint64_t>(nrec, 1) * 4ull, "hipMalloc(record lists)")) != VR_OK) return st;
+        if ((st = grow(c->rec_list, cap * kListCap * 4ull, "hipMalloc(record lists)")) != VR_OK) return st;
+        if ((st = grow(c->rec_nlist, cap * 4ull, "hipMalloc(record lists)")) != VR_OK) return st;
         A.rec_list = (int32_t*)c->rec_list.p;
         A.rec_nlist = (uint32_t*)c->rec_nlist.p;
     }
     HIP_TRY(hipEventRecord(c->ev_stage[1], s), "hipEventRecord");
-    HIP_TRY(gauss_lists(A, nrec, s), "neighbour lists");
+    HIP_TRY(gauss_lists(A, s), "neighbour lists");
     HIP_TRY(hipEventRecord(c->ev_stage[2], s), "hipEventRecord");
-    {  // environment rays traced in direction order within chunks of 256 records (see ray_slot)
-        static const bool no_order = getenv("VR_NO_ENV_ORDER") && getenv("VR_NO_ENV_ORDER")[0] == '1';
-        static const uint32_t order_cr = getenv("VR_ENV_CHUNK") ? (uint32_t)atoi(getenv("VR_ENV_CHUNK")) : 64u;
-        uint32_t cr = 64u, shift = 6u;  // power of 2 in [64, 256] (entries hold record-in-chunk in 8 bits)
-        while (cr < order_cr && cr < 256u) cr <<= 1, ++shift;
+    {  // environment rays traced in direction order within chunks of 64 records (see ray_slot; 128/256-record
+       // chunks measured 2-20 % slower: record locality is lost)
+        constexpr uint32_t cr = 64u, shift = 6u;  // entries hold record-in-chunk in 8 bits
         A.env_order = nullptr;
-        A.chunk_rec = 64u;
-        A.chunk_shift = 6u;
-        if (!no_order && A.env_samples > 0 && A.env_samples <= 256) {
-            const uint64_t nch = ((uint64_t)nrec + cr - 1) / cr;
-            if ((st = grow(c->env_order, std::max<uint64_t>(nch, 1) * cr * (uint64_t)A.env_samples * 2ull,
-                           "hipMalloc(environment-ray order)")) != VR_OK)
+        A.chunk_rec = cr;
+        A.chunk_shift = shift;
+        if (A.env_samples > 0 && A.env_samples <= 256) {
+            const uint64_t nch = (cap + cr - 1) / cr;
+            if ((st = grow(c->env_order, nch * cr * (uint64_t)A.env_samples * 2ull, "hipMalloc(environment-ray order)")) != VR_OK)
                 return st;
             A.env_order = (uint16_t*)c->env_order.p;
-            A.chunk_rec = cr;
-            A.chunk_shift = shift;
         }
     }
-    HIP_TRY(gauss_secondary(A, nrec, s, stats), "secondary rays");
+    HIP_TRY(gauss_secondary(A, s, stats), "secondary rays");
     HIP_TRY(hipEventRecord(c->ev_stage[3], s), "hipEventRecord");
-    HIP_TRY(gauss_accumulate(A, nrec, s), "accumulate");
+    HIP_TRY(gauss_accumulate(A, s), "accumulate");
     c->staged = true;
-    c->last_records = nrec;
-    c->last_secondary = (int64_t)nsec;
+    c->report_gauss = true;
+    c->last_secondary_per_record = S;
     return VR_OK;
 }
 
@@ -569,7 +568,7 @@ vr_status free_flight_pipeline(vr_ctx* c, RenderArgs& A, hipStream_t s) {
     A.ff_threads = threads;
     A.ff_hit_cap = kFFHitCap;
     A.ff_act_cap = kFFActCap;
-    A.ff_hit_cap0 = getenv("VR_FF_CAP0") ? std::max(1, std::min(kFFHitCap, atoi(getenv("VR_FF_CAP0")))) : 8;
+    A.ff_hit_cap0 = (int32_t)std::max<int64_t>(1, std::min<int64_t>(kFFHitCap, c->opt_ff_window0));
     A.ff_key = base;
     A.ff_t1 = base + (size_t)kFFHitCap * threads;
     A.ff_gid = (int32_t*)(base + (size_t)2 * kFFHitCap * threads);
@@ -578,14 +577,6 @@ vr_status free_flight_pipeline(vr_ctx* c, RenderArgs& A, hipStream_t s) {
     A.ff_next = (unsigned long long*)(base + (size_t)(3 * kFFHitCap + 8 * kFFActCap) * threads);
     A.ff_path = (float*)c->ff_path.p;
     A.ff_sum = (float*)c->ff_sum.p;
-    A.ff_refill = getenv("VR_FF_REFILL") ? atoi(getenv("VR_FF_REFILL")) : 0;
-    const char* dbg = getenv("VR_FF_DEBUG");  // EXPERIMENT: first-bounce dump of a one-step render
-    vr_ctx::Buf dbuf;
-    if (dbg) {
-        if ((st = grow(dbuf, (size_t)threads * 8 * sizeof(float), "dbg")) != VR_OK) return st;
-        HIP_TRY(hipMemsetAsync(dbuf.p, 0, (size_t)threads * 8 * sizeof(float), s), "memset");
-        A.ff_dbg = (float*)dbuf.p;
-    }
     for (uint32_t t0 = 0; t0 < A.num_tiles; t0 += chunk) {
         const uint32_t nt = std::min(chunk, A.num_tiles - t0);
         for (uint32_t si = 0; si < spp; si += nsb) {
@@ -596,35 +587,36 @@ vr_status free_flight_pipeline(vr_ctx* c, RenderArgs& A, hipStream_t s) {
             HIP_TRY(launch_free_flight(A, nt, s), "free-flight launch");
         }
     }
-    if (dbg) {
-        std::vector<float> h((size_t)threads * 8);
-        HIP_TRY(hipMemcpyAsync(h.data(), dbuf.p, h.size() * 4, hipMemcpyDeviceToHost, s), "dbg copy");
-        HIP_TRY(hipStreamSynchronize(s), "dbg sync");
-        FILE* fp = fopen(dbg, "wb");
-        if (fp) {
-            fwrite(h.data(), 4, h.size(), fp);
-            fclose(fp);
-        }
-        (void)hipFree(dbuf.p);
+    return VR_OK;
+}
+
+// Collect the report of the last frame (waits for it). Grows the record capacity hints from its
+// counts, so a frame that outgrew them renders correctly the next time.
+vr_status collect(vr_ctx* c) {
+    if (!c->stats_pending) return VR_OK;
+    HIP_TRY(hipEventSynchronize(c->ev_report), "hipEventSynchronize");
+    c->stats_pending = false;
+    if (c->report_gauss) {
+        const uint64_t nrec = c->h_report[2], nact = c->h_report[3];
+        c->rec_hint = std::max<uint64_t>(c->rec_hint, nrec + nrec / 8);
+        c->ovf_hint = std::max<uint64_t>(c->ovf_hint, nact + nact / 8);
     }
     return VR_OK;
 }
+
+bool frame_exceeded(const vr_ctx* c) { return c->report_gauss && c->h_report[4] != 0; }
 
 vr_status launch(vr_ctx* c, RenderArgs& A, const vr_render_params* p, hipStream_t s, bool stats = false) {
     vr_status st = ensure_queue(c, (uint64_t)A.num_tiles * 256u);
     if (st != VR_OK) return st;
     A.queue = c->d_queue;
     A.queue_cap = c->queue_cap;
-    if (c->stats_pending) {  // previous stats copy must land before we reuse the pinned buffer
-        HIP_TRY(hipEventSynchronize(c->ev_stop), "hipEventSynchronize");
-        c->stats_pending = false;
-    }
+    if ((st = collect(c)) != VR_OK) return st;  // the previous report must land before the pinned buffer is reused
     HIP_TRY(hipMemsetAsync(c->d_queue, 0, sizeof(uint32_t), s), "hipMemsetAsync(queue)");
     HIP_TRY(hipMemsetAsync(c->d_counters, 0, 4 * sizeof(uint32_t), s), "hipMemsetAsync(counters)");
     HIP_TRY(hipEventRecord(c->ev_start, s), "hipEventRecord");
     c->staged = false;
-    c->last_records = 0;
-    c->last_secondary = 0;
+    c->report_gauss = false;
     if (c->type == VR_VOLUME_GAUSSIANS && (p->integrator == VR_RAYMARCH_GAUSSIANS || p->integrator == VR_PURE_RAYMARCH)) {
         st = gauss_pipeline(c, A, s, stats);
         if (st != VR_OK) return st;
@@ -635,10 +627,30 @@ vr_status launch(vr_ctx* c, RenderArgs& A, const vr_render_params* p, hipStream_
         HIP_TRY(launch_render(A, s, c->type, p->integrator), "kernel launch");
     }
     HIP_TRY(hipEventRecord(c->ev_stop, s), "hipEventRecord");
-    HIP_TRY(hipMemcpyAsync(&c->h_counters[0], c->d_queue, sizeof(uint32_t), hipMemcpyDeviceToHost, s), "hipMemcpyAsync(stats)");
-    HIP_TRY(hipMemcpyAsync(&c->h_counters[1], c->d_counters, sizeof(uint32_t), hipMemcpyDeviceToHost, s), "hipMemcpyAsync(stats)");
+    HIP_TRY(hipMemcpyAsync(&c->h_report[0], c->d_queue, sizeof(uint32_t), hipMemcpyDeviceToHost, s), "hipMemcpyAsync(report)");
+    HIP_TRY(hipMemcpyAsync(&c->h_report[1], c->d_counters, sizeof(uint32_t), hipMemcpyDeviceToHost, s), "hipMemcpyAsync(report)");
+    if (c->report_gauss)
+        HIP_TRY(hipMemcpyAsync(&c->h_report[2], A.rec_alloc, 3 * sizeof(uint32_t), hipMemcpyDeviceToHost, s),
+                "hipMemcpyAsync(report)");
+    HIP_TRY(hipEventRecord(c->ev_report, s), "hipEventRecord");
     c->stats_pending = true;
     c->last_pixels = (int64_t)A.num_tiles * 256;
+    return VR_OK;
+}
+
+// Synchronous frame into the context's device frame buffer (vr_render, vr_render_record,
+// vr_count_work): a frame that outgrew the record buffers sized from earlier frames is rendered
+// again with grown ones; pixels / paths over every per-ray capacity fail the call.
+vr_status render_sync(vr_ctx* c, RenderArgs& A, const vr_render_params* p, bool stats, const char* what) {
+    for (int attempt = 0;; ++attempt) {
+        vr_status st = launch(c, A, p, c->stream, stats);
+        if (st != VR_OK) return st;
+        if ((st = collect(c)) != VR_OK) return st;
+        if (!frame_exceeded(c)) break;
+        if (attempt >= 3) return fail(VR_ERR_OVERFLOW, "scatter-record capacity could not be sized");
+    }
+    if (c->h_report[1] != 0)
+        return fail(VR_ERR_OVERFLOW, std::to_string(c->h_report[1]) + std::string(" ") + what);
     return VR_OK;
 }
 
@@ -657,15 +669,16 @@ vr_status vr_init(int device, vr_ctx** out) {
     c->device = device;
     if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
         hipMalloc(&c->d_counters, 4 * sizeof(uint32_t)) != hipSuccess ||
-        hipHostMalloc(&c->h_counters, 4 * sizeof(uint32_t), hipHostMallocDefault) != hipSuccess ||
-        hipHostMalloc(&c->h_totals, 4 * sizeof(uint32_t), hipHostMallocDefault) != hipSuccess ||
+        hipHostMalloc(&c->h_report, 8 * sizeof(uint32_t), hipHostMallocDefault) != hipSuccess ||
+        hipHostMalloc(&c->h_sizing, 4 * sizeof(uint32_t), hipHostMallocDefault) != hipSuccess ||
         hipEventCreate(&c->ev_start) != hipSuccess || hipEventCreate(&c->ev_stop) != hipSuccess ||
+        hipEventCreate(&c->ev_report) != hipSuccess ||
         hipEventCreate(&c->ev_stage[0]) != hipSuccess || hipEventCreate(&c->ev_stage[1]) != hipSuccess ||
         hipEventCreate(&c->ev_stage[2]) != hipSuccess || hipEventCreate(&c->ev_stage[3]) != hipSuccess) {
         vr_destroy(c);
         return fail(VR_ERR_HIP, "vr_init: failed to create stream/workspace");
     }
-    std::memset(c->h_counters, 0, 4 * sizeof(uint32_t));
+    std::memset(c->h_report, 0, 8 * sizeof(uint32_t));
     *out = c;
     return VR_OK;
 }
@@ -678,8 +691,8 @@ void vr_destroy(vr_ctx* c) {
     for (auto& kv : c->tables) (void)hipFree(kv.second.d);
     if (c->d_queue) (void)hipFree(c->d_queue);
     if (c->d_counters) (void)hipFree(c->d_counters);
-    if (c->h_counters) (void)hipHostFree(c->h_counters);
-    if (c->h_totals) (void)hipHostFree(c->h_totals);
+    if (c->h_report) (void)hipHostFree(c->h_report);
+    if (c->h_sizing) (void)hipHostFree(c->h_sizing);
     for (vr_ctx::Buf* b : {&c->px_first, &c->px_T, &c->rec_pos, &c->rec_meta, &c->rec_next, &c->rec_act, &c->tr,
                            &c->rec_alloc, &c->rec_bloom, &c->slowq, &c->pcg_jump, &c->ray_next, &c->rec_list, &c->rec_nlist,
                            &c->stack_ovf, &c->env_order, &c->rec_cut, &c->ff_scratch, &c->ff_path, &c->ff_sum, &c->rec_bits[0], &c->rec_bits[1], &c->sfd_tmp})
@@ -687,6 +700,7 @@ void vr_destroy(vr_ctx* c) {
     if (c->d_frame) (void)hipFree(c->d_frame);
     if (c->ev_start) (void)hipEventDestroy(c->ev_start);
     if (c->ev_stop) (void)hipEventDestroy(c->ev_stop);
+    if (c->ev_report) (void)hipEventDestroy(c->ev_report);
     for (hipEvent_t e : c->ev_stage)
         if (e) (void)hipEventDestroy(e);
     if (c->stream) (void)hipStreamDestroy(c->stream);
@@ -756,8 +770,6 @@ vr_status vr_upload_scene(vr_ctx* c, const vr_scene* sc) {
             for (int k = 0; k < 6; ++k) ok = ok && std::isfinite(p.inv_cov[k]);
             c->list_ok = ok;
         }
-        if (getenv("VR_DEBUG"))
-            fprintf(stderr, "[vr] BVH: %zu prims, %zu nodes, depth %d\n", N, b.nodes.size(), b.max_depth);
         c->num_nodes = b.nodes.size();
     } else {
         const size_t N = s.spheres.size();
@@ -803,13 +815,9 @@ vr_status vr_render(vr_ctx* c, const vr_camera* cam, const vr_render_params* p, 
     A.num_tiles = vr_num_tiles(W, H);
     A.packed = 0;
     A.out = c->d_frame;
-    st = launch(c, A, p, c->stream);
+    st = render_sync(c, A, p, false, "pixels / paths exceeded a per-ray capacity (NaN)");
     if (st != VR_OK) return st;
-    HIP_TRY(hipMemcpyAsync(rgb, c->d_frame, bytes, hipMemcpyDeviceToHost, c->stream), "hipMemcpyAsync(frame)");
-    HIP_TRY(hipStreamSynchronize(c->stream), "render");
-    c->stats_pending = false;
-    if (c->h_counters[1] != 0)
-        return fail(VR_ERR_OVERFLOW, std::to_string(c->h_counters[1]) + " pixels exceeded the active-set capacity (NaN)");
+    HIP_TRY(hipMemcpy(rgb, c->d_frame, bytes, hipMemcpyDeviceToHost), "hipMemcpy(frame)");
     return VR_OK;
 }
 
@@ -832,7 +840,7 @@ vr_status vr_render_tiles_device(vr_ctx* c, const vr_camera* cam, const vr_rende
     A.num_tiles = num_tiles;
     A.packed = packed ? 1 : 0;
     A.out = d_out;
-    return launch(c, A, p, (hipStream_t)stream);
+    return launch(c, A, p, (hipStream_t)stream);  // outcome: vr_synchronize / vr_get_stats
 }
 
 vr_status vr_count_work(vr_ctx* c, const vr_camera* cam, const vr_render_params* p, uint32_t W, uint32_t H,
@@ -858,14 +866,17 @@ vr_status vr_count_work(vr_ctx* c, const vr_camera* cam, const vr_render_params*
     A.packed = 1;
     A.out = d_out;
     A.work = d_work;
-    st = launch(c, A, p, c->stream, true);
     unsigned long long h[16] = {0};
+    for (int attempt = 0;; ++attempt) {  // a frame over the record capacity is counted again (grown)
+        if (hipMemsetAsync(d_work, 0, 16 * sizeof(unsigned long long), c->stream) != hipSuccess) break;
+        st = launch(c, A, p, c->stream, true);
+        if (st == VR_OK) st = collect(c);
+        if (st != VR_OK || !frame_exceeded(c) || attempt >= 3) break;
+    }
     if (st == VR_OK) {
-        hipError_t e = hipMemcpyAsync(h, d_work, sizeof(h), hipMemcpyDeviceToHost, c->stream);
-        if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+        hipError_t e = hipMemcpy(h, d_work, sizeof(h), hipMemcpyDeviceToHost);
         if (e != hipSuccess) st = hip_fail(e, "vr_count_work");
     }
-    c->stats_pending = false;
     (void)hipFree(d_out);
     (void)hipFree(d_work);
     for (int i = 0; i < 16; ++i) counts[i] = h[i];
@@ -911,13 +922,9 @@ vr_status vr_render_record(vr_ctx* c, const vr_camera* cam, const vr_render_para
     A.num_tiles = vr_num_tiles(W, H);
     A.packed = 0;
     A.out = c->d_frame;
-    st = launch(c, A, p, c->stream);
+    st = render_sync(c, A, p, false, "paths exceeded the per-path capacity (NaN)");
     if (st != VR_OK) return st;
-    HIP_TRY(hipMemcpyAsync(rgb, c->d_frame, fb, hipMemcpyDeviceToHost, c->stream), "hipMemcpyAsync(frame)");
-    HIP_TRY(hipStreamSynchronize(c->stream), "render");
-    c->stats_pending = false;
-    if (c->h_counters[1] != 0)
-        return fail(VR_ERR_OVERFLOW, std::to_string(c->h_counters[1]) + " paths exceeded the per-path capacity (NaN)");
+    HIP_TRY(hipMemcpy(rgb, c->d_frame, fb, hipMemcpyDeviceToHost), "hipMemcpy(frame)");
     return VR_OK;
 }
 
@@ -954,24 +961,63 @@ vr_status vr_sfd_loss_diff(vr_ctx* c, const float* loss_base, const float* loss_
     return VR_OK;
 }
 
+vr_status vr_set_option(vr_ctx* c, int32_t option, int64_t value) {
+    if (!c) return fail(VR_ERR_INVALID, "vr_set_option: NULL ctx");
+    switch (option) {
+        case VR_OPT_HALF_NODES:
+            if (value != 0 && value != 1) return fail(VR_ERR_INVALID, "VR_OPT_HALF_NODES must be 0 or 1");
+            c->opt_half_nodes = value;
+            return VR_OK;
+        case VR_OPT_SECONDARY_BUDGET:
+            if (value != 0 && value != 1) return fail(VR_ERR_INVALID, "VR_OPT_SECONDARY_BUDGET must be 0 or 1");
+            c->opt_secondary_budget = value;
+            return VR_OK;
+        case VR_OPT_FF_WINDOW0:
+            if (value < 1 || value > kFFHitCap) return fail(VR_ERR_INVALID, "VR_OPT_FF_WINDOW0 must be in [1, 128]");
+            c->opt_ff_window0 = value;
+            return VR_OK;
+        default:
+            return fail(VR_ERR_INVALID, "vr_set_option: unknown option " + std::to_string(option));
+    }
+}
+
+vr_status vr_get_option(vr_ctx* c, int32_t option, int64_t* value) {
+    if (!c || !value) return fail(VR_ERR_INVALID, "vr_get_option: NULL argument");
+    switch (option) {
+        case VR_OPT_HALF_NODES: *value = c->opt_half_nodes; return VR_OK;
+        case VR_OPT_SECONDARY_BUDGET: *value = c->opt_secondary_budget; return VR_OK;
+        case VR_OPT_FF_WINDOW0: *value = c->opt_ff_window0; return VR_OK;
+        default: return fail(VR_ERR_INVALID, "vr_get_option: unknown option " + std::to_string(option));
+    }
+}
+
 vr_status vr_synchronize(vr_ctx* c) {
     if (!c) return fail(VR_ERR_INVALID, "vr_synchronize: NULL ctx");
     HIP_TRY(hipSetDevice(c->device), "hipSetDevice");
     HIP_TRY(hipDeviceSynchronize(), "hipDeviceSynchronize");
+    const bool pending = c->stats_pending;
+    vr_status st = collect(c);
+    if (st != VR_OK || !pending) return st;
+    if (frame_exceeded(c))
+        return fail(VR_ERR_OVERFLOW, "the last frame outgrew the scatter-record buffers sized from earlier frames; "
+                                     "they have been grown: render it again");
+    if (c->h_report[1] != 0)
+        return fail(VR_ERR_OVERFLOW, std::to_string(c->h_report[1]) + " pixels / paths of the last frame exceeded a "
+                                     "per-ray capacity (NaN)");
     return VR_OK;
 }
 
 vr_status vr_get_stats(vr_ctx* c, vr_render_stats* o) {
     if (!c || !o) return fail(VR_ERR_INVALID, "vr_get_stats: NULL argument");
     HIP_TRY(hipSetDevice(c->device), "hipSetDevice");
-    HIP_TRY(hipEventSynchronize(c->ev_stop), "hipEventSynchronize");
-    c->stats_pending = false;
+    vr_status st = collect(c);
+    if (st != VR_OK) return st;
     float ms = 0.0f;
     HIP_TRY(hipEventElapsedTime(&ms, c->ev_start, c->ev_stop), "hipEventElapsedTime");
     o->kernel_ms = ms;
     o->pixels = c->last_pixels;
-    o->fallback_pixels = c->h_counters[0];
-    o->error_pixels = c->h_counters[1];
+    o->fallback_pixels = c->h_report[0];
+    o->error_pixels = c->h_report[1];
     for (double& v : o->stage_ms) v = 0.0;
     if (c->staged) {
         hipEvent_t b[6] = {c->ev_start, c->ev_stage[0], c->ev_stage[1], c->ev_stage[2], c->ev_stage[3], c->ev_stop};
@@ -981,8 +1027,9 @@ vr_status vr_get_stats(vr_ctx* c, vr_render_stats* o) {
             o->stage_ms[i] = m;
         }
     }
-    o->scatter_records = c->last_records;
-    o->secondary_rays = c->last_secondary;
+    o->scatter_records = c->report_gauss ? (int64_t)c->h_report[2] : 0;
+    o->secondary_rays = o->scatter_records * (int64_t)c->last_secondary_per_record;
+    o->record_overflow = frame_exceeded(c) ? 1 : 0;
     return VR_OK;
 }
 

@@ -381,10 +381,6 @@ __device__ float free_flight_distance(const RenderArgs& A, const FFScratch& S, c
             }
             if (acc + seg > (Acc)target) {
                 float rem = (float)((Acc)target - acc);
-                if (A.ff_dbg) {
-                    float* d = A.ff_dbg + (size_t)(blockIdx.x * kFFBlock + threadIdx.x) * 8;
-                    d[2] = t_prev, d[3] = t_evt, d[4] = (float)m, d[5] = (float)n, d[6] = rem, d[7] = (float)seg;
-                }
                 return solve_distance(A, S, m, r, t_prev, t_evt, rem);
             }
             acc += seg;
@@ -469,10 +465,6 @@ __device__ __forceinline__ void ff_one_path(const RenderArgs& A, const FFScratch
                 Li2 = (Tr * A.env[2]) * k4Pi;
             }
             const float w = (albedo * kInv4Pi) * w_ne;
-            if (A.ff_dbg && bounce == 0) {
-                float* d = A.ff_dbg + (size_t)(blockIdx.x * kFFBlock + threadIdx.x) * 8;
-                d[0] = target, d[1] = ts;
-            }
             if constexpr (!MULTI) {  // integrator.h:396-399
                 L0 = w * Li0;
                 L1 = w * Li1;
@@ -525,157 +517,6 @@ __global__ void __launch_bounds__(kFFBlock, 4) ff_path_kernel(RenderArgs A) {
         if (base >= A.ff_total) break;  // wave-uniform: every wave leaves once the work is handed out
         const unsigned long long pid = base + lane;
         if (pid < A.ff_total) ff_one_path<MULTI>(A, S, stack, (uint32_t)(pid / kFFBlock), (uint32_t)(pid % kFFBlock), pid);
-    }
-}
-
-// Persistent with per-lane refill: a lane whose path ended takes the next path at once (one
-// wave-aggregated atomic for all idle lanes of the wave), so a wave always has up to 64 paths in
-// flight at possibly different bounces; one iteration of the wave = one bounce of every busy lane.
-template <bool MULTI>
-__global__ void __launch_bounds__(kFFBlock, 4) ff_path_refill_kernel(RenderArgs A) {
-    __shared__ int s_stack[kStackSize * kFFBlock];
-    int* stack = s_stack + threadIdx.x;
-    const uint32_t gt = blockIdx.x * kFFBlock + threadIdx.x;
-    const size_t AC = (size_t)A.ff_act_cap * A.ff_threads;
-    float* cache = A.ff_cache + gt;
-    const FFScratch S{A.ff_key + gt, A.ff_t1 + gt, A.ff_gid + gt, A.ff_act + gt,
-                      cache, cache + AC, cache + 2 * AC, cache + 3 * AC, cache + 4 * AC, cache + 5 * AC, cache + 6 * AC,
-                      A.ff_threads};
-    const uint32_t lane = threadIdx.x & 63u;
-    const int nl = A.num_lights;
-    const float w_ne = (float)(nl + 1);
-    const float p_env = __fdiv_rn(1.0f, (float)(nl + 1));
-    bool active = false, drained = false;
-    unsigned long long pid = 0;
-    Ray ray{};
-    PCG32 rng(0ull, 1ull);
-    float tp0 = 1.0f, tp1 = 1.0f, tp2 = 1.0f, L0 = 0.0f, L1 = 0.0f, L2 = 0.0f;
-    int bounce = 0, x = 0, y = 0;
-    for (;;) {
-        if (!drained) {
-            const unsigned long long need = __ballot(!active);
-            if (need) {
-                const uint32_t cnt = (uint32_t)__popcll(need);
-                const int leader = __ffsll((long long)need) - 1;
-                unsigned long long base = 0;
-                if ((int)lane == leader) base = atomicAdd(A.ff_next, (unsigned long long)cnt);
-                base = __shfl(base, leader, 64);
-                if (!active) {
-                    pid = base + (unsigned long long)__popcll(need & ((1ull << lane) - 1ull));
-                    if (pid < A.ff_total) {
-                        const uint32_t bb = (uint32_t)(pid / kFFBlock), lane_id = (uint32_t)(pid % kFFBlock);
-                        const uint32_t tile_local = A.ff_tile_base + bb / A.ff_nsb;
-                        const int si = (int)(A.ff_si0 + bb % A.ff_nsb);
-                        int lx, ly;
-                        tile_pixel(A, tile_local, (int)lane_id, lx, ly, x, y);
-                        if (x < (int)A.width && y < (int)A.height) {
-                            rng = PCG32(derive_path_seed(x, y, si), 1);
-                            const int n = A.ff_n;
-                            const int sx = si % n, sy = si / n;
-                            float xi = rng.uniform();
-                            float u = __fdiv_rn((float)x + __fdiv_rn((float)sx + xi, (float)n), (float)A.width);
-                            xi = rng.uniform();
-                            float v = __fdiv_rn((float)y + __fdiv_rn((float)sy + xi, (float)n), (float)A.height);
-                            ray = camera_ray(A, u, v);
-                            tp0 = tp1 = tp2 = 1.0f;
-                            L0 = L1 = L2 = 0.0f;
-                            bounce = 0;
-                            active = true;
-                        } else {
-                            A.ff_path[pid * 3 + 0] = 0.0f;
-                            A.ff_path[pid * 3 + 1] = 0.0f;
-                            A.ff_path[pid * 3 + 2] = 0.0f;
-                        }
-                    }
-                }
-                if (base + cnt >= A.ff_total) drained = true;  // wave-uniform
-            }
-        }
-        if (!__any(active)) {
-            if (drained) break;  // every wave leaves once the work is handed out and its paths ended
-            continue;
-        }
-        if (active) {
-            bool cont = false;
-            do {
-                int m = 0;
-                const float target = -logf(1.0f - rng.uniform());
-                const float ts = free_flight_distance<MULTI>(A, S, ray, target, m, stack, kFFBlock);
-                if (MULTI && A.rec_bits && ts != -2.0f)
-                    record_hits(A, ray, ts >= 0.0f ? ts + 1e-6f : INFINITY, (uint32_t)y * A.width + (uint32_t)x, stack, kFFBlock);
-                if (ts == -2.0f || bounce >= A.ff_max_bounces) {
-                    L0 = L1 = L2 = __builtin_nanf("");
-                    atomicAdd(A.counters, 1u);
-                    break;
-                }
-                if (ts < 0.0f) {  // no event, or no scatter before the last event: environment
-                    L0 += tp0 * A.env[0];
-                    L1 += tp1 * A.env[1];
-                    L2 += tp2 * A.env[2];
-                    break;
-                }
-                const float px = ray.ox + ts * ray.dx, py = ray.oy + ts * ray.dy, pz = ray.oz + ts * ray.dz;
-                const float albedo = evaluate_albedo(A, S, m, px, py, pz);
-                const bool is_env = rng.uniform() < p_env;
-                float Li0, Li1, Li2;
-                if (!is_env) {
-                    int li = (int)(rng.uniform() * (float)nl);
-                    const LightRecord& Lt = A.lights[li];
-                    float wx = Lt.px - px, wy = Lt.py - py, wz = Lt.pz - pz;
-                    float dist = sqrtf(dot3(wx, wy, wz, wx, wy, wz));
-                    normalize3(wx, wy, wz);
-                    Ray sr = make_ray(px, py, pz, wx, wy, wz);
-                    float Tr = transmittance_up_to(A, sr, dist, stack, kFFBlock);
-                    float d2 = dist * dist;
-                    Li0 = __fdiv_rn(Tr * Lt.ix, d2);
-                    Li1 = __fdiv_rn(Tr * Lt.iy, d2);
-                    Li2 = __fdiv_rn(Tr * Lt.iz, d2);
-                } else {
-                    float wx, wy, wz;
-                    sample_uniform_direction(rng, wx, wy, wz);
-                    Ray er = make_ray(px, py, pz, wx, wy, wz);
-                    float Tr = transmittance_up_to(A, er, INFINITY, stack, kFFBlock);
-                    Li0 = (Tr * A.env[0]) * k4Pi;
-                    Li1 = (Tr * A.env[1]) * k4Pi;
-                    Li2 = (Tr * A.env[2]) * k4Pi;
-                }
-                const float w = (albedo * kInv4Pi) * w_ne;
-                if (A.ff_dbg && bounce == 0) {
-                    float* d = A.ff_dbg + (size_t)(blockIdx.x * kFFBlock + threadIdx.x) * 8;
-                    d[0] = target, d[1] = ts;
-                }
-                if constexpr (!MULTI) {  // integrator.h:396-399
-                    L0 = w * Li0;
-                    L1 = w * Li1;
-                    L2 = w * Li2;
-                    break;
-                }
-                L0 += (tp0 * w) * Li0;  // integrator.h:681-687
-                L1 += (tp1 * w) * Li1;
-                L2 += (tp2 * w) * Li2;
-                tp0 *= albedo;
-                tp1 *= albedo;
-                tp2 *= albedo;
-                if (bounce >= A.ff_min_bounces) {  // integrator.h:691-695
-                    float rr = fminf(fmaxf(tp0, fmaxf(tp1, tp2)), 0.9f);
-                    if (rng.uniform() > rr) break;
-                    tp0 = __fdiv_rn(tp0, rr);
-                    tp1 = __fdiv_rn(tp1, rr);
-                    tp2 = __fdiv_rn(tp2, rr);
-                }
-                float nx, ny, nz;
-                sample_uniform_direction(rng, nx, ny, nz);
-                ray = make_ray(px, py, pz, nx, ny, nz);
-                ++bounce;
-                cont = true;
-            } while (false);
-            if (!cont) {
-                A.ff_path[pid * 3 + 0] = L0;
-                A.ff_path[pid * 3 + 1] = L1;
-                A.ff_path[pid * 3 + 2] = L2;
-                active = false;
-            }
-        }
     }
 }
 
@@ -752,12 +593,7 @@ hipError_t launch_free_flight(const RenderArgs& A, uint32_t chunk_tiles, hipStre
     hipError_t e0 = hipMemsetAsync(A.ff_next, 0, sizeof(unsigned long long), stream);
     if (e0 != hipSuccess) return e0;
     dim3 grid(A.ff_threads / dev::kFFBlock);
-    if (A.ff_refill) {
-        if (A.ff_multi)
-            hipLaunchKernelGGL(dev::ff_path_refill_kernel<true>, grid, dim3(dev::kFFBlock), 0, stream, A);
-        else
-            hipLaunchKernelGGL(dev::ff_path_refill_kernel<false>, grid, dim3(dev::kFFBlock), 0, stream, A);
-    } else if (A.ff_multi)
+    if (A.ff_multi)
         hipLaunchKernelGGL(dev::ff_path_kernel<true>, grid, dim3(dev::kFFBlock), 0, stream, A);
     else
         hipLaunchKernelGGL(dev::ff_path_kernel<false>, grid, dim3(dev::kFFBlock), 0, stream, A);

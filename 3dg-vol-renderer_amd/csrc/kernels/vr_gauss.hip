@@ -31,8 +31,8 @@
 // fallback kernels (64), so results never depend on capacity.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cstdio>
-#include <cstdlib>
 
 #include "vr_dev_common.h"
 
@@ -44,6 +44,11 @@ namespace dev {
 // else it crosses — the traversal stops there. (The reference's product of per-segment
 // exponentials reaches 0 or a denormal <= 1.4e-45 at the same point.)
 constexpr float kTauCut = 104.0f;
+
+// Scatter records of the frame, read on the device: the host never waits for the march (the
+// buffers are sized from the previous frame; a frame that outgrew them is reported and re-run).
+// Clamped to the capacity, so an overflowing frame stays in bounds.
+__device__ __forceinline__ uint32_t dev_nrec(const RenderArgs& A) { return min(A.rec_alloc[0], A.rec_cap); }
 
 // ---------------------------------------------------------------------------------------------
 // Exact light-ray transmittance (the slow path of Stage 2)
@@ -389,7 +394,7 @@ struct SecRay {
     bool light, needs_stop;
     uint32_t nsteps;  // instrumented build only: node steps taken by this ray
     uint32_t rec;     // record index
-    uint32_t slot;    // result slot s * nrec + rec in tr
+    uint32_t slot;    // result slot s * rec_cap + rec in tr
     bool listed;      // the record has a neighbour list (tree leaves then skip its members)
 };
 
@@ -407,8 +412,8 @@ __device__ __forceinline__ void env_sample_dir(const RenderArgs& A, const uint4&
     const int px = (int)(meta.x & 0xffffu), py = (int)(meta.x >> 16);
     PCG32 rng(derive_path_seed(px, py, (int)meta.y), 1);
     rng.state = A.pcg_jump[4 * e] * rng.state + A.pcg_jump[4 * e + 1];
-    float xi1 = rng.uniform();
-    float xi2 = rng.uniform();
+    float xi1 = rng.uniform_env();
+    float xi2 = rng.uniform_env();
     env_dir(xi1, xi2, wx, wy, wz);
 }
 
@@ -435,48 +440,53 @@ __device__ __forceinline__ uint32_t dir_key(float x, float y, float z) {
 // One workgroup per record chunk: counting sort of the chunk's environment rays by direction key
 // (order inside a key is arbitrary: every ray's result is independent of when it is traced).
 template <int BLOCK>
-__global__ __launch_bounds__(BLOCK) void env_order_kernel(RenderArgs A, uint32_t nrec) {
+__global__ __launch_bounds__(BLOCK) void env_order_kernel(RenderArgs A) {
     constexpr uint32_t kKeyCap = 16384;  // keys kept in LDS (one byte each); larger chunks recompute them
     __shared__ uint32_t hist[kEnvCells];
     __shared__ uint8_t keys[kKeyCap];
+    const uint32_t nrec = dev_nrec(A);
     const uint32_t cr = A.chunk_rec, ne = (uint32_t)A.env_samples;
-    const uint32_t n = cr * ne, r0 = blockIdx.x * cr;
+    const uint32_t n = cr * ne, nch = (nrec + cr - 1) / cr;
     const bool cached = n <= kKeyCap;
-    for (uint32_t i = threadIdx.x; i < kEnvCells; i += BLOCK) hist[i] = 0;
-    __syncthreads();
-    auto key = [&](uint32_t i) -> uint32_t {
-        const uint32_t rl = i / ne, r = r0 + rl;
-        if (r >= nrec) return kEnvCells - 1;  // padding records
-        float wx, wy, wz;
-        env_sample_dir(A, A.rec_meta[r], i - rl * ne, wx, wy, wz);
-        return dir_key(wx, wy, wz);
-    };
-    for (uint32_t i = threadIdx.x; i < n; i += BLOCK) {
-        const uint32_t k = key(i);
-        if (cached) keys[i] = (uint8_t)k;
-        atomicAdd(&hist[k], 1u);
-    }
-    __syncthreads();
-    if (threadIdx.x < 64) {  // exclusive scan of the 256 counts by one wave (4 per lane)
-        const uint32_t l = threadIdx.x;
-        const uint32_t a = hist[4 * l], b = hist[4 * l + 1], c = hist[4 * l + 2], d = hist[4 * l + 3];
-        uint32_t sum = a + b + c + d, incl = sum;
-#pragma unroll
-        for (int o = 1; o < 64; o <<= 1) {
-            const uint32_t y = __shfl_up(incl, o, 64);
-            if (l >= (uint32_t)o) incl += y;
+    for (uint32_t chunk = blockIdx.x; chunk < nch; chunk += gridDim.x) {  // block-uniform loop
+        const uint32_t r0 = chunk * cr;
+        for (uint32_t i = threadIdx.x; i < kEnvCells; i += BLOCK) hist[i] = 0;
+        __syncthreads();
+        auto key = [&](uint32_t i) -> uint32_t {
+            const uint32_t rl = i / ne, r = r0 + rl;
+            if (r >= nrec) return kEnvCells - 1;  // padding records
+            float wx, wy, wz;
+            env_sample_dir(A, A.rec_meta[r], i - rl * ne, wx, wy, wz);
+            return dir_key(wx, wy, wz);
+        };
+        for (uint32_t i = threadIdx.x; i < n; i += BLOCK) {
+            const uint32_t k = key(i);
+            if (cached) keys[i] = (uint8_t)k;
+            atomicAdd(&hist[k], 1u);
         }
-        const uint32_t ex = incl - sum;
-        hist[4 * l] = ex;
-        hist[4 * l + 1] = ex + a;
-        hist[4 * l + 2] = ex + a + b;
-        hist[4 * l + 3] = ex + a + b + c;
-    }
-    __syncthreads();
-    uint16_t* out = A.env_order + (size_t)blockIdx.x * n;
-    for (uint32_t i = threadIdx.x; i < n; i += BLOCK) {
-        const uint32_t rl = i / ne;
-        out[atomicAdd(&hist[cached ? (uint32_t)keys[i] : key(i)], 1u)] = (uint16_t)((rl << 8) | (i - rl * ne));
+        __syncthreads();
+        if (threadIdx.x < 64) {  // exclusive scan of the 256 counts by one wave (4 per lane)
+            const uint32_t l = threadIdx.x;
+            const uint32_t a = hist[4 * l], b = hist[4 * l + 1], c = hist[4 * l + 2], d = hist[4 * l + 3];
+            uint32_t sum = a + b + c + d, incl = sum;
+#pragma unroll
+            for (int o = 1; o < 64; o <<= 1) {
+                const uint32_t y = __shfl_up(incl, o, 64);
+                if (l >= (uint32_t)o) incl += y;
+            }
+            const uint32_t ex = incl - sum;
+            hist[4 * l] = ex;
+            hist[4 * l + 1] = ex + a;
+            hist[4 * l + 2] = ex + a + b;
+            hist[4 * l + 3] = ex + a + b + c;
+        }
+        __syncthreads();
+        uint16_t* out = A.env_order + (size_t)chunk * n;
+        for (uint32_t i = threadIdx.x; i < n; i += BLOCK) {
+            const uint32_t rl = i / ne;
+            out[atomicAdd(&hist[cached ? (uint32_t)keys[i] : key(i)], 1u)] = (uint16_t)((rl << 8) | (i - rl * ne));
+        }
+        __syncthreads();  // hist / keys are reused by the next chunk
     }
 }
 
@@ -486,7 +496,7 @@ __global__ __launch_bounds__(BLOCK) void env_order_kernel(RenderArgs A, uint32_t
 // once per sample. Light rays of a chunk go sample-major (neighbouring records towards the same
 // light: coherent). Environment rays are random directions; with A.env_order they are handed
 // out in the direction order env_order_kernel computed for the chunk, so a wave traces similar
-// directions from nearby records. The result slot stays sample-major: tr[s * nrec + r].
+// directions from nearby records. The result slot stays sample-major: tr[s * rec_cap + r].
 __device__ __forceinline__ bool ray_slot(const RenderArgs& A, uint32_t chunk, uint32_t rem, uint32_t nrec, uint32_t& s,
                                          uint32_t& r) {
     const uint32_t cr = A.chunk_rec, lights = cr * (uint32_t)A.num_lights;
@@ -508,7 +518,7 @@ __device__ __forceinline__ bool sec_init(const RenderArgs& A, uint32_t nrec, uin
                                          bool norm = false) {
     uint32_t s, r;
     if (!ray_slot(A, chunk, rem, nrec, s, r)) return false;  // padding id
-    R.slot = s * nrec + r;
+    R.slot = s * A.rec_cap + r;
     const float4 pos = A.rec_pos[r];
     const uint4 meta = A.rec_meta[r];
     R.rec = r;
@@ -664,63 +674,6 @@ __device__ __forceinline__ void sec_finish(const RenderArgs& A, SecRay& R, Ctr& 
     A.tr[R.slot] = expf(-R.tau);
 }
 
-// One BVH node pair of secondary ray R (plus the primitives of leaf children). Returns true when
-// the ray is complete (stack exhausted or optical depth past the cut-off).
-template <int BLOCK, bool S, bool FAST, bool PURE>
-__device__ __forceinline__ bool sec_step(const RenderArgs& A, SecRay& R, int* stack, int& sp, int& node, Ctr& c) {
-    if constexpr (S) c.v[kCtrNodes]++;
-    const float4* np = reinterpret_cast<const float4*>(A.nodes + node);
-    const float4 n0 = np[0], n1 = np[1], n2 = np[2];
-    const int4 nc = reinterpret_cast<const int4*>(A.nodes + node)[3];
-    float lmin, lmax, rmin, rmax;
-    {
-        float tx1 = fmaf(n0.x, R.ix, -R.oxi), tx2 = fmaf(n0.w, R.ix, -R.oxi);
-        float ty1 = fmaf(n0.y, R.iy, -R.oyi), ty2 = fmaf(n1.x, R.iy, -R.oyi);
-        float tz1 = fmaf(n0.z, R.iz, -R.ozi), tz2 = fmaf(n1.y, R.iz, -R.ozi);
-        lmin = fmaxf(fmaxf(fminf(tx1, tx2), fminf(ty1, ty2)), fminf(tz1, tz2));
-        lmax = fminf(fminf(fmaxf(tx1, tx2), fmaxf(ty1, ty2)), fmaxf(tz1, tz2));
-        float ux1 = fmaf(n1.z, R.ix, -R.oxi), ux2 = fmaf(n2.y, R.ix, -R.oxi);
-        float uy1 = fmaf(n1.w, R.iy, -R.oyi), uy2 = fmaf(n2.z, R.iy, -R.oyi);
-        float uz1 = fmaf(n2.x, R.iz, -R.ozi), uz2 = fmaf(n2.w, R.iz, -R.ozi);
-        rmin = fmaxf(fmaxf(fminf(ux1, ux2), fminf(uy1, uy2)), fminf(uz1, uz2));
-        rmax = fminf(fminf(fmaxf(ux1, ux2), fmaxf(uy1, uy2)), fmaxf(uz1, uz2));
-    }
-    const float lim = R.light ? R.lim + kTPad * (1.0f + R.lim) : INFINITY;
-    bool hl = nc.x != 0 && lmax >= fmaxf(lmin, 0.0f) && lmin <= lim;
-    bool hr = nc.y != 0 && rmax >= fmaxf(rmin, 0.0f) && rmin <= lim;
-    const bool ll = hl && ref_is_leaf(nc.x), lr = hr && ref_is_leaf(nc.y);
-    if (ll || lr) {
-        const bool r_first = lr && (!ll || rmin < lmin);
-        sec_leaf<S, FAST, PURE>(A, R, r_first ? nc.y : nc.x, c);
-        if (ll && lr && R.tau < R.cut) sec_leaf<S, FAST, PURE>(A, R, r_first ? nc.x : nc.y, c);
-        if (ll) hl = false;
-        if (lr) hr = false;
-    }
-    bool done = R.tau >= R.cut;
-    if (!done) {
-        if (hl && hr) {
-            int nearer = nc.x, farther = nc.y;
-            if (rmin < lmin) {
-                nearer = nc.y;
-                farther = nc.x;
-            }
-            stack[sp * BLOCK] = farther;
-            ++sp;
-            node = nearer;
-        } else if (hl) {
-            node = nc.x;
-        } else if (hr) {
-            node = nc.y;
-        } else if (sp > 0) {
-            --sp;
-            node = stack[sp * BLOCK];
-        } else {
-            done = true;
-        }
-    }
-    return done;
-}
-
 // ---------------------------------------------------------------------------------------------
 // Stage 2 (default): persistent while-while tracing with postponed leaves.
 //
@@ -787,14 +740,14 @@ struct LeafQueue {
     }
 };
 
-// Traversal-stack entries past the STACK held in LDS spill to this lane's slots of the global
-// overflow buffer (kMaxDepth - STACK entries per lane of the resident grid; rarely touched).
-template <int BLOCK, int STACK, int PER = kMaxDepth>
-__device__ __forceinline__ uint32_t ovf_slot(int sp) {
-    const uint32_t lane_id = blockIdx.x * BLOCK + threadIdx.x;
-    return lane_id * (uint32_t)(PER - STACK) + (uint32_t)(sp - STACK);
+// Traversal-stack entries past the STACK held in LDS spill to the global overflow buffer, laid
+// out [depth - STACK][lane of the resident grid]: the lanes of a wave that are at the same depth
+// share cache lines, and the shallow overflow levels every deep walk touches stay a small, dense,
+// L2-resident region (a per-lane [lane][depth] layout gives every lane its own line per level).
+template <int BLOCK, int STACK>
+__device__ __forceinline__ uint32_t ovf_slot(const RenderArgs& A, int sp) {
+    return (uint32_t)(sp - STACK) * A.stack_ovf_lanes + blockIdx.x * BLOCK + threadIdx.x;
 }
-
 
 // One step of the 4-wide traversal: the four children of HNode4 `node` are tested, sorted near to
 // far (misses last); leaf children go to the leaf queue in that order, the nearest inner child
@@ -855,7 +808,7 @@ __device__ __forceinline__ void sec_node4(const RenderArgs& A, SecRay& R, int* s
     for (int i = 3; i >= 0; --i) {
         if (kr[i] > 0 && i != first) {
             if (sp < STACK) stack[sp * BLOCK] = kr[i];
-            else A.stack_ovf[ovf_slot<BLOCK, STACK, kWideStackMax>(sp)] = kr[i];
+            else A.stack_ovf[ovf_slot<BLOCK, STACK>(A, sp)] = kr[i];
             ++sp;
         }
     }
@@ -863,7 +816,7 @@ __device__ __forceinline__ void sec_node4(const RenderArgs& A, SecRay& R, int* s
         node = next;
     } else if (sp > 0) {
         --sp;
-        node = sp < STACK ? stack[sp * BLOCK] : A.stack_ovf[ovf_slot<BLOCK, STACK, kWideStackMax>(sp)];
+        node = sp < STACK ? stack[sp * BLOCK] : A.stack_ovf[ovf_slot<BLOCK, STACK>(A, sp)];
     } else {
         node = -1;
     }
@@ -907,14 +860,14 @@ __device__ __forceinline__ void sec_node(const RenderArgs& A, SecRay& R, int* st
     const bool il = hl & !ll, ir = hr & !lr;
     if (il & ir) {
         if (sp < STACK) stack[sp * BLOCK] = far_ref;
-        else A.stack_ovf[ovf_slot<BLOCK, STACK>(sp)] = far_ref;
+        else A.stack_ovf[ovf_slot<BLOCK, STACK>(A, sp)] = far_ref;
         ++sp;
     }
     if (il | ir) {
         node = (il & ir) ? near_ref : (il ? nc.x : nc.y);
     } else if (sp > 0) {
         --sp;
-        node = sp < STACK ? stack[sp * BLOCK] : A.stack_ovf[ovf_slot<BLOCK, STACK>(sp)];
+        node = sp < STACK ? stack[sp * BLOCK] : A.stack_ovf[ovf_slot<BLOCK, STACK>(A, sp)];
     } else {
         node = -1;
     }
@@ -926,9 +879,10 @@ __device__ __forceinline__ void sec_node(const RenderArgs& A, SecRay& R, int* st
 // of the record test this list first — most of them become opaque right there, without touching
 // the tree — and the tree walk that follows skips exactly these members (same q, bit for bit).
 template <int BLOCK, bool H, bool W = false>
-__global__ __launch_bounds__(BLOCK) void record_list_kernel(RenderArgs A, uint32_t nrec) {
+__global__ __launch_bounds__(BLOCK) void record_list_kernel(RenderArgs A) {
     __shared__ int s_stack[kStackSize * BLOCK];
     int* stack = s_stack + threadIdx.x;
+    const uint32_t nrec = dev_nrec(A);
     for (uint32_t r = blockIdx.x * BLOCK + threadIdx.x; r < nrec; r += gridDim.x * BLOCK) {
         const float4 pos = A.rec_pos[r];
         float bx = pos.x, by = pos.y, bz = pos.z;  // the point in the node boxes' coordinates
@@ -1069,26 +1023,16 @@ __device__ __forceinline__ void list_advance(LeafQueue& Q, int& node) {
     }
 }
 
-// Shader clock read ordered after the values a, b exist (diagnostics only: the compiler would
-// otherwise move a plain clock read across the arithmetic it is meant to time).
-__device__ __forceinline__ uint64_t clock_after(float a, int b) {
-    uint64_t t;
-    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t) : "v"(a), "v"(b) : "memory");
-    return t;
-}
+// Scheduling constants of the persistent kernel (tuned on C4): refill once this many
+// lanes are idle (amortises sec_init), and up to this many NODE / PRIM steps per lane per iteration
+// (amortises the per-iteration ballots and decisions).
+constexpr int kRefillMin = 24, kNodeSteps = 6, kPrimSteps = 6;
 
-// P = true (diagnostics, VR_WW_PROF=1 on the instrumented run): lane 0 of every wave accumulates
-// into the secondary counter slots: [0] NODE iterations, [1] PRIM iterations, [2] lanes in NODE
-// iterations, [3] lanes in PRIM iterations, [4] live lanes, [5] lanes whose NODE step waits for
-// leaf-queue room, [6] lanes that could take either step, [7] iterations with a refill (sums over
-// iterations). VR_WW_PROF=2: [4] NODE, [5] PRIM, [6] refill + finish shader-clock cycles instead.
 // 6 waves/SIMD = 80 VGPRs: the ray state is kept small enough for that without scratch spills (a
 // spilling 6-wave build measured 9 % slower than 5 waves; this one is 5 % faster than 5 waves).
-template <int BLOCK, int STACK, bool S, bool PURE, int WAVES = 6, bool P = false, int QCAP = 2, bool H = false,
-          bool W = false>
-__global__ __launch_bounds__(BLOCK, WAVES) void secondary_ww_kernel(RenderArgs A, uint32_t nrec, uint32_t nchunks,
-                                                                    int refill_min, int prim_bias, int prof_clock, int node_steps,
-                                                                    int prim_steps) {
+// S = true is the instrumented build (vr_count_work): the same schedule, counting its own work.
+template <int BLOCK, int STACK, bool S, bool PURE, int WAVES, int QCAP, bool H, bool W>
+__global__ __launch_bounds__(BLOCK, WAVES) void secondary_ww_kernel(RenderArgs A) {
     __shared__ int s_stack[(STACK + kQueueLds<QCAP>) * BLOCK];
     int* stack = s_stack + threadIdx.x;
     const uint32_t lane = threadIdx.x & 63u;
@@ -1102,14 +1046,11 @@ __global__ __launch_bounds__(BLOCK, WAVES) void secondary_ww_kernel(RenderArgs A
     uint32_t chunk = 0, pool = 0, pool_end = 0;
     bool counter_done = false;  // wave-uniform: the global chunk counter has passed nchunks
     const uint32_t per = A.chunk_rec * (uint32_t)(A.num_lights + A.env_samples);
-    uint64_t pc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    uint64_t tA = 0, tB = 0;
+    const uint32_t nrec = dev_nrec(A), nchunks = (nrec + A.chunk_rec - 1u) >> A.chunk_shift;
+    counter_done = nchunks == 0u;
     for (;;) {
-        if constexpr (P)
-            if (prof_clock) tA = clock_after(R.tau, node);
         const uint64_t idle = __ballot(!live);
-        if (__popcll(idle) >= refill_min) {
-            if constexpr (P) pc[7]++;  // refill once enough lanes are idle (amortises sec_init)
+        if (__popcll(idle) >= kRefillMin) {  // refill once enough lanes are idle (amortises sec_init)
             if (pool == pool_end && !counter_done) {  // next record chunk (all samples of its records)
                 uint32_t cnext = 0;
                 if (lane == 0) cnext = (uint32_t)atomicAdd(A.ray_next, 1ull);
@@ -1139,25 +1080,15 @@ __global__ __launch_bounds__(BLOCK, WAVES) void secondary_ww_kernel(RenderArgs A
             if (counter_done && pool == pool_end) break;
             continue;
         }
-        if constexpr (P) {
-            if (prof_clock) {
-                tB = clock_after(R.tau, node + (int)t + (int)live);
-                pc[6] += tB - tA;
-            } else {
-                pc[4] += (uint64_t)__popcll(__ballot(live));
-                pc[5] += (uint64_t)__popcll(__ballot(live && node >= 0 && Q.n > 0));
-                pc[6] += (uint64_t)__popcll(__ballot(live && node >= 0 && Q.n == 0 && Q.has_prim()));
-            }
-        }
         const bool has_prim = live && Q.has_prim();
         constexpr int kRoom = W ? 4 : 2;  // leaves one NODE step can queue
         const bool can_node = live && node >= 0 && (QCAP == 2 ? Q.n == 0 : Q.n <= QCAP - kRoom);
         const int np = __popcll(__ballot(has_prim)), nn = __popcll(__ballot(can_node));
         // whichever kind more lanes can use; never a kind no lane can use (that would not progress)
-        const bool prim_iter = nn == 0 || (np > 0 && np + prim_bias >= nn);
-        if (prim_iter) {  // PRIM iteration: up to `prim_steps` primitive tests per lane
+        const bool prim_iter = nn == 0 || (np > 0 && np >= nn);
+        if (prim_iter) {  // PRIM iteration: up to kPrimSteps primitive tests per lane
             bool go = has_prim;
-            for (int k = 0; k < prim_steps; ++k) {
+            for (int k = 0; k < kPrimSteps; ++k) {
                 if (go) {
                     const bool from_list = node <= kNodeListCentral;
                     const uint32_t j = from_list ? (uint32_t)A.rec_list[Q.j++] : Q.next<QCAP, BLOCK>(stack + STACK * BLOCK);
@@ -1179,9 +1110,9 @@ __global__ __launch_bounds__(BLOCK, WAVES) void secondary_ww_kernel(RenderArgs A
                 }
                 go = go && Q.has_prim() && R.tau < R.cut;
             }
-        } else {  // NODE iteration: up to `node_steps` child-pair steps per lane
+        } else {  // NODE iteration: up to kNodeSteps node steps per lane
             bool go = can_node;
-            for (int k = 0; k < node_steps; ++k) {
+            for (int k = 0; k < kNodeSteps; ++k) {
                 if (go) {
                     if constexpr (W) sec_node4<BLOCK, S, QCAP, STACK>(A, R, stack, sp, node, Q, c);
                     else sec_node<BLOCK, S, QCAP, STACK, H>(A, R, stack, sp, node, Q, c);
@@ -1189,65 +1120,25 @@ __global__ __launch_bounds__(BLOCK, WAVES) void secondary_ww_kernel(RenderArgs A
                 go = go && node >= 0 && Q.n <= QCAP - kRoom;
             }
         }
-        if constexpr (P) {
-            pc[prim_iter ? 1 : 0]++;
-            pc[prim_iter ? 3 : 2] += (uint64_t)(prim_iter ? np : nn);
-            if (prof_clock) {
-                const uint64_t tC = clock_after(R.tau, node + sp + Q.n + (int)Q.j);
-                pc[prim_iter ? 5 : 4] += tC - tB;
-                tA = tC;
-            }
-        }
         if (live && (R.tau >= R.cut || (node == -1 && !Q.has_prim()))) {
             sec_finish<S, true, PURE>(A, R, c);
             live = false;
         }
-        if constexpr (P)
-            if (prof_clock) pc[6] += clock_after(R.tau, (int)live) - tA;
     }
     if constexpr (S) flush_counters(A.work + kNumCtr, c);
-    if constexpr (P)
-        if (lane == 0)
-            for (int i = 0; i < 8; ++i) atomicAdd(A.work + kNumCtr + i, (unsigned long long)pc[i]);
 }
-
-// One ray per lane, grid-stride over ray ids [t_begin, t_end) (light rays: already coherent —
-// neighbouring lanes trace from neighbouring pixels towards the same light).
-template <int BLOCK, bool S, bool FAST, bool PURE>
-__global__ __launch_bounds__(BLOCK) void secondary_simple_kernel(RenderArgs A, uint32_t nrec, uint64_t t_begin,
-                                                                 uint64_t t_end) {
-    __shared__ int s_stack[kStackSize * BLOCK];
-    int* stack = s_stack + threadIdx.x;
-    Ctr c{};
-    const uint64_t stride_t = (uint64_t)gridDim.x * BLOCK;
-    for (uint64_t t = t_begin + (uint64_t)blockIdx.x * BLOCK + threadIdx.x; t < t_end; t += stride_t) {
-        SecRay R;
-        if constexpr (S) c.v[kCtrSecRays]++;
-        const uint32_t per = A.chunk_rec * (uint32_t)(A.num_lights + A.env_samples);
-        const uint32_t ch = (uint32_t)t / per;
-        if (!sec_init(A, nrec, ch, (uint32_t)t - ch * per, R)) continue;
-        int sp = 0, node = 0;
-        while (!sec_step<BLOCK, S, FAST, PURE>(A, R, stack, sp, node, c)) {
-        }
-        sec_finish<S, FAST, PURE>(A, R, c);
-    }
-    if constexpr (S)
-        for (int i = 0; i < kNumCtr; ++i)
-            if (c.v[i]) atomicAdd(A.work + kNumCtr + i, (unsigned long long)c.v[i]);
-}
-
 
 // Exact three-pass light transmittance for the queued rays (see light_transmittance).
 template <int BLOCK, bool S>
-__global__ __launch_bounds__(BLOCK) void secondary_slow_kernel(RenderArgs A, uint32_t nrec) {
+__global__ __launch_bounds__(BLOCK) void secondary_slow_kernel(RenderArgs A) {
     __shared__ int s_stack[kStackSize * BLOCK];
     int* stack = s_stack + threadIdx.x;
     const uint32_t n = min(A.slowq[0], A.slowq_cap);
     Ctr c{};
     for (uint32_t q = blockIdx.x * BLOCK + threadIdx.x; q < n; q += gridDim.x * BLOCK) {
-        const uint64_t t = A.slowq[1 + q];  // result slot s * nrec + r
-        const uint32_t s = (uint32_t)(t / nrec);
-        const uint32_t r = (uint32_t)(t - (uint64_t)s * nrec);
+        const uint64_t t = A.slowq[1 + q];  // result slot s * rec_cap + r
+        const uint32_t s = (uint32_t)(t / A.rec_cap);
+        const uint32_t r = (uint32_t)(t - (uint64_t)s * A.rec_cap);
         const float4 pos = A.rec_pos[r];
         const uint4 meta = A.rec_meta[r];
         ActList act{A.rec_act + meta.z, 1, (int)meta.w, A.rec_bloom[r]};
@@ -1296,7 +1187,7 @@ __global__ __launch_bounds__(256) void record_cut_kernel(RenderArgs A, float bud
         A.rec_cut[r] = fminf(kTauCut, fmaxf(0.0f, logf(1.001f * record_weight(A, A.rec_pos[r]) * rays / budget)));
 }
 
-__global__ __launch_bounds__(256) void accumulate_kernel(RenderArgs A, uint32_t nrec) {
+__global__ __launch_bounds__(256) void accumulate_kernel(RenderArgs A) {
     const uint32_t tile_local = blockIdx.x;
     const int tid = threadIdx.x;
     const uint32_t p = tile_local * 256u + (uint32_t)tid;
@@ -1316,7 +1207,7 @@ __global__ __launch_bounds__(256) void accumulate_kernel(RenderArgs A, uint32_t 
             const LightRecord& lr = A.lights[l];
             float dx = lr.px - pos.x, dy = lr.py - pos.y, dz = lr.pz - pos.z;
             float dist = sqrtf(dot3(dx, dy, dz, dx, dy, dz));
-            float Tr = A.tr[(size_t)l * nrec + r];
+            float Tr = A.tr[(size_t)l * A.rec_cap + r];
             float d2 = dist * dist;
             Li0 += __fdiv_rn(Tr * lr.ix, d2);
             Li1 += __fdiv_rn(Tr * lr.iy, d2);
@@ -1324,7 +1215,7 @@ __global__ __launch_bounds__(256) void accumulate_kernel(RenderArgs A, uint32_t 
         }
         float Le0 = 0.0f, Le1 = 0.0f, Le2 = 0.0f;
         for (int e = 0; e < A.env_samples; ++e) {
-            float Tr = A.tr[(size_t)(A.num_lights + e) * nrec + r];
+            float Tr = A.tr[(size_t)(A.num_lights + e) * A.rec_cap + r];
             Le0 += Tr * A.env[0];
             Le1 += Tr * A.env[1];
             Le2 += Tr * A.env[2];
@@ -1356,8 +1247,7 @@ static hipError_t march_pass(const RenderArgs& A, hipStream_t stream) {
     // 24-entry stack; the 16-slot active list overflows to the 64-slot fallback kernel. H: the
     // half-precision node copy (boxes only propose candidates; every decision is the exact quadratic).
     const bool shallow = A.bvh_depth <= kShallowStack + 1;
-    static const bool pair_march = getenv("VR_MARCH_PAIR") && getenv("VR_MARCH_PAIR")[0] == '1';  // A/B
-    if (H && A.hnodes4 != nullptr && !pair_march)  // 4-wide tree; a query that could overflow the stack goes to the fallback
+    if (H && A.hnodes4 != nullptr)  // 4-wide tree; a query that could overflow the stack goes to the fallback
         hipLaunchKernelGGL((dev::march_kernel<kActFast, kBlockFast, S, kShallowStack, true, true>), dim3(A.num_tiles),
                            dim3(kBlockFast), 0, stream, A);
     else if (shallow)
@@ -1374,133 +1264,79 @@ static hipError_t march_pass(const RenderArgs& A, hipStream_t stream) {
 }
 
 hipError_t gauss_march(const RenderArgs& A, hipStream_t stream, bool stats) {
-    static const bool f32_march = getenv("VR_MARCH_F32") && getenv("VR_MARCH_F32")[0] == '1';  // A/B
-    if (A.hnodes != nullptr && !f32_march) return stats ? march_pass<true, true>(A, stream) : march_pass<false, true>(A, stream);
+    if (A.hnodes != nullptr) return stats ? march_pass<true, true>(A, stream) : march_pass<false, true>(A, stream);
     return stats ? march_pass<true, false>(A, stream) : march_pass<false, false>(A, stream);
 }
 
 // One launch of the persistent kernel: one resident grid (every CU filled to the kernel's occupancy).
-template <int STACK, bool S, bool PURE, bool P, int QCAP, int WAVES = 6, bool H = false, bool W = false>
-static hipError_t ww_launch(const RenderArgs& A, uint32_t nrec, uint64_t total, uint32_t nchunks, hipStream_t stream,
-                            int refill_min,
-                            int prim_bias, int prof_clock) {
-    static const int node_steps = getenv("VR_WW_NK") ? atoi(getenv("VR_WW_NK")) : 6;
-    static const int prim_steps = getenv("VR_WW_PK") ? atoi(getenv("VR_WW_PK")) : 6;
-    constexpr int kWaves = PURE ? 5 : WAVES;  // PureRayMarching's marched depth does not fit 80 VGPRs without spills
-    const void* fn = (const void*)dev::secondary_ww_kernel<kBlockSecondary, STACK, S, PURE, kWaves, P, QCAP, H, W>;
+// LDS words per lane: 18 traversal-stack entries (deeper ones overflow to global memory) + the
+// 8-entry LDS ring of the 9-entry leaf queue = 26 (6 blocks of 256 lanes per CU).
+template <bool S, bool PURE, bool H, bool W>
+static hipError_t ww_launch(const RenderArgs& A, hipStream_t stream) {
+    constexpr int kStack = 18, kQueue = 9;
+    constexpr int kWaves = PURE ? 5 : 6;  // PureRayMarching's marched depth does not fit 80 VGPRs without spills
+    const void* fn = (const void*)dev::secondary_ww_kernel<kBlockSecondary, kStack, S, PURE, kWaves, kQueue, H, W>;
     int dv = 0, cus = 0, per_cu = 0;
     if (hipGetDevice(&dv) != hipSuccess) return hipErrorUnknown;
     if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dv) != hipSuccess) return hipErrorUnknown;
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, kBlockSecondary, 0) != hipSuccess || per_cu < 1)
         per_cu = 1;
     uint64_t grid = (uint64_t)cus * (uint64_t)per_cu;
-    const uint64_t need = (total + kBlockSecondary - 1) / kBlockSecondary;
-    if (grid > need) grid = need;
     if (grid * kBlockSecondary > A.stack_ovf_lanes) grid = A.stack_ovf_lanes / kBlockSecondary;  // overflow slots
     if (grid == 0) return hipErrorInvalidValue;
-    hipLaunchKernelGGL((dev::secondary_ww_kernel<kBlockSecondary, STACK, S, PURE, kWaves, P, QCAP, H, W>), dim3((unsigned)grid),
-                       dim3(kBlockSecondary), 0, stream, A, nrec, nchunks, refill_min, prim_bias, prof_clock,
-                       node_steps < 1 ? 1 : node_steps, prim_steps < 1 ? 1 : prim_steps);
+    hipError_t e = hipMemsetAsync(A.ray_next, 0, sizeof(unsigned long long), stream);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL((dev::secondary_ww_kernel<kBlockSecondary, kStack, S, PURE, kWaves, kQueue, H, W>), dim3((unsigned)grid),
+                       dim3(kBlockSecondary), 0, stream, A);
     return hipGetLastError();
 }
 
-template <bool S, bool FAST, bool PURE>
-static hipError_t secondary_launch(const RenderArgs& A, uint32_t nrec, uint64_t total, uint32_t nchunks, hipStream_t stream,
-                                   int variant) {
-    if (variant == 2) {  // persistent while-while kernel (default)
-        static const int refill_min = getenv("VR_WW_REFILL") ? atoi(getenv("VR_WW_REFILL")) : 24;
-        static const int prim_bias = getenv("VR_WW_BIAS") ? atoi(getenv("VR_WW_BIAS")) : 0;
-        const int rmin = refill_min < 1 ? 1 : (refill_min > 64 ? 64 : refill_min);
-        hipError_t e = hipMemsetAsync(A.ray_next, 0, sizeof(unsigned long long), stream);
-        if (e != hipSuccess) return e;
-        static const int prof = getenv("VR_WW_PROF") ? atoi(getenv("VR_WW_PROF")) : 0;
-        static const bool waves7 = getenv("VR_WW_WAVES") && atoi(getenv("VR_WW_WAVES")) == 7;
-        // LDS words per lane: 18 traversal-stack entries (deeper ones overflow to global memory) +
-        // the 8-entry LDS ring of the 9-entry leaf queue = 26 (6 blocks of 256 lanes per CU).
-        const bool half = A.hnodes != nullptr;
-        if (S && prof)  // diagnostics in place of the work counts (S selects the counting run)
-            e = half ? ww_launch<18, false, PURE, true, 9, 6, true, true>(A, nrec, total, nchunks, stream, rmin, prim_bias,
-                                                                          prof == 2)
-                     : ww_launch<18, false, PURE, true, 9, 6, false>(A, nrec, total, nchunks, stream, rmin, prim_bias, prof == 2);
-        else if (half && A.hnodes4 != nullptr && waves7)  // EXPERIMENT
-            e = ww_launch<14, S, PURE, false, 9, 7, true, true>(A, nrec, total, nchunks, stream, rmin, prim_bias, 0);
-        else if (half && A.hnodes4 != nullptr)
-            e = ww_launch<18, S, PURE, false, 9, 6, true, true>(A, nrec, total, nchunks, stream, rmin, prim_bias, 0);
-        else if (half)
-            e = ww_launch<18, S, PURE, false, 9, 6, true>(A, nrec, total, nchunks, stream, rmin, prim_bias, 0);
-        else
-            e = ww_launch<18, S, PURE, false, 9, 6, false>(A, nrec, total, nchunks, stream, rmin, prim_bias, 0);
-        if (e != hipSuccess) return e;
-    } else {  // one ray per thread
-        uint64_t blocks = (total + kBlockSecondary - 1) / kBlockSecondary;
-        if (blocks > 65536ull * 16ull) blocks = 65536ull * 16ull;
-        hipLaunchKernelGGL((dev::secondary_simple_kernel<kBlockSecondary, S, FAST, PURE>), dim3((unsigned)blocks),
-                           dim3(kBlockSecondary), 0, stream, A, nrec, (uint64_t)0, total);
-    }
-    hipError_t e = hipGetLastError();
+template <bool S, bool PURE>
+static hipError_t secondary_launch(const RenderArgs& A, hipStream_t stream) {
+    hipError_t e;
+    if (A.hnodes != nullptr && A.hnodes4 != nullptr)  // 4-wide half-precision tree
+        e = ww_launch<S, PURE, true, true>(A, stream);
+    else if (A.hnodes != nullptr)
+        e = ww_launch<S, PURE, true, false>(A, stream);
+    else  // f32 child-pair tree (scenes whose leaf boxes are too small for f16 boxes)
+        e = ww_launch<S, PURE, false, false>(A, stream);
     if (e != hipSuccess) return e;
     if (!PURE) {  // PureRayMarching has no first-event-past-the-light quirk, hence no slow path
-        hipLaunchKernelGGL((dev::secondary_slow_kernel<64, S>), dim3(512), dim3(64), 0, stream, A, nrec);
+        hipLaunchKernelGGL((dev::secondary_slow_kernel<64, S>), dim3(512), dim3(64), 0, stream, A);
         e = hipGetLastError();
     }
     return e;
 }
 
-hipError_t gauss_lists(const RenderArgs& A, uint32_t nrec, hipStream_t stream) {
-    if (!A.list_ok || nrec == 0) return hipSuccess;
-    uint64_t lb = ((uint64_t)nrec + kBlockSecondary - 1) / kBlockSecondary;
-    if (lb > 65536ull * 4ull) lb = 65536ull * 4ull;
-    static const bool pair_lists = getenv("VR_LISTS_PAIR") && getenv("VR_LISTS_PAIR")[0] == '1';  // A/B
-    if (A.hnodes4 != nullptr && !pair_lists)
-        hipLaunchKernelGGL((dev::record_list_kernel<kBlockSecondary, true, true>), dim3((unsigned)lb), dim3(kBlockSecondary),
-                           0, stream, A, nrec);
+// Grid for a per-record kernel over at most rec_cap records (the live count is read on the device).
+static unsigned record_grid(const RenderArgs& A, uint32_t per_block, unsigned max_blocks) {
+    const uint64_t b = ((uint64_t)A.rec_cap + per_block - 1) / per_block;
+    return (unsigned)std::max<uint64_t>(1, std::min<uint64_t>(b, max_blocks));
+}
+
+hipError_t gauss_lists(const RenderArgs& A, hipStream_t stream) {
+    if (!A.list_ok) return hipSuccess;
+    const unsigned lb = record_grid(A, kBlockSecondary, 8192);
+    if (A.hnodes4 != nullptr)
+        hipLaunchKernelGGL((dev::record_list_kernel<kBlockSecondary, true, true>), dim3(lb), dim3(kBlockSecondary), 0, stream, A);
     else if (A.hnodes != nullptr)
-        hipLaunchKernelGGL((dev::record_list_kernel<kBlockSecondary, true>), dim3((unsigned)lb), dim3(kBlockSecondary), 0,
-                           stream, A, nrec);
+        hipLaunchKernelGGL((dev::record_list_kernel<kBlockSecondary, true>), dim3(lb), dim3(kBlockSecondary), 0, stream, A);
     else
-        hipLaunchKernelGGL((dev::record_list_kernel<kBlockSecondary, false>), dim3((unsigned)lb), dim3(kBlockSecondary), 0,
-                           stream, A, nrec);
+        hipLaunchKernelGGL((dev::record_list_kernel<kBlockSecondary, false>), dim3(lb), dim3(kBlockSecondary), 0, stream, A);
     return hipGetLastError();
 }
 
-hipError_t gauss_secondary(const RenderArgs& A, uint32_t nrec, hipStream_t stream, bool stats) {
-    // padded ray-id space of the record-chunk schedule (see ray_slot)
-    const uint64_t cr = A.chunk_rec;
-    const uint64_t nchunks = ((uint64_t)nrec + cr - 1) / cr;
-    const uint64_t total = nchunks * cr * (uint64_t)(A.num_lights + A.env_samples);
-    if (total == 0) return hipSuccess;
-    if (total >= 0xffffffffull) return hipErrorInvalidValue;
+hipError_t gauss_secondary(const RenderArgs& A, hipStream_t stream, bool stats) {
+    if (A.num_lights + A.env_samples == 0) return hipSuccess;
     if (A.env_order != nullptr) {
-        hipLaunchKernelGGL(dev::env_order_kernel<256>, dim3((unsigned)nchunks), dim3(256), 0, stream, A, nrec);
+        hipLaunchKernelGGL(dev::env_order_kernel<256>, dim3(record_grid(A, A.chunk_rec, 4096)), dim3(256), 0, stream, A);
         hipError_t e = hipGetLastError();
         if (e != hipSuccess) return e;
     }
-    // A/B switches (read once): VR_SECONDARY=s one ray per thread, =p refill-only persistent kernel; VR_SEC_EXACT=1 correctly rounded
-    // secondary-ray arithmetic (the fast form is the default).
-    static const int variant = [] {  // 2: while-while persistent (default), 0: one ray per thread
-        const char* v = getenv("VR_SECONDARY");
-        return (v && v[0] == 's') ? 0 : 2;
-    }();
-    static const bool exact = [] {
-        const char* v = getenv("VR_SEC_EXACT");
-        return v && v[0] == '1';
-    }();
-    // The instrumented (work-counting) run uses the one-ray-per-thread kernel: its counts are the
-    // canonical, non-speculative work of a near-first BVH traversal per secondary ray, which is
-    // what the roofline's algorithmic flops are defined on (the persistent kernel's postponed
-    // leaves make it do a little more, speculatively).
-    // VR_WW_COUNT=1: instrument the persistent kernel itself instead (diagnostics; list-member
-    // tests are then counted in the kCtrMu slot).
-    static const bool ww_count = getenv("VR_WW_COUNT") && getenv("VR_WW_COUNT")[0] == '1';
-    const int v = stats ? (ww_count ? 2 : 0) : variant;
-    if (A.pure) {
-        if (stats) return secondary_launch<true, true, true>(A, nrec, total, (uint32_t)nchunks, stream, v);
-        return secondary_launch<false, true, true>(A, nrec, total, (uint32_t)nchunks, stream, v);
-    }
-    if (stats) return exact ? secondary_launch<true, false, false>(A, nrec, total, (uint32_t)nchunks, stream, v)
-                            : secondary_launch<true, true, false>(A, nrec, total, (uint32_t)nchunks, stream, v);
-    return exact ? secondary_launch<false, false, false>(A, nrec, total, (uint32_t)nchunks, stream, v)
-                 : secondary_launch<false, true, false>(A, nrec, total, (uint32_t)nchunks, stream, v);
+    // stats: the instrumented build of the same persistent kernel (vr_count_work), which counts
+    // the work this schedule really does (node steps, list and leaf primitive tests, optical depths)
+    if (A.pure) return stats ? secondary_launch<true, true>(A, stream) : secondary_launch<false, true>(A, stream);
+    return stats ? secondary_launch<true, false>(A, stream) : secondary_launch<false, false>(A, stream);
 }
 
 hipError_t gauss_record_cut(const RenderArgs& A, float budget, hipStream_t stream) {
@@ -1509,8 +1345,8 @@ hipError_t gauss_record_cut(const RenderArgs& A, float budget, hipStream_t strea
     return hipGetLastError();
 }
 
-hipError_t gauss_accumulate(const RenderArgs& A, uint32_t nrec, hipStream_t stream) {
-    hipLaunchKernelGGL(dev::accumulate_kernel, dim3(A.num_tiles), dim3(256), 0, stream, A, nrec);
+hipError_t gauss_accumulate(const RenderArgs& A, hipStream_t stream) {
+    hipLaunchKernelGGL(dev::accumulate_kernel, dim3(A.num_tiles), dim3(256), 0, stream, A);
     return hipGetLastError();
 }
 

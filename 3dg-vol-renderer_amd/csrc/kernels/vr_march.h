@@ -223,6 +223,17 @@ struct PCG32 {
         return (shifted >> rot) | (shifted << ((-rot + 1u) & 31));
     }
     __device__ __forceinline__ float uniform() { return (float)(next_u32() >> 8) * (1.0f / 16777216.0f); }
+    // Textbook PCG32 output ((-rot) & 31) of the same state sequence: the deterministic stand-in
+    // for the reference's unbiased mt19937 environment sampler (integrator.h:13-28). rng.h:43's
+    // (-rot + 1) & 31 ORs overlapping halves whenever rot <= 1, biasing uniform() upwards; the
+    // free-flight integrators keep it (that is the reference's own PCG32), the env sampler does not.
+    __device__ __forceinline__ float uniform_env() {
+        uint64_t old = state;
+        state = old * 6364136223846793005ULL + inc;
+        uint32_t shifted = (uint32_t)(((old >> 18u) ^ old) >> 27u);
+        uint32_t rot = (uint32_t)(old >> 59u);
+        return (float)(((shifted >> rot) | (shifted << ((0u - rot) & 31))) >> 8) * (1.0f / 16777216.0f);
+    }
 };
 __device__ __forceinline__ uint64_t derive_path_seed(int x, int y, int si) {
     uint64_t seed = ((uint64_t)(uint32_t)si << 32) | ((uint64_t)(uint32_t)y << 16) | (uint64_t)(uint32_t)x;

@@ -138,8 +138,8 @@ __device__ void march_spheres(const RenderArgs& A, int px, int py, float& R0, fl
             float Le0 = 0.0f, Le1 = 0.0f, Le2 = 0.0f;
             PCG32 rng(derive_path_seed(px, py, k), 1);
             for (int s = 0; s < A.env_samples; ++s) {
-                float xi1 = rng.uniform();
-                float xi2 = rng.uniform();
+                float xi1 = rng.uniform_env();
+                float xi2 = rng.uniform_env();
                 float wx, wy, wz;
                 env_dir(xi1, xi2, wx, wy, wz);
                 Ray er = make_ray(px_, py_, pz_, wx, wy, wz);

@@ -117,8 +117,8 @@ struct RenderArgs {
     float step_size;
     int32_t env_samples;
     float t_eps;
-    float tau_cut;
-    int32_t pure;         // PureRayMarching: marched (point-sampled) transmittance, integrator.h:100-267        // secondary rays: Tr := 0 once the optical depth reaches this (see vr_device.cpp)
+    float tau_cut;        // secondary rays: Tr := 0 once the optical depth reaches this (see vr_device.cpp)
+    int32_t pure;         // PureRayMarching: marched (point-sampled) transmittance, integrator.h:100-267
     const float* tsteps;  // iterated float step sequence t_k (test_integrators.h:184,289)
     int32_t num_tsteps;
     // fallback queue (active-set overflow) and error counters
@@ -169,15 +169,13 @@ struct RenderArgs {
     int32_t* ff_gid;         // scratch [hit_cap][threads]
     int32_t* ff_act;         // scratch [act_cap][threads]
     unsigned long long* ff_next;  // persistent path kernel: next unclaimed path of the launch
-    unsigned long long ff_total;
-    int32_t ff_refill;            // per-lane path refill kernel (A/B: VR_FF_REFILL)  // paths of the launch (tiles of the chunk x samples x 256)
+    unsigned long long ff_total;  // paths of the launch (tiles of the chunk x samples x 256)
     float* ff_cache;         // scratch [7][act_cap][threads]: per active entry P, B, 2A, den, F, F_next, t1
     float* ff_path;          // [threads][3] path radiance of the step
     float* ff_sum;           // [tile-local pixel][3] running sum over sample batches
     const uint32_t* gauss_order;  // record (leaf order) -> scene index
     uint32_t* rec_bits;      // RECORD_PIXEL_GAUSSIANS bitset [word][pixel] (nullptr: not recording)
     uint32_t rec_npix;       // W * H
-    float* ff_dbg;           // debug (VR_FF_DEBUG): per path of the step, 8 floats of its first bounce
     const unsigned long long* pcg_jump;  // [2k] = A^k, [2k+1] = inc (A^(k-1) + ... + 1): PCG32 state after k draws
 };
 

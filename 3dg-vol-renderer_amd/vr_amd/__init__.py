@@ -328,12 +328,29 @@ class Device:
         check(lib().vr_get_stats(self._h, ctypes.byref(s)))
         return {"kernel_ms": s.kernel_ms, "pixels": s.pixels, "fallback_pixels": s.fallback_pixels,
                 "error_pixels": s.error_pixels, "stage_ms": dict(zip(self.STAGES, list(s.stage_ms))),
-                "scatter_records": s.scatter_records, "secondary_rays": s.secondary_rays}
+                "scatter_records": s.scatter_records, "secondary_rays": s.secondary_rays,
+                "record_overflow": bool(s.record_overflow)}
+
+    OPTIONS = {"half_nodes": L.VR_OPT_HALF_NODES, "secondary_budget": L.VR_OPT_SECONDARY_BUDGET,
+               "ff_window0": L.VR_OPT_FF_WINDOW0}
+
+    def set_option(self, name, value):
+        """vr_set_option (include/vr_hip.h): explicit per-context tuning (half_nodes applies at the
+        next upload, so the scene is re-uploaded)."""
+        check(lib().vr_set_option(self._h, self.OPTIONS[name], int(value)))
+        if name == "half_nodes":
+            self._scene_key = None
+
+    def get_option(self, name):
+        v = ctypes.c_int64()
+        check(lib().vr_get_option(self._h, self.OPTIONS[name], ctypes.byref(v)))
+        return int(v.value)
 
     # vr_render_stats.stage_ms (include/vr_hip.h)
     STAGES = ("march", "sizing", "lists", "secondary", "accumulate")
 
     def synchronize(self):
+        """Waits for the device; raises VRError(VR_ERR_OVERFLOW) if the last frame is invalid."""
         check(lib().vr_synchronize(self._h))
 
     def render_tiles_device(self, camera, params, width, height, first_tile, tile_stride, num_tiles, packed,
@@ -342,26 +359,24 @@ class Device:
                                            height, first_tile, tile_stride, num_tiles, int(packed),
                                            ctypes.c_void_p(out_ptr), ctypes.c_void_p(stream_ptr)))
 
-    # Algorithmic FP32 work per counted operation (SURVEY.md §8(d) accounting; sqrt, div, exp and
-    # erf counted at 4 flops each = quarter-rate transcendental model). See DESIGN.md §Roofline.
-    FLOP_WEIGHTS = {"node_pair_tests": 44, "gaussian_tests": 72, "optical_depths": 98, "densities": 34}
-    WORK_NAMES = ("node_pair_tests", "gaussian_tests", "optical_depths", "densities", "secondary_rays",
-                  "active_steps", "primary_queries", "pixels")
+    # Work counters of the instrumented build (include/vr_hip.h vr_count_work), per stage.
+    WORK_NAMES = {
+        "march": ("node_tests", "gaussian_tests", "optical_depths", "densities", "unused", "active_steps",
+                  "primary_queries", "pixels"),
+        # secondary stage = the persistent kernel's own schedule (+ the exact slow path)
+        "secondary": ("node_tests", "gaussian_tests", "optical_depths", "list_tests", "secondary_rays",
+                      "cut_rays", "cut_ray_node_steps", "full_ray_node_steps"),
+    }
 
     def count_work(self, camera, params, width, height, first_tile=0, tile_stride=1, num_tiles=None):
-        """Instrumented (untimed) render of the given tiles; returns counts + algorithmic flops."""
+        """Instrumented (untimed) render of the given tiles; returns the raw counts per stage."""
         if num_tiles is None:
             num_tiles = len(range(first_tile, num_tiles_of(width, height), tile_stride))
         arr = (ctypes.c_uint64 * 16)()
         check(lib().vr_count_work(self._h, ctypes.byref(camera.struct), ctypes.byref(params), width, height,
                                   first_tile, tile_stride, num_tiles, arr))
-        out = {}
-        for s, stage in enumerate(("march", "secondary")):
-            d = {k: int(arr[8 * s + i]) for i, k in enumerate(self.WORK_NAMES)}
-            d["flops"] = float(sum(self.FLOP_WEIGHTS[k] * d[k] for k in self.FLOP_WEIGHTS))
-            out[stage] = d
-        out["flops"] = out["march"]["flops"] + out["secondary"]["flops"]
-        return out
+        return {stage: {k: int(arr[8 * s + i]) for i, k in enumerate(self.WORK_NAMES[stage])}
+                for s, stage in enumerate(("march", "secondary"))}
 
     def unshuffle_tiles_device(self, slabs_ptr, nslabs, tiles_per_slab, width, height, image_ptr, stream_ptr=0):
         check(lib().vr_unshuffle_tiles_device(self._h, ctypes.c_void_p(slabs_ptr), nslabs, tiles_per_slab, width,

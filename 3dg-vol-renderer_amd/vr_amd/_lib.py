@@ -18,6 +18,7 @@ VR_VOLUME_GAUSSIANS, VR_VOLUME_SPHERES = 0, 1
 VR_CAMERA_PINHOLE, VR_CAMERA_ORTHOGRAPHIC = 0, 1
 VR_RAYMARCH_GAUSSIANS, VR_RAYMARCH_SPHERES, VR_TEST_HITMASK, VR_PURE_RAYMARCH = 0, 1, 2, 3
 VR_FREE_FLIGHT, VR_MULTI_SCATTER = 4, 5
+VR_OPT_HALF_NODES, VR_OPT_SECONDARY_BUDGET, VR_OPT_FF_WINDOW0 = 1, 2, 3  # vr_option
 
 f3 = ctypes.c_float * 3
 
@@ -55,7 +56,8 @@ class vr_scene_info(ctypes.Structure):
 class vr_render_stats(ctypes.Structure):
     _fields_ = [("kernel_ms", ctypes.c_double), ("pixels", ctypes.c_int64), ("fallback_pixels", ctypes.c_int64),
                 ("error_pixels", ctypes.c_int64), ("stage_ms", ctypes.c_double * 5),
-                ("scatter_records", ctypes.c_int64), ("secondary_rays", ctypes.c_int64)]
+                ("scatter_records", ctypes.c_int64), ("secondary_rays", ctypes.c_int64),
+                ("record_overflow", ctypes.c_int64)]
 
 
 # name -> (restype, argtypes). Every symbol declared in include/vr_hip.h.
@@ -107,6 +109,8 @@ SIGNATURES = {
     "vr_sfd_loss_diff": (ST, [P, ctypes.POINTER(ctypes.c_float), ctypes.POINTER(ctypes.c_float), ctypes.c_uint32,
                               ctypes.c_uint32, ctypes.POINTER(ctypes.c_double), ctypes.c_size_t]),
     "vr_num_tiles": (ctypes.c_uint32, [ctypes.c_uint32, ctypes.c_uint32]),
+    "vr_set_option": (ST, [P, ctypes.c_int32, ctypes.c_int64]),
+    "vr_get_option": (ST, [P, ctypes.c_int32, ctypes.POINTER(ctypes.c_int64)]),
     "vr_synchronize": (ST, [P]),
     "vr_get_stats": (ST, [P, ctypes.POINTER(vr_render_stats)]),
 }

@@ -49,12 +49,28 @@ def unshuffle_reference(slabs, W, H):
 
 def render_local(dev, camera, params, W, H, rank, world, slab, frame, stream_ptr):
     """This rank's share of one frame (device buffers are torch tensors). World 1 renders straight
-    into `frame`; otherwise the rank's interleaved tiles go into its packed `slab`."""
+    into `frame`; otherwise the rank's interleaved tiles go into its packed `slab`. Asynchronous on
+    the stream; the frame's outcome is checked by `finish_local`."""
     first, stride, count, per = rank_tiles(W, H, rank, world)
     if world == 1:
         dev.render_tiles_device(camera, params, W, H, 0, 1, count, False, frame.data_ptr(), stream_ptr)
     else:
         dev.render_tiles_device(camera, params, W, H, first, stride, count, True, slab.data_ptr(), stream_ptr)
+
+
+def finish_local(dev, camera, params, W, H, rank, world, slab, frame, stream_ptr, retries=2):
+    """Waits for this rank's share and surfaces its outcome (vr_synchronize): a share that outgrew
+    the record buffers sized from earlier frames is rendered again (they have been grown); pixels
+    over every per-ray capacity raise VRError (VR_ERR_OVERFLOW), never a silent NaN frame."""
+    from . import _lib as L
+    for attempt in range(retries + 1):
+        try:
+            dev.synchronize()
+            return
+        except L.VRError as e:
+            if attempt == retries or "render it again" not in str(e):
+                raise
+        render_local(dev, camera, params, W, H, rank, world, slab, frame, stream_ptr)
 
 
 def gather_frame(dev, W, H, rank, world, slab, slabs, frame, stream_ptr, dist, via_host=False):

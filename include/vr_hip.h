@@ -23,7 +23,7 @@
 extern "C" {
 #endif
 
-#define VR_ABI_VERSION 2
+#define VR_ABI_VERSION 3
 
 typedef enum vr_status {
     VR_OK = 0,
@@ -111,7 +111,7 @@ typedef struct vr_scene_info {
     float bounds_max[3];
 } vr_scene_info;
 
-/* Statistics of the last vr_render / vr_render_tiles_device call on a context. */
+/* Statistics of the last vr_render / vr_render_tiles_device call on a context (waits for it). */
 typedef struct vr_render_stats {
     double kernel_ms;         /* device time of the render kernels (HIP events) */
     int64_t pixels;           /* pixels rendered */
@@ -124,6 +124,9 @@ typedef struct vr_render_stats {
     double stage_ms[5];
     int64_t scatter_records;  /* march steps with sigma_s > 0 (each spawns lights + env_samples rays) */
     int64_t secondary_rays;   /* records * (lights + env_samples) */
+    int64_t record_overflow;  /* 1: the frame outgrew the scatter-record buffers sized from earlier
+                                 frames (its output is invalid; the buffers have been grown, render
+                                 again). vr_render does that itself. */
 } vr_render_stats;
 
 typedef struct vr_scene vr_scene; /* host-side scene: primitives, lights, env colour */
@@ -188,7 +191,11 @@ vr_status vr_upload_scene(vr_ctx* ctx, const vr_scene* s);
  * idx = 3*(y*W + x) as image.h:13-17). Synchronous. */
 vr_status vr_render(vr_ctx* ctx, const vr_camera* cam, const vr_render_params* p, uint32_t width,
                     uint32_t height, float* rgb_host);
-/* Multi-GPU building block (asynchronous on `stream`, a hipStream_t or NULL for the default).
+/* Multi-GPU building block (asynchronous on `stream`, a hipStream_t or NULL for the default; the
+ * host never waits for the device inside a frame once the context has rendered one frame of this
+ * kind — the first sizes the scatter-record buffers). The frame's outcome is reported by
+ * vr_synchronize (VR_ERR_OVERFLOW if pixels exceeded a per-ray capacity or the frame outgrew the
+ * record buffers, which are then grown: render it again) and by vr_get_stats.
  * The frame is cut into 16x16 tiles numbered row-major; this call renders tiles
  * first_tile, first_tile + tile_stride, ... (num_tiles of them). If `packed` is non-zero the
  * output is a slab of num_tiles * 256 pixels (tile-major, row-major inside a tile, 3 floats per
@@ -203,13 +210,16 @@ vr_status vr_render_tiles_device(vr_ctx* ctx, const vr_camera* cam, const vr_ren
 vr_status vr_unshuffle_tiles_device(vr_ctx* ctx, const float* d_slabs, uint32_t nslabs,
                                     uint32_t tiles_per_slab, uint32_t width, uint32_t height,
                                     float* d_image, void* stream);
-/* Diagnostics (untimed): render the given tiles once with the instrumented kernel build and return
- * the algorithmic work it executed, per stage: counts[0..7] the march kernels (both passes),
- * counts[8..15] the secondary-ray kernels. Within a stage: [0] BVH node-pair tests,
- * [1] ray-Gaussian quadratic + intersect evaluations, [2] optical-depth evaluations, [3] density
- * (mu_t) evaluations, [4] secondary (light + environment) rays, [5] active march steps,
- * [6] primary-ray BVH queries, [7] pixels completed. Synchronous; RayMarchingGaussians only. Used
- * for the roofline report. */
+/* Diagnostics (untimed): render the given tiles once with the instrumented build of the same
+ * kernels and return the work they executed. counts[0..7], the march kernels (both passes):
+ * [0] BVH node tests (4-wide nodes, or child pairs on the fallback path), [1] ray-Gaussian
+ * quadratic + intersect evaluations, [2] optical-depth evaluations, [3] density (mu_t)
+ * evaluations, [4] unused, [5] active march steps, [6] primary-ray BVH queries, [7] pixels completed.
+ * counts[8..15], the secondary-ray stage (the persistent kernel's own schedule + the exact slow path):
+ * [8] BVH node steps, [9] tree-leaf primitive tests, [10] optical-depth evaluations, [11] neighbour-
+ * list primitive tests, [12] secondary rays started, [13] rays ended by the optical-depth cut-off,
+ * [14] node steps of those rays, [15] node steps of the rays that ran to the end of the tree.
+ * Synchronous; RayMarchingGaussians / PureRayMarching only. Used for the roofline report. */
 vr_status vr_count_work(vr_ctx* ctx, const vr_camera* cam, const vr_render_params* p, uint32_t width,
                         uint32_t height, uint32_t first_tile, uint32_t tile_stride, uint32_t num_tiles,
                         uint64_t counts[16]);
@@ -231,6 +241,23 @@ vr_status vr_sfd_loss_diff(vr_ctx* ctx, const float* loss_base, const float* los
                            uint32_t height, double* out, size_t n);
 /* Number of 16x16 tiles of a W x H frame. */
 uint32_t vr_num_tiles(uint32_t width, uint32_t height);
+/* Per-context tuning options (defaults are the benchmark/product settings). Explicit and
+ * re-entrant: the library reads no environment variables. */
+typedef enum vr_option {
+    VR_OPT_HALF_NODES = 1,       /* 1 (default): upload f16 copies of the BVH (pair + 4-wide) when the
+                                    scene's leaf boxes suit them; 0: f32 nodes only. Applies at the next
+                                    vr_upload_scene. Results are identical either way (boxes only
+                                    propose candidates; every decision is the exact quadratic). */
+    VR_OPT_SECONDARY_BUDGET = 2, /* 1 (default): with t_eps > 0, stop secondary rays at a per-record
+                                    optical depth that keeps each pixel within t_eps (DESIGN.md error
+                                    budget); 0: the frame-wide cut-off ln(1/t_eps) + ln(1000) only. */
+    VR_OPT_FF_WINDOW0 = 3        /* free-flight integrators: first hit-window capacity, 1..128 (default
+                                    8; doubles per window). Results do not depend on it. */
+} vr_option;
+vr_status vr_set_option(vr_ctx* ctx, int32_t option, int64_t value);
+vr_status vr_get_option(vr_ctx* ctx, int32_t option, int64_t* value);
+/* Waits for the context's device work; returns VR_ERR_OVERFLOW if the last frame is invalid (see
+ * vr_render_tiles_device). */
 vr_status vr_synchronize(vr_ctx* ctx);
 vr_status vr_get_stats(vr_ctx* ctx, vr_render_stats* out);
 

@@ -31,6 +31,7 @@
 #include <fstream>
 #include <limits>
 #include <numbers>
+#include <random>
 #include <sstream>
 #include <stdexcept>
 #include <string>
@@ -116,6 +117,12 @@ static inline uint64_t splitmix64(uint64_t x) {
     x = (x ^ (x >> 27)) * 0x94d049bb133111ebULL;
     return x ^ (x >> 31);
 }
+// rng.h:43 rotates with (-rot + 1u) & 31, not PCG's (-rot) & 31: whenever rot is 0 or 1 the two
+// shifted halves overlap and are OR-ed, so outputs are biased upwards (mean of uniform() ~0.503,
+// E[-log(1 - u)] ~1.08 instead of 1). The oracle keeps that (it is the reference's behaviour);
+// g_pcg_textbook = true (test switch, orc_set_pcg_textbook) selects textbook PCG32 instead, which is
+// how the free-flight goldens in tests/renders were evidently rendered (tests/test_oracle_freeflight.py).
+static bool g_pcg_textbook = false;
 struct PCG32 {
     uint64_t state, inc;
     PCG32(uint64_t seed_state, uint64_t seed_seq) {
@@ -130,9 +137,18 @@ struct PCG32 {
         state = old * 6364136223846793005ULL + inc;
         uint32_t shifted = (uint32_t)(((old >> 18u) ^ old) >> 27u);
         uint32_t rot = (uint32_t)(old >> 59u);
-        return (shifted >> rot) | (shifted << ((-rot + 1u) & 31));
+        return (shifted >> rot) | (shifted << ((-rot + (g_pcg_textbook ? 0u : 1u)) & 31));
     }
     float uniform() { return (next_u32() >> 8) * (1.0f / 16777216.0f); }
+    // Textbook PCG32 output of the same state sequence: the deterministic stand-in for the
+    // reference's mt19937 environment sampler (integrator.h:13-28), which draws unbiased uniforms.
+    float uniform_env() {
+        uint64_t old = state;
+        state = old * 6364136223846793005ULL + inc;
+        uint32_t shifted = (uint32_t)(((old >> 18u) ^ old) >> 27u);
+        uint32_t rot = (uint32_t)(old >> 59u);
+        return (((shifted >> rot) | (shifted << ((-rot) & 31))) >> 8) * (1.0f / 16777216.0f);
+    }
 };
 static inline uint64_t derive_path_seed(int x, int y, int sample_index) {
     uint64_t seed = (uint64_t(sample_index) << 32) | (uint64_t(y) << 16) | (uint64_t(x));
@@ -623,8 +639,8 @@ static V3 rm_gaussians_pixel(const Scene& scene, const Camera& cam, int x, int y
             V3 Le{0, 0, 0};
             PCG32 rng(derive_path_seed(x, y, k), 1);
             for (int si = 0; si < env_samples; ++si) {
-                float xi1 = rng.uniform();
-                float xi2 = rng.uniform();
+                float xi1 = rng.uniform_env();
+                float xi2 = rng.uniform_env();
                 V3 wi = env_dir(xi1, xi2);
                 Ray env_ray(pos, wi);
                 std::vector<PrimitiveHitEvent> env_ev;
@@ -731,8 +747,8 @@ static V3 rm_pure_pixel(const Scene& scene, const Camera& cam, int x, int y, int
             V3 Le{0, 0, 0};
             PCG32 rng(derive_path_seed(x, y, k), 1);
             for (int s = 0; s < env_samples; ++s) {
-                float xi1 = rng.uniform();
-                float xi2 = rng.uniform();
+                float xi1 = rng.uniform_env();
+                float xi2 = rng.uniform_env();
                 Ray env_ray(pos, env_dir(xi1, xi2));
                 std::vector<PrimitiveHitEvent> env_events;
                 gmm.intersect_events(env_ray, env_events);
@@ -860,8 +876,8 @@ static V3 rm_gaussians_pixel_lists(const Scene& scene, const Camera& cam, int x,
             V3 Le{0, 0, 0};
             PCG32 rng(derive_path_seed(x, y, k), 1);
             for (int si = 0; si < env_samples; ++si) {
-                float xi1 = rng.uniform();
-                float xi2 = rng.uniform();
+                float xi1 = rng.uniform_env();
+                float xi2 = rng.uniform_env();
                 Ray env_ray(pos, env_dir(xi1, xi2));
                 std::vector<PrimitiveHitEvent> env_ev;
                 gmm.intersect_events(env_ray, env_ev);
@@ -925,8 +941,8 @@ static V3 rm_spheres_pixel(const Scene& scene, const Camera& cam, int i, int j, 
             V3 Le_env{0, 0, 0};
             PCG32 rng(derive_path_seed(i, j, k), 1);
             for (int s = 0; s < env_samples; ++s) {
-                float xi1 = rng.uniform();
-                float xi2 = rng.uniform();
+                float xi1 = rng.uniform_env();
+                float xi2 = rng.uniform_env();
                 V3 wi = env_dir(xi1, xi2);
                 Ray shadow(pos, wi);
                 std::vector<PrimitiveHitEvent> shadow_ev;
@@ -1062,14 +1078,26 @@ static float solve_distance_newton_raphson(const Ray& ray, float ta, float tb, c
     return solve_distance_bisection(ray, ta, tb, act, target_tau, gmm);
 }
 
-// distance_solvers.h:150-187, ANALYTIC_PLUS_NEWTON (the compiled-in mode, :146).
+// distance_solvers.h:150-187. The reference selects the solver at compile time (:143-147);
+// ANALYTIC_PLUS_NEWTON is the compiled-in mode (:146) and the default here. g_solver picks the
+// others for the goldens rendered with them (tests/renders/250_rand_{bisection,newton,uniform}_big).
+enum { kSolverAnalyticNewton = 0, kSolverBisection = 1, kSolverNewton = 2, kSolverAnalyticBisection = 3, kSolverUniform = 4 };
+static int g_solver = kSolverAnalyticNewton;
 static float solve_distance(const Ray& ray, float ta, float tb, const std::vector<size_t>& act, float remaining_tau,
                             const GMM& gmm) {
+    if (g_solver == kSolverUniform) {  // :132-137: rand01() is mt19937(random_device) (rng.h:6-10); seeded here
+        static thread_local std::mt19937 gen(12345u);
+        float u = std::uniform_real_distribution<float>(0.0f, 1.0f)(gen);
+        return ta + u * (tb - ta);
+    }
+    if (g_solver == kSolverBisection) return solve_distance_bisection(ray, ta, tb, act, remaining_tau, gmm);
+    if (g_solver == kSolverNewton) return solve_distance_newton_raphson(ray, ta, tb, act, remaining_tau, gmm);
     if (act.size() == 1) {
         float t_analytic = 0.0f;
         if (solve_for_t_given_tau(gmm.gaussians[act[0]], ray, ta, tb, remaining_tau, t_analytic))
             return std::clamp(t_analytic, ta, tb);
     }
+    if (g_solver == kSolverAnalyticBisection) return solve_distance_bisection(ray, ta, tb, act, remaining_tau, gmm);
     return solve_distance_newton_raphson(ray, ta, tb, act, remaining_tau, gmm);
 }
 
@@ -1449,7 +1477,7 @@ void orc_debug_secondary(void* sp, const float* pos, const float* vd, float fov,
             }
             PCG32 rng(derive_path_seed(x, y, k), 1);
             for (int si = 0; si < env_samples; ++si) {
-                float xi1 = rng.uniform(), xi2 = rng.uniform();
+                float xi1 = rng.uniform_env(), xi2 = rng.uniform_env();
                 Ray er(p, env_dir(xi1, xi2));
                 std::vector<PrimitiveHitEvent> eev;
                 gmm.intersect_events(er, eev);
@@ -1520,6 +1548,10 @@ int orc_render(void* sp, int cam_type, const float* pos, const float* vd, float 
 }
 
 void orc_ff_debug(float* buf) { g_ff_dbg = buf; }
+// distance solver of the free-flight integrators (see solve_distance); returns the previous one
+int orc_set_solver(int mode) { int o = g_solver; g_solver = mode; return o; }
+// PCG32 output rotation: 0 = the reference's rng.h:43 (default), 1 = textbook PCG32 (see PCG32)
+int orc_set_pcg_textbook(int on) { int o = g_pcg_textbook; g_pcg_textbook = on != 0; return o; }
 
 // MultiScatterGaussians::render with RECORD_PIXEL_GAUSSIANS (integrator.h:532-536, 616-644): the
 // frame into out[3*W*H] and the per-pixel Gaussian sets into bits[(g >> 5) * W*H + p] (bit g & 31).

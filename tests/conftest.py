@@ -17,3 +17,20 @@ RENDERS = os.path.join(GOLDEN, "renders")
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X (runs through libvr_hip.so on the device)")
     config.addinivalue_line("markers", "slow: longer CPU oracle runs")
+
+
+@pytest.fixture
+def device_options():
+    """Set vr_set_option values on the cuda:0 context for one test; restored afterwards."""
+    import vr_amd as vr
+    dev = vr.Device.get(0)
+    saved = {}
+
+    def set_opt(name, value):
+        if name not in saved:
+            saved[name] = dev.get_option(name)
+        dev.set_option(name, value)
+
+    yield set_opt
+    for name, value in saved.items():
+        dev.set_option(name, value)

@@ -155,10 +155,10 @@ def test_overlap_beyond_capacity_fails_loudly():
 
 
 @pytest.mark.parametrize("cap0", ["1", "128"])
-def test_window_capacity_does_not_change_results(cap0, monkeypatch):
+def test_window_capacity_does_not_change_results(cap0, device_options):
     # first-window capacity 1 (a window per event) vs 128 (one window): the event sweep must be the
     # reference's either way
-    monkeypatch.setenv("VR_FF_CAP0", cap0)
+    device_options("ff_window0", int(cap0))
     path = scene_path("50_random.txt")
     g = _gpu(vr.Scene.load_GMM(path), 32, 32, True, 4)
     r = O.render_ff(O.OracleScene.load_gmm(path), O.PINHOLE, CAM_POS, main_view_dir(), FOV, 32, 32, multi=True,

@@ -239,13 +239,13 @@ def test_render_is_bitwise_deterministic():
 
 
 @pytest.mark.parametrize("name", ["50_random.txt", "1000_random.txt"])
-def test_half_precision_nodes_match_f32_nodes(name, monkeypatch):
+def test_half_precision_nodes_match_f32_nodes(name, device_options):
     """The secondary kernel's 32-B half-precision BVH nodes (boxes rounded outward in scene-
     normalised coordinates) visit a superset of the f32 tree's boxes: the same Gaussians are hit,
-    so the frames agree up to summation order. VR_NO_HALF_NODES is read at every scene upload."""
+    so the frames agree up to summation order (VR_OPT_HALF_NODES applies at the next upload)."""
     path = scene_path(name)
     a, _ = _render_gpu_gmm(path, 96, 96)
-    monkeypatch.setenv("VR_NO_HALF_NODES", "1")
+    device_options("half_nodes", 0)
     b, _ = _render_gpu_gmm(path, 96, 96)
     assert float(np.max(np.abs(a - b))) < 2e-6
 
@@ -374,7 +374,7 @@ def test_full_size_benchmark_settings_match_exact_oracle(W, H, n, npix):
 
 
 @pytest.mark.parametrize("name,W", [("1000_random.txt", 192), ("many_gaussians.txt", 96)])
-def test_secondary_cut_off_stays_within_its_pixel_budget(name, W, monkeypatch):
+def test_secondary_cut_off_stays_within_its_pixel_budget(name, W, device_options):
     """With t_eps > 0 each pixel's secondary rays stop at cut = ln(W_p / t_eps) (W_p: the pixel's
     radiance if every Tr were 1), which bounds the frame change the cut can cause by t_eps per
     pixel. Compare against the same render with only the frame-wide cut-off."""
@@ -382,7 +382,7 @@ def test_secondary_cut_off_stays_within_its_pixel_budget(name, W, monkeypatch):
     cam = vr.Pinhole_Camera(CAM_POS, main_view_dir(), FOV)
     a, b = vr.Image(W, W), vr.Image(W, W)
     vr.RayMarchingGaussians(cam, t_eps=1e-6).render(vr.Scene.load_GMM(path), a)
-    monkeypatch.setenv("VR_NO_REC_CUT", "1")
+    device_options("secondary_budget", 0)
     vr.RayMarchingGaussians(cam, t_eps=1e-6).render(vr.Scene.load_GMM(path), b)
     d = float(np.max(np.abs(a.pixels.astype(np.float64) - b.pixels)))
     print(f"{name}: max |cut - no cut| = {d:.3e}")

@@ -28,16 +28,28 @@ def _sample_pixels(W, H, n, seed=0):
     ("many_gaussians.txt", "7_gaussian_ref.ppm", 0.35, 20),
     ("1_gaussian.txt", "baseline_1.ppm", 0.35, 20),
     ("50_random.txt", "50_rand_baseline.ppm", 1.2, 20),
+    ("250_random.txt", "250_rand_baseline.ppm", 1.5, 20),
+    ("2_gaussian_x70", "baseline_2.ppm", 0.2, 20),
+    ("2_gaussian_x70", "2_gaussian_ref.ppm", 0.2, 20),
 ])
-def test_raymarch_gaussians_matches_reference_render(scene, golden, mean_tol, env_samples):
+def test_raymarch_gaussians_matches_reference_render(tmp_path, scene, golden, mean_tol, env_samples):
     """RayMarchingGaussians restatement vs the reference's own 512x512 renders (tests/main.cpp camera).
     Statistical: mean |diff| over a 6000-pixel sample within MC noise (0.15 / 0.15 /
-    1.05 per 255 with independent restatements), no systematic bias."""
+    1.05 per 255 with independent restatements), no systematic bias. baseline_2 / 2_gaussian_ref
+    were rendered with 2_gaussian.txt's light at intensity 70 (the file was edited afterwards,
+    SURVEY §4); measured here: mean |diff| 0.094, signed -0.025."""
     g = read_ppm(f"{RENDERS}/{golden}")
     W = H = 512
     pix = _sample_pixels(W, H, 6000)
-    s = O.OracleScene.load_gmm(scene_path(scene))
-    out = O.render(s, O.PINHOLE, CAM_POS, main_view_dir(), FOV, W, H, O.RAYMARCH_GAUSSIANS, 0.01, env_samples,
+    if scene == "2_gaussian_x70":
+        p = tmp_path / "2g_x70.txt"
+        p.write_text(open(scene_path("2_gaussian.txt")).read().replace("1.0  1.0  1.0", "70.0  70.0  70.0", 1))
+        s = O.OracleScene.load_gmm(str(p))
+    else:
+        s = O.OracleScene.load_gmm(scene_path(scene))
+    # the sorted-active-list variant: bit-identical to the faithful restatement
+    # (test_sparse_list_baseline_bitwise_equals_faithful) and ~50x faster at 250 Gaussians
+    out = O.render(s, O.PINHOLE, CAM_POS, main_view_dir(), FOV, W, H, O.RAYMARCH_GAUSSIANS_LISTS, 0.01, env_samples,
                    pixels=pix)
     mine = to8(out).astype(int)
     ref = g[pix[:, 1], pix[:, 0]].astype(int)
@@ -49,7 +61,8 @@ def test_raymarch_gaussians_matches_reference_render(scene, golden, mean_tol, en
 
 @pytest.mark.parametrize("golden,scene", [("baseline_1.ppm", "1_gaussian.txt"), ("baseline_7.ppm", "many_gaussians.txt"),
                                           ("7_gaussian_ref.ppm", "many_gaussians.txt"),
-                                          ("50_rand_baseline.ppm", "50_random.txt")])
+                                          ("50_rand_baseline.ppm", "50_random.txt"),
+                                          ("250_rand_baseline.ppm", "250_random.txt")])
 def test_miss_mask_known_answer(golden, scene):
     """Exact KAT: every pixel whose centre ray misses all Gaussians is env colour in the golden, and
     the oracle renders exactly env colour there too (events.empty() -> set_pixel(env),
@@ -67,14 +80,14 @@ def test_miss_mask_known_answer(golden, scene):
         if not hit:
             misses.append((x, y))
     misses = np.asarray(misses, np.int32)
-    assert len(misses) > 100
+    assert len(misses) > 30  # 250_random covers all but ~2 % of the frame
     assert np.all(g[misses[:, 1], misses[:, 0]] == ENV8)
     out = O.render(s, O.PINHOLE, CAM_POS, main_view_dir(), FOV, W, H, pixels=misses, env_samples=2)
     assert np.all(out == np.float32([0.53, 0.81, 0.92]))
 
 
 @pytest.mark.parametrize("scene,W,env", [("many_gaussians.txt", 64, None), ("50_random.txt", 48, None),
-                                         ("1000_random.txt", 32, None), ("2_gaussian.txt", 48, (0.0, 0.0, 0.0))])
+                                         ("1000_random.txt", 20, None), ("2_gaussian.txt", 48, (0.0, 0.0, 0.0))])
 def test_sparse_list_baseline_bitwise_equals_faithful(scene, W, env):
     """The CPU-baseline variant (sorted active lists instead of O(N) masks, stop at T == 0) is the
     same function bit for bit: bench.py times it because the faithful O(N) scans take minutes per
@@ -109,6 +122,31 @@ def test_pcg32_and_path_seed_known_answers():
     assert [int(v) for v in O.pcg32(seed, 1, 4)] == [0xF1B41A15, 0x1C900260, 0xBE464F5E, 0xAB35ED12]
     u = (O.pcg32(seed, 1, 4) >> 8).astype(np.float32) * np.float32(1.0 / 16777216.0)
     np.testing.assert_allclose(u, [0.94415438, 0.11157238, 0.74326032, 0.66879159], rtol=0, atol=1e-7)
+
+
+def test_env_sampler_stream_is_unbiased():
+    """The ray-march environment sampler draws its uniforms with textbook PCG32 output from the
+    (x, y, step) stream (PCG32::uniform_env): unlike rng.h:43's rotation (test_oracle_freeflight.py)
+    it is unbiased, like the reference's mt19937 (integrator.h:13-28)."""
+    n = 20000
+    # textbook output of the stream, computed here from the state recurrence (rng.h:27-44)
+    mask = (1 << 64) - 1
+    vals = []
+    for k in range(n // 8):
+        seed = O.derive_path_seed(17, 5, k)
+        state, inc = 0, 3
+        state = (state * 6364136223846793005 + inc) & mask
+        state = (state + seed) & mask
+        state = (state * 6364136223846793005 + inc) & mask
+        for _ in range(8):
+            old = state
+            state = (old * 6364136223846793005 + inc) & mask
+            sh = (((old >> 18) ^ old) >> 27) & 0xFFFFFFFF
+            rot = old >> 59
+            vals.append((((sh >> rot) | (sh << ((-rot) & 31))) & 0xFFFFFFFF) >> 8)
+    v = np.array(vals, np.float64) / 16777216.0
+    assert abs(v.mean() - 0.5) < 0.006, v.mean()
+    assert abs((-np.log1p(-v)).mean() - 1.0) < 0.025
 
 
 def test_env_direction_sampler_is_uniform_on_sphere():
