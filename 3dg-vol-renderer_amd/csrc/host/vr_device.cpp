@@ -72,6 +72,7 @@ struct vr_ctx {
     bool staged = false;                                            // last launch recorded ev_stage
     bool stats_pending = false;  // h_report of the last frame has not been collected yet
     int64_t last_pixels = 0;
+    uint32_t last_first_tile = 0, last_tile_stride = 1, last_tiles_x = 1, last_w = 0, last_h = 0;  // tile map of the last frame
     uint32_t last_secondary_per_record = 0;
     // wavefront pipeline buffers (grown on demand, never shrunk)
     struct Buf {
@@ -635,6 +636,11 @@ vr_status launch(vr_ctx* c, RenderArgs& A, const vr_render_params* p, hipStream_
     HIP_TRY(hipEventRecord(c->ev_report, s), "hipEventRecord");
     c->stats_pending = true;
     c->last_pixels = (int64_t)A.num_tiles * 256;
+    c->last_first_tile = A.first_tile;
+    c->last_tile_stride = A.tile_stride;
+    c->last_tiles_x = A.tiles_x;
+    c->last_w = A.width;
+    c->last_h = A.height;
     return VR_OK;
 }
 
@@ -976,6 +982,11 @@ vr_status vr_set_option(vr_ctx* c, int32_t option, int64_t value) {
             if (value < 1 || value > kFFHitCap) return fail(VR_ERR_INVALID, "VR_OPT_FF_WINDOW0 must be in [1, 128]");
             c->opt_ff_window0 = value;
             return VR_OK;
+        case VR_OPT_RECORD_CAPACITY:
+            if ((value != 0 && value < 4096) || value > 0x3fffffff)
+                return fail(VR_ERR_INVALID, "VR_OPT_RECORD_CAPACITY must be 0 or in [4096, 2^30)");
+            c->rec_hint = c->ovf_hint = (uint64_t)value;
+            return VR_OK;
         default:
             return fail(VR_ERR_INVALID, "vr_set_option: unknown option " + std::to_string(option));
     }
@@ -987,6 +998,7 @@ vr_status vr_get_option(vr_ctx* c, int32_t option, int64_t* value) {
         case VR_OPT_HALF_NODES: *value = c->opt_half_nodes; return VR_OK;
         case VR_OPT_SECONDARY_BUDGET: *value = c->opt_secondary_budget; return VR_OK;
         case VR_OPT_FF_WINDOW0: *value = c->opt_ff_window0; return VR_OK;
+        case VR_OPT_RECORD_CAPACITY: *value = (int64_t)c->rec_hint; return VR_OK;
         default: return fail(VR_ERR_INVALID, "vr_get_option: unknown option " + std::to_string(option));
     }
 }
@@ -1004,6 +1016,25 @@ vr_status vr_synchronize(vr_ctx* c) {
     if (c->h_report[1] != 0)
         return fail(VR_ERR_OVERFLOW, std::to_string(c->h_report[1]) + " pixels / paths of the last frame exceeded a "
                                      "per-ray capacity (NaN)");
+    return VR_OK;
+}
+
+vr_status vr_get_fallback_pixels(vr_ctx* c, uint32_t* xy, size_t cap, size_t* n) {
+    if (!c || !n || (cap > 0 && !xy)) return fail(VR_ERR_INVALID, "vr_get_fallback_pixels: bad argument");
+    HIP_TRY(hipSetDevice(c->device), "hipSetDevice");
+    vr_status st = collect(c);
+    if (st != VR_OK) return st;
+    const size_t count = std::min<size_t>(c->h_report[0], c->queue_cap);
+    *n = count;
+    if (count == 0 || cap == 0) return VR_OK;
+    std::vector<uint32_t> q(std::min(count, cap));
+    HIP_TRY(hipMemcpy(q.data(), c->d_queue + 1, q.size() * sizeof(uint32_t), hipMemcpyDeviceToHost), "hipMemcpy(queue)");
+    for (size_t i = 0; i < q.size(); ++i) {  // tile_pixel (kernels/vr_dev_common.h): tile-local id << 8 | lane
+        const uint32_t lane = q[i] & 255u, wv = lane >> 6, ln = lane & 63u;
+        const uint32_t tile = c->last_first_tile + (q[i] >> 8) * c->last_tile_stride;
+        xy[2 * i] = (tile % c->last_tiles_x) * kTile + (wv & 1u) * 8u + (ln & 7u);
+        xy[2 * i + 1] = (tile / c->last_tiles_x) * kTile + (wv >> 1) * 8u + (ln >> 3);
+    }
     return VR_OK;
 }
 

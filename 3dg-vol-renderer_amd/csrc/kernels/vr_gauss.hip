@@ -149,6 +149,28 @@ __device__ float light_transmittance(const RenderArgs& A, const Ray& sr, float d
 // ---------------------------------------------------------------------------------------------
 // Stage 1: primary march
 // ---------------------------------------------------------------------------------------------
+// Early-out weight (t_eps > 0). Stopping after step k drops
+//   sum_{j>k} T_j sigma_s,j dt (Li_j + Le_j) / (4 pi) + T_end env
+// and T_j sigma_s,j dt is not bounded by T alone: the reference's point-sampled estimator can
+// weigh a step by sigma_t dt >> 1 inside an opaque blob (C4's blobs carry tau ~ 400 per chord).
+// With every Tr <= 1 a record adds at most T sigma_s dt W per channel, W = max_c (sum_l I_lc /
+// (4 pi d_l^2) + env_c), and for exponentially falling T the tail sums to <= T_{k+1} W (1 +
+// sigma_t,k+1 dt). The ray therefore stops once T (1 + sigma_t,k dt) W <= t_eps: this step's
+// point density stands in for the next one's (one step of look-ahead), so a ray inside a dense
+// blob takes the extra step that drives T to 0 instead of dropping it.
+__device__ __forceinline__ float tail_weight(const RenderArgs& A, float x, float y, float z, float sigma_t) {
+    float w0 = fabsf(A.env[0]), w1 = fabsf(A.env[1]), w2 = fabsf(A.env[2]);
+    for (int l = 0; l < A.num_lights; ++l) {
+        const LightRecord& lr = A.lights[l];
+        const float dx = lr.px - x, dy = lr.py - y, dz = lr.pz - z;
+        const float s = kInv4Pi / (dx * dx + dy * dy + dz * dz);
+        w0 += fabsf(lr.ix) * s;
+        w1 += fabsf(lr.iy) * s;
+        w2 += fabsf(lr.iz) * s;
+    }
+    return fmaxf(fmaxf(w0, w1), w2) * (1.0f + sigma_t * A.step_size);
+}
+
 // One pass: each scattering step allocates its record with a wave-aggregated atomic and links it
 // to the pixel's previous record (px_first / rec_next), so a pixel's records are visited in step
 // order by accumulate_kernel wherever they landed in memory. Records that do not fit the
@@ -296,7 +318,15 @@ __device__ int march(const RenderArgs& A, uint32_t p, int px, int py, int* act_b
                     else A.rec_next[prev] = r;
                     prev = r;
                 } else {
-                    A.rec_alloc[2] = 1u;  // capacity exceeded: the host re-runs the march
+                    A.rec_alloc[2] = 1u;  // capacity exceeded: the frame is reported and rendered again
+                    if (r < A.rec_cap) {  // a slot inside [0, nrec) whose active list did not fit the pool:
+                        // the later stages still read it (the host does not wait for the march), so
+                        // it must be a valid record, not the previous frame's: an empty one
+                        A.rec_pos[r] = make_float4(px_, py_, pz_, 0.0f);
+                        A.rec_meta[r] = make_uint4((uint32_t)px | ((uint32_t)py << 16), (uint32_t)k, 0u, 0u);
+                        A.rec_bloom[r] = 0ull;
+                        A.rec_next[r] = kNoRecord;
+                    }
                 }
             }
             if (A.pure) {  // integrator.h:196-198, 259: T *= exp(-sigma_t * step), sigma_t = sigma_a + sigma_s
@@ -310,7 +340,8 @@ __device__ int march(const RenderArgs& A, uint32_t p, int px, int py, int* act_b
             } else {
                 T *= expf(-tau_seg);
             }
-            if (T <= A.t_eps) break;
+            if (T <= 0.0f) break;  // exact: nothing after this step can add to L or to T * env
+            if (A.t_eps > 0.0f && T * tail_weight(A, px_, py_, pz_, smu) <= A.t_eps) break;
         }
     }
     A.px_T[p] = T;

@@ -331,8 +331,18 @@ class Device:
                 "scatter_records": s.scatter_records, "secondary_rays": s.secondary_rays,
                 "record_overflow": bool(s.record_overflow)}
 
+    def fallback_pixels(self):
+        """(n, 2) int array of the (x, y) pixels of the last ray-march frame that were re-run on the
+        large-capacity fallback path (vr_get_fallback_pixels)."""
+        n = ctypes.c_size_t()
+        check(lib().vr_get_fallback_pixels(self._h, None, 0, ctypes.byref(n)))
+        xy = np.zeros((max(n.value, 1), 2), np.uint32)
+        check(lib().vr_get_fallback_pixels(self._h, xy.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32)), n.value,
+                                           ctypes.byref(n)))
+        return xy[:n.value].astype(np.int32)
+
     OPTIONS = {"half_nodes": L.VR_OPT_HALF_NODES, "secondary_budget": L.VR_OPT_SECONDARY_BUDGET,
-               "ff_window0": L.VR_OPT_FF_WINDOW0}
+               "ff_window0": L.VR_OPT_FF_WINDOW0, "record_capacity": L.VR_OPT_RECORD_CAPACITY}
 
     def set_option(self, name, value):
         """vr_set_option (include/vr_hip.h): explicit per-context tuning (half_nodes applies at the

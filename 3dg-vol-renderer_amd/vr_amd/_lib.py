@@ -18,7 +18,7 @@ VR_VOLUME_GAUSSIANS, VR_VOLUME_SPHERES = 0, 1
 VR_CAMERA_PINHOLE, VR_CAMERA_ORTHOGRAPHIC = 0, 1
 VR_RAYMARCH_GAUSSIANS, VR_RAYMARCH_SPHERES, VR_TEST_HITMASK, VR_PURE_RAYMARCH = 0, 1, 2, 3
 VR_FREE_FLIGHT, VR_MULTI_SCATTER = 4, 5
-VR_OPT_HALF_NODES, VR_OPT_SECONDARY_BUDGET, VR_OPT_FF_WINDOW0 = 1, 2, 3  # vr_option
+VR_OPT_HALF_NODES, VR_OPT_SECONDARY_BUDGET, VR_OPT_FF_WINDOW0, VR_OPT_RECORD_CAPACITY = 1, 2, 3, 4  # vr_option
 
 f3 = ctypes.c_float * 3
 
@@ -113,6 +113,7 @@ SIGNATURES = {
     "vr_get_option": (ST, [P, ctypes.c_int32, ctypes.POINTER(ctypes.c_int64)]),
     "vr_synchronize": (ST, [P]),
     "vr_get_stats": (ST, [P, ctypes.POINTER(vr_render_stats)]),
+    "vr_get_fallback_pixels": (ST, [P, ctypes.POINTER(ctypes.c_uint32), ctypes.c_size_t, ctypes.POINTER(ctypes.c_size_t)]),
 }
 
 _lib = None

@@ -177,7 +177,9 @@ class SFDConfig:
 
 class StochasticFiniteDiffInverseIntegrator:
     """inverse_integrator.h:61-246 — optimize(scene_initial, I_ref) -> bool. `history` holds the
-    mean L1 loss of every base render."""
+    mean L1 loss of every base render, `last_grads` the last SFD gradient estimate (float64),
+    `final_loss` / `final_image` the final render at cfg.final_samples paths/pixel (:229-238;
+    final_samples = 0 skips it)."""
 
     def __init__(self, camera, forward_integrator, cfg=None):
         if not isinstance(forward_integrator, MultiScatterGaussians):
@@ -185,6 +187,9 @@ class StochasticFiniteDiffInverseIntegrator:
         self.camera, self.fwd, self.cfg = camera, forward_integrator, cfg or SFDConfig()
         self.history = []
         self.params = None
+        self.last_grads = None
+        self.final_loss = None
+        self.final_image = None
 
     def optimize(self, scene_initial, I_ref):
         cfg = self.cfg
@@ -218,6 +223,7 @@ class StochasticFiniteDiffInverseIntegrator:
                                              fdiff.ctypes.data_as(_dp), n))
                 grads += np.repeat(fdiff, PER) * s.astype(np.float64) / eps.astype(np.float64)
             grads /= cfg.num_stoch_samples
+            self.last_grads = grads.copy()
             if not adam.step(params, grads.astype(np.float32)):
                 return False
             scene_opt = apply_params(params, lights, env)
@@ -226,6 +232,13 @@ class StochasticFiniteDiffInverseIntegrator:
                 I_base.make_PPM(os.path.join(cfg.out_dir, f"iter_{it:04d}.ppm"))
         self.params = params
         self.scene = scene_opt
+        if cfg.final_samples > 0:  # final save (:229-238): the optimised GMM at final_samples paths/pixel
+            self.fwd.set_num_samples(cfg.final_samples)  # left set, as the reference leaves it
+            self.fwd.render(scene_opt, I_base)
+            self.final_loss = float(compute_pixel_losses(I_base, I_ref).astype(np.float64).mean())
+            self.final_image = I_base
+            if cfg.out_dir:
+                I_base.make_PPM(os.path.join(cfg.out_dir, f"iter_{cfg.max_iters - 1:04d}.ppm"))
         return True
 
 

@@ -136,7 +136,8 @@ def bench_sfd(args, scene, camera, W, H, t_setup):
 
     def one_iter():
         opt = inv.StochasticFiniteDiffInverseIntegrator(camera, vr.MultiScatterGaussians(camera, args.spp),
-                                                        inv.SFDConfig(max_iters=1, num_stoch_samples=4, lr=1e-2))
+                                                        inv.SFDConfig(max_iters=1, num_stoch_samples=4, lr=1e-2,
+                                                                      final_samples=0))
         if not opt.optimize(start, I_ref):
             raise SystemExit("SFD iteration failed")
         return opt

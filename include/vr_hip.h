@@ -251,8 +251,14 @@ typedef enum vr_option {
     VR_OPT_SECONDARY_BUDGET = 2, /* 1 (default): with t_eps > 0, stop secondary rays at a per-record
                                     optical depth that keeps each pixel within t_eps (DESIGN.md error
                                     budget); 0: the frame-wide cut-off ln(1/t_eps) + ln(1000) only. */
-    VR_OPT_FF_WINDOW0 = 3        /* free-flight integrators: first hit-window capacity, 1..128 (default
+    VR_OPT_FF_WINDOW0 = 3,       /* free-flight integrators: first hit-window capacity, 1..128 (default
                                     8; doubles per window). Results do not depend on it. */
+    VR_OPT_RECORD_CAPACITY = 4   /* scatter-record buffer capacity (records; the active-list pool gets the
+                                    same) carried into the next frame: 0 (size it at the next frame, with one
+                                    host sync) or >= 4096. The context normally sizes it
+                                    from earlier frames; setting it lets a test drive a frame over capacity
+                                    (reported, then rendered again with grown buffers). Results do not
+                                    depend on it. */
 } vr_option;
 vr_status vr_set_option(vr_ctx* ctx, int32_t option, int64_t value);
 vr_status vr_get_option(vr_ctx* ctx, int32_t option, int64_t* value);
@@ -260,6 +266,10 @@ vr_status vr_get_option(vr_ctx* ctx, int32_t option, int64_t* value);
  * vr_render_tiles_device). */
 vr_status vr_synchronize(vr_ctx* ctx);
 vr_status vr_get_stats(vr_ctx* ctx, vr_render_stats* out);
+/* Diagnostics: the pixels of the last RayMarchingGaussians / PureRayMarching frame that were re-run
+ * on the large-capacity fallback path (vr_render_stats.fallback_pixels of them). Writes up to `cap`
+ * (x, y) pairs into xy[2*cap] (global frame coordinates, queue order) and the total count into *n. */
+vr_status vr_get_fallback_pixels(vr_ctx* ctx, uint32_t* xy, size_t cap, size_t* n);
 
 #ifdef __cplusplus
 } /* extern "C" */

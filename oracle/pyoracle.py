@@ -67,8 +67,24 @@ def lib():
                                        ctypes.c_int, fp, ctypes.POINTER(ctypes.c_uint32), ctypes.c_int]
     L.orc_render.argtypes = [P, ctypes.c_int, fp, fp, ctypes.c_float, ctypes.c_int, ctypes.c_float,
                              ctypes.c_int, ctypes.c_int, ctypes.c_int, ip, ctypes.c_int64, fp, ctypes.c_int]
+    L.orc_set_stable_ties.argtypes = [ctypes.c_int]
+    L.orc_set_stable_ties.restype = ctypes.c_int
     _lib = L
     return L
+
+
+class stable_ties:
+    """Context manager: the oracle resolves event-sort ties (a ray grazing a 3-sigma ellipsoid with
+    t0 == t1 in float) in emission order instead of the reference's unstable std::sort (see
+    g_stable_ties in vr_oracle.cpp)."""
+
+    def __enter__(self):
+        self._old = lib().orc_set_stable_ties(1)
+        return self
+
+    def __exit__(self, *exc):
+        lib().orc_set_stable_ties(self._old)
+        return False
 
 
 def _f(a):

@@ -123,6 +123,14 @@ static inline uint64_t splitmix64(uint64_t x) {
 // g_pcg_textbook = true (test switch, orc_set_pcg_textbook) selects textbook PCG32 instead, which is
 // how the free-flight goldens in tests/renders were evidently rendered (tests/test_oracle_freeflight.py).
 static bool g_pcg_textbook = false;
+// Event-sort tie order. The reference sorts a ray's events with std::sort on t alone (gmm.h:508-511),
+// which is not stable: when a ray grazes a 3-sigma ellipsoid so closely that both roots round to the
+// same float (t0 == t1), libstdc++'s introsort may put that Gaussian's exit before its entry, and the
+// event loop then leaves it active for the rest of the ray. Which way it falls depends on the whole
+// event array (BVH traversal order, partition pivots), not on the scene geometry. g_stable_ties = true
+// (test switch, orc_set_stable_ties) resolves ties in emission order (entry before exit: the Gaussian
+// is never active), which is the device path's rule; the default is the reference's std::sort.
+static bool g_stable_ties = false;
 struct PCG32 {
     uint64_t state, inc;
     PCG32(uint64_t seed_state, uint64_t seed_seq) {
@@ -442,8 +450,11 @@ struct GMM {
                 }
             }
         }
-        if (!out.empty())
-            std::sort(out.begin(), out.end(), [](const PrimitiveHitEvent& a, const PrimitiveHitEvent& b) { return a.t < b.t; });
+        if (!out.empty()) {
+            auto by_t = [](const PrimitiveHitEvent& a, const PrimitiveHitEvent& b) { return a.t < b.t; };
+            if (g_stable_ties) std::stable_sort(out.begin(), out.end(), by_t);
+            else std::sort(out.begin(), out.end(), by_t);
+        }
     }
     // gmm.h:98-126
     void evaluate_sigma(const std::vector<bool>& active, V3 pos, float& sigma_a, float& sigma_s) const {
@@ -584,6 +595,8 @@ static const float kInv4Pi = (float)(1.0f / (4.0f * std::numbers::pi));  // Vect
 static const float k4Pi = (float)(4.0f * std::numbers::pi);
 
 // test_integrators.h:160-296 — RayMarchingGaussians per pixel.
+// DEBUG trace of one rm_gaussians_pixel call (orc_debug_march): per step (t, #active, sigma_s, T after)
+static thread_local std::vector<float>* g_rm_trace = nullptr;
 static V3 rm_gaussians_pixel(const Scene& scene, const Camera& cam, int x, int y, int W, int H,
                              float step_size, int env_samples) {
     const GMM& gmm = scene.gmm;
@@ -674,6 +687,10 @@ static V3 rm_gaussians_pixel(const Scene& scene, const Camera& cam, int x, int y
             if (active[i]) active_idxs.push_back(i);
         float segmentTr = gmm.transmittance_over_segment(ray, t, t + step_size, active_idxs);
         T *= segmentTr;
+        if (g_rm_trace && !active_idxs.empty()) {
+            g_rm_trace->insert(g_rm_trace->end(), {t, (float)active_idxs.size(), sigma_s, T});
+            for (size_t i : active_idxs) g_rm_trace->push_back((float)i);
+        }
         t += step_size;
         ++k;
     }
@@ -1548,8 +1565,24 @@ int orc_render(void* sp, int cam_type, const float* pos, const float* vd, float 
 }
 
 void orc_ff_debug(float* buf) { g_ff_dbg = buf; }
+// DEBUG: the faithful RayMarchingGaussians march of one pixel; out gets, per step with a non-empty
+// active set, (t, n_active, sigma_s, T after the step, active ids...). Returns the floats written.
+int64_t orc_debug_march(void* sp, const float* pos, const float* vd, float fov, int x, int y, int W, int H,
+                        float step_size, int env_samples, float* L_out, float* out, int64_t cap) {
+    Scene& s = *(Scene*)sp;
+    Camera c = Camera::make_pinhole({pos[0], pos[1], pos[2]}, {vd[0], vd[1], vd[2]}, fov);
+    std::vector<float> tr;
+    g_rm_trace = &tr;
+    V3 L = rm_gaussians_pixel(s, c, x, y, W, H, step_size, env_samples);
+    g_rm_trace = nullptr;
+    L_out[0] = L.x; L_out[1] = L.y; L_out[2] = L.z;
+    for (int64_t i = 0; i < (int64_t)tr.size() && i < cap; ++i) out[i] = tr[i];
+    return (int64_t)tr.size();
+}
 // distance solver of the free-flight integrators (see solve_distance); returns the previous one
 int orc_set_solver(int mode) { int o = g_solver; g_solver = mode; return o; }
+// event-sort tie order: 0 = the reference's std::sort (default), 1 = stable (see g_stable_ties)
+int orc_set_stable_ties(int on) { int o = g_stable_ties; g_stable_ties = on != 0; return o; }
 // PCG32 output rotation: 0 = the reference's rng.h:43 (default), 1 = textbook PCG32 (see PCG32)
 int orc_set_pcg_textbook(int on) { int o = g_pcg_textbook; g_pcg_textbook = on != 0; return o; }
 

@@ -34,3 +34,29 @@ def read_ppm(path):
 
 def to8(img):
     return np.clip(np.asarray(img, np.float32) * np.float32(255.0), 0.0, 255.0).astype(np.uint8)
+
+
+def tie_aware_linf(got, pixels, render, tol):
+    """Per-pixel L-inf of device pixels `got` ((n, 3)) against the oracle `render(pixels)` run with the
+    reference's std::sort event order. A pixel over `tol` is re-rendered with stable tie order
+    (pyoracle.stable_ties): it is tie-dependent only if the two oracle orders disagree there, and is
+    then held to the same bar against the stable order (the device's rule). Returns (max error,
+    number of tie-dependent pixels, number of NaN mismatches, pixels over the bar that are not
+    tie-dependent, the reference-order oracle pixels)."""
+    import pyoracle as O
+    got = np.asarray(got, np.float64)
+    ref = np.asarray(render(pixels), np.float64)
+    nan_mismatch = int(np.sum(np.isnan(got) != np.isnan(ref)))
+    d = np.abs(got - ref)
+    d[np.isnan(got) & np.isnan(ref)] = 0.0
+    d = np.nanmax(d, axis=-1) if d.size else np.zeros(0)
+    bad = np.nonzero(d >= tol)[0]
+    untied = 0
+    if bad.size:
+        with O.stable_ties():
+            ref_s = np.asarray(render(pixels[bad]), np.float64)
+        tie = np.any(ref_s != ref[bad], axis=-1)
+        d_s = np.nanmax(np.abs(got[bad] - ref_s), axis=-1)
+        untied = int(np.sum(~tie | (d_s >= tol)))
+        d[bad] = np.where(tie, d_s, d[bad])
+    return float(d.max()) if d.size else 0.0, int(bad.size - untied), nan_mismatch, untied, ref

@@ -85,6 +85,114 @@ def test_sfd_optimize_runs_and_is_reproducible():
                                                         inv.SFDConfig(max_iters=6, num_stoch_samples=2, lr=0.05, seed=1))
         assert opt.optimize(start, I_ref)
         assert np.all(np.isfinite(opt.history)) and np.all(np.isfinite(opt.params))
+        assert opt.final_loss is not None and np.isfinite(opt.final_loss)  # final save (:229-238)
+        assert opt.fwd.params.num_samples == 16384
         runs.append(opt.params.copy())
     assert np.array_equal(runs[0], runs[1])
     assert not np.array_equal(runs[0], p)
+
+
+# ---- BASELINE config 5: scenes/gaussians/10k_random.txt at 512x512 ------------------------------
+C5_W = 512
+C5_SPP = 4
+
+
+def _oracle_scene(scene):
+    g = scene.gaussians()
+    return O.OracleScene.from_gaussians(g[:, 0:3], g[:, 3:9], g[:, 9], g[:, 10],
+                                        np.array([l.position for l in scene.lights], np.float32),
+                                        np.array([l.intensity for l in scene.lights], np.float32))
+
+
+def _same_sets(bits, obits):
+    return np.all(bits == obits, axis=0)
+
+
+@pytest.mark.timeout(600)
+def test_c5_recording_matches_oracle_full_frame():
+    """MultiScatterGaussians with RECORD_PIXEL_GAUSSIANS on the C5 scene, whole 512x512 frame: the
+    recorded Gaussian set of every pixel and the image against the oracle."""
+    path = scene_path("10k_random.txt")
+    scene = vr.Scene.load_GMM(path)
+    assert scene.get_num_primitives() == 10_000
+    integ = vr.MultiScatterGaussians(_cam(), C5_SPP)
+    img = vr.Image(C5_W, C5_W)
+    integ.record(scene, img, slot=0)
+    bits = integ.pixel_gaussian_bits(0)
+    osc = O.OracleScene.load_gmm(path)
+    res = {}
+    for order in ("reference", "stable"):
+        if order == "stable":
+            with O.stable_ties():  # tangent-hit ties in emission order: the device's rule (see helpers)
+                oimg, obits = O.render_ms_record(osc, O.PINHOLE, CAM_POS, main_view_dir(), FOV, C5_W, C5_W, C5_SPP)
+        else:
+            oimg, obits = O.render_ms_record(osc, O.PINHOLE, CAM_POS, main_view_dir(), FOV, C5_W, C5_W, C5_SPP)
+        same = _same_sets(bits, obits)
+        d = np.abs(img.pixels.astype(np.float64) - oimg).max(axis=-1).reshape(-1)
+        res[order] = (same.mean(), np.mean(d < 1e-4), d.mean())
+        print(f"C5 512x512/10k vs the {order}-order oracle: identical Gaussian sets on {same.mean():.5f} of "
+              f"{same.size} pixels; pixels within 1e-4 {np.mean(d < 1e-4):.5f}, mean |d| {d.mean():.3e}, "
+              f"max {d.max():.3e}")
+    for order in res:  # free-flight paths can part ways on a libm ulp: the bar is statistical
+        assert res[order][0] >= 0.99 and res[order][1] >= 0.99 and res[order][2] < 1e-4
+
+
+@pytest.mark.timeout(900)
+def test_c5_one_sfd_iteration_matches_oracle():
+    """One StochasticFiniteDiffInverseIntegrator iteration (inverse_integrator.h:114-200) on C5: the
+    device loop (recorded renders, vr_sfd_loss_diff) against the same iteration assembled from the
+    oracle's recorded renders, a host union-of-pixels sum and the reference's Adam update
+    (optimizer.h:31-50) — base loss, gradient estimate and updated parameters."""
+    from vr_amd import inverse as inv
+    target = vr.Scene.load_GMM(scene_path("10k_random.txt"))
+    I_ref = vr.Image(C5_W, C5_W)
+    vr.MultiScatterGaussians(_cam(), C5_SPP).render(target, I_ref)
+    p0 = inv.pack_parameters(target.gaussians())
+    p0[9::11] += np.float32(np.log(0.5))  # start from half densities
+    start = inv.apply_params(p0, target.lights, target.env_color)
+    cfg = inv.SFDConfig(max_iters=1, num_stoch_samples=2, lr=1e-2, seed=7, final_samples=0)
+    opt = inv.StochasticFiniteDiffInverseIntegrator(_cam(), vr.MultiScatterGaussians(_cam(), C5_SPP), cfg)
+    assert opt.optimize(start, I_ref)
+
+    # the same iteration from the oracle
+    params = inv.pack_parameters(start.gaussians())
+    eps = inv.make_default_eps_for_params(params)
+    rng = np.random.default_rng(cfg.seed)
+    n = start.get_num_primitives()
+
+    def rec(scene):
+        img, bits = O.render_ms_record(_oracle_scene(scene), O.PINHOLE, CAM_POS, main_view_dir(), FOV, C5_W, C5_W,
+                                       C5_SPP)
+        return np.abs(img.astype(np.float32) - I_ref.pixels).sum(axis=2).reshape(-1).astype(np.float32), bits
+
+    with O.stable_ties():  # the device's tie rule (tangent hits in emission order)
+        lb, b0 = rec(start)
+        grads = np.zeros(params.size, np.float64)
+        for _ in range(cfg.num_stoch_samples):
+            s = np.where(rng.random(params.size) < 0.5, 1.0, -1.0).astype(np.float32)
+            lp, b1 = rec(inv.apply_params((params + s * eps).astype(np.float32), start.lights, start.env_color))
+            u = np.unpackbits((b0 | b1).T.copy().view(np.uint8), axis=1, bitorder="little")[:, :n].astype(bool)
+            fdiff = (u * (lp.astype(np.float64) - lb.astype(np.float64))[:, None]).sum(axis=0)
+            grads += np.repeat(fdiff, inv.PER) * s.astype(np.float64) / eps.astype(np.float64)
+        grads /= cfg.num_stoch_samples
+    # Adam's first step (optimizer.h:31-50): m = (1-b1) g, v = (1-b2) g^2, a = lr sqrt(1-b2) / (1-b1)
+    g = grads.astype(np.float32)
+    m = (np.float32(1) - np.float32(0.9)) * g
+    v = (np.float32(1) - np.float32(0.999)) * g * g
+    a = np.float32(1e-2) * np.sqrt(np.float32(1) - np.float32(0.999)) / (np.float32(1) - np.float32(0.9))
+    p_ref = params - (a * (m / (np.sqrt(v) + np.float32(1e-8)))).astype(np.float32)
+
+    base_rel = abs(opt.history[0] - float(lb.astype(np.float64).mean())) / float(lb.mean())
+    gmax = float(np.abs(grads).max())
+    gerr = float(np.abs(opt.last_grads - grads).max())
+    big = np.abs(grads) > 1e-3 * gmax
+    pdiff = np.abs(opt.params - p_ref)
+    print(f"C5 SFD iteration: base loss rel diff {base_rel:.2e}; grad max|g| {gmax:.3e}, max|dg| {gerr:.3e}; "
+          f"{big.mean():.4f} of parameters with |g| > 1e-3 max; param update identical on "
+          f"{np.mean(pdiff[big] <= 1e-6):.5f} of them")
+    # a few of the 4 x 262144 paths per render part ways on a libm ulp (see the recording test), so the
+    # losses agree to ~1e-3 and the SFD sums to ~1e-2 of the largest gradient, and Adam's first step
+    # (a sign step, |update| = lr) is identical wherever the gradient is not near 0
+    assert base_rel < 5e-3
+    assert gerr <= 2e-2 * gmax
+    assert np.mean(pdiff[big] <= 1e-6) >= 0.999
