@@ -48,7 +48,43 @@ CAM_POS = np.array([0.0, 1.0, 6.0], np.float32)  # tests/main.cpp:21-34
 CAM_VIEW = np.array([0.0, 0.0, -1.0], np.float32)
 FOV = np.float32(0.25 * np.pi)
 HBM_PEAK_GBPS = 8000.0   # MI355X_MICROARCH.md: 8.0 TB/s spec
-FP32_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md: FP32 vector = FP32-input MFMA peak
+FP32_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md: FP32 vector peak
+PMC_SUMMARY = "r02_c4_pmc_summary.json"  # rocprofv3 --pmc passes of this command (profiles/)
+
+# Flops per executed operation of the secondary stage (an FMA counts 2, min / max / compare 1, and
+# sqrt / rcp / div / exp / erf 4, the quarter-rate transcendental model of SURVEY §8(d)):
+#   node4: one step of the 4-wide half-precision walk = 4 children x (6 FMA slab planes = 12, 10 min/max,
+#          3 compares) + the 5 compare-exchanges of the near-to-far sort = 105
+#   prim:  ray-Gaussian quadratic form + 3-sigma intersection (quad_fast + intersect_fast) = 72
+#   od:    closed-form optical depth over an interval (optical_depth_fast: exp + 2 erf + sqrt + rcp) = 98
+FLOP_WEIGHTS = {"node4": 105, "prim": 72, "od": 98}
+ALG_FLOPS_PER_CROSSED = FLOP_WEIGHTS["prim"] + FLOP_WEIGHTS["od"]
+
+
+def secondary_flops(sec):
+    """Flops the persistent secondary kernel executed, from vr_count_work's counters of that kernel."""
+    return (FLOP_WEIGHTS["node4"] * sec["node_tests"] + FLOP_WEIGHTS["prim"] * (sec["gaussian_tests"] + sec["list_tests"])
+            + FLOP_WEIGHTS["od"] * sec["optical_depths"])
+
+
+def host_cores():
+    """Cores this process may run on (affinity, capped by OMP_NUM_THREADS when the box sets it), the
+    machine's CPU count and the CPU model."""
+    try:
+        avail = len(os.sched_getaffinity(0))
+    except AttributeError:
+        avail = os.cpu_count() or 1
+    omp = os.environ.get("OMP_NUM_THREADS")
+    use = min(avail, int(omp)) if omp and omp.isdigit() and int(omp) > 0 else avail
+    model = "unknown"
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    return use, {"nproc": os.cpu_count(), "affinity": avail, "omp_num_threads": omp, "cpu_model": model}
 
 
 def build_scene(cfg, seed):
@@ -174,13 +210,17 @@ def main():
                     help="stop a ray once T <= t_eps (SURVEY §8(d) benchmark setting; error bound in DESIGN.md)")
     ap.add_argument("--seed", type=int, default=2025)
     ap.add_argument("--cpu-budget", type=float, default=20.0, help="seconds of CPU-baseline work (0 = skip)")
-    ap.add_argument("--cpu-threads", type=int, default=min(16, os.cpu_count() or 1))
+    ap.add_argument("--cpu-threads", type=int, default=0,
+                    help="CPU-baseline threads (0 = every core this process may use, see host_cores)")
     ap.add_argument("--flops", type=int, default=1, help="run one instrumented frame to count algorithmic work")
     ap.add_argument("--integrator", default="raymarch", choices=["raymarch", "freeflight", "multiscatter", "sfd"],
                     help="raymarch = RayMarchingGaussians (the headline); the free-flight integrators are "
                          "secondary lines (unit Mpaths/s = pixel samples per second)")
     ap.add_argument("--spp", type=int, default=16, help="free-flight paths per pixel")
     args = ap.parse_args()
+    cores, host = host_cores()
+    if args.cpu_threads <= 0:
+        args.cpu_threads = cores
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -277,6 +317,7 @@ def main():
             if world == 1 and args.cpu_budget > 0:
                 cpu = cpu_baseline_ff(scene, W, H, args.integrator == "multiscatter", args.spp, args.cpu_budget,
                                       args.cpu_threads, log)
+                cpu.update(host)
             print(json.dumps({
                 "metric": f"Mpaths/s, {args.integrator} render", "value": paths / (ms_per_step * 1e-3) / 1e6,
                 "unit": "Mpaths/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
@@ -291,47 +332,70 @@ def main():
             dist.destroy_process_group()
         return
 
-    # ---- algorithmic work of this rank's share of one frame (instrumented kernels, untimed) ----
+    # ---- work of this rank's share of one frame (instrumented build of the same kernels, untimed) ----
     work = None
     if args.flops and rank == 0:
         work = dev.count_work(camera, integ.params, W, H, first_tile=rank, tile_stride=world, num_tiles=mine)
 
     if rank == 0:
         n_g = scene.get_num_primitives()
-        # Dominant kernel = the secondary-ray stage (light + environment transmittance rays). It
-        # does FP32 VALU work only (no MFMA: a 3x3 quadratic form is not a dense contraction); its
-        # roof is the FP32 vector peak, which equals the f32 MFMA peak.
+        # Dominant kernel = the secondary-ray stage (secondary_ww_kernel + secondary_slow_kernel: light +
+        # environment transmittance rays). FP32 VALU work only (no MFMA: a 3x3 quadratic form per
+        # ray-Gaussian pair is not a dense contraction), so the roof is the FP32 vector peak.
         sec_ms = stage_ms["secondary"]
-        roof = {"bound": "mfma", "unit": "TFLOP/s", "peak": FP32_PEAK_TFLOPS, "achieved": None, "frac": None,
+        roof = {"bound": "valu", "unit": "TFLOP/s", "peak": FP32_PEAK_TFLOPS, "achieved": None, "frac": None,
                 "traffic": None,
                 "kernel": "secondary_ww_kernel + secondary_slow_kernel (stage 'secondary')",
-                "kernel_ms": sec_ms, "peak_note": "FP32 vector peak (= f32 MFMA peak); VALU-only kernel",
+                "kernel_ms": sec_ms, "peak_note": "FP32 vector peak (MI355X_MICROARCH.md); VALU-only kernel",
                 "stage_ms": stage_ms, "frame_kernel_ms": kernel_ms,
                 "secondary_rays": per_step[-1]["secondary_rays"], "scatter_records": per_step[-1]["scatter_records"]}
         if work is not None:
-            sec_flops = work["secondary"]["flops"]
-            tflops = sec_flops / (sec_ms * 1e-3) / 1e12
-            roof.update(achieved=tflops, frac=tflops / FP32_PEAK_TFLOPS, alg_flops=sec_flops, work=work,
-                        frame_tflops=work["flops"] / (kernel_ms * 1e-3) / 1e12)
+            sec = work["secondary"]
+            executed = secondary_flops(sec)
+            alg = ALG_FLOPS_PER_CROSSED * sec["optical_depths"]
+            roof.update(achieved=executed / (sec_ms * 1e-3) / 1e12, alg_flops=alg, executed_flops=executed,
+                        alg_achieved=alg / (sec_ms * 1e-3) / 1e12, work=work, flop_weights=FLOP_WEIGHTS,
+                        flops_note="achieved/frac: the flops the timed persistent kernel itself executes "
+                                   "(its own node steps, leaf + neighbour-list primitive tests and optical "
+                                   "depths, counted by the instrumented build of the same kernel x the "
+                                   "per-operation weights in flop_weights). alg_*: the implementation-"
+                                   "independent part, every Gaussian a secondary ray crosses before its "
+                                   "cut-off found (ray-ellipsoid test) and integrated (optical depth)")
+            roof["frac"] = roof["achieved"] / FP32_PEAK_TFLOPS
+            roof["alg_frac"] = roof["alg_achieved"] / FP32_PEAK_TFLOPS
         # HBM traffic of the dominant kernel: rocprofv3 PMC passes of this same command (FETCH_SIZE x 2,
         # the gfx950 correction of MI355X_MICROARCH.md, + WRITE_SIZE), committed under profiles/
-        pmc_path = os.path.join(ROOT, "profiles", "r01_c4_pmc_summary.json")
+        pmc_path = os.path.join(ROOT, "profiles", PMC_SUMMARY)
         if args.config == "c4" and world == 1 and os.path.exists(pmc_path):
             pmc = json.load(open(pmc_path))
             for k, d in pmc.items():
                 if k.startswith("vr::dev::secondary_ww_kernel") and "hbm_read_bytes_gfx950_corrected" in d:
                     roof["traffic"] = d["hbm_read_bytes_gfx950_corrected"] + d.get("hbm_write_bytes", 0.0)
                     roof["traffic_unit"] = "bytes per launch"
-                    roof["traffic_source"] = "profiles/r01_c4_pmc_summary.json (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE)"
-        # HBM view of the whole frame (the north star's requested metric): compulsory bytes = every
-        # 48-B Gaussian record read once + every 12-B output pixel written once, over frame time.
-        alg_bytes = 48.0 * n_g + 12.0 * mine * 256
+                    roof["traffic_source"] = f"profiles/{PMC_SUMMARY} (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE)"
+        # HBM view of the whole frame (the north star's metric): SURVEY §8(d) B_frame = 48 sum n_t + 4 sum n_t
+        # + 12 W H, n_t = Gaussians overlapping tile t's frustum up to its termination depth (tile binning of
+        # the CPU restatement's termination depths, tests/bframe_fixture.py -> tests/golden/bframe_*.json)
+        bf = None
+        bf_path = os.path.join(ROOT, "tests", "golden", f"bframe_{args.config}.json")
+        if os.path.exists(bf_path):
+            bf = json.load(open(bf_path))
+            if not (bf["width"] == W and bf["height"] == H and bf["gaussians"] == n_g and bf["seed"] == args.seed
+                    and bf["t_eps"] == args.t_eps):
+                bf = None
+        if bf is not None and world == 1:
+            alg_bytes = float(bf["B_frame"])
+            note = f"SURVEY §8(d) B_frame from {os.path.relpath(bf_path, ROOT)} (sum n_t = {bf['sum_n_t']})"
+        else:
+            alg_bytes = 48.0 * n_g + 12.0 * mine * 256
+            note = "compulsory bytes (every 48-B record read once + every 12-B pixel written once)"
         hbm_gbps = alg_bytes / (kernel_ms * 1e-3) / 1e9
         roof["hbm"] = {"achieved": hbm_gbps, "peak": HBM_PEAK_GBPS, "unit": "GB/s", "frac": hbm_gbps / HBM_PEAK_GBPS,
-                       "alg_bytes": alg_bytes, "over": "whole frame (all stages)"}
+                       "alg_bytes": alg_bytes, "alg_bytes_def": note, "over": "whole frame (all stages)"}
         cpu = None
         if world == 1 and args.cpu_budget > 0:
             cpu = cpu_baseline(scene, W, H, args.env_samples, args.cpu_budget, args.cpu_threads, log)
+            cpu.update(host)
         out = {
             "metric": "Mrays/s + achieved HBM GB/s, 4096² render of 1M Gaussians, 1/2/4/8 GPU",
             "value": value, "unit": "Mrays/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,

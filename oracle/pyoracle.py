@@ -67,10 +67,37 @@ def lib():
                                        ctypes.c_int, fp, ctypes.POINTER(ctypes.c_uint32), ctypes.c_int]
     L.orc_render.argtypes = [P, ctypes.c_int, fp, fp, ctypes.c_float, ctypes.c_int, ctypes.c_float,
                              ctypes.c_int, ctypes.c_int, ctypes.c_int, ip, ctypes.c_int64, fp, ctypes.c_int]
+    L.orc_primary_depths.argtypes = [P, ctypes.c_int, fp, fp, ctypes.c_float, ctypes.c_int, ctypes.c_int,
+                                     ctypes.c_float, ctypes.c_float, fp, ctypes.c_int]
+    L.orc_tile_bins.restype = ctypes.c_int64
+    L.orc_tile_bins.argtypes = [P, fp, fp, ctypes.c_float, ctypes.c_int, ctypes.c_int, fp,
+                                ctypes.POINTER(ctypes.c_uint32), ctypes.c_int]
     L.orc_set_stable_ties.argtypes = [ctypes.c_int]
     L.orc_set_stable_ties.restype = ctypes.c_int
     _lib = L
     return L
+
+
+def primary_depths(scene, cam_type, pos, view_dir, fov, W, H, step_size=0.01, t_eps=1e-6, nthreads=0):
+    """(H, W) termination distance of every primary ray (-1: no events); see orc_primary_depths."""
+    pos, pp = _f(pos)
+    vd, pv = _f(view_dir)
+    out = np.zeros((H, W), np.float32)
+    lib().orc_primary_depths(scene.h, cam_type, pp, pv, float(fov), W, H, float(step_size), float(t_eps),
+                             out.ctypes.data_as(ctypes.POINTER(ctypes.c_float)), int(nthreads))
+    return out
+
+
+def tile_bins(scene, pos, view_dir, fov, W, H, depth, nthreads=0):
+    """Per 16x16 tile (row-major) the Gaussians overlapping its frustum up to its termination depth
+    (SURVEY §8(d) n_t); see orc_tile_bins. Pinhole camera."""
+    pos, pp = _f(pos)
+    vd, pv = _f(view_dir)
+    d, pd = _f(depth)
+    nt = np.zeros(((W + 15) // 16) * ((H + 15) // 16), np.uint32)
+    lib().orc_tile_bins(scene.h, pp, pv, float(fov), W, H, pd, nt.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32)),
+                        int(nthreads))
+    return nt
 
 
 class stable_ties:

@@ -1565,6 +1565,122 @@ int orc_render(void* sp, int cam_type, const float* pos, const float* vd, float 
 }
 
 void orc_ff_debug(float* buf) { g_ff_dbg = buf; }
+// SURVEY.md §8(d) algorithmic bytes, step 1: each pixel's primary-ray termination distance under
+// the RayMarchingGaussians march (test_integrators.h:178-290, the list variant's active sets, no
+// secondary rays): the end of the first step after which T <= t_eps, or t_end (the last event) if T
+// never falls that far; -1 for a ray without events. depth[y * W + x].
+int orc_primary_depths(void* sp, int cam_type, const float* pos, const float* vd, float fov, int W, int H,
+                       float step_size, float t_eps, float* depth, int nthreads) {
+    const Scene& s = *(const Scene*)sp;
+    const GMM& gmm = s.gmm;
+    Camera c = cam_type == 0 ? Camera::make_pinhole({pos[0], pos[1], pos[2]}, {vd[0], vd[1], vd[2]}, fov)
+                             : Camera::make_ortho({pos[0], pos[1], pos[2]}, {vd[0], vd[1], vd[2]});
+    if (nthreads > 0) omp_set_num_threads(nthreads);
+#pragma omp parallel for schedule(dynamic, 64)
+    for (int64_t q = 0; q < (int64_t)W * H; ++q) {
+        static thread_local std::vector<uint8_t> mask;
+        if (mask.size() != gmm.gaussians.size()) mask.assign(gmm.gaussians.size(), 0);
+        const int x = (int)(q % W), y = (int)(q / W);
+        Ray ray = c.sample_ray((x + 0.5f) / W, (y + 0.5f) / H);
+        std::vector<PrimitiveHitEvent> events;
+        gmm.intersect_events(ray, events);
+        if (events.empty()) { depth[q] = -1.0f; continue; }
+        const float t_end = events.back().t;
+        SparseSet active{&mask, {}};
+        size_t evt_i = 0;
+        float t = 0.0f, T = 1.0f, d = t_end;
+        while (t < t_end) {
+            while (evt_i < events.size() && events[evt_i].t <= t) {
+                active.set(events[evt_i].index, events[evt_i].entering);
+                ++evt_i;
+            }
+            T *= gmm.transmittance_over_segment(ray, t, t + step_size, active.list);
+            t += step_size;
+            if (T <= t_eps) { d = t; break; }
+        }
+        active.clear();
+        depth[q] = d;
+    }
+    return 0;
+}
+
+// SURVEY.md §8(d) algorithmic bytes, step 2: per 16x16 tile, n_t = the Gaussians whose conservative
+// 3-sigma box (gaussian.h:304-319) overlaps the tile's frustum and whose conservative near depth is
+// <= D_t (the largest termination distance of the tile's rays, orc_primary_depths). Pinhole camera:
+// every ray of the tile passes through the pinhole, so the frustum is the pyramid from the pinhole
+// through the tile's four outer pixel-corner rays; a ray reaches the pinhole at t >= focal length
+// (the sensor plane's distance), so a box's near depth is >= f + |box - pinhole|. The query walks
+// the oracle's BVH. n_tiles[t] for row-major tiles; returns the sum of n_t.
+int64_t orc_tile_bins(void* sp, const float* pos, const float* vd, float fov, int W, int H, const float* depth,
+                      uint32_t* n_tiles, int nthreads) {
+    const Scene& s = *(const Scene*)sp;
+    const GMM& gmm = s.gmm;
+    Camera c = Camera::make_pinhole({pos[0], pos[1], pos[2]}, {vd[0], vd[1], vd[2]}, fov);
+    const int tx = (W + 15) / 16, ty = (H + 15) / 16;
+    const V3 apex = c.pinhole;
+    int64_t total = 0;
+    if (nthreads > 0) omp_set_num_threads(nthreads);
+#pragma omp parallel for schedule(dynamic, 16) reduction(+ : total)
+    for (int64_t t = 0; t < (int64_t)tx * ty; ++t) {
+        const int x0 = (int)(t % tx) * 16, y0 = (int)(t / tx) * 16;
+        const int x1 = std::min(x0 + 16, W), y1 = std::min(y0 + 16, H);
+        float D = -1.0f;
+        for (int y = y0; y < y1; ++y)
+            for (int x = x0; x < x1; ++x) D = std::max(D, depth[(int64_t)y * W + x]);
+        n_tiles[t] = 0;
+        if (D < 0.0f || gmm.nodes.empty()) continue;
+        V3 dir[4];  // outer corner rays, counter-clockwise
+        const double cu[4] = {(double)x0 / W, (double)x1 / W, (double)x1 / W, (double)x0 / W};
+        const double cv[4] = {(double)y0 / H, (double)y0 / H, (double)y1 / H, (double)y1 / H};
+        V3 centre{0, 0, 0};
+        for (int k = 0; k < 4; ++k) {
+            dir[k] = c.sample_ray(cu[k], cv[k]).direction;
+            centre = centre + dir[k];
+        }
+        V3 nrm[4];  // side planes through the apex, normals pointing into the pyramid
+        for (int k = 0; k < 4; ++k) {
+            V3 n = cross(dir[k], dir[(k + 1) % 4]);
+            if (dot(n, centre) < 0.0f) n = V3{-n.x, -n.y, -n.z};
+            nrm[k] = n;
+        }
+        const float limit = D - c.focal_length;  // |box - apex| must not exceed this
+        auto overlaps = [&](const V3& bmin, const V3& bmax) {
+            double d2 = 0.0;  // squared distance apex -> box
+            for (int k = 0; k < 3; ++k) {
+                const double v = std::max({(double)bmin[k] - apex[k], 0.0, (double)apex[k] - bmax[k]});
+                d2 += v * v;
+            }
+            if (d2 > (double)limit * limit * (1.0 + 1e-6) + 1e-12 && limit >= 0.0f) return false;
+            if (limit < 0.0f) return false;
+            for (int k = 0; k < 4; ++k) {  // box entirely outside one side plane -> no overlap
+                const V3& n = nrm[k];
+                const V3 p{n.x >= 0 ? bmax.x : bmin.x, n.y >= 0 ? bmax.y : bmin.y, n.z >= 0 ? bmax.z : bmin.z};
+                if (dot(n, p - apex) < 0.0f) return false;
+            }
+            return true;
+        };
+        uint32_t cnt = 0;
+        std::vector<uint32_t> stack{0};
+        while (!stack.empty()) {
+            const GMM::Node& nd = gmm.nodes[stack.back()];
+            stack.pop_back();
+            if (!overlaps(nd.bmin, nd.bmax)) continue;
+            if (nd.isLeaf()) {
+                for (uint32_t i = 0; i < nd.count; ++i) {
+                    const Gaussian& g = gmm.gaussians[gmm.indices[nd.leftFirst + i]];
+                    if (overlaps(g.bmin, g.bmax)) ++cnt;
+                }
+            } else {
+                stack.push_back(nd.leftFirst);
+                stack.push_back(nd.leftFirst + 1);
+            }
+        }
+        n_tiles[t] = cnt;
+        total += cnt;
+    }
+    return total;
+}
+
 // DEBUG: the faithful RayMarchingGaussians march of one pixel; out gets, per step with a non-empty
 // active set, (t, n_active, sigma_s, T after the step, active ids...). Returns the floats written.
 int64_t orc_debug_march(void* sp, const float* pos, const float* vd, float fov, int x, int y, int W, int H,

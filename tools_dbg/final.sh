@@ -1,11 +1,12 @@
 #!/bin/bash
-# Round-end check: full GPU suite, smoke, headline bench, rocprofv3 kernel stats of the headline.
+# Round check: full GPU suite, smoke, headline bench, rocprofv3 kernel stats of the headline.
 cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
 OUT=gpurun_out/final; mkdir -p $OUT
-timeout -k 10 600 python3 -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > $OUT/gpu_tests.log 2>&1 || { tail -20 $OUT/gpu_tests.log; exit 1; }
+timeout -k 10 900 python3 -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread > $OUT/gpu_tests.log 2>&1 || { tail -30 $OUT/gpu_tests.log; exit 1; }
 tail -2 $OUT/gpu_tests.log
 timeout -k 10 200 python3 -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1 || { tail -20 $OUT/smoke.log; exit 1; }
 tail -1 $OUT/smoke.log
-timeout -k 10 300 python3 bench.py > $OUT/bench.json 2> $OUT/bench.log || exit 1
+timeout -k 10 400 python3 bench.py > $OUT/bench.json 2> $OUT/bench.log || { tail -20 $OUT/bench.log; exit 1; }
+cut -c1-400 $OUT/bench.json
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/stats -o run --output-format csv -- python3 bench.py --steps 3 --warmup 1 --cpu-budget 0 --flops 0 > $OUT/stats.log 2>&1 || exit 1
 echo done
