@@ -63,3 +63,18 @@ std::vector<float> step_table(float step, float t_max);
 struct vr_scene {
     vr::HostScene s;
 };
+
+// Multi-GPU group behind a vr_init_multi context (host/vr_multi.cpp).
+struct vr_group;
+namespace vr {
+vr_status group_create(int ndev, const int* devices, vr_group** out);
+void group_destroy(vr_group* g);
+int group_size(const vr_group* g);
+vr_ctx* group_rank(vr_group* g, int rank);
+bool group_uses_rccl(const vr_group* g);
+vr_status group_upload(vr_group* g, const vr_scene* s);
+vr_status group_render(vr_group* g, const vr_camera* cam, const vr_render_params* p, uint32_t W, uint32_t H, float* rgb);
+vr_status group_set_option(vr_group* g, int32_t option, int64_t value);
+vr_status group_synchronize(vr_group* g);
+vr_status group_stats(vr_group* g, vr_render_stats* out);
+}  // namespace vr

@@ -94,7 +94,11 @@ struct vr_ctx {
     int64_t opt_half_nodes = 1;        // VR_OPT_HALF_NODES
     int64_t opt_secondary_budget = 1;  // VR_OPT_SECONDARY_BUDGET
     int64_t opt_ff_window0 = 8;        // VR_OPT_FF_WINDOW0
+    vr_group* group = nullptr;         // vr_init_multi: the devices this context drives (host/vr_multi.cpp)
 };
+
+// Single-device entry points called on a multi-GPU context act on its first device.
+static inline vr_ctx* first_device(vr_ctx* c) { return (c && c->group) ? vr::group_rank(c->group, 0) : c; }
 
 namespace {
 
@@ -689,8 +693,51 @@ vr_status vr_init(int device, vr_ctx** out) {
     return VR_OK;
 }
 
+vr_status vr_device_count(int32_t* n) {
+    if (!n) return fail(VR_ERR_INVALID, "vr_device_count: NULL argument");
+    int k = 0;
+    if (hipGetDeviceCount(&k) != hipSuccess) k = 0;
+    *n = k;
+    return VR_OK;
+}
+
+vr_status vr_init_multi(int32_t ndev, const int32_t* devices, vr_ctx** out) {
+    if (!out) return fail(VR_ERR_INVALID, "vr_init_multi: out is NULL");
+    vr_group* g = nullptr;
+    vr_status st = vr::group_create(ndev, devices, &g);
+    if (st != VR_OK) return st;
+    vr_ctx* c = nullptr;
+    if ((st = vr_init(devices ? devices[0] : 0, &c)) != VR_OK) {
+        std::string m = vr_last_error();
+        vr::group_destroy(g);
+        return fail(st, m);
+    }
+    c->group = g;
+    *out = c;
+    return VR_OK;
+}
+
+int32_t vr_ctx_num_devices(const vr_ctx* c) { return !c ? 0 : c->group ? vr::group_size(c->group) : 1; }
+
+int32_t vr_ctx_uses_rccl(const vr_ctx* c) { return c && c->group && vr::group_uses_rccl(c->group) ? 1 : 0; }
+
+vr_status vr_get_rank_stats(vr_ctx* c, int32_t rank, vr_render_stats* out) {
+    if (!c || !out) return fail(VR_ERR_INVALID, "vr_get_rank_stats: NULL argument");
+    if (!c->group) {
+        if (rank != 0) return fail(VR_ERR_INVALID, "vr_get_rank_stats: rank out of range");
+        return vr_get_stats(c, out);
+    }
+    vr_ctx* r = vr::group_rank(c->group, rank);
+    if (!r) return fail(VR_ERR_INVALID, "vr_get_rank_stats: rank out of range");
+    return vr_get_stats(r, out);
+}
+
 void vr_destroy(vr_ctx* c) {
     if (!c) return;
+    if (c->group) {
+        vr::group_destroy(c->group);
+        c->group = nullptr;
+    }
     (void)hipSetDevice(c->device);
     (void)hipDeviceSynchronize();
     free_scene(c);
@@ -715,6 +762,7 @@ void vr_destroy(vr_ctx* c) {
 
 vr_status vr_upload_scene(vr_ctx* c, const vr_scene* sc) {
     if (!c || !sc) return fail(VR_ERR_INVALID, "vr_upload_scene: NULL argument");
+    if (c->group) return vr::group_upload(c->group, sc);
     const HostScene& s = sc->s;
     if (s.lights.size() > (size_t)kMaxLights) return fail(VR_ERR_UNSUPPORTED, "more than 16 lights");
     HIP_TRY(hipSetDevice(c->device), "hipSetDevice");
@@ -805,6 +853,7 @@ uint32_t vr_num_tiles(uint32_t W, uint32_t H) { return ((W + kTile - 1) / kTile)
 
 vr_status vr_render(vr_ctx* c, const vr_camera* cam, const vr_render_params* p, uint32_t W, uint32_t H, float* rgb) {
     if (!c || !rgb) return fail(VR_ERR_INVALID, "vr_render: NULL argument");
+    if (c->group) return vr::group_render(c->group, cam, p, W, H, rgb);
     HIP_TRY(hipSetDevice(c->device), "hipSetDevice");
     RenderArgs A;
     vr_status st = fill_args(c, cam, p, W, H, A);
@@ -830,6 +879,7 @@ vr_status vr_render(vr_ctx* c, const vr_camera* cam, const vr_render_params* p, 
 vr_status vr_render_tiles_device(vr_ctx* c, const vr_camera* cam, const vr_render_params* p, uint32_t W, uint32_t H,
                                  uint32_t first_tile, uint32_t tile_stride, uint32_t num_tiles, int32_t packed,
                                  float* d_out, void* stream) {
+    c = first_device(c);
     if (!c || !d_out) return fail(VR_ERR_INVALID, "vr_render_tiles_device: NULL argument");
     HIP_TRY(hipSetDevice(c->device), "hipSetDevice");
     RenderArgs A;
@@ -851,6 +901,7 @@ vr_status vr_render_tiles_device(vr_ctx* c, const vr_camera* cam, const vr_rende
 
 vr_status vr_count_work(vr_ctx* c, const vr_camera* cam, const vr_render_params* p, uint32_t W, uint32_t H,
                         uint32_t first_tile, uint32_t tile_stride, uint32_t num_tiles, uint64_t counts[16]) {
+    c = first_device(c);
     if (!c || !counts) return fail(VR_ERR_INVALID, "vr_count_work: NULL argument");
     HIP_TRY(hipSetDevice(c->device), "hipSetDevice");
     RenderArgs A;
@@ -891,6 +942,7 @@ vr_status vr_count_work(vr_ctx* c, const vr_camera* cam, const vr_render_params*
 
 vr_status vr_unshuffle_tiles_device(vr_ctx* c, const float* d_slabs, uint32_t nslabs, uint32_t tiles_per_slab, uint32_t W,
                                     uint32_t H, float* d_image, void* stream) {
+    c = first_device(c);
     if (!c || !d_slabs || !d_image || nslabs == 0) return fail(VR_ERR_INVALID, "vr_unshuffle_tiles_device: bad argument");
     HIP_TRY(hipSetDevice(c->device), "hipSetDevice");
     HIP_TRY(launch_unshuffle(d_slabs, nslabs, tiles_per_slab, (W + kTile - 1) / kTile, W, H, d_image, (hipStream_t)stream),
@@ -900,6 +952,7 @@ vr_status vr_unshuffle_tiles_device(vr_ctx* c, const float* d_slabs, uint32_t ns
 
 vr_status vr_render_record(vr_ctx* c, const vr_camera* cam, const vr_render_params* p, uint32_t W, uint32_t H, float* rgb,
                            int32_t slot) {
+    c = first_device(c);
     if (!c || !rgb || !p) return fail(VR_ERR_INVALID, "vr_render_record: NULL argument");
     if (slot != 0 && slot != 1) return fail(VR_ERR_INVALID, "vr_render_record: slot must be 0 or 1");
     if (p->integrator != VR_MULTI_SCATTER)
@@ -935,6 +988,7 @@ vr_status vr_render_record(vr_ctx* c, const vr_camera* cam, const vr_render_para
 }
 
 vr_status vr_get_pixel_gaussians(vr_ctx* c, int32_t slot, uint32_t* bits, size_t n_words) {
+    c = first_device(c);
     if (!c || !bits || (slot != 0 && slot != 1)) return fail(VR_ERR_INVALID, "vr_get_pixel_gaussians: bad argument");
     const size_t need = (size_t)((c->rec_n[slot] + 31) / 32) * c->rec_npix[slot];
     if (!c->rec_bits[slot].p || c->rec_npix[slot] == 0) return fail(VR_ERR_INVALID, "slot holds no recording");
@@ -946,6 +1000,7 @@ vr_status vr_get_pixel_gaussians(vr_ctx* c, int32_t slot, uint32_t* bits, size_t
 
 vr_status vr_sfd_loss_diff(vr_ctx* c, const float* loss_base, const float* loss_plus, uint32_t W, uint32_t H, double* out,
                            size_t n) {
+    c = first_device(c);
     if (!c || !loss_base || !loss_plus || !out) return fail(VR_ERR_INVALID, "vr_sfd_loss_diff: NULL argument");
     const uint32_t npix = W * H;
     if (c->rec_npix[0] != npix || c->rec_npix[1] != npix || c->rec_n[0] != c->rec_n[1] || n != c->rec_n[0])
@@ -969,6 +1024,7 @@ vr_status vr_sfd_loss_diff(vr_ctx* c, const float* loss_base, const float* loss_
 
 vr_status vr_set_option(vr_ctx* c, int32_t option, int64_t value) {
     if (!c) return fail(VR_ERR_INVALID, "vr_set_option: NULL ctx");
+    if (c->group) return vr::group_set_option(c->group, option, value);
     switch (option) {
         case VR_OPT_HALF_NODES:
             if (value != 0 && value != 1) return fail(VR_ERR_INVALID, "VR_OPT_HALF_NODES must be 0 or 1");
@@ -993,6 +1049,7 @@ vr_status vr_set_option(vr_ctx* c, int32_t option, int64_t value) {
 }
 
 vr_status vr_get_option(vr_ctx* c, int32_t option, int64_t* value) {
+    c = first_device(c);
     if (!c || !value) return fail(VR_ERR_INVALID, "vr_get_option: NULL argument");
     switch (option) {
         case VR_OPT_HALF_NODES: *value = c->opt_half_nodes; return VR_OK;
@@ -1005,6 +1062,7 @@ vr_status vr_get_option(vr_ctx* c, int32_t option, int64_t* value) {
 
 vr_status vr_synchronize(vr_ctx* c) {
     if (!c) return fail(VR_ERR_INVALID, "vr_synchronize: NULL ctx");
+    if (c->group) return vr::group_synchronize(c->group);
     HIP_TRY(hipSetDevice(c->device), "hipSetDevice");
     HIP_TRY(hipDeviceSynchronize(), "hipDeviceSynchronize");
     const bool pending = c->stats_pending;
@@ -1020,6 +1078,7 @@ vr_status vr_synchronize(vr_ctx* c) {
 }
 
 vr_status vr_get_fallback_pixels(vr_ctx* c, uint32_t* xy, size_t cap, size_t* n) {
+    c = first_device(c);
     if (!c || !n || (cap > 0 && !xy)) return fail(VR_ERR_INVALID, "vr_get_fallback_pixels: bad argument");
     HIP_TRY(hipSetDevice(c->device), "hipSetDevice");
     vr_status st = collect(c);
@@ -1040,6 +1099,7 @@ vr_status vr_get_fallback_pixels(vr_ctx* c, uint32_t* xy, size_t cap, size_t* n)
 
 vr_status vr_get_stats(vr_ctx* c, vr_render_stats* o) {
     if (!c || !o) return fail(VR_ERR_INVALID, "vr_get_stats: NULL argument");
+    if (c->group) return vr::group_stats(c->group, o);
     HIP_TRY(hipSetDevice(c->device), "hipSetDevice");
     vr_status st = collect(c);
     if (st != VR_OK) return st;

@@ -658,6 +658,15 @@ __device__ __forceinline__ void sec_leaf(const RenderArgs& A, SecRay& R, int32_t
     }
 }
 
+// VR_DIAG_SKIP_TR_STORES: diagnostic builds only (tools_dbg, never the product library): the
+// secondary rays' Tr stores are dropped so that rocprofv3 WRITE_SIZE attributes the kernel's write
+// traffic (Tr stores vs traversal-stack spills). The traversal itself is unchanged.
+#ifdef VR_DIAG_SKIP_TR_STORES
+#define VR_TR_STORE(A, slot, v) ((void)(slot), (void)(v))
+#else
+#define VR_TR_STORE(A, slot, v) ((A).tr[slot] = (v))
+#endif
+
 // Ray complete: write its transmittance (or hand it to the exact slow path).
 template <bool S, bool FAST, bool PURE>
 __device__ __forceinline__ void sec_finish(const RenderArgs& A, SecRay& R, Ctr& c) {
@@ -670,7 +679,7 @@ __device__ __forceinline__ void sec_finish(const RenderArgs& A, SecRay& R, Ctr& 
         }
     }
     if (R.tau >= R.cut) {
-        A.tr[R.slot] = 0.0f;
+        VR_TR_STORE(A, R.slot, 0.0f);
         return;
     }
     const uint64_t all = R.act_n >= 64 ? ~0ull : ((1ull << R.act_n) - 1ull);
@@ -702,7 +711,7 @@ __device__ __forceinline__ void sec_finish(const RenderArgs& A, SecRay& R, Ctr& 
             R.tau += FAST ? optical_depth_fast(g, q, 0.0f, R.lim) : optical_depth(g, q, 0.0f, R.lim);
         }
     }
-    A.tr[R.slot] = expf(-R.tau);
+    VR_TR_STORE(A, R.slot, expf(-R.tau));
 }
 
 // ---------------------------------------------------------------------------------------------

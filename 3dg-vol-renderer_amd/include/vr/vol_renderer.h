@@ -48,6 +48,28 @@ inline vr_ctx* device(int dev = 0) {
     return ctxs[dev].get();
 }
 
+// Number of visible GPUs.
+inline int device_count() {
+    int32_t n = 0;
+    check(vr_device_count(&n));
+    return n;
+}
+
+// One multi-GPU context per device list (vr_init_multi), created on first use.
+inline vr_ctx* device_group(const std::vector<int>& devs) {
+    static std::mutex mu;
+    static std::map<std::vector<int>, std::unique_ptr<vr_ctx, void (*)(vr_ctx*)>> groups;
+    std::lock_guard<std::mutex> lock(mu);
+    auto it = groups.find(devs);
+    if (it == groups.end()) {
+        std::vector<int32_t> d(devs.begin(), devs.end());
+        vr_ctx* c = nullptr;
+        check(vr_init_multi((int32_t)d.size(), d.data(), &c));
+        it = groups.emplace(devs, std::unique_ptr<vr_ctx, void (*)(vr_ctx*)>(c, &vr_destroy)).first;
+    }
+    return it->second.get();
+}
+
 inline uint64_t next_serial() {
     static std::atomic<uint64_t> serial{0};
     return ++serial;
@@ -367,10 +389,15 @@ public:
     virtual void render(const Scene& scene, Image& image) = 0;
 };
 
+// The device integrators render on every visible GPU by default, as the reference's render uses
+// every CPU core (OpenMP): one GPU renders on its own; several split the frame's tiles and gather
+// over RCCL (vr_init_multi). set_devices() picks the GPUs explicitly (a device
+// listed more than once rehearses the split on one GPU); the `dev` constructor argument pins one GPU.
 class HipIntegrator : public Integrator {
 protected:
     vr_render_params params_{};
-    int device_ = 0;
+    int device_ = -1;            // >= 0: this one GPU
+    std::vector<int> devices_;   // explicit device list (multi-GPU context, even for one device)
 
 public:
     HipIntegrator(const std::shared_ptr<Camera>& camera, int integrator, float step_size, int env_samples, int dev)
@@ -382,9 +409,19 @@ public:
         params_.flags = 0;
     }
     void set_t_eps(float t) { params_.t_eps = t; }
+    void set_devices(const std::vector<int>& devs) { devices_ = devs; }
     const vr_render_params& params() const { return params_; }
+    vr_ctx* context() const {
+        if (!devices_.empty()) return vr_cpp::device_group(devices_);
+        if (device_ >= 0) return vr_cpp::device(device_);
+        const int n = vr_cpp::device_count();
+        if (n <= 1) return vr_cpp::device(0);
+        std::vector<int> all(n);
+        for (int i = 0; i < n; ++i) all[i] = i;
+        return vr_cpp::device_group(all);
+    }
     void render(const Scene& scene, Image& image) override {
-        vr_ctx* ctx = vr_cpp::device(device_);
+        vr_ctx* ctx = context();
         // re-upload when the scene (or the scene object) changed since the last render on this device
         static std::mutex mu;
         static std::map<vr_ctx*, std::pair<const void*, uint64_t>> uploaded;  // per device context
@@ -401,7 +438,7 @@ public:
     }
     vr_render_stats stats() const {
         vr_render_stats s{};
-        vr_cpp::check(vr_get_stats(vr_cpp::device(device_), &s));
+        vr_cpp::check(vr_get_stats(context(), &s));
         return s;
     }
 };
@@ -410,28 +447,28 @@ public:
 class RayMarchingGaussians : public HipIntegrator {
 public:
     RayMarchingGaussians(const std::shared_ptr<Camera>& camera, float step_size = 0.01f, int env_samples = 20,
-                         int dev = 0)
+                         int dev = -1)
         : HipIntegrator(camera, VR_RAYMARCH_GAUSSIANS, step_size, env_samples, dev) {}
 };
 
 // integrator.h:100-142 — PureRayMarching(camera, step_size = 0.01, env_samples = 20)
 class PureRayMarching : public HipIntegrator {
 public:
-    PureRayMarching(const std::shared_ptr<Camera>& camera, float step_size = 0.01f, int env_samples = 20, int dev = 0)
+    PureRayMarching(const std::shared_ptr<Camera>& camera, float step_size = 0.01f, int env_samples = 20, int dev = -1)
         : HipIntegrator(camera, VR_PURE_RAYMARCH, step_size, env_samples, dev) {}
 };
 
 // test_integrators.h:11-21 — RayMarchingSpheres(camera, step_size = 0.01, env_samples = 5)
 class RayMarchingSpheres : public HipIntegrator {
 public:
-    RayMarchingSpheres(const std::shared_ptr<Camera>& camera, float step_size = 0.01f, int env_samples = 5, int dev = 0)
+    RayMarchingSpheres(const std::shared_ptr<Camera>& camera, float step_size = 0.01f, int env_samples = 5, int dev = -1)
         : HipIntegrator(camera, VR_RAYMARCH_SPHERES, step_size, env_samples, dev) {}
 };
 
 // integrator.h:273-408 — FreeFlightGaussians(camera, num_samples = 256)
 class FreeFlightGaussians : public HipIntegrator {
 public:
-    FreeFlightGaussians(const std::shared_ptr<Camera>& camera, int num_samples = 256, int dev = 0)
+    FreeFlightGaussians(const std::shared_ptr<Camera>& camera, int num_samples = 256, int dev = -1)
         : HipIntegrator(camera, VR_FREE_FLIGHT, 0.01f, 0, dev) {
         params_.num_samples = num_samples;
     }
@@ -440,7 +477,7 @@ public:
 // integrator.h:416-720 — MultiScatterGaussians(camera, samples = 16, min_bounces = 5)
 class MultiScatterGaussians : public HipIntegrator {
 public:
-    MultiScatterGaussians(const std::shared_ptr<Camera>& camera, int samples = 16, int min_bounces = 5, int dev = 0)
+    MultiScatterGaussians(const std::shared_ptr<Camera>& camera, int samples = 16, int min_bounces = 5, int dev = -1)
         : HipIntegrator(camera, VR_MULTI_SCATTER, 0.01f, 0, dev) {
         params_.num_samples = samples;
         params_.min_bounces = min_bounces;
@@ -451,6 +488,6 @@ public:
 // integrator.h:65-94 — TestIntegrator(camera)
 class TestIntegrator : public HipIntegrator {
 public:
-    TestIntegrator(const std::shared_ptr<Camera>& camera, int dev = 0)
+    TestIntegrator(const std::shared_ptr<Camera>& camera, int dev = -1)
         : HipIntegrator(camera, VR_TEST_HITMASK, 0.01f, 0, dev) {}
 };

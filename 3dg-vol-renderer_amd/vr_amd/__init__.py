@@ -298,19 +298,49 @@ class Image:
 
 
 class Device:
-    """One GPU context (vr_ctx). Scenes are uploaded lazily and re-uploaded when they change."""
+    """A device context (vr_ctx). `device` is a GPU index (vr_init) or a tuple of GPU indices: a
+    multi-GPU context (vr_init_multi) that splits every frame's tiles over those GPUs and gathers
+    them over RCCL (a GPU listed twice rehearses the split on one GPU, gathering with device copies).
+    Scenes are uploaded lazily and re-uploaded when they change."""
 
     _cache = {}
 
     def __init__(self, device=0):
         h = ctypes.c_void_p()
-        check(lib().vr_init(int(device), ctypes.byref(h)))
+        if isinstance(device, (tuple, list)):
+            devs = (ctypes.c_int32 * len(device))(*[int(d) for d in device])
+            check(lib().vr_init_multi(len(device), devs, ctypes.byref(h)))
+            device = tuple(int(d) for d in device)
+        else:
+            check(lib().vr_init(int(device), ctypes.byref(h)))
         self._h = h
         self.device = device
         self._scene_key = None
 
+    @staticmethod
+    def count():
+        n = ctypes.c_int32()
+        check(lib().vr_device_count(ctypes.byref(n)))
+        return int(n.value)
+
+    @property
+    def num_devices(self):
+        return int(lib().vr_ctx_num_devices(self._h))
+
+    @property
+    def uses_rccl(self):
+        return bool(lib().vr_ctx_uses_rccl(self._h))
+
+    def rank_stats(self, rank):
+        s = L.vr_render_stats()
+        check(lib().vr_get_rank_stats(self._h, int(rank), ctypes.byref(s)))
+        return {"kernel_ms": s.kernel_ms, "pixels": s.pixels, "fallback_pixels": s.fallback_pixels,
+                "error_pixels": s.error_pixels, "scatter_records": s.scatter_records}
+
     @classmethod
     def get(cls, device=0):
+        if isinstance(device, list):
+            device = tuple(device)
         d = cls._cache.get(device)
         if d is None:
             d = cls._cache[device] = cls(device)

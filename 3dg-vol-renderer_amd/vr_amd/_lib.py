@@ -91,6 +91,11 @@ SIGNATURES = {
     "vr_image_write_ppm": (ST, [ctypes.c_char_p, FP, ctypes.c_uint32, ctypes.c_uint32]),
     "vr_image_read_ppm": (ST, [ctypes.c_char_p, FP, U32P, U32P]),
     "vr_init": (ST, [ctypes.c_int, PP]),
+    "vr_device_count": (ST, [ctypes.POINTER(ctypes.c_int32)]),
+    "vr_init_multi": (ST, [ctypes.c_int32, ctypes.POINTER(ctypes.c_int32), PP]),
+    "vr_ctx_num_devices": (ctypes.c_int32, [P]),
+    "vr_ctx_uses_rccl": (ctypes.c_int32, [P]),
+    "vr_get_rank_stats": (ST, [P, ctypes.c_int32, ctypes.POINTER(vr_render_stats)]),
     "vr_destroy": (None, [P]),
     "vr_upload_scene": (ST, [P, P]),
     "vr_render": (ST, [P, ctypes.POINTER(vr_camera), ctypes.POINTER(vr_render_params), ctypes.c_uint32,

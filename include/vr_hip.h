@@ -23,7 +23,7 @@
 extern "C" {
 #endif
 
-#define VR_ABI_VERSION 3
+#define VR_ABI_VERSION 4
 
 typedef enum vr_status {
     VR_OK = 0,
@@ -184,6 +184,23 @@ vr_status vr_image_read_ppm(const char* path, float* rgb, uint32_t* width, uint3
 
 /* ---------------- device ---------------- */
 vr_status vr_init(int device, vr_ctx** out);
+/* Number of visible GPUs. */
+vr_status vr_device_count(int32_t* n);
+/* Multi-GPU context: one host thread drives `ndev` GPUs (devices[0..ndev-1], or
+ * 0..ndev-1 if devices is NULL). vr_upload_scene replicates the scene on every device; vr_render cuts
+ * the frame into 16x16 tiles, rank r renders tiles r, r+ndev, r+2ndev, ... into a packed slab on its
+ * device, the slabs are gathered to devices[0] with RCCL (one ncclGroupStart/End of every rank's
+ * ncclSend and the root's ncclRecv over xGMI; librccl is loaded at this call) and unshuffled there
+ * into the row-major frame. A device listed more than once shares its GPU between ranks (rehearsal
+ * of the split on one GPU; the slabs then move with device copies, RCCL holds one rank per device).
+ * vr_synchronize / vr_set_option apply to every device; vr_get_stats sums counts over the ranks and
+ * reports the slowest rank's times (vr_get_rank_stats: one rank). The other entry points act on the
+ * first device. vr_destroy releases the whole group. */
+vr_status vr_init_multi(int32_t ndev, const int32_t* devices, vr_ctx** out);
+/* Devices a context drives (1 for vr_init contexts); whether its gather runs over RCCL. */
+int32_t vr_ctx_num_devices(const vr_ctx* ctx);
+int32_t vr_ctx_uses_rccl(const vr_ctx* ctx);
+vr_status vr_get_rank_stats(vr_ctx* ctx, int32_t rank, vr_render_stats* out);
 void vr_destroy(vr_ctx* ctx);
 /* Prepare (BVH build) and upload the scene; replaces any previous one. Host copies are not kept. */
 vr_status vr_upload_scene(vr_ctx* ctx, const vr_scene* s);

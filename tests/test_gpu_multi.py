@@ -1,0 +1,89 @@
+"""Multi-GPU context through the C ABI (vr_init_multi): the frame's 16x16 tiles are
+dealt round-robin over the ranks, gathered to the first device (RCCL ncclSend/ncclRecv when every
+rank has its own GPU, device copies when ranks share one) and unshuffled there. On the one-GPU test
+box: a one-rank group exercises the whole RCCL path (self send/receive); groups that list GPU 0
+several times exercise the split, the gather and the unshuffle. Every result must equal the
+single-device render bit for bit (pixels are independent; env and path RNG are keyed by pixel)."""
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+import vr_amd as vr
+from helpers import CAM_POS, FOV, ROOT, main_view_dir, read_ppm, scene_path
+
+pytestmark = pytest.mark.gpu
+
+
+def _cam():
+    return vr.Pinhole_Camera(CAM_POS, main_view_dir(), FOV)
+
+
+def _render(integ_cls, scene, W, H, device, **kw):
+    img = vr.Image(W, H)
+    integ = integ_cls(_cam(), device=device, **kw)
+    integ.render(scene, img)
+    return img.pixels.copy(), integ.last_stats
+
+
+@pytest.mark.parametrize("devices", [(0,), (0, 0), (0, 0, 0), (0, 0, 0, 0, 0, 0, 0, 0)])
+def test_group_render_equals_single_device(devices):
+    scene = vr.Scene.load_GMM(scene_path("50_random.txt"))
+    W, H = 100, 70
+    ref, _ = _render(vr.RayMarchingGaussians, scene, W, H, 0)
+    got, st = _render(vr.RayMarchingGaussians, scene, W, H, devices)
+    dev = vr.Device.get(devices)
+    assert dev.num_devices == len(devices)
+    assert dev.uses_rccl == (len(set(devices)) == len(devices))
+    assert np.array_equal(got, ref)
+    nt = vr.num_tiles(W, H)
+    per_rank = [dev.rank_stats(r)["pixels"] for r in range(len(devices))]
+    assert per_rank == [len(range(r, nt, len(devices))) * 256 for r in range(len(devices))]
+    assert st["pixels"] == nt * 256
+
+
+def test_group_with_more_ranks_than_tiles():
+    scene = vr.Scene.load_GMM(scene_path("2_gaussian.txt"))
+    ref, _ = _render(vr.RayMarchingGaussians, scene, 20, 12, 0)  # 2 tiles
+    got, _ = _render(vr.RayMarchingGaussians, scene, 20, 12, (0, 0, 0))
+    assert np.array_equal(got, ref)
+
+
+@pytest.mark.parametrize("integ,kw", [(vr.MultiScatterGaussians, {"samples": 4}),
+                                      (vr.PureRayMarching, {"env_samples": 4})])
+def test_group_other_integrators(integ, kw):
+    scene = vr.Scene.load_GMM(scene_path("many_gaussians.txt"))
+    ref, _ = _render(integ, scene, 48, 40, 0, **kw)
+    got, _ = _render(integ, scene, 48, 40, (0, 0), **kw)
+    assert np.array_equal(got, ref)
+
+
+def test_group_overflow_fails_loudly():
+    n = 80
+    mean = np.tile(np.array([[0.0, 1.0, 0.0]], np.float32), (n, 1))
+    sig = np.linspace(0.3, 0.4, n)
+    cov = np.stack([sig ** 2, 0 * sig, 0 * sig, sig ** 2, 0 * sig, sig ** 2], 1).astype(np.float32)
+    scene = vr.Scene.from_gaussians(mean, cov, np.full(n, 1e-4, np.float32), np.full(n, 0.5, np.float32),
+                                    [vr.Light([0, 5, 0], [1, 1, 1])])
+    with pytest.raises(vr.VRError) as e:
+        _render(vr.RayMarchingGaussians, scene, 16, 16, (0, 0), env_samples=1)
+    assert e.value.status == 6
+
+
+@pytest.mark.parametrize("devices", ["0", "0,0,0"])
+def test_cpp_driver_on_a_group(tmp_path, devices):
+    tools = os.path.join(ROOT, "tools")
+    r = subprocess.run(["make", "-C", tools], capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr
+    outs = {}
+    for tag, extra in (("single", []), ("group", ["--devices", devices])):
+        out = tmp_path / f"{tag}.ppm"
+        r = subprocess.run([os.path.join(tools, "vol_render"), "--scene", scene_path("many_gaussians.txt"), "--size",
+                            "96x64", "--out", str(out), *extra], capture_output=True, text=True, timeout=300)
+        assert r.returncode == 0, r.stdout + r.stderr
+        outs[tag] = (read_ppm(str(out)), r.stdout)
+    ndev = len(devices.split(","))
+    assert f"{ndev} device(s)" in outs["group"][1]
+    assert ("RCCL gather" in outs["group"][1]) == (ndev == 1)
+    assert np.array_equal(outs["single"][0], outs["group"][0])

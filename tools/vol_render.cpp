@@ -5,8 +5,10 @@
 //              [--integrator gaussians|pure|spheres|test|freeflight|multiscatter] [--step 0.01] [--env 20]
 //              [--spp N] (free-flight paths per pixel; main.cpp:42 renders MultiScatterGaussians at 256)
 //              [--camera pinhole|ortho] [--pos 0,1,6] [--lookat 0,1,0] [--fov 0.785398]
-//              [--out output.ppm] [--dump-rays N]
+//              [--out output.ppm] [--dump-rays N] [--devices 0,1,...]
 //
+// --devices renders on a multi-GPU context over exactly these GPUs (tiles split, RCCL gather); by
+// default every visible GPU is used (one GPU: a plain single-device context).
 // --dump-rays N prints the first N primary rays (host only, no GPU) — used by the CPU tests.
 #include <chrono>
 #include <cstdio>
@@ -30,6 +32,7 @@ int main(int argc, char** argv) try {
     unsigned W = 512, H = 512;
     float step = 0.01f, fov = 0.25f * std::numbers::pi_v<float>;
     int env = -1, dump = 0, spp = -1;
+    std::vector<int> devices;
     Eigen::Vector3f pos(0, 1, 6), lookat(0, 1, 0);
     for (int i = 1; i < argc; ++i) {
         std::string a = argv[i];
@@ -51,6 +54,15 @@ int main(int argc, char** argv) try {
         else if (a == "--fov") fov = std::strtof(next(), nullptr);
         else if (a == "--out") out = next();
         else if (a == "--dump-rays") dump = std::atoi(next());
+        else if (a == "--devices") {
+            std::string v = next();
+            for (size_t p = 0; p <= v.size();) {
+                size_t q = v.find(',', p);
+                if (q == std::string::npos) q = v.size();
+                devices.push_back(std::stoi(v.substr(p, q - p)));
+                p = q + 1;
+            }
+        }
         else throw std::runtime_error("unknown argument " + a);
     }
     if (scene_path.empty()) throw std::runtime_error("--scene is required");
@@ -96,14 +108,16 @@ int main(int argc, char** argv) try {
     else if (integ == "multiscatter") integrator = std::make_unique<MultiScatterGaussians>(camera, spp < 0 ? 16 : spp);
     else throw std::runtime_error("unknown integrator " + integ);
 
+    if (!devices.empty()) integrator->set_devices(devices);
     Image image(W, H);
     auto t0 = std::chrono::high_resolution_clock::now();
     integrator->render(scene, image);
     auto t1 = std::chrono::high_resolution_clock::now();
     vr_render_stats st = integrator->stats();
-    std::printf("Render time: %.6f seconds (device %.3f ms, %lld pixels, %lld fallback)\n",
+    std::printf("Render time: %.6f seconds (device %.3f ms, %lld pixels, %lld fallback, %d device(s)%s)\n",
                 std::chrono::duration<double>(t1 - t0).count(), st.kernel_ms, (long long)st.pixels,
-                (long long)st.fallback_pixels);
+                (long long)st.fallback_pixels, vr_ctx_num_devices(integrator->context()),
+                vr_ctx_uses_rccl(integrator->context()) ? ", RCCL gather" : "");
     image.make_PPM(out);
     return 0;
 } catch (const std::exception& e) {
