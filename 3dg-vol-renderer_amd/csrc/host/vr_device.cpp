@@ -23,6 +23,17 @@ hipError_t launch_free_flight(const RenderArgs& A, uint32_t chunk_tiles, hipStre
 hipError_t launch_sfd_loss_diff(const uint32_t* bits0, const uint32_t* bits1, const float* lb, const float* lp, uint32_t npix,
                                 uint32_t n, double* out, hipStream_t stream);
 hipError_t gauss_record_cut(const RenderArgs& A, float budget, hipStream_t stream);
+struct LbvhResult {
+    GaussianRecord* gauss = nullptr;
+    uint32_t* order = nullptr;
+    BVHNode* nodes = nullptr;
+    HNode* hnodes = nullptr;
+    HNode4* hnodes4 = nullptr;
+    size_t num_nodes = 0, num_nodes4 = 0;
+    int max_depth = 0;
+};
+hipError_t lbvh_build(const GaussianRecord* d_rec, const float* d_boxes, uint32_t n, const float cmin[3], const float cmax[3],
+                      bool half, const float hc[3], float hs, hipStream_t s, LbvhResult& R);
 hipError_t launch_unshuffle(const float* slabs, uint32_t nslabs, uint32_t tiles_per_slab, uint32_t tiles_x, uint32_t W,
                             uint32_t H, float* img, hipStream_t stream);
 }  // namespace vr
@@ -94,6 +105,8 @@ struct vr_ctx {
     int64_t opt_half_nodes = 1;        // VR_OPT_HALF_NODES
     int64_t opt_secondary_budget = 1;  // VR_OPT_SECONDARY_BUDGET
     int64_t opt_ff_window0 = 8;        // VR_OPT_FF_WINDOW0
+    int64_t opt_device_bvh = 0;        // VR_OPT_DEVICE_BVH
+    bool last_upload_device_bvh = false;  // the current scene's tree came from the device builder
     vr_group* group = nullptr;         // vr_init_multi: the devices this context drives (host/vr_multi.cpp)
 };
 
@@ -263,6 +276,83 @@ vr_status upload_half_nodes(vr_ctx* c, const std::vector<BVHNode>& nodes) {
     }
     HIP_TRY(hipMalloc(&c->d_hnodes4, w4.size() * sizeof(HNode4)), "hipMalloc(wide nodes)");
     HIP_TRY(hipMemcpy(c->d_hnodes4, w4.data(), w4.size() * sizeof(HNode4), hipMemcpyHostToDevice), "hipMemcpy(wide nodes)");
+    return VR_OK;
+}
+
+// Neighbour lists rely on the 3.15-sigma boxes bounding {q <= kListR2}: true for positive definite
+// covariances with a finite inverse.
+bool lists_exact(const HostScene& s) {
+    for (const GaussianPre& p : s.pre) {
+        const double a = p.cov[0], b2 = p.cov[1], c2 = p.cov[2], d = p.cov[3], e = p.cov[4], f = p.cov[5];
+        const double m2 = a * d - b2 * b2;
+        const double det = a * (d * f - e * e) - b2 * (b2 * f - e * c2) + c2 * (b2 * e - d * c2);
+        bool ok = a > 0.0 && m2 > 0.0 && det > 0.0;
+        for (int k = 0; k < 6; ++k) ok = ok && std::isfinite(p.inv_cov[k]);
+        if (!ok) return false;
+    }
+    return true;
+}
+
+// Scenes at least this large may use the device builder (VR_OPT_DEVICE_BVH); smaller ones build on
+// the host in well under a millisecond.
+constexpr size_t kDeviceBvhMin = 256;
+
+// Device BVH build (kernels/vr_lbvh.hip): records and boxes go up in scene order, the device sorts
+// them by Morton code and emits the child-pair, half-precision and 4-wide trees. VR_ERR_UNSUPPORTED:
+// the tree is deeper than the traversal stacks allow (the caller builds on the host instead).
+vr_status upload_device_bvh(vr_ctx* c, const HostScene& s, const std::vector<float>& boxes) {
+    const size_t N = s.pre.size();
+    std::vector<GaussianRecord> rec(N);
+    float cmin[3] = {INFINITY, INFINITY, INFINITY}, cmax[3] = {-INFINITY, -INFINITY, -INFINITY};
+    std::vector<float> ext(N);
+    for (size_t i = 0; i < N; ++i) {
+        const GaussianPre& p = s.pre[i];
+        rec[i] = GaussianRecord{p.mean[0], p.mean[1], p.mean[2], p.density, p.inv_cov[0], p.inv_cov[1], p.inv_cov[2],
+                                p.inv_cov[3], p.inv_cov[4], p.inv_cov[5], p.norm, p.albedo};
+        float e = 0.0f;
+        for (int k = 0; k < 3; ++k) {
+            const float ce = 0.5f * (boxes[6 * i + k] + boxes[6 * i + 3 + k]);
+            cmin[k] = std::min(cmin[k], ce);
+            cmax[k] = std::max(cmax[k], ce);
+            e = std::max(e, boxes[6 * i + 3 + k] - boxes[6 * i + k]);
+        }
+        ext[i] = e;
+    }
+    // half-precision trees: the host rule (median leaf box >= 3 % of the half extent) with the
+    // primitive boxes (leaves hold up to kLeafMax of them) standing in for the leaf boxes
+    double half = 0.0;
+    for (int k = 0; k < 3; ++k) {
+        c->hn_center[k] = 0.5f * (c->bmin[k] + c->bmax[k]);
+        half = std::max(half, 0.5 * ((double)c->bmax[k] - (double)c->bmin[k]));
+    }
+    bool use_half = c->opt_half_nodes && half > 0.0 && std::isfinite(half);
+    if (use_half) {
+        c->hn_scale = (float)(1.0 / half);
+        std::nth_element(ext.begin(), ext.begin() + N / 2, ext.end());
+        use_half = ext[N / 2] >= 0.03 * half;
+    }
+    GaussianRecord* d_rec = nullptr;
+    float* d_boxes = nullptr;
+    HIP_TRY(hipMalloc(&d_rec, N * sizeof(GaussianRecord)), "hipMalloc(records)");
+    HIP_TRY(hipMalloc(&d_boxes, N * 24), "hipMalloc(boxes)");
+    HIP_TRY(hipMemcpyAsync(d_rec, rec.data(), N * sizeof(GaussianRecord), hipMemcpyHostToDevice, c->stream), "hipMemcpy(records)");
+    HIP_TRY(hipMemcpyAsync(d_boxes, boxes.data(), N * 24, hipMemcpyHostToDevice, c->stream), "hipMemcpy(boxes)");
+    LbvhResult R;
+    hipError_t e = lbvh_build(d_rec, d_boxes, (uint32_t)N, cmin, cmax, use_half, c->hn_center, c->hn_scale, c->stream, R);
+    (void)hipFree(d_rec);
+    (void)hipFree(d_boxes);
+    if (e == hipErrorNotSupported) return fail(VR_ERR_UNSUPPORTED, "device BVH deeper than the traversal stacks");
+    if (e != hipSuccess) return hip_fail(e, "device BVH build");
+    c->d_gauss = R.gauss;
+    c->d_order = R.order;
+    c->d_nodes = R.nodes;
+    c->d_hnodes = R.hnodes;
+    c->d_hnodes4 = R.hnodes4;
+    c->num_nodes = R.num_nodes;
+    c->bvh_depth = R.max_depth;
+    c->num_prims = (int32_t)N;
+    c->list_ok = lists_exact(s);
+    c->last_upload_device_bvh = true;
     return VR_OK;
 }
 
@@ -791,6 +881,16 @@ vr_status vr_upload_scene(vr_ctx* c, const vr_scene* sc) {
                 c->bmax[k] = std::max(c->bmax[k], boxes[6 * i + 3 + k]);
             }
         }
+        c->last_upload_device_bvh = false;
+        if (c->opt_device_bvh && N >= kDeviceBvhMin) {
+            vr_status ds = upload_device_bvh(c, s, boxes);
+            if (ds == VR_OK) {
+                c->has_scene = true;
+                return VR_OK;
+            }
+            if (ds != VR_ERR_UNSUPPORTED) return ds;  // UNSUPPORTED: too deep for the stacks -> host build
+            free_scene(c);
+        }
         BVHBuild b = build_bvh(boxes);
         if (b.max_depth > kMaxDepth + 1) return fail(VR_ERR_OVERFLOW, "BVH deeper than the traversal stack");
         std::vector<GaussianRecord> rec(std::max<size_t>(N, 1));
@@ -812,18 +912,7 @@ vr_status vr_upload_scene(vr_ctx* c, const vr_scene* sc) {
         c->num_prims = (int32_t)N;
         c->bvh_depth = b.max_depth;
         if (vr_status hs = upload_half_nodes(c, b.nodes); hs != VR_OK) return hs;
-        // neighbour lists rely on the 3.15-sigma boxes bounding {q <= kListR2}: true for positive
-        // definite covariances with a finite inverse
-        c->list_ok = true;
-        for (size_t i = 0; i < N && c->list_ok; ++i) {
-            const GaussianPre& p = s.pre[i];
-            const double a = p.cov[0], b2 = p.cov[1], c2 = p.cov[2], d = p.cov[3], e = p.cov[4], f = p.cov[5];
-            const double m2 = a * d - b2 * b2;
-            const double det = a * (d * f - e * e) - b2 * (b2 * f - e * c2) + c2 * (b2 * e - d * c2);
-            bool ok = a > 0.0 && m2 > 0.0 && det > 0.0;
-            for (int k = 0; k < 6; ++k) ok = ok && std::isfinite(p.inv_cov[k]);
-            c->list_ok = ok;
-        }
+        c->list_ok = lists_exact(s);
         c->num_nodes = b.nodes.size();
     } else {
         const size_t N = s.spheres.size();
@@ -1038,6 +1127,10 @@ vr_status vr_set_option(vr_ctx* c, int32_t option, int64_t value) {
             if (value < 1 || value > kFFHitCap) return fail(VR_ERR_INVALID, "VR_OPT_FF_WINDOW0 must be in [1, 128]");
             c->opt_ff_window0 = value;
             return VR_OK;
+        case VR_OPT_DEVICE_BVH:
+            if (value != 0 && value != 1) return fail(VR_ERR_INVALID, "VR_OPT_DEVICE_BVH must be 0 or 1");
+            c->opt_device_bvh = value;
+            return VR_OK;
         case VR_OPT_RECORD_CAPACITY:
             if ((value != 0 && value < 4096) || value > 0x3fffffff)
                 return fail(VR_ERR_INVALID, "VR_OPT_RECORD_CAPACITY must be 0 or in [4096, 2^30)");
@@ -1056,6 +1149,7 @@ vr_status vr_get_option(vr_ctx* c, int32_t option, int64_t* value) {
         case VR_OPT_SECONDARY_BUDGET: *value = c->opt_secondary_budget; return VR_OK;
         case VR_OPT_FF_WINDOW0: *value = c->opt_ff_window0; return VR_OK;
         case VR_OPT_RECORD_CAPACITY: *value = (int64_t)c->rec_hint; return VR_OK;
+        case VR_OPT_DEVICE_BVH: *value = c->opt_device_bvh; return VR_OK;
         default: return fail(VR_ERR_INVALID, "vr_get_option: unknown option " + std::to_string(option));
     }
 }

@@ -372,13 +372,14 @@ class Device:
         return xy[:n.value].astype(np.int32)
 
     OPTIONS = {"half_nodes": L.VR_OPT_HALF_NODES, "secondary_budget": L.VR_OPT_SECONDARY_BUDGET,
-               "ff_window0": L.VR_OPT_FF_WINDOW0, "record_capacity": L.VR_OPT_RECORD_CAPACITY}
+               "ff_window0": L.VR_OPT_FF_WINDOW0, "record_capacity": L.VR_OPT_RECORD_CAPACITY,
+               "device_bvh": L.VR_OPT_DEVICE_BVH}
 
     def set_option(self, name, value):
         """vr_set_option (include/vr_hip.h): explicit per-context tuning (half_nodes applies at the
         next upload, so the scene is re-uploaded)."""
         check(lib().vr_set_option(self._h, self.OPTIONS[name], int(value)))
-        if name == "half_nodes":
+        if name in ("half_nodes", "device_bvh"):
             self._scene_key = None
 
     def get_option(self, name):

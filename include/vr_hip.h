@@ -270,12 +270,16 @@ typedef enum vr_option {
                                     budget); 0: the frame-wide cut-off ln(1/t_eps) + ln(1000) only. */
     VR_OPT_FF_WINDOW0 = 3,       /* free-flight integrators: first hit-window capacity, 1..128 (default
                                     8; doubles per window). Results do not depend on it. */
-    VR_OPT_RECORD_CAPACITY = 4   /* scatter-record buffer capacity (records; the active-list pool gets the
+    VR_OPT_RECORD_CAPACITY = 4,  /* scatter-record buffer capacity (records; the active-list pool gets the
                                     same) carried into the next frame: 0 (size it at the next frame, with one
-                                    host sync) or >= 4096. The context normally sizes it
-                                    from earlier frames; setting it lets a test drive a frame over capacity
-                                    (reported, then rendered again with grown buffers). Results do not
-                                    depend on it. */
+                                    host sync) or >= 4096. The context normally sizes it from earlier frames;
+                                    setting it lets a test drive a frame over capacity (reported, then
+                                    rendered again with grown buffers). Results do not depend on it. */
+    VR_OPT_DEVICE_BVH = 5        /* 0 (default): vr_upload_scene builds the BVH on the host (binned SAH);
+                                    1: on the device (linear BVH: Morton sort + radix tree, kernels/
+                                    vr_lbvh.hip) for scenes of >= 256 Gaussians — the fast path for the
+                                    inverse loop's re-upload after every parameter update. Results are
+                                    identical up to summation order (the event set is tree-independent). */
 } vr_option;
 vr_status vr_set_option(vr_ctx* ctx, int32_t option, int64_t value);
 vr_status vr_get_option(vr_ctx* ctx, int32_t option, int64_t* value);
