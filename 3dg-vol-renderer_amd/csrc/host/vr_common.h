@@ -77,4 +77,9 @@ vr_status group_render(vr_group* g, const vr_camera* cam, const vr_render_params
 vr_status group_set_option(vr_group* g, int32_t option, int64_t value);
 vr_status group_synchronize(vr_group* g);
 vr_status group_stats(vr_group* g, vr_render_stats* out);
+// device side of the inverse loop (host/vr_device.cpp)
+vr_status sfd_set_reference(vr_ctx* c, const float* I_ref, uint32_t W, uint32_t H);
+vr_status sfd_render(vr_ctx* c, const vr_camera* cam, const vr_render_params* p, uint32_t W, uint32_t H, int32_t slot,
+                     int which, float* loss_host, float* rgb);
+vr_status sfd_loss_diff_device(vr_ctx* c, uint32_t npix, double* out, size_t n);
 }  // namespace vr

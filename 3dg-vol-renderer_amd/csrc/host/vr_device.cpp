@@ -23,6 +23,7 @@ hipError_t launch_free_flight(const RenderArgs& A, uint32_t chunk_tiles, hipStre
 hipError_t launch_sfd_loss_diff(const uint32_t* bits0, const uint32_t* bits1, const float* lb, const float* lp, uint32_t npix,
                                 uint32_t n, double* out, hipStream_t stream);
 hipError_t gauss_record_cut(const RenderArgs& A, float budget, hipStream_t stream);
+hipError_t launch_pixel_losses(const float* img, const float* ref, uint32_t npix, float* out, hipStream_t stream);
 struct LbvhResult {
     GaussianRecord* gauss = nullptr;
     uint32_t* order = nullptr;
@@ -97,6 +98,7 @@ struct vr_ctx {
     Buf rec_bits[2];                  // RECORD_PIXEL_GAUSSIANS bitsets (vr_render_record slots)
     uint32_t rec_npix[2] = {0, 0}, rec_n[2] = {0, 0};
     Buf sfd_tmp;                      // vr_sfd_loss_diff: losses + output
+    Buf sfd_ref, sfd_loss[2], sfd_out;  // device inverse loop (vr_sfd_optimize): I_ref, base / perturbed losses
     bool list_ok = false;  // all covariances positive definite: neighbour lists are exact
     int pcg_jump_n = -1;
     uint32_t* h_sizing = nullptr;  // pinned copy of rec_alloc for the sizing march of a context's first frame
@@ -838,7 +840,8 @@ void vr_destroy(vr_ctx* c) {
     if (c->h_sizing) (void)hipHostFree(c->h_sizing);
     for (vr_ctx::Buf* b : {&c->px_first, &c->px_T, &c->rec_pos, &c->rec_meta, &c->rec_next, &c->rec_act, &c->tr,
                            &c->rec_alloc, &c->rec_bloom, &c->slowq, &c->pcg_jump, &c->ray_next, &c->rec_list, &c->rec_nlist,
-                           &c->stack_ovf, &c->env_order, &c->rec_cut, &c->ff_scratch, &c->ff_path, &c->ff_sum, &c->rec_bits[0], &c->rec_bits[1], &c->sfd_tmp})
+                           &c->stack_ovf, &c->env_order, &c->rec_cut, &c->ff_scratch, &c->ff_path, &c->ff_sum, &c->rec_bits[0], &c->rec_bits[1], &c->sfd_tmp, &c->sfd_ref,
+                           &c->sfd_loss[0], &c->sfd_loss[1], &c->sfd_out})
         if (b->p) (void)hipFree(b->p);
     if (c->d_frame) (void)hipFree(c->d_frame);
     if (c->ev_start) (void)hipEventDestroy(c->ev_start);
@@ -1039,25 +1042,25 @@ vr_status vr_unshuffle_tiles_device(vr_ctx* c, const float* d_slabs, uint32_t ns
     return VR_OK;
 }
 
-vr_status vr_render_record(vr_ctx* c, const vr_camera* cam, const vr_render_params* p, uint32_t W, uint32_t H, float* rgb,
-                           int32_t slot) {
-    c = first_device(c);
-    if (!c || !rgb || !p) return fail(VR_ERR_INVALID, "vr_render_record: NULL argument");
-    if (slot != 0 && slot != 1) return fail(VR_ERR_INVALID, "vr_render_record: slot must be 0 or 1");
-    if (p->integrator != VR_MULTI_SCATTER)
-        return fail(VR_ERR_INVALID, "vr_render_record: MultiScatterGaussians only (integrator.h:532-536)");
+// A full frame into the context's device frame buffer; slot 0/1 records RECORD_PIXEL_GAUSSIANS
+// bitsets (MultiScatterGaussians only), slot -1 renders without recording.
+static vr_status render_frame_device(vr_ctx* c, const vr_camera* cam, const vr_render_params* p, uint32_t W, uint32_t H,
+                                     int32_t slot) {
     HIP_TRY(hipSetDevice(c->device), "hipSetDevice");
     RenderArgs A;
     vr_status st = fill_args(c, cam, p, W, H, A);
     if (st != VR_OK) return st;
-    const uint64_t npix = (uint64_t)W * H, words = ((uint64_t)c->num_prims + 31) / 32;
-    const size_t bytes = std::max<size_t>((size_t)(words * npix * 4), 4);
-    if ((st = grow(c->rec_bits[slot], bytes, "hipMalloc(pixel Gaussian bits)")) != VR_OK) return st;
-    HIP_TRY(hipMemsetAsync(c->rec_bits[slot].p, 0, bytes, c->stream), "hipMemsetAsync(bits)");
-    c->rec_npix[slot] = (uint32_t)npix;
-    c->rec_n[slot] = (uint32_t)c->num_prims;
-    A.rec_bits = (uint32_t*)c->rec_bits[slot].p;
-    A.rec_npix = (uint32_t)npix;
+    const uint64_t npix = (uint64_t)W * H;
+    if (slot >= 0) {
+        const uint64_t words = ((uint64_t)c->num_prims + 31) / 32;
+        const size_t bytes = std::max<size_t>((size_t)(words * npix * 4), 4);
+        if ((st = grow(c->rec_bits[slot], bytes, "hipMalloc(pixel Gaussian bits)")) != VR_OK) return st;
+        HIP_TRY(hipMemsetAsync(c->rec_bits[slot].p, 0, bytes, c->stream), "hipMemsetAsync(bits)");
+        c->rec_npix[slot] = (uint32_t)npix;
+        c->rec_n[slot] = (uint32_t)c->num_prims;
+        A.rec_bits = (uint32_t*)c->rec_bits[slot].p;
+        A.rec_npix = (uint32_t)npix;
+    }
     size_t fb = npix * 3 * sizeof(float);
     if (fb > c->frame_cap) {
         if (c->d_frame) (void)hipFree(c->d_frame);
@@ -1070,9 +1073,19 @@ vr_status vr_render_record(vr_ctx* c, const vr_camera* cam, const vr_render_para
     A.num_tiles = vr_num_tiles(W, H);
     A.packed = 0;
     A.out = c->d_frame;
-    st = render_sync(c, A, p, false, "paths exceeded the per-path capacity (NaN)");
+    return render_sync(c, A, p, false, "pixels / paths exceeded a per-ray capacity (NaN)");
+}
+
+vr_status vr_render_record(vr_ctx* c, const vr_camera* cam, const vr_render_params* p, uint32_t W, uint32_t H, float* rgb,
+                           int32_t slot) {
+    c = first_device(c);
+    if (!c || !rgb || !p) return fail(VR_ERR_INVALID, "vr_render_record: NULL argument");
+    if (slot != 0 && slot != 1) return fail(VR_ERR_INVALID, "vr_render_record: slot must be 0 or 1");
+    if (p->integrator != VR_MULTI_SCATTER)
+        return fail(VR_ERR_INVALID, "vr_render_record: MultiScatterGaussians only (integrator.h:532-536)");
+    vr_status st = render_frame_device(c, cam, p, W, H, slot);
     if (st != VR_OK) return st;
-    HIP_TRY(hipMemcpy(rgb, c->d_frame, fb, hipMemcpyDeviceToHost), "hipMemcpy(frame)");
+    HIP_TRY(hipMemcpy(rgb, c->d_frame, (size_t)W * H * 3 * sizeof(float), hipMemcpyDeviceToHost), "hipMemcpy(frame)");
     return VR_OK;
 }
 
@@ -1110,6 +1123,62 @@ vr_status vr_sfd_loss_diff(vr_ctx* c, const float* loss_base, const float* loss_
     HIP_TRY(hipStreamSynchronize(c->stream), "sfd");
     return VR_OK;
 }
+
+}  // extern "C"
+
+namespace vr {
+
+// ---- device side of the inverse loop (host/vr_inverse.cpp) ----
+vr_status sfd_set_reference(vr_ctx* c, const float* I_ref, uint32_t W, uint32_t H) {
+    c = first_device(c);
+    HIP_TRY(hipSetDevice(c->device), "hipSetDevice");
+    const size_t npix = (size_t)W * H;
+    vr_status st;
+    if ((st = grow(c->sfd_ref, npix * 12, "hipMalloc(I_ref)")) != VR_OK) return st;
+    for (auto& b : c->sfd_loss)
+        if ((st = grow(b, npix * 4, "hipMalloc(pixel losses)")) != VR_OK) return st;
+    HIP_TRY(hipMemcpy(c->sfd_ref.p, I_ref, npix * 12, hipMemcpyHostToDevice), "hipMemcpy(I_ref)");
+    return VR_OK;
+}
+
+// One forward render of the loop (slot 0/1: recorded, -1: plain) and its per-pixel L1 losses against
+// the reference image into device loss buffer `which`; loss_host (W*H floats) receives a copy, and
+// rgb (3*W*H floats, may be NULL) the frame.
+vr_status sfd_render(vr_ctx* c, const vr_camera* cam, const vr_render_params* p, uint32_t W, uint32_t H, int32_t slot,
+                     int which, float* loss_host, float* rgb) {
+    c = first_device(c);
+    vr_status st = render_frame_device(c, cam, p, W, H, slot);
+    if (st != VR_OK) return st;
+    const uint32_t npix = W * H;
+    HIP_TRY(launch_pixel_losses(c->d_frame, (const float*)c->sfd_ref.p, npix, (float*)c->sfd_loss[which].p, c->stream),
+            "pixel losses");
+    HIP_TRY(hipMemcpyAsync(loss_host, c->sfd_loss[which].p, (size_t)npix * 4, hipMemcpyDeviceToHost, c->stream),
+            "hipMemcpyAsync(losses)");
+    if (rgb)
+        HIP_TRY(hipMemcpyAsync(rgb, c->d_frame, (size_t)npix * 12, hipMemcpyDeviceToHost, c->stream), "hipMemcpyAsync(frame)");
+    HIP_TRY(hipStreamSynchronize(c->stream), "sfd render");
+    return VR_OK;
+}
+
+// out[g] = sum over the union of the pixels recorded for g in slots 0 and 1 of loss[1] - loss[0].
+vr_status sfd_loss_diff_device(vr_ctx* c, uint32_t npix, double* out, size_t n) {
+    c = first_device(c);
+    vr_status st = grow(c->sfd_out, std::max<size_t>(n, 1) * 8, "hipMalloc(sfd)");
+    if (st != VR_OK) return st;
+    HIP_TRY(hipMemsetAsync(c->sfd_out.p, 0, n * 8, c->stream), "hipMemsetAsync");
+    if (n > 0)
+        HIP_TRY(launch_sfd_loss_diff((const uint32_t*)c->rec_bits[0].p, (const uint32_t*)c->rec_bits[1].p,
+                                     (const float*)c->sfd_loss[0].p, (const float*)c->sfd_loss[1].p, npix, (uint32_t)n,
+                                     (double*)c->sfd_out.p, c->stream),
+                "sfd launch");
+    HIP_TRY(hipMemcpyAsync(out, c->sfd_out.p, n * 8, hipMemcpyDeviceToHost, c->stream), "hipMemcpyAsync");
+    HIP_TRY(hipStreamSynchronize(c->stream), "sfd");
+    return VR_OK;
+}
+
+}  // namespace vr
+
+extern "C" {
 
 vr_status vr_set_option(vr_ctx* c, int32_t option, int64_t value) {
     if (!c) return fail(VR_ERR_INVALID, "vr_set_option: NULL ctx");

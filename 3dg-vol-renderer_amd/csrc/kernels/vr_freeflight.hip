@@ -578,7 +578,24 @@ __global__ void __launch_bounds__(256) sfd_loss_diff_kernel(const uint32_t* __re
     }
 }
 
+// compute_pixel_losses (inverse_integrator.h:21-30): per-pixel L1 over RGB, d.cwiseAbs().sum()
+// (Eigen's 3-term reduction: |d0| + (|d1| + |d2|)).
+__global__ void __launch_bounds__(256) pixel_loss_kernel(const float* __restrict__ img, const float* __restrict__ ref,
+                                                         uint32_t npix, float* __restrict__ out) {
+    const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= npix) return;
+    const float d0 = img[3 * (size_t)p] - ref[3 * (size_t)p];
+    const float d1 = img[3 * (size_t)p + 1] - ref[3 * (size_t)p + 1];
+    const float d2 = img[3 * (size_t)p + 2] - ref[3 * (size_t)p + 2];
+    out[p] = fabsf(d0) + (fabsf(d1) + fabsf(d2));
+}
+
 }  // namespace dev
+
+hipError_t launch_pixel_losses(const float* img, const float* ref, uint32_t npix, float* out, hipStream_t stream) {
+    hipLaunchKernelGGL(dev::pixel_loss_kernel, dim3((npix + 255) / 256), dim3(256), 0, stream, img, ref, npix, out);
+    return hipGetLastError();
+}
 
 hipError_t launch_sfd_loss_diff(const uint32_t* bits0, const uint32_t* bits1, const float* lb, const float* lp, uint32_t npix,
                                 uint32_t n, double* out, hipStream_t stream) {

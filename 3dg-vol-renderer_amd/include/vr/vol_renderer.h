@@ -17,6 +17,8 @@
 #include <atomic>
 #include <cstdint>
 #include <cstring>
+#include <filesystem>
+#include <iostream>
 #include <map>
 #include <memory>
 #include <mutex>
@@ -186,6 +188,9 @@ public:
     GaussianMixtureModel() = default;
     explicit GaussianMixtureModel(const std::vector<Gaussian>& gs) : gaussians(gs) {}
     size_t get_num_gaussians() const { return gaussians.size(); }
+    bool empty() const { return gaussians.empty(); }
+    // gmm.h:583-628 (native vr_gmm_pack_parameters)
+    void pack_parameters(std::vector<float>& out) const;
 };
 
 struct Sphere {
@@ -273,6 +278,8 @@ struct Scene {
     }
     // process-unique id of the current native copy (a freed handle's address may be reused)
     uint64_t native_version() const { return native_version_; }
+    // A Scene owning a native scene handle (e.g. vr_gmm_apply_parameters' result).
+    static Scene adopt_native(vr_scene* h) { return from_native(h); }
 
 private:
     mutable std::shared_ptr<vr_scene> native_;
@@ -377,6 +384,71 @@ public:
 };
 
 // ---------------------------------------------------------------------------------------------
+// gmm.h:583-706: GMM <-> feature vector (11 floats per Gaussian), native (host/vr_inverse.cpp)
+// ---------------------------------------------------------------------------------------------
+namespace vr_cpp {
+inline vr_scene* gaussians_native(const GaussianMixtureModel& g) {
+    vr_scene* h = nullptr;
+    check(vr_scene_create(VR_VOLUME_GAUSSIANS, &h));
+    std::vector<vr_gaussian> r;
+    r.reserve(g.gaussians.size());
+    for (const Gaussian& x : g.gaussians) r.push_back(x.to_record());
+    vr_status st = vr_scene_add_gaussians(h, r.data(), r.size());
+    if (st != VR_OK) {
+        vr_scene_destroy(h);
+        check(st);
+    }
+    return h;
+}
+}  // namespace vr_cpp
+
+inline void GaussianMixtureModel::pack_parameters(std::vector<float>& out) const {
+    std::unique_ptr<vr_scene, void (*)(vr_scene*)> h(vr_cpp::gaussians_native(*this), &vr_scene_destroy);
+    out.assign(gaussians.size() * 11, 0.0f);
+    vr_cpp::check(vr_gmm_pack_parameters(h.get(), out.data(), out.size()));
+}
+
+// gmm.h:634-674: rebuild every Gaussian of gmm from params (throws on a size mismatch, :637)
+inline void apply_params_to_gmm_local(const std::vector<float>& params, GaussianMixtureModel& gmm) {
+    std::unique_ptr<vr_scene, void (*)(vr_scene*)> base(vr_cpp::gaussians_native(gmm), &vr_scene_destroy);
+    vr_scene* out = nullptr;
+    vr_cpp::check(vr_gmm_apply_parameters(base.get(), params.data(), params.size(), &out));
+    Scene s = Scene::adopt_native(out);
+    gmm = (*s.gmm)[0];
+}
+
+// gmm.h:678-706
+inline std::vector<float> make_default_eps_for_params(const std::vector<float>& base_params) {
+    std::vector<float> eps(base_params.size());
+    vr_cpp::check(vr_gmm_default_eps(eps.data(), eps.size()));
+    return eps;
+}
+
+// optimizer.h:13-55 — AdamOptimizer (the step is vr_adam_step)
+class AdamOptimizer {
+public:
+    AdamOptimizer(size_t ndim, float lr = 1e-3f, float beta1 = 0.9f, float beta2 = 0.999f, float eps = 1e-8f)
+        : m(ndim, 0.0f), v(ndim, 0.0f), lr(lr), beta1(beta1), beta2(beta2), eps(eps), t(0) {}
+    bool step(std::vector<float>& params, const std::vector<float>& grads) {
+        if (params.size() != grads.size() || params.size() != m.size() || params.size() != v.size()) return false;
+        ++t;
+        vr_cpp::check(vr_adam_step(params.data(), grads.data(), m.data(), v.data(), params.size(), t, lr, beta1, beta2, eps));
+        return true;
+    }
+    void reset_state() {
+        std::fill(m.begin(), m.end(), 0.0f);
+        std::fill(v.begin(), v.end(), 0.0f);
+        t = 0;
+    }
+    size_t dim() const { return m.size(); }
+
+private:
+    std::vector<float> m, v;
+    float lr, beta1, beta2, eps;
+    int t;
+};
+
+// ---------------------------------------------------------------------------------------------
 // integrator.h:49-57 and the device integrators
 // ---------------------------------------------------------------------------------------------
 class Integrator {
@@ -422,20 +494,37 @@ public:
     }
     void render(const Scene& scene, Image& image) override {
         vr_ctx* ctx = context();
-        // re-upload when the scene (or the scene object) changed since the last render on this device
-        static std::mutex mu;
-        static std::map<vr_ctx*, std::pair<const void*, uint64_t>> uploaded;  // per device context
-        vr_scene* ns = scene.native();
-        {
-            std::lock_guard<std::mutex> lock(mu);
-            auto it = uploaded.find(ctx);
-            if (it == uploaded.end() || it->second.first != (const void*)ns || it->second.second != scene.native_version()) {
-                vr_cpp::check(vr_upload_scene(ctx, ns));
-                uploaded[ctx] = {ns, scene.native_version()};
-            }
-        }
+        upload(ctx, scene);
         vr_cpp::check(vr_render(ctx, &camera->state(), &params_, image.get_width(), image.get_height(), image.data()));
     }
+    // re-upload when the scene (or the scene object) changed since the last upload to this context
+    static void upload(vr_ctx* ctx, const Scene& scene) {
+        vr_scene* ns = scene.native();
+        std::lock_guard<std::mutex> lock(upload_mutex());
+        auto& uploaded = upload_cache();
+        auto it = uploaded.find(ctx);
+        if (it == uploaded.end() || it->second.first != (const void*)ns || it->second.second != scene.native_version()) {
+            vr_cpp::check(vr_upload_scene(ctx, ns));
+            uploaded[ctx] = {ns, scene.native_version()};
+        }
+    }
+    // a context's scene was replaced behind upload()'s back (vr_sfd_optimize re-uploads): forget it
+    static void forget(vr_ctx* ctx) {
+        std::lock_guard<std::mutex> lock(upload_mutex());
+        upload_cache().erase(ctx);
+    }
+
+private:
+    static std::mutex& upload_mutex() {
+        static std::mutex mu;
+        return mu;
+    }
+    static std::map<vr_ctx*, std::pair<const void*, uint64_t>>& upload_cache() {  // per device context
+        static std::map<vr_ctx*, std::pair<const void*, uint64_t>> uploaded;
+        return uploaded;
+    }
+
+public:
     vr_render_stats stats() const {
         vr_render_stats s{};
         vr_cpp::check(vr_get_stats(context(), &s));
@@ -483,6 +572,95 @@ public:
         params_.min_bounces = min_bounces;
     }
     void set_num_samples(int n) { params_.num_samples = n; }  // integrator.h:719
+    using HipIntegrator::render;
+    // integrator.h:532-536 with RECORD_PIXEL_GAUSSIANS: per_pixel_gaussians[y * W + x] receives the
+    // sorted indices of the Gaussians recorded at that pixel (integrator.h:616-644, 700-705).
+    void render(const Scene& scene, Image& image, std::vector<std::vector<uint32_t>>* per_pixel_gaussians) {
+        if (!per_pixel_gaussians) return render(scene, image);
+        vr_ctx* ctx = context();
+        upload(ctx, scene);
+        vr_cpp::check(vr_render_record(ctx, &camera->state(), &params_, image.get_width(), image.get_height(), image.data(), 0));
+        const size_t npix = (size_t)image.get_width() * image.get_height(), n = scene.get_num_primitives();
+        const size_t words = (n + 31) / 32;
+        std::vector<uint32_t> bits(words * npix);
+        vr_cpp::check(vr_get_pixel_gaussians(ctx, 0, bits.data(), bits.size()));
+        per_pixel_gaussians->assign(npix, {});
+        for (size_t w = 0; w < words; ++w)
+            for (size_t p = 0; p < npix; ++p)
+                for (uint32_t b = bits[w * npix + p]; b; b &= b - 1)
+                    (*per_pixel_gaussians)[p].push_back((uint32_t)(32 * w + __builtin_ctz(b)));
+    }
+    int num_samples() const { return params_.num_samples; }
+};
+
+// ---------------------------------------------------------------------------------------------
+// inverse_integrator.h:34-246 — the stochastic finite-difference inverse loop (vr_sfd_optimize)
+// ---------------------------------------------------------------------------------------------
+class InverseIntegrator {
+protected:
+    const std::shared_ptr<Camera> camera;
+
+public:
+    InverseIntegrator(const std::shared_ptr<Camera>& camera) : camera(camera) {}
+    virtual ~InverseIntegrator() = default;
+    virtual bool optimize(Scene scene_initial, const Image& I_ref) = 0;
+};
+
+// inverse_integrator.h:52-57, plus the run's sign-vector seed, final-render samples (:230) and image
+// directory (the reference writes ./sfd_output; "" writes nothing)
+struct SFDDConfig {
+    int max_iters = 1000;
+    int save_every = 25;
+    int num_stoch_samples = 4;
+    float lr = 1e-2f;
+    uint64_t seed = 0;
+    int final_samples = 16384;
+    std::string out_dir = "./sfd_output";
+};
+
+class StochasticFiniteDiffInverseIntegrator : public InverseIntegrator {
+public:
+    StochasticFiniteDiffInverseIntegrator(const std::shared_ptr<Camera>& cam,
+                                          const std::shared_ptr<MultiScatterGaussians>& forward_integrator,
+                                          const SFDDConfig& cfg = SFDDConfig())
+        : InverseIntegrator(cam), forward_integrator(forward_integrator), cfg(cfg) {}
+
+    bool optimize(Scene scene_initial, const Image& I_ref) override {
+        const size_t n = scene_initial.get_num_primitives();
+        if (n == 0) return false;  // "Scene has no GMM." (:71-74)
+        params_.assign(11 * n, 0.0f);
+        history_.assign(std::max(cfg.max_iters, 0), 0.0);
+        grads_.assign(11 * n, 0.0);
+        final_image_ = Image(I_ref.get_width(), I_ref.get_height());
+        vr_sfd_config c{cfg.max_iters, cfg.save_every, cfg.num_stoch_samples, cfg.lr, cfg.seed, cfg.final_samples,
+                        cfg.out_dir.c_str()};
+        vr_sfd_result r{params_.data(), history_.data(), grads_.data(), final_image_.data(), 0.0};
+        if (!cfg.out_dir.empty()) std::filesystem::create_directories(cfg.out_dir);
+        vr_ctx* ctx = forward_integrator->context();
+        vr_status st = vr_sfd_optimize(ctx, &camera->state(), &forward_integrator->params(), scene_initial.native(),
+                                       I_ref.data(), I_ref.get_width(), I_ref.get_height(), &c, &r);
+        HipIntegrator::forget(ctx);  // the context now holds the last parameter set
+        if (st != VR_OK) {
+            std::cerr << "[SFD] " << vr_last_error() << std::endl;
+            return false;
+        }
+        final_loss_ = r.final_loss;
+        if (cfg.final_samples > 0) forward_integrator->set_num_samples(cfg.final_samples);  // as the reference leaves it
+        return true;
+    }
+    const std::vector<float>& parameters() const { return params_; }
+    const std::vector<double>& loss_history() const { return history_; }
+    const std::vector<double>& last_gradients() const { return grads_; }
+    double final_loss() const { return final_loss_; }
+    const Image& final_image() const { return final_image_; }
+
+private:
+    std::shared_ptr<MultiScatterGaussians> forward_integrator;
+    SFDDConfig cfg;
+    std::vector<float> params_;
+    std::vector<double> history_, grads_;
+    double final_loss_ = -1.0;
+    Image final_image_{1, 1};
 };
 
 // integrator.h:65-94 — TestIntegrator(camera)

@@ -60,6 +60,18 @@ class vr_render_stats(ctypes.Structure):
                 ("record_overflow", ctypes.c_int64)]
 
 
+class vr_sfd_config(ctypes.Structure):
+    _fields_ = [("max_iters", ctypes.c_int32), ("save_every", ctypes.c_int32), ("num_stoch_samples", ctypes.c_int32),
+                ("lr", ctypes.c_float), ("seed", ctypes.c_uint64), ("final_samples", ctypes.c_int32),
+                ("out_dir", ctypes.c_char_p)]
+
+
+class vr_sfd_result(ctypes.Structure):
+    _fields_ = [("params", ctypes.POINTER(ctypes.c_float)), ("loss_history", ctypes.POINTER(ctypes.c_double)),
+                ("last_grads", ctypes.POINTER(ctypes.c_double)), ("final_image", ctypes.POINTER(ctypes.c_float)),
+                ("final_loss", ctypes.c_double)]
+
+
 # name -> (restype, argtypes). Every symbol declared in include/vr_hip.h.
 P = ctypes.c_void_p
 PP = ctypes.POINTER(ctypes.c_void_p)
@@ -91,6 +103,14 @@ SIGNATURES = {
     "vr_image_write_ppm": (ST, [ctypes.c_char_p, FP, ctypes.c_uint32, ctypes.c_uint32]),
     "vr_image_read_ppm": (ST, [ctypes.c_char_p, FP, U32P, U32P]),
     "vr_init": (ST, [ctypes.c_int, PP]),
+    "vr_gmm_pack_parameters": (ST, [P, FP, ctypes.c_size_t]),
+    "vr_gmm_apply_parameters": (ST, [P, FP, ctypes.c_size_t, PP]),
+    "vr_gmm_default_eps": (ST, [FP, ctypes.c_size_t]),
+    "vr_adam_step": (ST, [FP, FP, FP, FP, ctypes.c_size_t, ctypes.c_int32, ctypes.c_float, ctypes.c_float,
+                          ctypes.c_float, ctypes.c_float]),
+    "vr_sfd_sign_vector": (ST, [ctypes.c_uint64, ctypes.c_uint64, FP, ctypes.c_size_t]),
+    "vr_sfd_optimize": (ST, [P, ctypes.POINTER(vr_camera), ctypes.POINTER(vr_render_params), P, FP, ctypes.c_uint32,
+                             ctypes.c_uint32, ctypes.POINTER(vr_sfd_config), ctypes.POINTER(vr_sfd_result)]),
     "vr_device_count": (ST, [ctypes.POINTER(ctypes.c_int32)]),
     "vr_init_multi": (ST, [ctypes.c_int32, ctypes.POINTER(ctypes.c_int32), PP]),
     "vr_ctx_num_devices": (ctypes.c_int32, [P]),

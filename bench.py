@@ -40,7 +40,7 @@ CONFIGS = {
     "c4": (4096, 4096, 1_000_000, "4096x4096, 1M Gaussians (make_random distribution)"),
     "c3": (1920, 1080, 100_000, "1920x1080, 100k Gaussians (make_random distribution)"),
     "c2": (512, 512, "1000_random.txt", "512x512, scenes/gaussians/1000_random.txt"),
-    "c5": (512, 512, 10_000, "512x512, 10k Gaussians (make_random distribution; 10k_random.txt's generator)"),
+    "c5": (512, 512, "10k_random.txt", "512x512, scenes/gaussians/10k_random.txt (BASELINE config 5)"),
 }
 LIGHTS = [((0.0, 5.0, 0.1), (50.0, 0.0, 0.0)), ((-3.0, 3.0, 0.3), (0.0, 30.0, 0.0)),
           ((3.0, 3.0, -0.2), (0.0, 0.0, 30.0))]  # scenes/gaussians/1000_random.txt:1-3
@@ -159,10 +159,11 @@ def cpu_baseline_ff(scene, W, H, multi, spp, budget_s, threads, log):
 
 def bench_sfd(args, scene, camera, W, H, t_setup):
     """Config 5: one step = one StochasticFiniteDiffInverseIntegrator iteration (inverse_integrator.h:
-    115-200): a recorded base render + num_stoch_samples (4) recorded perturbed renders of
-    MultiScatterGaussians at --spp paths/pixel, the device union-of-pixels loss statistic, Adam, and
-    the scene re-uploads (host BVH builds). Target image: the scene itself rendered at --spp; start:
-    densities scaled by 0.5. One GPU (the loop is sequential)."""
+    115-200) of the native loop (vr_sfd_optimize): a recorded base render + num_stoch_samples (4)
+    recorded perturbed renders of MultiScatterGaussians at --spp paths/pixel, per-pixel losses and the
+    union-of-pixels statistic on the device, Adam, and the re-uploads with the device BVH build.
+    Target image: the scene itself rendered at --spp; start: densities scaled by 0.5. One GPU (the
+    loop is sequential)."""
     from vr_amd import inverse as inv
     I_ref = vr.Image(W, H)
     vr.MultiScatterGaussians(camera, args.spp).render(scene, I_ref)

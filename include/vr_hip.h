@@ -256,6 +256,48 @@ vr_status vr_get_pixel_gaussians(vr_ctx* ctx, int32_t slot, uint32_t* bits, size
  * loss_* are host arrays of W*H per-pixel L1 losses (compute_pixel_losses, :21-30); n = N. */
 vr_status vr_sfd_loss_diff(vr_ctx* ctx, const float* loss_base, const float* loss_plus, uint32_t width,
                            uint32_t height, double* out, size_t n);
+/* ---------------- inverse rendering (gmm.h:583-706, optimizer.h, inverse_integrator.h) ---------------- */
+/* GaussianMixtureModel::pack_parameters (gmm.h:583-628): 11 floats per Gaussian, scene order: mean(3),
+ * Rodrigues rotation of the covariance eigenbasis (3), log scale (3), log density, logit albedo.
+ * n_params must be 11 * N. (Eigenbasis from a Jacobi solver, made right-handed: DESIGN.md §3c.) */
+vr_status vr_gmm_pack_parameters(const vr_scene* s, float* params, size_t n_params);
+/* apply_params_to_gmm_local (gmm.h:634-674): a new scene with base's lights / environment and every
+ * Gaussian rebuilt from params (covariance R S S^T R^T, density exp, albedo sigmoid). */
+vr_status vr_gmm_apply_parameters(const vr_scene* base, const float* params, size_t n_params, vr_scene** out);
+/* make_default_eps_for_params (gmm.h:678-706). */
+vr_status vr_gmm_default_eps(float* eps, size_t n_params);
+/* AdamOptimizer::step (optimizer.h:31-44) for step number t >= 1 (m, v: the moment vectors). */
+vr_status vr_adam_step(float* params, const float* grads, float* m, float* v, size_t n, int32_t t, float lr, float beta1,
+                       float beta2, float eps);
+/* Sign vector k of vr_sfd_optimize's run with `seed` (+1 / -1 per parameter): the deterministic
+ * stand-in for the reference's coin(mt19937(random_device)) (inverse_integrator.h:101-103, 139-141). */
+vr_status vr_sfd_sign_vector(uint64_t seed, uint64_t k, float* signs, size_t n);
+
+/* SFDDConfig (inverse_integrator.h:52-57) + run options. */
+typedef struct vr_sfd_config {
+    int32_t max_iters;          /* reference default 1000 */
+    int32_t save_every;         /* 25: render + write out_dir/iter_NNNN.ppm every save_every iterations */
+    int32_t num_stoch_samples;  /* 4: sign vectors per iteration */
+    float lr;                   /* 1e-2 (Adam) */
+    uint64_t seed;              /* sign-vector stream (vr_sfd_sign_vector) */
+    int32_t final_samples;      /* 16384: paths per pixel of the final render (:229-238); 0 skips it */
+    const char* out_dir;        /* NULL / "": write no images (the reference writes ./sfd_output) */
+} vr_sfd_config;
+typedef struct vr_sfd_result {
+    float* params;         /* out, 11 * N: the optimised parameters (caller-allocated) */
+    double* loss_history;  /* out, max_iters: mean L1 loss of every base render */
+    double* last_grads;    /* out (may be NULL), 11 * N: the last iteration's SFD gradient estimate */
+    float* final_image;    /* out (may be NULL), 3 * W * H: the final render */
+    double final_loss;     /* out: its mean L1 loss (-1 if final_samples == 0) */
+} vr_sfd_result;
+/* StochasticFiniteDiffInverseIntegrator::optimize(scene_initial, I_ref) (inverse_integrator.h:61-238)
+ * on the context's device: per iteration a recorded base render (RECORD_PIXEL_GAUSSIANS bitsets in
+ * HBM), num_stoch_samples perturbed recorded renders, the per-Gaussian union-of-pixels loss
+ * statistic and per-pixel L1 losses on the device, Adam on the host; every parameter update is
+ * re-uploaded with the device BVH build. fwd: MultiScatterGaussians parameters; I_ref: 3 * W * H. */
+vr_status vr_sfd_optimize(vr_ctx* ctx, const vr_camera* cam, const vr_render_params* fwd, const vr_scene* scene_initial,
+                          const float* I_ref, uint32_t width, uint32_t height, const vr_sfd_config* cfg,
+                          vr_sfd_result* result);
 /* Number of 16x16 tiles of a W x H frame. */
 uint32_t vr_num_tiles(uint32_t width, uint32_t height);
 /* Per-context tuning options (defaults are the benchmark/product settings). Explicit and

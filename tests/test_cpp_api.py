@@ -90,3 +90,43 @@ def test_cpp_render_equals_python_render(exe, tmp_path, scene, extra):
     py = tmp_path / "py.ppm"
     img.make_PPM(str(py))
     assert np.array_equal(read_ppm(str(out)), read_ppm(str(py)))
+
+
+@pytest.mark.gpu
+def test_cpp_record_render_equals_python(exe, tmp_path):
+    """MultiScatterGaussians::render(scene, image, &per_pixel_gaussians) (integrator.h:532-536) through the
+    C++ mirror records the same (pixel, Gaussian) pairs as the Python mirror."""
+    import vr_amd as vr
+    r = _run(exe, "--scene", scene_path("50_random.txt"), "--size", "32x32", "--integrator", "multiscatter", "--spp",
+             "4", "--record", "--out", str(tmp_path / "r.ppm"))
+    pairs = int([ln for ln in r.stdout.splitlines() if ln.startswith("recorded pairs")][0].split()[-1])
+    integ = vr.MultiScatterGaussians(vr.Pinhole_Camera(CAM_POS, main_view_dir(), FOV), 4)
+    lists = []
+    integ.render(vr.Scene.load_GMM(scene_path("50_random.txt")), vr.Image(32, 32), per_pixel_gaussians=lists)
+    assert pairs == sum(len(l) for l in lists) > 0
+
+
+@pytest.mark.gpu
+def test_cpp_inverse_loop_equals_python(exe, tmp_path):
+    """StochasticFiniteDiffInverseIntegrator through the C++ mirror and through the Python mirror (both
+    over vr_sfd_optimize) give the same loss history bit for bit on the same inputs."""
+    import vr_amd as vr
+    from vr_amd import inverse as inv
+    cam = vr.Pinhole_Camera(CAM_POS, main_view_dir(), FOV)
+    ref = vr.Image(24, 24)
+    vr.MultiScatterGaussians(cam, 16).render(vr.Scene.load_GMM(scene_path("2g_altered.txt")), ref)
+    ref_path = tmp_path / "ref.ppm"
+    ref.make_PPM(str(ref_path))
+    r = _run(exe, "--scene", scene_path("2_gaussian.txt"), "--size", "24x24", "--integrator", "multiscatter", "--spp",
+             "4", "--inverse", "3", "--ref", str(ref_path), "--seed", "5", "--stoch", "2", "--lr", "0.05",
+             "--final-spp", "8")
+    cpp = [float(ln.split()[-1]) for ln in r.stdout.splitlines() if ln.startswith("sfd iter")]
+    cpp_final = float([ln for ln in r.stdout.splitlines() if ln.startswith("sfd final")][0].split()[-1])
+    opt = inv.StochasticFiniteDiffInverseIntegrator(cam, vr.MultiScatterGaussians(cam, 4),
+                                                    inv.SFDConfig(max_iters=3, num_stoch_samples=2, lr=0.05, seed=5,
+                                                                  final_samples=8))
+    assert opt.optimize(vr.Scene.load_GMM(scene_path("2_gaussian.txt")), vr.Image(str(ref_path)))
+    assert len(cpp) == 3 and cpp == opt.history
+    assert cpp_final == opt.final_loss
+    assert np.all(np.isfinite(opt.history)) and not np.array_equal(opt.params, inv.pack_parameters(
+        vr.Scene.load_GMM(scene_path("2_gaussian.txt"))))

@@ -43,3 +43,22 @@ def test_default_eps_layout():
 def test_sigmoid_pair():
     y = np.float32([0.1, 0.5, 0.9])
     np.testing.assert_allclose(inv.sigmoidf_safe(inv.inv_sigmoidf(y)), y, rtol=1e-6)
+
+
+def test_sign_vectors_are_balanced_and_keyed():
+    a = inv.sign_vector(7, 0, 20000)
+    b = inv.sign_vector(7, 1, 20000)
+    assert set(np.unique(a)) == {-1.0, 1.0} and abs(a.mean()) < 0.03
+    assert not np.array_equal(a, b) and np.array_equal(a, inv.sign_vector(7, 0, 20000))
+
+
+def test_pack_matches_numpy_eigh_up_to_rotation_sign():
+    """The native eigenbasis (Jacobi) gives the LAPACK eigenvalues; apply(pack) is the identity on
+    covariances, so any sign choice of the eigenvectors is equivalent."""
+    rng = np.random.default_rng(3)
+    Q, _ = np.linalg.qr(rng.normal(size=(3, 3)))
+    d = np.array([0.01, 0.02, 0.05]) ** 2
+    C = Q @ np.diag(d) @ Q.T
+    g = np.array([[0, 0, 0, C[0, 0], C[0, 1], C[0, 2], C[1, 1], C[1, 2], C[2, 2], 1.0, 0.5]], np.float32)
+    p = inv.pack_parameters(g)
+    np.testing.assert_allclose(np.exp(p[6:9]), np.sqrt(np.linalg.eigvalsh(C.astype(np.float32))), rtol=1e-4)

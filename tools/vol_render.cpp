@@ -7,6 +7,11 @@
 //              [--camera pinhole|ortho] [--pos 0,1,6] [--lookat 0,1,0] [--fov 0.785398]
 //              [--out output.ppm] [--dump-rays N] [--devices 0,1,...]
 //
+// --record (multiscatter): the 3-argument render with per-pixel Gaussian lists (RECORD_PIXEL_GAUSSIANS);
+// prints the number of recorded (pixel, Gaussian) pairs.
+// --inverse N --ref I_ref.ppm [--seed S] [--stoch K] [--lr X] [--final-spp F] [--sfd-out DIR]: N iterations
+// of StochasticFiniteDiffInverseIntegrator from --scene towards I_ref (MultiScatterGaussians at --spp);
+// prints every iteration's mean loss (the reference's tests/main.cpp inverse mode, main.cpp:48-75).
 // --devices renders on a multi-GPU context over exactly these GPUs (tiles split, RCCL gather); by
 // default every visible GPU is used (one GPU: a plain single-device context).
 // --dump-rays N prints the first N primary rays (host only, no GPU) — used by the CPU tests.
@@ -16,6 +21,7 @@
 #include <iostream>
 #include <numbers>
 #include <string>
+#include <vector>
 
 #include "vr/integrator.h"
 #include "vr/test_integrators.h"
@@ -33,6 +39,11 @@ int main(int argc, char** argv) try {
     float step = 0.01f, fov = 0.25f * std::numbers::pi_v<float>;
     int env = -1, dump = 0, spp = -1;
     std::vector<int> devices;
+    bool record = false;
+    int inverse = 0, stoch = 4, final_spp = 0;
+    uint64_t seed = 0;
+    float lr = 1e-2f;
+    std::string ref_path, sfd_out;
     Eigen::Vector3f pos(0, 1, 6), lookat(0, 1, 0);
     for (int i = 1; i < argc; ++i) {
         std::string a = argv[i];
@@ -54,6 +65,14 @@ int main(int argc, char** argv) try {
         else if (a == "--fov") fov = std::strtof(next(), nullptr);
         else if (a == "--out") out = next();
         else if (a == "--dump-rays") dump = std::atoi(next());
+        else if (a == "--record") record = true;
+        else if (a == "--inverse") inverse = std::atoi(next());
+        else if (a == "--ref") ref_path = next();
+        else if (a == "--seed") seed = std::strtoull(next(), nullptr, 10);
+        else if (a == "--stoch") stoch = std::atoi(next());
+        else if (a == "--lr") lr = std::strtof(next(), nullptr);
+        else if (a == "--final-spp") final_spp = std::atoi(next());
+        else if (a == "--sfd-out") sfd_out = next();
         else if (a == "--devices") {
             std::string v = next();
             for (size_t p = 0; p <= v.size();) {
@@ -109,9 +128,37 @@ int main(int argc, char** argv) try {
     else throw std::runtime_error("unknown integrator " + integ);
 
     if (!devices.empty()) integrator->set_devices(devices);
+    if (inverse > 0) {  // main.cpp:48-75: optimise the scene towards a reference image
+        if (integ != "multiscatter") throw std::runtime_error("--inverse needs --integrator multiscatter");
+        Image I_ref(ref_path);
+        auto fwd = std::make_shared<MultiScatterGaussians>(camera, spp < 0 ? 16 : spp);
+        if (!devices.empty()) fwd->set_devices(devices);
+        SFDDConfig cfg;
+        cfg.max_iters = inverse;
+        cfg.num_stoch_samples = stoch;
+        cfg.lr = lr;
+        cfg.seed = seed;
+        cfg.final_samples = final_spp;
+        cfg.out_dir = sfd_out;
+        StochasticFiniteDiffInverseIntegrator sfd(camera, fwd, cfg);
+        if (!sfd.optimize(scene, I_ref)) throw std::runtime_error("SFD optimisation failed");
+        for (size_t i = 0; i < sfd.loss_history().size(); ++i) std::printf("sfd iter %zu loss %.17g\n", i, sfd.loss_history()[i]);
+        if (final_spp > 0) std::printf("sfd final loss %.17g\n", sfd.final_loss());
+        return 0;
+    }
     Image image(W, H);
     auto t0 = std::chrono::high_resolution_clock::now();
-    integrator->render(scene, image);
+    if (record) {
+        auto* ms = dynamic_cast<MultiScatterGaussians*>(integrator.get());
+        if (!ms) throw std::runtime_error("--record needs --integrator multiscatter");
+        std::vector<std::vector<uint32_t>> per_pixel;
+        ms->render(scene, image, &per_pixel);
+        size_t pairs = 0;
+        for (const auto& l : per_pixel) pairs += l.size();
+        std::printf("recorded pairs %zu\n", pairs);
+    } else {
+        integrator->render(scene, image);
+    }
     auto t1 = std::chrono::high_resolution_clock::now();
     vr_render_stats st = integrator->stats();
     std::printf("Render time: %.6f seconds (device %.3f ms, %lld pixels, %lld fallback, %d device(s)%s)\n",
