@@ -103,6 +103,9 @@ SIGNATURES = {
     "vr_image_write_ppm": (ST, [ctypes.c_char_p, FP, ctypes.c_uint32, ctypes.c_uint32]),
     "vr_image_read_ppm": (ST, [ctypes.c_char_p, FP, U32P, U32P]),
     "vr_init": (ST, [ctypes.c_int, PP]),
+    "vr_gif_begin": (ST, [ctypes.c_char_p, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, PP]),
+    "vr_gif_write_frame": (ST, [P, ctypes.POINTER(ctypes.c_uint8), ctypes.c_uint32]),
+    "vr_gif_end": (ST, [P]),
     "vr_gmm_pack_parameters": (ST, [P, FP, ctypes.c_size_t]),
     "vr_gmm_apply_parameters": (ST, [P, FP, ctypes.c_size_t, PP]),
     "vr_gmm_default_eps": (ST, [FP, ctypes.c_size_t]),

@@ -182,6 +182,16 @@ vr_status vr_image_write_ppm(const char* path, const float* rgb, uint32_t width,
  * to query width/height only. */
 vr_status vr_image_read_ppm(const char* path, float* rgb, uint32_t* width, uint32_t* height);
 
+/* ---------------- animated GIF (tests/main.cpp:81-114 turntable; gif-h's role) ---------------- */
+typedef struct vr_gif vr_gif;
+/* GifBegin: a looping GIF89a of width x height frames (delay_cs: the default frame delay, 1/100 s). */
+vr_status vr_gif_begin(const char* path, uint32_t width, uint32_t height, uint32_t delay_cs, vr_gif** out);
+/* GifWriteFrame: one RGBA8 frame (Image::get_rgba_buffer, image.h:89-104) shown for delay_cs
+ * hundredths of a second; its own 256-colour palette (median cut), LZW-compressed. */
+vr_status vr_gif_write_frame(vr_gif* gif, const uint8_t* rgba, uint32_t delay_cs);
+/* GifEnd: trailer, close, free. */
+vr_status vr_gif_end(vr_gif* gif);
+
 /* ---------------- device ---------------- */
 vr_status vr_init(int device, vr_ctx** out);
 /* Number of visible GPUs. */

@@ -12,6 +12,9 @@
 // --inverse N --ref I_ref.ppm [--seed S] [--stoch K] [--lr X] [--final-spp F] [--sfd-out DIR]: N iterations
 // of StochasticFiniteDiffInverseIntegrator from --scene towards I_ref (MultiScatterGaussians at --spp);
 // prints every iteration's mean loss (the reference's tests/main.cpp inverse mode, main.cpp:48-75).
+// --gif out.gif [--frames 120] [--fps 30]: the reference driver's turntable (main.cpp:81-114): an
+// Orthographic_Camera orbiting the look-at point at radius 6 and height +1, RayMarchingGaussians
+// (step 0.01, --env samples), one GIF frame each.
 // --devices renders on a multi-GPU context over exactly these GPUs (tiles split, RCCL gather); by
 // default every visible GPU is used (one GPU: a plain single-device context).
 // --dump-rays N prints the first N primary rays (host only, no GPU) — used by the CPU tests.
@@ -19,11 +22,13 @@
 #include <cstdio>
 #include <cstdlib>
 #include <iostream>
+#include <cmath>
 #include <numbers>
 #include <string>
 #include <vector>
 
 #include "vr/integrator.h"
+#include "vr/gif.h"
 #include "vr/test_integrators.h"
 
 static Eigen::Vector3f parse3(const char* s) {
@@ -43,7 +48,9 @@ int main(int argc, char** argv) try {
     int inverse = 0, stoch = 4, final_spp = 0;
     uint64_t seed = 0;
     float lr = 1e-2f;
-    std::string ref_path, sfd_out;
+    std::string ref_path, sfd_out, gif_path;
+    int frames = 120;
+    float fps = 30.0f;
     Eigen::Vector3f pos(0, 1, 6), lookat(0, 1, 0);
     for (int i = 1; i < argc; ++i) {
         std::string a = argv[i];
@@ -66,6 +73,9 @@ int main(int argc, char** argv) try {
         else if (a == "--out") out = next();
         else if (a == "--dump-rays") dump = std::atoi(next());
         else if (a == "--record") record = true;
+        else if (a == "--gif") gif_path = next();
+        else if (a == "--frames") frames = std::atoi(next());
+        else if (a == "--fps") fps = std::strtof(next(), nullptr);
         else if (a == "--inverse") inverse = std::atoi(next());
         else if (a == "--ref") ref_path = next();
         else if (a == "--seed") seed = std::strtoull(next(), nullptr, 10);
@@ -115,6 +125,28 @@ int main(int argc, char** argv) try {
             std::printf("ray %u %u %.9g %.9g %.9g %.9g %.9g %.9g\n", x, y, r.origin.x(), r.origin.y(), r.origin.z(),
                         r.direction.x(), r.direction.y(), r.direction.z());
         }
+        return 0;
+    }
+
+    if (!gif_path.empty()) {  // main.cpp:81-114
+        const float radius = 6.0f, height_pos = 1.0f;
+        GifWriter gif;
+        if (!GifBegin(&gif, gif_path.c_str(), W, H, (uint32_t)(100.0f / fps))) throw std::runtime_error(vr_last_error());
+        for (int frame = 0; frame < frames; ++frame) {
+            const float angle = 2.0f * std::numbers::pi_v<float> * ((float)frame / (float)frames);
+            Eigen::Vector3f cpos = lookat + Eigen::Vector3f(radius * std::sin(angle), height_pos, radius * std::cos(angle));
+            Eigen::Vector3f vd = (lookat - cpos).normalized();
+            auto cam = std::make_shared<Orthographic_Camera>(cpos, vd);
+            RayMarchingGaussians rm(cam, step, env < 0 ? 20 : env);
+            if (!devices.empty()) rm.set_devices(devices);
+            Image image(W, H);
+            rm.render(scene, image);
+            auto rgba = image.get_rgba_buffer();
+            if (!GifWriteFrame(&gif, rgba.data(), W, H, (uint32_t)(100.0f / fps))) throw std::runtime_error(vr_last_error());
+            std::printf("Frame %d / %d complete.\n", frame + 1, frames);
+        }
+        if (!GifEnd(&gif)) throw std::runtime_error(vr_last_error());
+        std::printf("GIF saved.\n");
         return 0;
     }
 
