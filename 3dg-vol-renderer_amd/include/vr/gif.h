@@ -3,7 +3,7 @@
 // (vr_gif_*: per-frame 256-colour median-cut palette, LZW, looping). bitDepth / dither are accepted
 // for signature compatibility; frames are always 8-bit palettes without dithering.
 #pragma once
-#include "vol_renderer.h"
+#include "runtime.h"
 
 struct GifWriter {
     vr_gif* g = nullptr;

@@ -164,3 +164,17 @@ def test_window_capacity_does_not_change_results(cap0, device_options):
     r = O.render_ff(O.OracleScene.load_gmm(path), O.PINHOLE, CAM_POS, main_view_dir(), FOV, 32, 32, multi=True,
                     num_samples=4)
     _check(g, r)
+
+
+@pytest.mark.parametrize("name", ["20k_bias.txt", "5000_random.txt", "10k_random.txt"])
+def test_dense_reference_scenes_stay_within_the_hit_capacity(name):
+    """The per-path hit buffer holds 128 Gaussians overlapping one point (the only capacity a path
+    can exceed, test_overlap_beyond_capacity_fails_loudly). The reference's densest scenes (20k_bias:
+    y-skewed, 20k Gaussians) render at the C5 settings without reaching it, and match the oracle
+    (stable tie order, the device's rule for tangent hits)."""
+    path = scene_path(name)
+    g = _gpu(vr.Scene.load_GMM(path), 64, 64, True, 4)
+    with O.stable_ties():
+        r = O.render_ff(O.OracleScene.load_gmm(path), O.PINHOLE, CAM_POS, main_view_dir(), FOV, 64, 64, multi=True,
+                        num_samples=4)
+    _check(g, r)

@@ -29,6 +29,7 @@
 
 #include "vr/integrator.h"
 #include "vr/gif.h"
+#include "vr/inverse_integrator.h"
 #include "vr/test_integrators.h"
 
 static Eigen::Vector3f parse3(const char* s) {
