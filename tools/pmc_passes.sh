@@ -1,5 +1,8 @@
 #!/bin/bash
-# PMC passes (one rocprofv3 run per counter set, kernel-trace only) for the r02 profiles:
+# PMC passes (one rocprofv3 run per counter set, kernel-trace only) behind profiles/r02_*_pmc_summary.json
+# (summarise with tools/pmc_summary.py OUT.json DIR/p1 DIR/p2 DIR/p3 DIR/p4). The c4_notr leg needs the
+# diagnostic build: make -C 3dg-vol-renderer_amd/csrc BUILD=../build-diag OUT=../../tools_dbg/libvr_diag.so
+#   DEVFLAGS="... -DVR_DIAG_SKIP_TR_STORES" (see DESIGN.md §3).
 #   C4 ray-march frame (product and the diagnostic no-Tr-store build) and C2 multi-scatter (ff_path_kernel).
 cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
 O=gpurun_out/pmc_r02; mkdir -p $O
