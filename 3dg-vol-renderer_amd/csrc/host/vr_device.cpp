@@ -656,22 +656,20 @@ vr_status free_flight_pipeline(vr_ctx* c, RenderArgs& A, hipStream_t s) {
     HIP_TRY(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, c->device), "hipDeviceGetAttribute");
     const uint32_t threads = (uint32_t)std::max(1, cus) * 4u * 256u;  // 4 waves/SIMD x 4 SIMDs = 4 blocks per CU
     const uint32_t chunk = (uint32_t)std::min<uint64_t>(A.num_tiles, kFFMaxPaths / ((uint64_t)spp * 256u));
-    vr_status st = grow(c->ff_scratch, (size_t)threads * (3 * kFFHitCap + 8 * kFFActCap) * 4 + 64, "free-flight scratch");
+    vr_status st = grow(c->ff_scratch, (size_t)threads * (kFFHitCap + 2 * kFFActCap) * 16 + 64, "free-flight scratch");
     if (st != VR_OK) return st;
     if ((st = grow(c->ff_path, (size_t)chunk * spp * 256 * 3 * sizeof(float), "free-flight paths")) != VR_OK) return st;
     if ((st = grow(c->ff_sum, (size_t)A.num_tiles * 256 * 3 * sizeof(float), "free-flight sums")) != VR_OK) return st;
     const uint32_t nsb = spp;
-    float* base = (float*)c->ff_scratch.p;
+    float4* base = (float4*)c->ff_scratch.p;
     A.ff_threads = threads;
     A.ff_hit_cap = kFFHitCap;
     A.ff_act_cap = kFFActCap;
     A.ff_hit_cap0 = (int32_t)std::max<int64_t>(1, std::min<int64_t>(kFFHitCap, c->opt_ff_window0));
-    A.ff_key = base;
-    A.ff_t1 = base + (size_t)kFFHitCap * threads;
-    A.ff_gid = (int32_t*)(base + (size_t)2 * kFFHitCap * threads);
-    A.ff_act = (int32_t*)(base + (size_t)3 * kFFHitCap * threads);
-    A.ff_cache = base + (size_t)(3 * kFFHitCap + kFFActCap) * threads;
-    A.ff_next = (unsigned long long*)(base + (size_t)(3 * kFFHitCap + 8 * kFFActCap) * threads);
+    A.ff_hit = base;
+    A.ff_act0 = base + (size_t)kFFHitCap * threads;
+    A.ff_act1 = base + (size_t)(kFFHitCap + kFFActCap) * threads;
+    A.ff_next = (unsigned long long*)(base + (size_t)(kFFHitCap + 2 * kFFActCap) * threads);
     A.ff_path = (float*)c->ff_path.p;
     A.ff_sum = (float*)c->ff_sum.p;
     for (uint32_t t0 = 0; t0 < A.num_tiles; t0 += chunk) {

@@ -30,57 +30,45 @@ namespace dev {
 
 constexpr int kFFBlock = 256;
 
-// Per-thread scratch rows (global memory, [slot][thread] so a wave's lanes touch one cache line).
+// Per-thread scratch rows (global memory, [slot][thread] so a wave's lanes touch consecutive 16-B
+// cells): every slot is one float4, so an insert shift, an entry or a cache read is ONE 16-B access
+// instead of three or seven 4-B ones (fewer memory instructions and dependent round trips).
+//   hit[slot]  = { entry key max(t0, W0), exit t1, record id (leaf order, as bits), - }
+//   a0[entry]  = { P, B, 2A, den }   per active entry, cached for the bounce's ray when it enters
+//   a1[entry]  = { F, F_next, t1, hit slot (bits) }
+// (optical_depth's factors, gaussian.h:208-231: od(t_prev, t) = P * (erf((B + 2A t) / den) - F) with
+// F = erf(.. t_prev ..), the same float operations as optical_depth(), so the values are bit-identical)
 struct FFScratch {
-    float* key;   // entry distance max(t0, W0)
-    float* t1;    // exit distance
-    int* gid;     // record id (leaf order)
-    int* act;     // active list: slots into the hit buffer
-    // per active entry, cached for the bounce's ray when it enters (optical_depth's factors,
-    // gaussian.h:208-231): od(t_prev, t) = P * (erf((B + 2A t) / den) - F) with F = erf(.. t_prev ..),
-    // the same float operations as optical_depth(), so the values are bit-identical
-    float* aP;    // pref * exp(-0.5 (C - B^2 / 4A))
-    float* aB;    // B
-    float* a2A;   // 2A
-    float* aDen;  // 2 sqrt(2A)
-    float* aF;    // erf argument value at t_prev
-    float* aFn;   // erf value at the segment end (committed when the segment is passed)
-    float* aT1;   // exit distance
+    float4* hit;
+    float4* a0;
+    float4* a1;
     uint32_t stride;
-    __device__ __forceinline__ float& K(int i) const { return key[(size_t)i * stride]; }
-    __device__ __forceinline__ float& T1(int i) const { return t1[(size_t)i * stride]; }
-    __device__ __forceinline__ int& G(int i) const { return gid[(size_t)i * stride]; }
-    __device__ __forceinline__ int& Act(int i) const { return act[(size_t)i * stride]; }
-    __device__ __forceinline__ float& P(int i) const { return aP[(size_t)i * stride]; }
-    __device__ __forceinline__ float& Bq(int i) const { return aB[(size_t)i * stride]; }
-    __device__ __forceinline__ float& TwoA(int i) const { return a2A[(size_t)i * stride]; }
-    __device__ __forceinline__ float& Den(int i) const { return aDen[(size_t)i * stride]; }
-    __device__ __forceinline__ float& F(int i) const { return aF[(size_t)i * stride]; }
-    __device__ __forceinline__ float& Fn(int i) const { return aFn[(size_t)i * stride]; }
-    __device__ __forceinline__ float& AT1(int i) const { return aT1[(size_t)i * stride]; }
+    __device__ __forceinline__ float4& H(int i) const { return hit[(size_t)i * stride]; }
+    __device__ __forceinline__ float4& A0(int i) const { return a0[(size_t)i * stride]; }
+    __device__ __forceinline__ float4& A1(int i) const { return a1[(size_t)i * stride]; }
+    __device__ __forceinline__ float K(int i) const { return H(i).x; }
+    __device__ __forceinline__ int G(int i) const { return __float_as_int(H(i).z); }
+    __device__ __forceinline__ int Act(int i) const { return __float_as_int(A1(i).w); }
     // entry i (hit slot `slot`) becomes active at t: cache its factors (optical_depth's own ops)
     __device__ __forceinline__ void enter(const RenderArgs& A, int i, int slot, const Ray& r, float t) const {
-        Act(i) = slot;
-        AT1(i) = T1(slot);
-        GRec g = load_rec(A.gauss, G(slot));
+        const float4 h = H(slot);
+        GRec g = load_rec(A.gauss, __float_as_int(h.z));
         Quad q = quad(g, r);
         float twoA = 2.0f * q.A;
         float pref = (g.density * g.norm) * sqrtf(__fdiv_rn(3.14159265358979323846f, twoA));
         float den = 2.0f * sqrtf(twoA);
         float e = expf(-0.5f * (q.Cq - __fdiv_rn(q.B * q.B, 4.0f * q.A)));
-        P(i) = pref * e;
-        Bq(i) = q.B;
-        TwoA(i) = twoA;
-        Den(i) = den;
-        F(i) = erff(__fdiv_rn(q.B + twoA * t, den));
+        A0(i) = make_float4(pref * e, q.B, twoA, den);
+        A1(i) = make_float4(erff(__fdiv_rn(q.B + twoA * t, den)), 0.0f, h.y, __int_as_float(slot));
     }
     __device__ __forceinline__ void move(int dst, int src) const {
-        Act(dst) = Act(src), AT1(dst) = AT1(src), P(dst) = P(src), Bq(dst) = Bq(src);
-        TwoA(dst) = TwoA(src), Den(dst) = Den(src), F(dst) = F(src);
+        A0(dst) = A0(src);
+        A1(dst) = A1(src);
     }
     // optical depth of active entry i on [t_prev, t]
     __device__ __forceinline__ float od_to(int i, float t) const {
-        return P(i) * (erff(__fdiv_rn(Bq(i) + TwoA(i) * t, Den(i))) - F(i));
+        const float4 c = A0(i);
+        return c.x * (erff(__fdiv_rn(c.y + c.z * t, c.w)) - A1(i).x);
     }
 };
 
@@ -335,15 +323,13 @@ __device__ float free_flight_distance(const RenderArgs& A, const FFScratch& S, c
                         --n;
                     }
                     int p = n;  // sorted insert after equal keys (walk order among ties)
-                    while (p > 0 && S.K(p - 1) > key) {
-                        S.K(p) = S.K(p - 1);
-                        S.T1(p) = S.T1(p - 1);
-                        S.G(p) = S.G(p - 1);
+                    while (p > 0) {
+                        const float4 prev = S.H(p - 1);
+                        if (!(prev.x > key)) break;
+                        S.H(p) = prev;
                         --p;
                     }
-                    S.K(p) = key;
-                    S.T1(p) = t1;
-                    S.G(p) = (int)j;
+                    S.H(p) = make_float4(key, t1, __int_as_float((int)j), 0.0f);
                     ++n;
                     if (n == cap) kfull = S.K(n - 1);
                 }
@@ -366,7 +352,7 @@ __device__ float free_flight_distance(const RenderArgs& A, const FFScratch& S, c
             float next_exit = INFINITY;
             int exit_pos = -1;
             for (int a = 0; a < m; ++a) {
-                float e = S.AT1(a);
+                float e = S.A1(a).z;
                 if (e < next_exit) next_exit = e, exit_pos = a;
             }
             float t_evt = fminf(next_entry, next_exit);
@@ -375,9 +361,11 @@ __device__ float free_flight_distance(const RenderArgs& A, const FFScratch& S, c
             if (t_evt == INFINITY) return -1.0f;  // past the last event: no scatter (integrator.h:362-366)
             Acc seg = 0;
             for (int a = 0; a < m; ++a) {
-                const float f1 = erff(__fdiv_rn(S.Bq(a) + S.TwoA(a) * t_evt, S.Den(a)));
-                S.Fn(a) = f1;
-                seg += (Acc)(S.P(a) * (f1 - S.F(a)));
+                const float4 c = S.A0(a);
+                const float f1 = erff(__fdiv_rn(c.y + c.z * t_evt, c.w));
+                float4& e1 = S.A1(a);
+                e1.y = f1;
+                seg += (Acc)(c.x * (f1 - e1.x));
             }
             if (acc + seg > (Acc)target) {
                 float rem = (float)((Acc)target - acc);
@@ -385,7 +373,10 @@ __device__ float free_flight_distance(const RenderArgs& A, const FFScratch& S, c
             }
             acc += seg;
             t_prev = t_evt;
-            for (int a = 0; a < m; ++a) S.F(a) = S.Fn(a);
+            for (int a = 0; a < m; ++a) {
+                float4& e1 = S.A1(a);
+                e1.x = e1.y;
+            }
             if (window_end) break;
             if (next_entry <= next_exit) {
                 if (m >= A.ff_act_cap) return -2.0f;
@@ -504,11 +495,7 @@ __global__ void __launch_bounds__(kFFBlock, 4) ff_path_kernel(RenderArgs A) {
     __shared__ int s_stack[kStackSize * kFFBlock];
     int* stack = s_stack + threadIdx.x;
     const uint32_t gt = blockIdx.x * kFFBlock + threadIdx.x;
-    const size_t AC = (size_t)A.ff_act_cap * A.ff_threads;
-    float* cache = A.ff_cache + gt;
-    const FFScratch S{A.ff_key + gt, A.ff_t1 + gt, A.ff_gid + gt, A.ff_act + gt,
-                      cache, cache + AC, cache + 2 * AC, cache + 3 * AC, cache + 4 * AC, cache + 5 * AC, cache + 6 * AC,
-                      A.ff_threads};
+    const FFScratch S{A.ff_hit + gt, A.ff_act0 + gt, A.ff_act1 + gt, A.ff_threads};
     const uint32_t lane = threadIdx.x & 63u;
     for (;;) {
         unsigned long long base = 0;

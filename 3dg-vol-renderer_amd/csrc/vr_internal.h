@@ -164,13 +164,11 @@ struct RenderArgs {
     uint32_t ff_threads;     // threads of one step = row stride of the scratch arrays
     int32_t ff_hit_cap, ff_act_cap;  // per-thread hit-buffer / active-list capacities
     int32_t ff_hit_cap0;     // first window's capacity (doubles per window up to ff_hit_cap)
-    float* ff_key;           // scratch [hit_cap][threads]
-    float* ff_t1;            // scratch [hit_cap][threads]
-    int32_t* ff_gid;         // scratch [hit_cap][threads]
-    int32_t* ff_act;         // scratch [act_cap][threads]
+    float4* ff_hit;          // scratch [hit_cap][threads]: entry key, exit t1, record id, -
+    float4* ff_act0;         // scratch [act_cap][threads]: per active entry P, B, 2A, den
+    float4* ff_act1;         // scratch [act_cap][threads]: per active entry F, F_next, t1, hit slot
     unsigned long long* ff_next;  // persistent path kernel: next unclaimed path of the launch
     unsigned long long ff_total;  // paths of the launch (tiles of the chunk x samples x 256)
-    float* ff_cache;         // scratch [7][act_cap][threads]: per active entry P, B, 2A, den, F, F_next, t1
     float* ff_path;          // [threads][3] path radiance of the step
     float* ff_sum;           // [tile-local pixel][3] running sum over sample batches
     const uint32_t* gauss_order;  // record (leaf order) -> scene index
