@@ -670,6 +670,7 @@ __device__ __forceinline__ void sec_leaf(const RenderArgs& A, SecRay& R, int32_t
 // Ray complete: write its transmittance (or hand it to the exact slow path).
 template <bool S, bool FAST, bool PURE>
 __device__ __forceinline__ void sec_finish(const RenderArgs& A, SecRay& R, Ctr& c) {
+#ifndef VR_DIAG_WAVE_UTIL
     if constexpr (S) {  // secondary-stage diagnostics in otherwise unused counter slots
         if (R.tau >= R.cut) {
             c.v[kCtrSteps]++;                 // rays ended by the optical-depth cut-off
@@ -678,6 +679,7 @@ __device__ __forceinline__ void sec_finish(const RenderArgs& A, SecRay& R, Ctr& 
             c.v[kCtrPixels] += R.nsteps;       // node steps of rays that ran to the end of the tree
         }
     }
+#endif
     if (R.tau >= R.cut) {
         VR_TR_STORE(A, R.slot, 0.0f);
         return;
@@ -830,11 +832,25 @@ __device__ __forceinline__ void sec_node4(const RenderArgs& A, SecRay& R, int* s
     cswap(key[1], kr[1], key[3], kr[3]);
     cswap(key[1], kr[1], key[2], kr[2]);
     // leaves -> queue, nearest first
+    if constexpr (kQueueRing<QCAP>) {
+        // Branch-free: every lane stores each child at the queue's end; a non-leaf store lands past
+        // the last entry (never read, overwritten by the next put). A NODE step starts with at most
+        // QCAP - 4 entries, so that slot is always a free ring word.
+        int* ext = stack + STACK * BLOCK;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-        const bool leaf = kr[i] < 0;
-        Q.put<QCAP, BLOCK>(leaf ? Q.n : -1, kr[i], stack + STACK * BLOCK);
-        Q.n += (int)leaf;
+        for (int i = 0; i < 4; ++i) {
+            const bool leaf = kr[i] < 0;
+            Q.q0 = (leaf && Q.n == 0) ? kr[i] : Q.q0;
+            ext[((Q.q1 + Q.n - 1) & (QCAP - 2)) * BLOCK] = kr[i];
+            Q.n += (int)leaf;
+        }
+    } else {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const bool leaf = kr[i] < 0;
+            Q.put<QCAP, BLOCK>(leaf ? Q.n : -1, kr[i], stack + STACK * BLOCK);
+            Q.n += (int)leaf;
+        }
     }
     // inner children: the nearest continues, the others are pushed far-first
     int first = -1;
@@ -843,6 +859,25 @@ __device__ __forceinline__ void sec_node4(const RenderArgs& A, SecRay& R, int* s
     for (int i = 3; i >= 0; --i) {
         first = kr[i] > 0 ? i : first;
         next = kr[i] > 0 ? kr[i] : next;
+    }
+    // Common case, wave-uniform: every stepping lane can take 3 pushes in LDS. Then the pushes
+    // are branch-free (a lane that does not push stores above its top: dead) and the pop is LDS.
+    // (Child 0 is never pushed: if it is inner it is the nearest inner child.)
+    if (__builtin_expect(__ballot(sp > STACK - 3) == 0ull, 1)) {
+#pragma unroll
+        for (int i = 3; i >= 1; --i) {
+            stack[sp * BLOCK] = kr[i];
+            sp += (int)((kr[i] > 0) & (i != first));
+        }
+        if (first >= 0) {
+            node = next;
+        } else if (sp > 0) {
+            --sp;
+            node = stack[sp * BLOCK];
+        } else {
+            node = -1;
+        }
+        return;
     }
 #pragma unroll
     for (int i = 3; i >= 0; --i) {
@@ -1120,6 +1155,9 @@ __global__ __launch_bounds__(BLOCK, WAVES) void secondary_ww_kernel(RenderArgs A
             if (counter_done && pool == pool_end) break;
             continue;
         }
+#ifdef VR_DIAG_WAVE_UTIL  // diagnostic builds only: wave iterations with a live lane, and live lanes in them
+        if constexpr (S) c.v[kCtrPixels] += (lane == 0u ? 1u : 0u);
+#endif
         const bool has_prim = live && Q.has_prim();
         constexpr int kRoom = W ? 4 : 2;  // leaves one NODE step can queue
         const bool can_node = live && node >= 0 && (QCAP == 2 ? Q.n == 0 : Q.n <= QCAP - kRoom);
@@ -1129,6 +1167,9 @@ __global__ __launch_bounds__(BLOCK, WAVES) void secondary_ww_kernel(RenderArgs A
         if (prim_iter) {  // PRIM iteration: up to kPrimSteps primitive tests per lane
             bool go = has_prim;
             for (int k = 0; k < kPrimSteps; ++k) {
+#ifdef VR_DIAG_WAVE_UTIL  // diagnostic builds only: wave-level PRIM steps (lane utilisation)
+                if constexpr (S) c.v[kCtrPrimQueries] += (__ballot(go) != 0ull && lane == 0u) ? 1u : 0u;
+#endif
                 if (go) {
                     const bool from_list = node <= kNodeListCentral;
                     const uint32_t j = from_list ? (uint32_t)A.rec_list[Q.j++] : Q.next<QCAP, BLOCK>(stack + STACK * BLOCK);
@@ -1153,6 +1194,9 @@ __global__ __launch_bounds__(BLOCK, WAVES) void secondary_ww_kernel(RenderArgs A
         } else {  // NODE iteration: up to kNodeSteps node steps per lane
             bool go = can_node;
             for (int k = 0; k < kNodeSteps; ++k) {
+#ifdef VR_DIAG_WAVE_UTIL  // diagnostic builds only: wave-level NODE steps (lane utilisation)
+                if constexpr (S) c.v[kCtrSteps] += (__ballot(go) != 0ull && lane == 0u) ? 1u : 0u;
+#endif
                 if (go) {
                     if constexpr (W) sec_node4<BLOCK, S, QCAP, STACK>(A, R, stack, sp, node, Q, c);
                     else sec_node<BLOCK, S, QCAP, STACK, H>(A, R, stack, sp, node, Q, c);
