@@ -35,22 +35,26 @@ constexpr int kFFBlock = 256;
 // instead of three or seven 4-B ones (fewer memory instructions and dependent round trips).
 //   hit[slot]  = { entry key max(t0, W0), exit t1, record id (leaf order, as bits), - }
 //   a0[entry]  = { P, B, 2A, den }   per active entry, cached for the bounce's ray when it enters
-//   a1[entry]  = { F, F_next, t1, hit slot (bits) }
+//   a1[entry]  = { F0, F1, t1, record id (bits) }
 // (optical_depth's factors, gaussian.h:208-231: od(t_prev, t) = P * (erf((B + 2A t) / den) - F) with
-// F = erf(.. t_prev ..), the same float operations as optical_depth(), so the values are bit-identical)
+// F = erf(.. t_prev ..), the same float operations as optical_depth(), so the values are bit-identical).
+// F at the current segment start is F0 or F1 as `ph` says: an event writes the new F into the other
+// component and flips ph, so the sweep touches every active entry once per event (one 16-B read
+// and one 4-B write) and the solver still sees F at t_prev when the target is crossed.
 struct FFScratch {
     float4* hit;
     float4* a0;
     float4* a1;
     uint32_t stride;
+    int ph;  // which of a1.x / a1.y holds F at the current segment start
     __device__ __forceinline__ float4& H(int i) const { return hit[(size_t)i * stride]; }
     __device__ __forceinline__ float4& A0(int i) const { return a0[(size_t)i * stride]; }
     __device__ __forceinline__ float4& A1(int i) const { return a1[(size_t)i * stride]; }
     __device__ __forceinline__ float K(int i) const { return H(i).x; }
-    __device__ __forceinline__ int G(int i) const { return __float_as_int(H(i).z); }
-    __device__ __forceinline__ int Act(int i) const { return __float_as_int(A1(i).w); }
-    // entry i (hit slot `slot`) becomes active at t: cache its factors (optical_depth's own ops)
-    __device__ __forceinline__ void enter(const RenderArgs& A, int i, int slot, const Ray& r, float t) const {
+    __device__ __forceinline__ int Rec(int i) const { return __float_as_int(A1(i).w); }  // record of active entry i
+    // entry i (hit slot `slot`) becomes active at t: cache its factors (optical_depth's own ops);
+    // returns its exit t1
+    __device__ __forceinline__ float enter(const RenderArgs& A, int i, int slot, const Ray& r, float t) const {
         const float4 h = H(slot);
         GRec g = load_rec(A.gauss, __float_as_int(h.z));
         Quad q = quad(g, r);
@@ -59,7 +63,9 @@ struct FFScratch {
         float den = 2.0f * sqrtf(twoA);
         float e = expf(-0.5f * (q.Cq - __fdiv_rn(q.B * q.B, 4.0f * q.A)));
         A0(i) = make_float4(pref * e, q.B, twoA, den);
-        A1(i) = make_float4(erff(__fdiv_rn(q.B + twoA * t, den)), 0.0f, h.y, __int_as_float(slot));
+        const float F = erff(__fdiv_rn(q.B + twoA * t, den));
+        A1(i) = make_float4(F, F, h.y, h.z);
+        return h.y;
     }
     __device__ __forceinline__ void move(int dst, int src) const {
         A0(dst) = A0(src);
@@ -68,7 +74,8 @@ struct FFScratch {
     // optical depth of active entry i on [t_prev, t]
     __device__ __forceinline__ float od_to(int i, float t) const {
         const float4 c = A0(i);
-        return c.x * (erff(__fdiv_rn(c.y + c.z * t, c.w)) - A1(i).x);
+        const float4 e = A1(i);
+        return c.x * (erff(__fdiv_rn(c.y + c.z * t, c.w)) - (ph ? e.y : e.x));
     }
 };
 
@@ -111,10 +118,19 @@ __device__ __forceinline__ void sample_uniform_direction(PCG32& rng, float& x, f
     z = cosf(phi);
 }
 
-// BVH walk over the 32-B half-precision child-pair nodes when the scene has them (boxes rounded
-// outward: the same hit set, since every candidate gets the exact ellipsoid test), else the f32 nodes.
-template <typename Prune, typename Leaf>
-__device__ __forceinline__ void walk(const RenderArgs& A, const Ray& r, int* stack, int stride, Prune prune, Leaf leaf) {
+// BVH walk over the 4-wide half-precision tree when the scene has one (half as many dependent node
+// fetches per ray as the child-pair tree), else the 32-B half-precision child-pair nodes, else the
+// f32 nodes. Boxes are rounded outward, so every tree yields the same hit set (every candidate gets
+// the exact ellipsoid test); only the walk order among equal keys differs. A 4-wide walk that could
+// overflow its LDS stack stops; `reset` then clears what the walk collected and the pair tree
+// (at most one push per level) redoes it.
+template <typename Prune, typename Leaf, typename Reset>
+__device__ __forceinline__ void walk(const RenderArgs& A, const Ray& r, int* stack, int stride, Prune prune, Leaf leaf,
+                                     Reset reset) {
+    if (A.hnodes4) {
+        if (traverse_wide<kStackSize>(A, r, stack, stride, prune, leaf)) return;
+        reset();
+    }
     if (A.hnodes)
         traverse<true>(A, r, stack, stride, prune, leaf);
     else
@@ -214,7 +230,7 @@ __device__ float solve_newton(const RenderArgs& A, const FFScratch& S, int m, co
 __device__ float solve_distance(const RenderArgs& A, const FFScratch& S, int m, const Ray& r, float ta, float tb, float rem) {
     if (m == 1) {
         float t_an = 0.0f;
-        if (solve_for_t_given_tau(load_rec(A.gauss, S.G(S.Act(0))), r, ta, tb, rem, t_an)) return fminf(fmaxf(t_an, ta), tb);
+        if (solve_for_t_given_tau(load_rec(A.gauss, S.Rec(0)), r, ta, tb, rem, t_an)) return fminf(fmaxf(t_an, ta), tb);
     }
     return solve_newton(A, S, m, r, ta, tb, rem);
 }
@@ -223,7 +239,7 @@ __device__ float solve_distance(const RenderArgs& A, const FFScratch& S, int m, 
 __device__ float evaluate_albedo(const RenderArgs& A, const FFScratch& S, int m, float x, float y, float z) {
     float sum = 0.0f, sum_alb = 0.0f;
     for (int i = 0; i < m; ++i) {
-        GRec g = load_rec(A.gauss, S.G(S.Act(i)));
+        GRec g = load_rec(A.gauss, S.Rec(i));
         float mt = mu_t(g, x, y, z);
         sum += mt;
         sum_alb += mt * g.albedo;
@@ -235,6 +251,9 @@ __device__ float evaluate_albedo(const RenderArgs& A, const FFScratch& S, int m,
 // gmm.h:517-578: exp(-sum tau_i(max(0,t0_i), min(tmax,t1_i))), unsorted, double accumulation.
 __device__ float transmittance_up_to(const RenderArgs& A, const Ray& r, float tmax, int* stack, int stride) {
     if (!(tmax > 0.0f)) return 1.0f;
+#ifdef VR_DIAG_FF_NO_NEE  // diagnostic builds only (cost attribution): the shadow walk is skipped
+    return 0.5f;
+#endif
     double sum = 0.0;
     walk(
         A, r, stack, stride, [&](float tmin, float) { return tmin <= tmax + kTPad * (1.0f + fminf(tmax, 1e30f)); },
@@ -249,7 +268,8 @@ __device__ float transmittance_up_to(const RenderArgs& A, const Ray& r, float tm
                 if (b > a) sum += (double)optical_depth(g, q, a, b);
             }
             return sum < 104.0;  // expf(-x) == 0 in f32 for x >= 104: later terms cannot change Tr
-        });
+        },
+        [&]() { sum = 0.0; });
     return expf(-(float)sum);
 }
 
@@ -269,7 +289,8 @@ __device__ void record_hits(const RenderArgs& A, const Ray& r, float lim, uint32
                 atomicOr(A.rec_bits + (size_t)(o >> 5) * A.rec_npix + p, 1u << (o & 31u));
             }
             return true;
-        });
+        },
+        [&]() {});  // marking again is idempotent
 }
 
 // Free-flight distance along r for target optical depth `target` (integrator.h:330-360 for
@@ -277,7 +298,7 @@ __device__ void record_hits(const RenderArgs& A, const Ray& r, float lim, uint32
 // -1 (no scatter before the last event) or -2 (a per-thread capacity was exceeded). On return
 // with t >= 0 the active list holds the critical segment's Gaussians (count in m).
 template <bool MULTI>
-__device__ float free_flight_distance(const RenderArgs& A, const FFScratch& S, const Ray& r, float target, int& m, int* stack,
+__device__ float free_flight_distance(const RenderArgs& A, FFScratch& S, const Ray& r, float target, int& m, int* stack,
                                       int stride) {
     using Acc = typename std::conditional<MULTI, double, float>::type;
     Acc acc = 0;
@@ -334,6 +355,11 @@ __device__ float free_flight_distance(const RenderArgs& A, const FFScratch& S, c
                     if (n == cap) kfull = S.K(n - 1);
                 }
                 return true;
+            },
+            [&]() {
+                n = 0;
+                t_cut = kfull = INFINITY;
+                pruned_full = false;
             });
         // skipped subtrees only hold keys beyond the (final) largest kept key
         if (pruned_full && n > 0) t_cut = fminf(t_cut, S.K(n - 1));
@@ -345,27 +371,39 @@ __device__ float free_flight_distance(const RenderArgs& A, const FFScratch& S, c
         }
         if (n == 0 && t_cut == INFINITY) return -1.0f;
         // ---- sweep the window's events (integrator.h:438-495) ----
+        // The active list's next exit (the first entry with the smallest t1, as the reference's
+        // scan finds it) is carried from event to event: the pass that integrates the segment also
+        // finds the smallest t1 of the list as it will be after this event (entry appended, or the
+        // exiting entry swap-removed), so each event reads every active entry once.
         int i = 0;
         m = 0;
+        float next_exit = INFINITY;
+        int exit_pos = -1;
         for (;;) {
-            float next_entry = i < n ? S.K(i) : INFINITY;
-            float next_exit = INFINITY;
-            int exit_pos = -1;
-            for (int a = 0; a < m; ++a) {
-                float e = S.A1(a).z;
-                if (e < next_exit) next_exit = e, exit_pos = a;
-            }
+            const float next_entry = i < n ? S.K(i) : INFINITY;
             float t_evt = fminf(next_entry, next_exit);
             const bool window_end = t_cut <= t_evt;
             if (window_end) t_evt = t_cut;
             if (t_evt == INFINITY) return -1.0f;  // past the last event: no scatter (integrator.h:362-366)
+            const bool is_entry = next_entry <= next_exit;
+            float nx = INFINITY;  // smallest t1 after the event, and its position in the list then
+            int npos = -1;
             Acc seg = 0;
             for (int a = 0; a < m; ++a) {
                 const float4 c = S.A0(a);
+                float4& e1r = S.A1(a);
+                const float4 e1 = e1r;
                 const float f1 = erff(__fdiv_rn(c.y + c.z * t_evt, c.w));
-                float4& e1 = S.A1(a);
-                e1.y = f1;
-                seg += (Acc)(c.x * (f1 - e1.x));
+                if (S.ph) e1r.x = f1;
+                else e1r.y = f1;
+                seg += (Acc)(c.x * (f1 - (S.ph ? e1.y : e1.x)));
+                int pp = a;  // position after a swap-remove of exit_pos
+                if (!is_entry && a == m - 1) pp = exit_pos;
+                const bool gone = !is_entry && a == exit_pos;
+                if (!gone && (e1.z < nx || (e1.z == nx && pp < npos))) {
+                    nx = e1.z;
+                    npos = pp;
+                }
             }
             if (acc + seg > (Acc)target) {
                 float rem = (float)((Acc)target - acc);
@@ -373,18 +411,22 @@ __device__ float free_flight_distance(const RenderArgs& A, const FFScratch& S, c
             }
             acc += seg;
             t_prev = t_evt;
-            for (int a = 0; a < m; ++a) {
-                float4& e1 = S.A1(a);
-                e1.x = e1.y;
-            }
+            S.ph ^= 1;  // F at t_evt is now the segment start
             if (window_end) break;
-            if (next_entry <= next_exit) {
+            if (is_entry) {
                 if (m >= A.ff_act_cap) return -2.0f;
-                S.enter(A, m++, i++, r, t_evt);
+                const float t1n = S.enter(A, m, i++, r, t_evt);
+                if (t1n < nx) {  // ties: the earlier position stays first
+                    nx = t1n;
+                    npos = m;
+                }
+                ++m;
             } else {
                 S.move(exit_pos, m - 1);
                 --m;
             }
+            next_exit = nx;
+            exit_pos = npos;
         }
         W0 = t_cut;
         cap = min(2 * cap, A.ff_hit_cap);
@@ -393,7 +435,7 @@ __device__ float free_flight_distance(const RenderArgs& A, const FFScratch& S, c
 
 // One path: path group b = (tile b / nsb, sample si0 + b % nsb), lane_id = pixel of the tile.
 template <bool MULTI>
-__device__ __forceinline__ void ff_one_path(const RenderArgs& A, const FFScratch& S, int* stack, uint32_t b,
+__device__ __forceinline__ void ff_one_path(const RenderArgs& A, FFScratch& S, int* stack, uint32_t b,
                                             uint32_t lane_id, size_t out) {
     const uint32_t tile_local = A.ff_tile_base + b / A.ff_nsb;
     const int si = (int)(A.ff_si0 + b % A.ff_nsb);
@@ -495,7 +537,7 @@ __global__ void __launch_bounds__(kFFBlock, 4) ff_path_kernel(RenderArgs A) {
     __shared__ int s_stack[kStackSize * kFFBlock];
     int* stack = s_stack + threadIdx.x;
     const uint32_t gt = blockIdx.x * kFFBlock + threadIdx.x;
-    const FFScratch S{A.ff_hit + gt, A.ff_act0 + gt, A.ff_act1 + gt, A.ff_threads};
+    FFScratch S{A.ff_hit + gt, A.ff_act0 + gt, A.ff_act1 + gt, A.ff_threads, 0};
     const uint32_t lane = threadIdx.x & 63u;
     for (;;) {
         unsigned long long base = 0;

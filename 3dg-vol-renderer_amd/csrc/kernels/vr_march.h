@@ -428,7 +428,13 @@ __device__ __forceinline__ bool traverse_wide(const RenderArgs& A, const Ray& r0
                                               Leaf leaf, OnNode on_node = OnNode()) {
     float ox = r0.ox, oy = r0.oy, oz = r0.oz;
     node_space<true>(A, ox, oy, oz);
-    const float ix = __frcp_rn(r0.dx * A.hn_scale), iy = __frcp_rn(r0.dy * A.hn_scale), iz = __frcp_rn(r0.dz * A.hn_scale);
+    // |d| clamped away from 0 (axis-parallel rays, e.g. an orthographic camera looking along an
+    // axis): the fma slab form b/d - o/d must never see inf - inf
+    auto inv = [&](float d) {
+        d *= A.hn_scale;
+        return __frcp_rn(fabsf(d) > 1e-30f ? d : copysignf(1e-30f, d));
+    };
+    const float ix = inv(r0.dx), iy = inv(r0.dy), iz = inv(r0.dz);
     const float oxi = ox * ix, oyi = oy * iy, ozi = oz * iz;
     int sp = 0;
     int node = 0;

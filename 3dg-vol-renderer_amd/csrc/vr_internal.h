@@ -53,7 +53,10 @@ struct HNode4 {
 };
 static_assert(sizeof(HNode4) == 64, "4-wide half node must be 64 B");
 
-constexpr int kLeafMax = 3;          // primitives per leaf (<= 16: leaf refs hold count - 1 in 4 bits)
+#ifndef VR_LEAF_MAX
+#define VR_LEAF_MAX 3
+#endif
+constexpr int kLeafMax = VR_LEAF_MAX;  // primitives per leaf (<= 16: leaf refs hold count - 1 in 4 bits)
 constexpr int kMaxDepth = 30;        // builder guarantees node depth <= kMaxDepth
 // Per-lane traversal-stack capacity of the 4-wide walk (up to 3 pushes per level; the collapsed
 // tree is no deeper than the pair tree): sizes the persistent kernel's global stack overflow.
