@@ -93,7 +93,7 @@ struct vr_ctx {
     };
     Buf px_first, px_T, rec_pos, rec_meta, rec_next, rec_act, tr, rec_alloc, rec_bloom, slowq;
     Buf pcg_jump, ray_next, rec_list, rec_nlist, stack_ovf, env_order, rec_cut;
-    Buf ff_scratch, ff_path, ff_sum;  // free-flight integrators (vr_freeflight.hip)
+    Buf ff_scratch, ff_tail, ff_sum, ff_nee;  // free-flight integrators (vr_freeflight.hip)
     uint32_t* d_order = nullptr;      // record (leaf order) -> scene index
     Buf rec_bits[2];                  // RECORD_PIXEL_GAUSSIANS bitsets (vr_render_record slots)
     uint32_t rec_npix[2] = {0, 0}, rec_n[2] = {0, 0};
@@ -107,6 +107,7 @@ struct vr_ctx {
     int64_t opt_half_nodes = 1;        // VR_OPT_HALF_NODES
     int64_t opt_secondary_budget = 1;  // VR_OPT_SECONDARY_BUDGET
     int64_t opt_ff_window0 = 8;        // VR_OPT_FF_WINDOW0
+    int64_t opt_ff_nee_queue = 6;      // VR_OPT_FF_NEE_QUEUE
     int64_t opt_device_bvh = 0;        // VR_OPT_DEVICE_BVH
     bool last_upload_device_bvh = false;  // the current scene's tree came from the device builder
     vr_group* group = nullptr;         // vr_init_multi: the devices this context drives (host/vr_multi.cpp)
@@ -642,25 +643,31 @@ vr_status gauss_pipeline(vr_ctx* c, RenderArgs& A, hipStream_t s, bool stats) {
     return VR_OK;
 }
 
-// Free-flight integrators: one persistent launch per chunk of tiles (all samples of those tiles,
-// at most kFFMaxPaths paths) on a grid of resident waves that claim 64-path groups from a counter;
-// then the chunk's path radiance is added to the pixels in sample order (vr_freeflight.hip).
-constexpr uint64_t kFFMaxPaths = 1ull << 27;
+// Free-flight integrators: one persistent launch per chunk of tiles x batch of samples (at most
+// kFFMaxPaths paths) on a grid of resident waves that claim 64-path groups from a counter, the
+// launch's queued shadow rays (deferred NEE), then the paths' radiance is added to the pixels in
+// sample order (vr_freeflight.hip).
+constexpr uint64_t kFFMaxPaths = 1ull << 23;
 // The active list indexes the hit buffer, so it never holds more than kFFHitCap entries: the only
 // capacity a path can exceed is kFFHitCap Gaussians overlapping one point (error path, NaN).
 constexpr int32_t kFFHitCap = 128, kFFActCap = kFFHitCap;
 vr_status free_flight_pipeline(vr_ctx* c, RenderArgs& A, hipStream_t s) {
     const uint32_t spp = (uint32_t)A.ff_samples;
-    if ((uint64_t)spp * 256u > kFFMaxPaths) return fail(VR_ERR_INVALID, "num_samples too large");
     int cus = 0;
     HIP_TRY(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, c->device), "hipDeviceGetAttribute");
     const uint32_t threads = (uint32_t)std::max(1, cus) * 4u * 256u;  // 4 waves/SIMD x 4 SIMDs = 4 blocks per CU
-    const uint32_t chunk = (uint32_t)std::min<uint64_t>(A.num_tiles, kFFMaxPaths / ((uint64_t)spp * 256u));
+    const uint32_t nsb = (uint32_t)std::min<uint64_t>(spp, kFFMaxPaths / 256u);  // samples per launch
+    const uint32_t chunk = (uint32_t)std::min<uint64_t>(A.num_tiles, kFFMaxPaths / ((uint64_t)nsb * 256u));
+    const uint64_t paths = (uint64_t)chunk * nsb * 256u;  // most paths of one launch
     vr_status st = grow(c->ff_scratch, (size_t)threads * (kFFHitCap + 2 * kFFActCap) * 16 + 64, "free-flight scratch");
     if (st != VR_OK) return st;
-    if ((st = grow(c->ff_path, (size_t)chunk * spp * 256 * 3 * sizeof(float), "free-flight paths")) != VR_OK) return st;
+    if ((st = grow(c->ff_tail, paths * sizeof(float4), "free-flight paths")) != VR_OK) return st;
     if ((st = grow(c->ff_sum, (size_t)A.num_tiles * 256 * 3 * sizeof(float), "free-flight sums")) != VR_OK) return st;
-    const uint32_t nsb = spp;
+    A.ff_nee_cap = (uint32_t)std::min<uint64_t>(paths * (uint64_t)c->opt_ff_nee_queue, kFFNone);
+    if (A.ff_nee_cap > 0) {
+        if ((st = grow(c->ff_nee, (size_t)A.ff_nee_cap * 3 * sizeof(float4), "free-flight shadow-ray queue")) != VR_OK) return st;
+        A.ff_nee = (float4*)c->ff_nee.p;
+    }
     float4* base = (float4*)c->ff_scratch.p;
     A.ff_threads = threads;
     A.ff_hit_cap = kFFHitCap;
@@ -670,7 +677,8 @@ vr_status free_flight_pipeline(vr_ctx* c, RenderArgs& A, hipStream_t s) {
     A.ff_act0 = base + (size_t)kFFHitCap * threads;
     A.ff_act1 = base + (size_t)(kFFHitCap + kFFActCap) * threads;
     A.ff_next = (unsigned long long*)(base + (size_t)(kFFHitCap + 2 * kFFActCap) * threads);
-    A.ff_path = (float*)c->ff_path.p;
+    A.ff_nee_n = (uint32_t*)(A.ff_next + 1);
+    A.ff_tail = (float4*)c->ff_tail.p;
     A.ff_sum = (float*)c->ff_sum.p;
     for (uint32_t t0 = 0; t0 < A.num_tiles; t0 += chunk) {
         const uint32_t nt = std::min(chunk, A.num_tiles - t0);
@@ -838,7 +846,7 @@ void vr_destroy(vr_ctx* c) {
     if (c->h_sizing) (void)hipHostFree(c->h_sizing);
     for (vr_ctx::Buf* b : {&c->px_first, &c->px_T, &c->rec_pos, &c->rec_meta, &c->rec_next, &c->rec_act, &c->tr,
                            &c->rec_alloc, &c->rec_bloom, &c->slowq, &c->pcg_jump, &c->ray_next, &c->rec_list, &c->rec_nlist,
-                           &c->stack_ovf, &c->env_order, &c->rec_cut, &c->ff_scratch, &c->ff_path, &c->ff_sum, &c->rec_bits[0], &c->rec_bits[1], &c->sfd_tmp, &c->sfd_ref,
+                           &c->stack_ovf, &c->env_order, &c->rec_cut, &c->ff_scratch, &c->ff_tail, &c->ff_sum, &c->ff_nee, &c->rec_bits[0], &c->rec_bits[1], &c->sfd_tmp, &c->sfd_ref,
                            &c->sfd_loss[0], &c->sfd_loss[1], &c->sfd_out})
         if (b->p) (void)hipFree(b->p);
     if (c->d_frame) (void)hipFree(c->d_frame);
@@ -1194,6 +1202,10 @@ vr_status vr_set_option(vr_ctx* c, int32_t option, int64_t value) {
             if (value < 1 || value > kFFHitCap) return fail(VR_ERR_INVALID, "VR_OPT_FF_WINDOW0 must be in [1, 128]");
             c->opt_ff_window0 = value;
             return VR_OK;
+        case VR_OPT_FF_NEE_QUEUE:
+            if (value < 0 || value > (int64_t)kFFNeeMaxPerPath) return fail(VR_ERR_INVALID, "VR_OPT_FF_NEE_QUEUE must be in [0, 16]");
+            c->opt_ff_nee_queue = value;
+            return VR_OK;
         case VR_OPT_DEVICE_BVH:
             if (value != 0 && value != 1) return fail(VR_ERR_INVALID, "VR_OPT_DEVICE_BVH must be 0 or 1");
             c->opt_device_bvh = value;
@@ -1217,6 +1229,7 @@ vr_status vr_get_option(vr_ctx* c, int32_t option, int64_t* value) {
         case VR_OPT_FF_WINDOW0: *value = c->opt_ff_window0; return VR_OK;
         case VR_OPT_RECORD_CAPACITY: *value = (int64_t)c->rec_hint; return VR_OK;
         case VR_OPT_DEVICE_BVH: *value = c->opt_device_bvh; return VR_OK;
+        case VR_OPT_FF_NEE_QUEUE: *value = c->opt_ff_nee_queue; return VR_OK;
         default: return fail(VR_ERR_INVALID, "vr_get_option: unknown option " + std::to_string(option));
     }
 }

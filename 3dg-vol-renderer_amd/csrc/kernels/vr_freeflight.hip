@@ -249,24 +249,34 @@ __device__ float evaluate_albedo(const RenderArgs& A, const FFScratch& S, int m,
 }
 
 // gmm.h:517-578: exp(-sum tau_i(max(0,t0_i), min(tmax,t1_i))), unsorted, double accumulation.
-__device__ float transmittance_up_to(const RenderArgs& A, const Ray& r, float tmax, int* stack, int stride) {
+// The shadow ray only feeds a continuous quantity (Tr), so it uses the FMA-contracted quadratic and
+// hardware rcp/rsq forms (vr_march.h *_fast, as the ray-march's secondary rays do); the path's own
+// discrete decisions keep the exact forms.
+__device__ __forceinline__ void shadow_leaf(const RenderArgs& A, const Ray& r, float tmax, uint32_t first, uint32_t count,
+                                            double& sum) {
+    for (uint32_t j = first; j < first + count; ++j) {
+        GRec g = load_rec(A.gauss, (int)j);
+        Quad q = quad_fast(g, r);
+        float t0, t1;
+        if (!intersect_fast(q, t0, t1)) continue;
+        float a = fmaxf(0.0f, t0);
+        float b = fminf(tmax, t1);
+        if (b > a) sum += (double)optical_depth_fast(g, q, a, b);
+    }
+}
+__device__ __forceinline__ float shadow_prune_lim(float tmax) { return tmax + kTPad * (1.0f + fminf(tmax, 1e30f)); }
+
+__device__ __forceinline__ float transmittance_up_to(const RenderArgs& A, const Ray& r, float tmax, int* stack, int stride) {
     if (!(tmax > 0.0f)) return 1.0f;
 #ifdef VR_DIAG_FF_NO_NEE  // diagnostic builds only (cost attribution): the shadow walk is skipped
     return 0.5f;
 #endif
     double sum = 0.0;
+    const float lim = shadow_prune_lim(tmax);
     walk(
-        A, r, stack, stride, [&](float tmin, float) { return tmin <= tmax + kTPad * (1.0f + fminf(tmax, 1e30f)); },
+        A, r, stack, stride, [&](float tmin, float) { return tmin <= lim; },
         [&](uint32_t first, uint32_t count) {
-            for (uint32_t j = first; j < first + count; ++j) {
-                GRec g = load_rec(A.gauss, (int)j);
-                Quad q = quad(g, r);
-                float t0, t1;
-                if (!intersect(q, t0, t1)) continue;
-                float a = fmaxf(0.0f, t0);
-                float b = fminf(tmax, t1);
-                if (b > a) sum += (double)optical_depth(g, q, a, b);
-            }
+            shadow_leaf(A, r, tmax, first, count, sum);
             return sum < 104.0;  // expf(-x) == 0 in f32 for x >= 104: later terms cannot change Tr
         },
         [&]() { sum = 0.0; });
@@ -433,6 +443,51 @@ __device__ float free_flight_distance(const RenderArgs& A, FFScratch& S, const R
     }
 }
 
+// Deferred NEE: queue the shadow ray r (tmax: the light distance, +inf for the environment; li: the
+// light, -1 the environment) with its weight m, linked after the path's previous queued ray. The
+// claim is wave-aggregated (one atomic per wave). Returns false if the ray must be traced inline
+// (deferral off, or the queue is full); from then on the path stays inline, so its deferred
+// contributions all come before its inline ones (bounce order).
+__device__ __forceinline__ bool nee_queue(const RenderArgs& A, const Ray& r, float tmax, int li, float m0, float m1,
+                                          float m2, uint32_t& first, uint32_t& last, bool& defer) {
+    const uint64_t mask = __ballot(defer);
+    if (!defer) return false;
+    const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u));
+    uint32_t base = 0;
+    if (rank == 0) base = atomicAdd(A.ff_nee_n, (uint32_t)__popcll(mask));
+    base = __shfl(base, __ffsll((unsigned long long)mask) - 1, 64);
+    const uint32_t q = base + rank;
+    if (q >= A.ff_nee_cap) {
+        defer = false;
+        return false;
+    }
+    float4* e = A.ff_nee + 3 * (size_t)q;
+    e[0] = make_float4(r.ox, r.oy, r.oz, tmax);
+    e[1] = make_float4(r.dx, r.dy, r.dz, __uint_as_float(kFFNone));
+    e[2] = make_float4(m0, m1, m2, __int_as_float(li));
+    if (last != kFFNone) A.ff_nee[3 * (size_t)last + 1].w = __uint_as_float(q);
+    else first = q;
+    last = q;
+    return true;
+}
+
+// Incident radiance of a shadow ray with transmittance Tr: I_l Tr / d^2 (integrator.h:385-388) or
+// env Tr 4 pi (:390-394), in the reference's operation order.
+__device__ __forceinline__ void nee_radiance(const RenderArgs& A, float Tr, int li, float dist, float& Li0, float& Li1,
+                                             float& Li2) {
+    if (li >= 0) {
+        const LightRecord& Lt = A.lights[li];
+        const float d2 = dist * dist;
+        Li0 = __fdiv_rn(Tr * Lt.ix, d2);
+        Li1 = __fdiv_rn(Tr * Lt.iy, d2);
+        Li2 = __fdiv_rn(Tr * Lt.iz, d2);
+    } else {
+        Li0 = (Tr * A.env[0]) * k4Pi;
+        Li1 = (Tr * A.env[1]) * k4Pi;
+        Li2 = (Tr * A.env[2]) * k4Pi;
+    }
+}
+
 // One path: path group b = (tile b / nsb, sample si0 + b % nsb), lane_id = pixel of the tile.
 template <bool MULTI>
 __device__ __forceinline__ void ff_one_path(const RenderArgs& A, FFScratch& S, int* stack, uint32_t b,
@@ -441,7 +496,11 @@ __device__ __forceinline__ void ff_one_path(const RenderArgs& A, FFScratch& S, i
     const int si = (int)(A.ff_si0 + b % A.ff_nsb);
     int lx, ly, x, y;
     tile_pixel(A, tile_local, (int)lane_id, lx, ly, x, y);
+    // L: the radiance this thread adds itself (inline NEE terms, the environment term); the path's
+    // total is its nd deferred contributions in bounce order, then L if `after` (ff_accumulate_kernel)
     float L0 = 0.0f, L1 = 0.0f, L2 = 0.0f;
+    uint32_t first = kFFNone, last = kFFNone;  // the path's queued shadow rays
+    bool defer = A.ff_nee_cap > 0, after = false;
     if (x < (int)A.width && y < (int)A.height) {
         PCG32 rng(derive_path_seed(x, y, si), 1);
         const int n = A.ff_n;
@@ -463,6 +522,7 @@ __device__ __forceinline__ void ff_one_path(const RenderArgs& A, FFScratch& S, i
                 record_hits(A, ray, ts >= 0.0f ? ts + 1e-6f : INFINITY, (uint32_t)y * A.width + (uint32_t)x, stack, kFFBlock);
             if (ts == -2.0f || bounce >= A.ff_max_bounces) {
                 L0 = L1 = L2 = __builtin_nanf("");
+                after = true;
                 atomicAdd(A.counters, 1u);
                 break;
             }
@@ -470,43 +530,46 @@ __device__ __forceinline__ void ff_one_path(const RenderArgs& A, FFScratch& S, i
                 L0 += tp0 * A.env[0];
                 L1 += tp1 * A.env[1];
                 L2 += tp2 * A.env[2];
+                after |= first != kFFNone;
                 break;
             }
             const float px = ray.ox + ts * ray.dx, py = ray.oy + ts * ray.dy, pz = ray.oz + ts * ray.dz;
             const float albedo = evaluate_albedo(A, S, m, px, py, pz);
+            // NEE (integrator.h:380-399 / 650-687): a light (distance-bounded) or environment shadow ray
             const bool is_env = rng.uniform() < p_env;
-            float Li0, Li1, Li2;
+            int li = -1;
+            float dist = INFINITY;
+            Ray sr;
             if (!is_env) {
-                int li = (int)(rng.uniform() * (float)nl);
+                li = (int)(rng.uniform() * (float)nl);
                 const LightRecord& Lt = A.lights[li];
                 float wx = Lt.px - px, wy = Lt.py - py, wz = Lt.pz - pz;
-                float dist = sqrtf(dot3(wx, wy, wz, wx, wy, wz));
+                dist = sqrtf(dot3(wx, wy, wz, wx, wy, wz));
                 normalize3(wx, wy, wz);
-                Ray sr = make_ray(px, py, pz, wx, wy, wz);
-                float Tr = transmittance_up_to(A, sr, dist, stack, kFFBlock);
-                float d2 = dist * dist;
-                Li0 = __fdiv_rn(Tr * Lt.ix, d2);
-                Li1 = __fdiv_rn(Tr * Lt.iy, d2);
-                Li2 = __fdiv_rn(Tr * Lt.iz, d2);
+                sr = make_ray(px, py, pz, wx, wy, wz);
             } else {
                 float wx, wy, wz;
                 sample_uniform_direction(rng, wx, wy, wz);
-                Ray er = make_ray(px, py, pz, wx, wy, wz);
-                float Tr = transmittance_up_to(A, er, INFINITY, stack, kFFBlock);
-                Li0 = (Tr * A.env[0]) * k4Pi;
-                Li1 = (Tr * A.env[1]) * k4Pi;
-                Li2 = (Tr * A.env[2]) * k4Pi;
+                sr = make_ray(px, py, pz, wx, wy, wz);
             }
             const float w = (albedo * kInv4Pi) * w_ne;
-            if constexpr (!MULTI) {  // integrator.h:396-399
-                L0 = w * Li0;
-                L1 = w * Li1;
-                L2 = w * Li2;
-                break;
+            // the contribution is m * Li: L += (tp * w) * Li (integrator.h:681-687), L = w * Li (:396-399)
+            const float m0 = MULTI ? tp0 * w : w, m1 = MULTI ? tp1 * w : w, m2 = MULTI ? tp2 * w : w;
+            if (!nee_queue(A, sr, dist, li, m0, m1, m2, first, last, defer)) {
+                float Li0, Li1, Li2;
+                nee_radiance(A, transmittance_up_to(A, sr, dist, stack, kFFBlock), li, dist, Li0, Li1, Li2);
+                after |= first != kFFNone;
+                if constexpr (!MULTI) {
+                    L0 = m0 * Li0;
+                    L1 = m1 * Li1;
+                    L2 = m2 * Li2;
+                } else {
+                    L0 += m0 * Li0;
+                    L1 += m1 * Li1;
+                    L2 += m2 * Li2;
+                }
             }
-            L0 += (tp0 * w) * Li0;  // integrator.h:681-687
-            L1 += (tp1 * w) * Li1;
-            L2 += (tp2 * w) * Li2;
+            if constexpr (!MULTI) break;
             tp0 *= albedo;
             tp1 *= albedo;
             tp2 *= albedo;
@@ -522,9 +585,7 @@ __device__ __forceinline__ void ff_one_path(const RenderArgs& A, FFScratch& S, i
             ray = make_ray(px, py, pz, nx, ny, nz);
         }
     }
-    A.ff_path[out * 3 + 0] = L0;
-    A.ff_path[out * 3 + 1] = L1;
-    A.ff_path[out * 3 + 2] = L2;
+    A.ff_tail[out] = make_float4(L0, L1, L2, __uint_as_float(first | (after ? kFFTailAfter : 0u)));
 }
 
 // Persistent: a grid of resident waves; each wave claims the next 64 paths (one 8x8 pixel block
@@ -549,6 +610,117 @@ __global__ void __launch_bounds__(kFFBlock, 4) ff_path_kernel(RenderArgs A) {
     }
 }
 
+// Traces the launch's queued shadow rays: the walk of transmittance_up_to (4-wide tree, near-first,
+// leaves as they are reached, the same double sum and early stop, so Tr is bit-identical to an
+// inline trace) as a persistent while-while loop: one node step per lane per iteration, and a lane
+// whose ray is done takes the next queued ray (claimed per wave once 16 lanes are idle), so a wave
+// never waits for its longest ray. Each ray's contribution m * Li replaces its weight m in place.
+__device__ __forceinline__ void nee_finish(const RenderArgs& A, uint32_t id, float tmax, float Tr) {
+    float4& c = A.ff_nee[3 * (size_t)id + 2];
+    const float4 m = c;
+    float Li0, Li1, Li2;
+    nee_radiance(A, Tr, __float_as_int(m.w), tmax, Li0, Li1, Li2);
+    c = make_float4(m.x * Li0, m.y * Li1, m.z * Li2, m.w);
+}
+
+#ifndef VR_NEE_REFILL
+#define VR_NEE_REFILL 40  // idle lanes that trigger a wave refill (A/B: 16-56; 40 balances C2 and C3)
+#endif
+#ifndef VR_NEE_BLOCKS
+#define VR_NEE_BLOCKS 4  // resident 256-lane blocks per CU
+#endif
+__global__ void __launch_bounds__(kFFBlock) ff_nee_kernel(RenderArgs A) {
+    __shared__ int s_stack[kStackSize * kFFBlock];
+    int* stack = s_stack + threadIdx.x;
+    const uint32_t n = min(A.ff_nee_n[0], A.ff_nee_cap);
+    const uint32_t lane = threadIdx.x & 63u;
+    bool live = false, exhausted = false;  // exhausted: wave-uniform, the queue is handed out
+    uint32_t id = 0;
+    Ray r{};
+    float tmax = 0.0f, lim = 0.0f, ix = 0.0f, iy = 0.0f, iz = 0.0f, oxi = 0.0f, oyi = 0.0f, ozi = 0.0f;
+    double sum = 0.0;
+    int sp = 0, node = 0;
+    for (;;) {
+        const uint64_t idle = __ballot(!live);
+        if (!exhausted && (idle == ~0ull || __popcll(idle) >= VR_NEE_REFILL)) {
+            uint32_t base = 0;
+            if (lane == 0) base = atomicAdd(A.ff_nee_n + 1, (uint32_t)__popcll(idle));
+            base = (uint32_t)__builtin_amdgcn_readfirstlane((int)base);
+            exhausted = base + (uint32_t)__popcll(idle) >= n;
+            if (!live) {
+                id = base + __builtin_amdgcn_mbcnt_hi((uint32_t)(idle >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)idle, 0u));
+                if (id < n) {
+                    const float4 a = A.ff_nee[3 * (size_t)id], b = A.ff_nee[3 * (size_t)id + 1];  // b.w: link
+                    r = Ray{a.x, a.y, a.z, b.x, b.y, b.z};
+                    tmax = a.w;
+                    if (!(tmax > 0.0f)) {
+                        nee_finish(A, id, tmax, 1.0f);
+                    } else {  // traverse_wide's ray setup
+                        float ox = r.ox, oy = r.oy, oz = r.oz;
+                        node_space<true>(A, ox, oy, oz);
+                        auto inv = [&](float d) {
+                            d *= A.hn_scale;
+                            return __frcp_rn(fabsf(d) > 1e-30f ? d : copysignf(1e-30f, d));
+                        };
+                        ix = inv(r.dx), iy = inv(r.dy), iz = inv(r.dz);
+                        oxi = ox * ix, oyi = oy * iy, ozi = oz * iz;
+                        lim = shadow_prune_lim(tmax);
+                        sum = 0.0;
+                        sp = 0;
+                        node = 0;
+                        live = true;
+                    }
+                }
+            }
+        }
+        if (!__any(live)) {
+            if (exhausted) break;
+            continue;
+        }
+        if (live) {  // one 4-wide node step (traverse_wide's body)
+            float key[4];
+            int32_t kr[4];
+            wide_children(A, node, ix, iy, iz, oxi, oyi, ozi, [&](float tmin, float) { return tmin <= lim; }, key, kr);
+            bool stop = false;
+#pragma unroll
+            for (int i = 0; i < 4; ++i)  // leaves, near first
+                if (!stop && kr[i] < 0) {
+                    shadow_leaf(A, r, tmax, leaf_first(kr[i]), leaf_count(kr[i]), sum);
+                    stop = !(sum < 104.0);
+                }
+            int first = -1;
+            int32_t next = 0;
+#pragma unroll
+            for (int i = 3; i >= 0; --i) {
+                first = kr[i] > 0 ? i : first;
+                next = kr[i] > 0 ? kr[i] : next;
+            }
+            bool done = stop;
+            if (!stop && sp + 3 > kStackSize) {  // the 4-wide stack could overflow: whole walk, pair-tree fallback
+                sum = -1.0;
+                done = true;
+            } else if (!stop) {
+#pragma unroll
+                for (int i = 3; i >= 0; --i)
+                    if (kr[i] > 0 && i != first) stack[(sp++) * kFFBlock] = kr[i];
+                if (first >= 0) {
+                    node = next;
+                } else if (sp == 0) {
+                    done = true;
+                } else {
+                    --sp;
+                    node = stack[sp * kFFBlock];
+                }
+            }
+            if (done) {
+                const float Tr = sum < 0.0 ? transmittance_up_to(A, r, tmax, stack, kFFBlock) : expf(-(float)sum);
+                nee_finish(A, id, tmax, Tr);
+                live = false;
+            }
+        }
+    }
+}
+
 // pixel_L += L_accum in sample order (integrator.h:706), then pixel_L / num_samples on the last batch.
 __global__ void __launch_bounds__(kFFBlock) ff_accumulate_kernel(RenderArgs A, uint32_t chunk_tiles) {
     const uint32_t tl = blockIdx.x;  // tile within the chunk
@@ -562,10 +734,27 @@ __global__ void __launch_bounds__(kFFBlock) ff_accumulate_kernel(RenderArgs A, u
         s2 = A.ff_sum[p * 3 + 2];
     }
     for (uint32_t s = 0; s < A.ff_nsb; ++s) {
-        const size_t q = ((size_t)(tl * A.ff_nsb + s) * kFFBlock + threadIdx.x) * 3;
-        s0 += A.ff_path[q + 0];
-        s1 += A.ff_path[q + 1];
-        s2 += A.ff_path[q + 2];
+        const size_t q = (size_t)(tl * A.ff_nsb + s) * kFFBlock + threadIdx.x;
+        const float4 t = A.ff_tail[q];  // the path's radiance: its queued contributions in order, then t.xyz
+        const uint32_t f = __float_as_uint(t.w);
+        float p0 = t.x, p1 = t.y, p2 = t.z;
+        if ((f & ~kFFTailAfter) != kFFNone) {
+            p0 = p1 = p2 = 0.0f;
+            for (uint32_t e = f & ~kFFTailAfter; e != kFFNone; e = __float_as_uint(A.ff_nee[3 * (size_t)e + 1].w)) {
+                const float4 c = A.ff_nee[3 * (size_t)e + 2];
+                p0 += c.x;
+                p1 += c.y;
+                p2 += c.z;
+            }
+            if (f & kFFTailAfter) {
+                p0 += t.x;
+                p1 += t.y;
+                p2 += t.z;
+            }
+        }
+        s0 += p0;
+        s1 += p1;
+        s2 += p2;
     }
     if (A.ff_si0 + A.ff_nsb < (uint32_t)A.ff_samples) {
         A.ff_sum[p * 3 + 0] = s0;
@@ -638,6 +827,7 @@ hipError_t launch_sfd_loss_diff(const uint32_t* bits0, const uint32_t* bits1, co
 hipError_t launch_free_flight(const RenderArgs& A, uint32_t chunk_tiles, hipStream_t stream) {
     hipError_t e0 = hipMemsetAsync(A.ff_next, 0, sizeof(unsigned long long), stream);
     if (e0 != hipSuccess) return e0;
+    if (A.ff_nee_cap > 0 && (e0 = hipMemsetAsync(A.ff_nee_n, 0, 2 * sizeof(uint32_t), stream)) != hipSuccess) return e0;
     dim3 grid(A.ff_threads / dev::kFFBlock);
     if (A.ff_multi)
         hipLaunchKernelGGL(dev::ff_path_kernel<true>, grid, dim3(dev::kFFBlock), 0, stream, A);
@@ -645,6 +835,10 @@ hipError_t launch_free_flight(const RenderArgs& A, uint32_t chunk_tiles, hipStre
         hipLaunchKernelGGL(dev::ff_path_kernel<false>, grid, dim3(dev::kFFBlock), 0, stream, A);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
+    if (A.ff_nee_cap > 0) {
+        hipLaunchKernelGGL(dev::ff_nee_kernel, dim3(A.ff_threads / 1024u * VR_NEE_BLOCKS), dim3(dev::kFFBlock), 0, stream, A);
+        if ((e = hipGetLastError()) != hipSuccess) return e;
+    }
     hipLaunchKernelGGL(dev::ff_accumulate_kernel, dim3(chunk_tiles), dim3(dev::kFFBlock), 0, stream, A, chunk_tiles);
     return hipGetLastError();
 }

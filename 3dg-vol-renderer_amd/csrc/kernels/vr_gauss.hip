@@ -553,7 +553,8 @@ __device__ __forceinline__ bool sec_init(const RenderArgs& A, uint32_t nrec, uin
     const float4 pos = A.rec_pos[r];
     const uint4 meta = A.rec_meta[r];
     R.rec = r;
-    R.cut = A.rec_cut != nullptr ? A.rec_cut[r] : A.tau_cut;
+    R.cut = A.tau_cut;  // (a select of the two addresses would make this one flat load)
+    if (A.rec_cut != nullptr) R.cut = __builtin_nontemporal_load(A.rec_cut + r);
     R.act_off = meta.z;
     R.act_n = meta.w;
     R.bloom = A.rec_bloom[r];
@@ -739,13 +740,18 @@ constexpr bool kQueueRing = QCAP > 4;
 template <int QCAP>
 constexpr int kQueueLds = kQueueRing<QCAP> ? QCAP - 1 : QCAP - 2;  // LDS words per lane of the queue
 
+// An int in LDS (address space 3). The traversal stack and leaf queue are reached through this type
+// so that a pop that may come from the LDS stack or the global overflow stays two typed loads (a
+// ds_read and a global_load) instead of one flat load whose wait covers every outstanding access.
+using LdsInt = __attribute__((address_space(3))) int;
+
 struct LeafQueue {
     int32_t q0, q1;
     int n;
     uint32_t j, end;  // current primitive range [j, end)
     // branch-free for the register entries: writes r at slot `idx` (no slot matches idx < 0)
     template <int QCAP, int BLOCK>
-    __device__ __forceinline__ void put(int idx, int32_t r, int* ext) {
+    __device__ __forceinline__ void put(int idx, int32_t r, LdsInt* ext) {
         if constexpr (kQueueRing<QCAP>) {
             q0 = idx == 0 ? r : q0;
             if (idx >= 1) ext[((q1 + idx - 1) & (QCAP - 2)) * BLOCK] = r;
@@ -758,7 +764,7 @@ struct LeafQueue {
     }
     __device__ __forceinline__ bool has_prim() const { return j < end || n > 0; }
     template <int QCAP, int BLOCK>
-    __device__ __forceinline__ uint32_t next(int* ext) {  // requires has_prim()
+    __device__ __forceinline__ uint32_t next(LdsInt* ext) {  // requires has_prim()
         if (j == end) {
             j = leaf_first(q0);
             end = j + leaf_count(q0);
@@ -795,7 +801,7 @@ __device__ __forceinline__ uint32_t ovf_slot(const RenderArgs& A, int sp) {
 // far (misses last); leaf children go to the leaf queue in that order, the nearest inner child
 // is walked next and the other inner ones are pushed far-first (so the nearer pop first).
 template <int BLOCK, bool S, int QCAP, int STACK>
-__device__ __forceinline__ void sec_node4(const RenderArgs& A, SecRay& R, int* stack, int& sp, int& node, LeafQueue& Q,
+__device__ __forceinline__ void sec_node4(const RenderArgs& A, SecRay& R, LdsInt* stack, int& sp, int& node, LeafQueue& Q,
                                           Ctr& c) {
     if constexpr (S) {
         c.v[kCtrNodes]++;
@@ -836,7 +842,7 @@ __device__ __forceinline__ void sec_node4(const RenderArgs& A, SecRay& R, int* s
         // Branch-free: every lane stores each child at the queue's end; a non-leaf store lands past
         // the last entry (never read, overwritten by the next put). A NODE step starts with at most
         // QCAP - 4 entries, so that slot is always a free ring word.
-        int* ext = stack + STACK * BLOCK;
+        LdsInt* ext = stack + STACK * BLOCK;
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
             const bool leaf = kr[i] < 0;
@@ -901,7 +907,7 @@ __device__ __forceinline__ void sec_node4(const RenderArgs& A, SecRay& R, int* s
 // first); node < 0 afterwards means the traversal is finished. Written branch-free (bitwise
 // predicates, selects) so a wave does not split inside the step.
 template <int BLOCK, bool S, int QCAP, int STACK, bool H>
-__device__ __forceinline__ void sec_node(const RenderArgs& A, SecRay& R, int* stack, int& sp, int& node, LeafQueue& Q,
+__device__ __forceinline__ void sec_node(const RenderArgs& A, SecRay& R, LdsInt* stack, int& sp, int& node, LeafQueue& Q,
                                          Ctr& c) {
     if constexpr (S) {
         c.v[kCtrNodes]++;
@@ -1109,7 +1115,7 @@ constexpr int kRefillMin = 24, kNodeSteps = 6, kPrimSteps = 6;
 template <int BLOCK, int STACK, bool S, bool PURE, int WAVES, int QCAP, bool H, bool W>
 __global__ __launch_bounds__(BLOCK, WAVES) void secondary_ww_kernel(RenderArgs A) {
     __shared__ int s_stack[(STACK + kQueueLds<QCAP>) * BLOCK];
-    int* stack = s_stack + threadIdx.x;
+    LdsInt* stack = (LdsInt*)(s_stack + threadIdx.x);  // LDS-typed: stack/queue accesses are ds_* ops, never flat
     const uint32_t lane = threadIdx.x & 63u;
     Ctr c{};
     SecRay R;

@@ -94,6 +94,11 @@ constexpr int kListCap = 48;
 constexpr float kListR2 = 9.5f;
 constexpr float kListCentral = 4.0f;  // members with q <= 4 (inside 2 sigma) are tested first
 constexpr int kMaxSpheres = 64;
+// Deferred NEE (free-flight): a path's queued shadow rays are a linked list in the queue (kFFNone ends
+// it); ff_tail's flag bit says its inline radiance follows them.
+constexpr uint32_t kFFNone = 0x7fffffffu;
+constexpr uint32_t kFFTailAfter = 0x80000000u;
+constexpr uint32_t kFFNeeMaxPerPath = 16;  // VR_OPT_FF_NEE_QUEUE bound (queue rays per path of a launch)
 
 // Kernel launch parameters (passed by value).
 struct RenderArgs {
@@ -172,8 +177,15 @@ struct RenderArgs {
     float4* ff_act1;         // scratch [act_cap][threads]: per active entry F, F_next, t1, hit slot
     unsigned long long* ff_next;  // persistent path kernel: next unclaimed path of the launch
     unsigned long long ff_total;  // paths of the launch (tiles of the chunk x samples x 256)
-    float* ff_path;          // [threads][3] path radiance of the step
     float* ff_sum;           // [tile-local pixel][3] running sum over sample batches
+    // Deferred next-event estimation: the path kernel queues a bounce's shadow ray instead of tracing
+    // it; ff_nee_kernel traces the queue and writes each contribution into its path's slot; the
+    // accumulation adds a path's slots in bounce order (see vr_freeflight.hip).
+    float4* ff_nee;          // queue, 3 float4 per ray: {o, tmax}, {d, next ray of the path (bits)},
+                             // {m0 m1 m2, light bits (-1: env)}; ff_nee_kernel overwrites m with m * Li
+    uint32_t* ff_nee_n;      // [0] rays queued in the launch (may pass ff_nee_cap: those rays went inline)
+    uint32_t ff_nee_cap;     // queue capacity in rays (0: every shadow ray is traced inline)
+    float4* ff_tail;         // [path of the launch]: {inline radiance xyz, first queued ray | kFFTailAfter}
     const uint32_t* gauss_order;  // record (leaf order) -> scene index
     uint32_t* rec_bits;      // RECORD_PIXEL_GAUSSIANS bitset [word][pixel] (nullptr: not recording)
     uint32_t rec_npix;       // W * H

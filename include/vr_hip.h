@@ -327,11 +327,17 @@ typedef enum vr_option {
                                     host sync) or >= 4096. The context normally sizes it from earlier frames;
                                     setting it lets a test drive a frame over capacity (reported, then
                                     rendered again with grown buffers). Results do not depend on it. */
-    VR_OPT_DEVICE_BVH = 5        /* 0 (default): vr_upload_scene builds the BVH on the host (binned SAH);
+    VR_OPT_DEVICE_BVH = 5,       /* 0 (default): vr_upload_scene builds the BVH on the host (binned SAH);
                                     1: on the device (linear BVH: Morton sort + radix tree, kernels/
                                     vr_lbvh.hip) for scenes of >= 256 Gaussians — the fast path for the
                                     inverse loop's re-upload after every parameter update. Results are
                                     identical up to summation order (the event set is tree-independent). */
+    VR_OPT_FF_NEE_QUEUE = 6      /* free-flight integrators: shadow-ray queue capacity, in rays per path of a
+                                    launch, 0..16 (default 6). The path kernel queues each bounce's next-event
+                                    shadow ray for a separate tracing kernel; 0 traces them inline. Results
+                                    are identical (the same walk and sums) except for a path that meets a full
+                                    queue: its later contributions are traced inline and added after the
+                                    queued ones as one partial sum (float association only). */
 } vr_option;
 vr_status vr_set_option(vr_ctx* ctx, int32_t option, int64_t value);
 vr_status vr_get_option(vr_ctx* ctx, int32_t option, int64_t* value);

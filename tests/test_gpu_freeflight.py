@@ -178,3 +178,23 @@ def test_dense_reference_scenes_stay_within_the_hit_capacity(name):
         r = O.render_ff(O.OracleScene.load_gmm(path), O.PINHOLE, CAM_POS, main_view_dir(), FOV, 64, 64, multi=True,
                         num_samples=4)
     _check(g, r)
+
+
+@pytest.mark.parametrize("multi", [False, True])
+def test_deferred_shadow_rays_equal_inline(multi, device_options):
+    """VR_OPT_FF_NEE_QUEUE: the path kernel queues each bounce's shadow ray for ff_nee_kernel (the same
+    walk and double sum as an inline transmittance_up_to), linked per path, and the accumulation adds a
+    path's contributions in bounce order, so frames equal inline NEE bit for bit while the queue has
+    room. A queue of 1 ray per path fills in every launch: the paths that meet it full switch to inline
+    NEE mid-path and add those contributions as one partial sum (float association only)."""
+    scene = vr.Scene.load_GMM(scene_path("50_random.txt"))
+    frames = {}
+    for q in (0, 16, 1):
+        device_options("ff_nee_queue", q)
+        frames[q] = _gpu(scene, 40, 40, multi, 16)
+    for q in (16, 1):
+        d = np.abs(frames[q].astype(np.float64) - frames[0]).max()
+        same = float(np.mean(np.all(frames[q] == frames[0], axis=-1)))
+        print(f"queue {q}: max|d| {d:.2e}, bitwise-equal pixels {same:.4f}")
+        assert d <= 1e-6
+        assert same >= (1.0 if q == 16 else 0.5)
