@@ -8,6 +8,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <vector>
 #include <map>
 #include <mutex>
 
@@ -19,7 +20,8 @@ hipError_t gauss_march(const RenderArgs& A, hipStream_t stream, bool stats);
 hipError_t gauss_lists(const RenderArgs& A, hipStream_t stream);
 hipError_t gauss_secondary(const RenderArgs& A, hipStream_t stream, bool stats);
 hipError_t gauss_accumulate(const RenderArgs& A, hipStream_t stream);
-hipError_t launch_free_flight(const RenderArgs& A, uint32_t chunk_tiles, hipStream_t stream);
+hipError_t launch_free_flight(const RenderArgs& A, uint32_t chunk_tiles, hipStream_t stream, hipEvent_t* ev);
+uint32_t free_flight_threads(int cus);
 hipError_t launch_sfd_loss_diff(const uint32_t* bits0, const uint32_t* bits1, const float* lb, const float* lp, uint32_t npix,
                                 uint32_t n, double* out, hipStream_t stream);
 hipError_t gauss_record_cut(const RenderArgs& A, float budget, hipStream_t stream);
@@ -82,6 +84,10 @@ struct vr_ctx {
     hipEvent_t ev_report = nullptr;  // after the frame report's copies (collect() waits for it)
     hipEvent_t ev_stage[4] = {nullptr, nullptr, nullptr, nullptr};  // stage boundaries of gauss_pipeline
     bool staged = false;                                            // last launch recorded ev_stage
+    // free-flight frames: per launch, events before the path kernel, after it, after the shadow-ray
+    // kernel and after the accumulation (stage_ms of vr_get_stats sums them over the frame's launches)
+    std::vector<hipEvent_t> ff_ev;
+    uint32_t ff_launches = 0;
     bool stats_pending = false;  // h_report of the last frame has not been collected yet
     int64_t last_pixels = 0;
     uint32_t last_first_tile = 0, last_tile_stride = 1, last_tiles_x = 1, last_w = 0, last_h = 0;  // tile map of the last frame
@@ -655,7 +661,7 @@ vr_status free_flight_pipeline(vr_ctx* c, RenderArgs& A, hipStream_t s) {
     const uint32_t spp = (uint32_t)A.ff_samples;
     int cus = 0;
     HIP_TRY(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, c->device), "hipDeviceGetAttribute");
-    const uint32_t threads = (uint32_t)std::max(1, cus) * 4u * 256u;  // 4 waves/SIMD x 4 SIMDs = 4 blocks per CU
+    const uint32_t threads = free_flight_threads(cus);  // the resident grid of the persistent path kernel
     const uint32_t nsb = (uint32_t)std::min<uint64_t>(spp, kFFMaxPaths / 256u);  // samples per launch
     const uint32_t chunk = (uint32_t)std::min<uint64_t>(A.num_tiles, kFFMaxPaths / ((uint64_t)nsb * 256u));
     const uint64_t paths = (uint64_t)chunk * nsb * 256u;  // most paths of one launch
@@ -680,6 +686,7 @@ vr_status free_flight_pipeline(vr_ctx* c, RenderArgs& A, hipStream_t s) {
     A.ff_nee_n = (uint32_t*)(A.ff_next + 1);
     A.ff_tail = (float4*)c->ff_tail.p;
     A.ff_sum = (float*)c->ff_sum.p;
+    c->ff_launches = 0;
     for (uint32_t t0 = 0; t0 < A.num_tiles; t0 += chunk) {
         const uint32_t nt = std::min(chunk, A.num_tiles - t0);
         for (uint32_t si = 0; si < spp; si += nsb) {
@@ -687,7 +694,14 @@ vr_status free_flight_pipeline(vr_ctx* c, RenderArgs& A, hipStream_t s) {
             A.ff_si0 = si;
             A.ff_nsb = std::min(nsb, spp - si);
             A.ff_total = (unsigned long long)nt * A.ff_nsb * 256ull;
-            HIP_TRY(launch_free_flight(A, nt, s), "free-flight launch");
+            const size_t e0 = 4 * (size_t)c->ff_launches;
+            while (c->ff_ev.size() < e0 + 4) {
+                hipEvent_t e = nullptr;
+                HIP_TRY(hipEventCreate(&e), "hipEventCreate");
+                c->ff_ev.push_back(e);
+            }
+            HIP_TRY(launch_free_flight(A, nt, s, &c->ff_ev[e0]), "free-flight launch");
+            ++c->ff_launches;
         }
     }
     return VR_OK;
@@ -720,6 +734,7 @@ vr_status launch(vr_ctx* c, RenderArgs& A, const vr_render_params* p, hipStream_
     HIP_TRY(hipEventRecord(c->ev_start, s), "hipEventRecord");
     c->staged = false;
     c->report_gauss = false;
+    c->ff_launches = 0;
     if (c->type == VR_VOLUME_GAUSSIANS && (p->integrator == VR_RAYMARCH_GAUSSIANS || p->integrator == VR_PURE_RAYMARCH)) {
         st = gauss_pipeline(c, A, s, stats);
         if (st != VR_OK) return st;
@@ -853,6 +868,7 @@ void vr_destroy(vr_ctx* c) {
     if (c->ev_start) (void)hipEventDestroy(c->ev_start);
     if (c->ev_stop) (void)hipEventDestroy(c->ev_stop);
     if (c->ev_report) (void)hipEventDestroy(c->ev_report);
+    for (hipEvent_t e : c->ff_ev) (void)hipEventDestroy(e);
     for (hipEvent_t e : c->ev_stage)
         if (e) (void)hipEventDestroy(e);
     if (c->stream) (void)hipStreamDestroy(c->stream);
@@ -1005,8 +1021,9 @@ vr_status vr_count_work(vr_ctx* c, const vr_camera* cam, const vr_render_params*
     RenderArgs A;
     vr_status st = fill_args(c, cam, p, W, H, A);
     if (st != VR_OK) return st;
-    if (p->integrator != VR_RAYMARCH_GAUSSIANS && p->integrator != VR_PURE_RAYMARCH)
-        return fail(VR_ERR_UNSUPPORTED, "vr_count_work: Gaussian ray-march integrators only");
+    if (p->integrator != VR_RAYMARCH_GAUSSIANS && p->integrator != VR_PURE_RAYMARCH && p->integrator != VR_FREE_FLIGHT &&
+        p->integrator != VR_MULTI_SCATTER)
+        return fail(VR_ERR_UNSUPPORTED, "vr_count_work: Gaussian ray-march and free-flight integrators only");
     uint32_t total = vr_num_tiles(W, H);
     if (tile_stride == 0 || num_tiles == 0 || (uint64_t)first_tile + (uint64_t)(num_tiles - 1) * tile_stride >= total)
         return fail(VR_ERR_INVALID, "vr_count_work: bad tile range");
@@ -1290,6 +1307,16 @@ vr_status vr_get_stats(vr_ctx* c, vr_render_stats* o) {
             float m = 0.0f;
             HIP_TRY(hipEventElapsedTime(&m, b[i], b[i + 1]), "hipEventElapsedTime");
             o->stage_ms[i] = m;
+        }
+    }
+    if (!c->report_gauss && c->ff_launches > 0) {  // free-flight: [0] path kernel, [3] shadow rays, [4] accumulation
+        for (uint32_t l = 0; l < c->ff_launches; ++l) {
+            const hipEvent_t* e = &c->ff_ev[4 * (size_t)l];
+            float m[3] = {0.0f, 0.0f, 0.0f};
+            for (int i = 0; i < 3; ++i) HIP_TRY(hipEventElapsedTime(&m[i], e[i], e[i + 1]), "hipEventElapsedTime");
+            o->stage_ms[0] += m[0];
+            o->stage_ms[3] += m[1];
+            o->stage_ms[4] += m[2];
         }
     }
     o->scatter_records = c->report_gauss ? (int64_t)c->h_report[2] : 0;

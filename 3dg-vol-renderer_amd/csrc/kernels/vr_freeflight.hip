@@ -21,6 +21,7 @@
 // exact (correctly rounded, uncontracted) forms of vr_march.h. libm functions (log, erf, acos,
 // sin, cos) come from the device library, so individual paths can diverge from the oracle when a
 // comparison lands within an ulp; parity is per pixel on most pixels and on the image mean.
+#include <algorithm>
 #include <type_traits>
 
 #include "vr_dev_common.h"
@@ -41,12 +42,27 @@ constexpr int kFFBlock = 256;
 // F at the current segment start is F0 or F1 as `ph` says: an event writes the new F into the other
 // component and flips ph, so the sweep touches every active entry once per event (one 16-B read
 // and one 4-B write) and the solver still sees F at t_prev when the target is crossed.
+// Work counters of the instrumented build (vr_count_work): CNT = false compiles them away.
+enum { kFFPaths = 0, kFFBounces, kFFNode4, kFFNode2, kFFPrims, kFFErf, kFFNeeInline, kFFNeeQueued, kFFNumCtr };
+enum { kNeeRays = 0, kNeeNode4, kNeePrims, kNeeOD };
+template <bool CNT>
+struct FFCount {
+    __device__ __forceinline__ void add(int, uint32_t = 1) {}
+};
+template <>
+struct FFCount<true> {
+    uint32_t v[kFFNumCtr] = {};
+    __device__ __forceinline__ void add(int k, uint32_t n = 1) { v[k] += n; }
+};
+
+template <bool CNT>
 struct FFScratch {
     float4* hit;
     float4* a0;
     float4* a1;
     uint32_t stride;
     int ph;  // which of a1.x / a1.y holds F at the current segment start
+    [[no_unique_address]] mutable FFCount<CNT> C;
     __device__ __forceinline__ float4& H(int i) const { return hit[(size_t)i * stride]; }
     __device__ __forceinline__ float4& A0(int i) const { return a0[(size_t)i * stride]; }
     __device__ __forceinline__ float4& A1(int i) const { return a1[(size_t)i * stride]; }
@@ -63,6 +79,7 @@ struct FFScratch {
         float den = 2.0f * sqrtf(twoA);
         float e = expf(-0.5f * (q.Cq - __fdiv_rn(q.B * q.B, 4.0f * q.A)));
         A0(i) = make_float4(pref * e, q.B, twoA, den);
+        C.add(kFFErf);
         const float F = erff(__fdiv_rn(q.B + twoA * t, den));
         A1(i) = make_float4(F, F, h.y, h.z);
         return h.y;
@@ -75,6 +92,7 @@ struct FFScratch {
     __device__ __forceinline__ float od_to(int i, float t) const {
         const float4 c = A0(i);
         const float4 e = A1(i);
+        C.add(kFFErf);
         return c.x * (erff(__fdiv_rn(c.y + c.z * t, c.w)) - (ph ? e.y : e.x));
     }
 };
@@ -124,17 +142,23 @@ __device__ __forceinline__ void sample_uniform_direction(PCG32& rng, float& x, f
 // the exact ellipsoid test); only the walk order among equal keys differs. A 4-wide walk that could
 // overflow its LDS stack stops; `reset` then clears what the walk collected and the pair tree
 // (at most one push per level) redoes it.
-template <typename Prune, typename Leaf, typename Reset>
+template <typename Prune, typename Leaf, typename Reset, typename Cnt = FFCount<false>>
 __device__ __forceinline__ void walk(const RenderArgs& A, const Ray& r, int* stack, int stride, Prune prune, Leaf leaf,
-                                     Reset reset) {
+                                     Reset reset, Cnt* cnt = nullptr) {
+    auto on4 = [&]() {
+        if (cnt) cnt->add(kFFNode4);
+    };
+    auto on2 = [&]() {
+        if (cnt) cnt->add(kFFNode2);
+    };
     if (A.hnodes4) {
-        if (traverse_wide<kStackSize>(A, r, stack, stride, prune, leaf)) return;
+        if (traverse_wide<kStackSize>(A, r, stack, stride, prune, leaf, on4)) return;
         reset();
     }
     if (A.hnodes)
-        traverse<true>(A, r, stack, stride, prune, leaf);
+        traverse<true>(A, r, stack, stride, prune, leaf, on2);
     else
-        traverse<false>(A, r, stack, stride, prune, leaf);
+        traverse<false>(A, r, stack, stride, prune, leaf, on2);
 }
 
 // gaussian.h:10-25
@@ -187,14 +211,16 @@ __device__ bool solve_for_t_given_tau(const GRec& g, const Ray& r, float t0, flo
 }
 
 // sum_i tau_i(ta, t) over the active list, in list order (distance_solvers.h:38-40, 72-78)
-__device__ __forceinline__ float act_tau(const RenderArgs& A, const FFScratch& S, int m, const Ray& r, float ta, float t) {
+template <class SC>
+__device__ __forceinline__ float act_tau(const RenderArgs& A, const SC& S, int m, const Ray& r, float ta, float t) {
     float s = 0.0f;  // ta is the segment start t_prev, where the cached F values were taken
     for (int i = 0; i < m; ++i) s += S.od_to(i, t);
     return s;
 }
 
 // distance_solvers.h:25-57
-__device__ float solve_bisection(const RenderArgs& A, const FFScratch& S, int m, const Ray& r, float ta, float tb, float target) {
+template <class SC>
+__device__ float solve_bisection(const RenderArgs& A, const SC& S, int m, const Ray& r, float ta, float tb, float target) {
     float a = ta, b = tb;
     for (int i = 0; i < 15; ++i) {
         float mid = 0.5f * (a + b);
@@ -207,7 +233,8 @@ __device__ float solve_bisection(const RenderArgs& A, const FFScratch& S, int m,
 }
 
 // distance_solvers.h:62-127
-__device__ float solve_newton(const RenderArgs& A, const FFScratch& S, int m, const Ray& r, float ta, float tb, float target) {
+template <class SC>
+__device__ float solve_newton(const RenderArgs& A, const SC& S, int m, const Ray& r, float ta, float tb, float target) {
     const float a = ta, b = tb, tol = 1e-6f;
     float t = 0.5f * (a + b);
     for (int iter = 0; iter < 8; ++iter) {
@@ -227,7 +254,8 @@ __device__ float solve_newton(const RenderArgs& A, const FFScratch& S, int m, co
 }
 
 // distance_solvers.h:150-187, ANALYTIC_PLUS_NEWTON
-__device__ float solve_distance(const RenderArgs& A, const FFScratch& S, int m, const Ray& r, float ta, float tb, float rem) {
+template <class SC>
+__device__ float solve_distance(const RenderArgs& A, const SC& S, int m, const Ray& r, float ta, float tb, float rem) {
     if (m == 1) {
         float t_an = 0.0f;
         if (solve_for_t_given_tau(load_rec(A.gauss, S.Rec(0)), r, ta, tb, rem, t_an)) return fminf(fmaxf(t_an, ta), tb);
@@ -236,7 +264,8 @@ __device__ float solve_distance(const RenderArgs& A, const FFScratch& S, int m, 
 }
 
 // gmm.h:128-143
-__device__ float evaluate_albedo(const RenderArgs& A, const FFScratch& S, int m, float x, float y, float z) {
+template <class SC>
+__device__ float evaluate_albedo(const RenderArgs& A, const SC& S, int m, float x, float y, float z) {
     float sum = 0.0f, sum_alb = 0.0f;
     for (int i = 0; i < m; ++i) {
         GRec g = load_rec(A.gauss, S.Rec(i));
@@ -252,16 +281,21 @@ __device__ float evaluate_albedo(const RenderArgs& A, const FFScratch& S, int m,
 // The shadow ray only feeds a continuous quantity (Tr), so it uses the FMA-contracted quadratic and
 // hardware rcp/rsq forms (vr_march.h *_fast, as the ray-march's secondary rays do); the path's own
 // discrete decisions keep the exact forms.
+template <class Cnt = FFCount<false>>
 __device__ __forceinline__ void shadow_leaf(const RenderArgs& A, const Ray& r, float tmax, uint32_t first, uint32_t count,
-                                            double& sum) {
+                                            double& sum, Cnt* cnt = nullptr) {
     for (uint32_t j = first; j < first + count; ++j) {
+        if (cnt) cnt->add(kNeePrims);
         GRec g = load_rec(A.gauss, (int)j);
         Quad q = quad_fast(g, r);
         float t0, t1;
         if (!intersect_fast(q, t0, t1)) continue;
         float a = fmaxf(0.0f, t0);
         float b = fminf(tmax, t1);
-        if (b > a) sum += (double)optical_depth_fast(g, q, a, b);
+        if (b > a) {
+            if (cnt) cnt->add(kNeeOD);
+            sum += (double)optical_depth_fast(g, q, a, b);
+        }
     }
 }
 __device__ __forceinline__ float shadow_prune_lim(float tmax) { return tmax + kTPad * (1.0f + fminf(tmax, 1e30f)); }
@@ -307,8 +341,8 @@ __device__ void record_hits(const RenderArgs& A, const Ray& r, float lim, uint32
 // MULTI = false with a float sum, :422-498 for MULTI = true with a double sum). Returns t >= 0,
 // -1 (no scatter before the last event) or -2 (a per-thread capacity was exceeded). On return
 // with t >= 0 the active list holds the critical segment's Gaussians (count in m).
-template <bool MULTI>
-__device__ float free_flight_distance(const RenderArgs& A, FFScratch& S, const Ray& r, float target, int& m, int* stack,
+template <bool MULTI, class SC>
+__device__ float free_flight_distance(const RenderArgs& A, SC& S, const Ray& r, float target, int& m, int* stack,
                                       int stride) {
     using Acc = typename std::conditional<MULTI, double, float>::type;
     Acc acc = 0;
@@ -338,6 +372,7 @@ __device__ float free_flight_distance(const RenderArgs& A, FFScratch& S, const R
             },
             [&](uint32_t first, uint32_t count) {
                 for (uint32_t j = first; j < first + count; ++j) {
+                    S.C.add(kFFPrims);
                     GRec g = load_rec(A.gauss, (int)j);
                     float t0, t1;
                     if (!intersect(quad(g, r), t0, t1)) continue;
@@ -370,7 +405,8 @@ __device__ float free_flight_distance(const RenderArgs& A, FFScratch& S, const R
                 n = 0;
                 t_cut = kfull = INFINITY;
                 pruned_full = false;
-            });
+            },
+            &S.C);
         // skipped subtrees only hold keys beyond the (final) largest kept key
         if (pruned_full && n > 0) t_cut = fminf(t_cut, S.K(n - 1));
         while (n > 0 && S.K(n - 1) >= t_cut) --n;  // entries past the window (t_cut fell after they were kept)
@@ -403,6 +439,7 @@ __device__ float free_flight_distance(const RenderArgs& A, FFScratch& S, const R
                 const float4 c = S.A0(a);
                 float4& e1r = S.A1(a);
                 const float4 e1 = e1r;
+                S.C.add(kFFErf);
                 const float f1 = erff(__fdiv_rn(c.y + c.z * t_evt, c.w));
                 if (S.ph) e1r.x = f1;
                 else e1r.y = f1;
@@ -489,8 +526,8 @@ __device__ __forceinline__ void nee_radiance(const RenderArgs& A, float Tr, int 
 }
 
 // One path: path group b = (tile b / nsb, sample si0 + b % nsb), lane_id = pixel of the tile.
-template <bool MULTI>
-__device__ __forceinline__ void ff_one_path(const RenderArgs& A, FFScratch& S, int* stack, uint32_t b,
+template <bool MULTI, class SC>
+__device__ __forceinline__ void ff_one_path(const RenderArgs& A, SC& S, int* stack, uint32_t b,
                                             uint32_t lane_id, size_t out) {
     const uint32_t tile_local = A.ff_tile_base + b / A.ff_nsb;
     const int si = (int)(A.ff_si0 + b % A.ff_nsb);
@@ -517,6 +554,7 @@ __device__ __forceinline__ void ff_one_path(const RenderArgs& A, FFScratch& S, i
         for (int bounce = 0;; ++bounce) {
             int m = 0;
             const float target = -logf(1.0f - rng.uniform());
+            S.C.add(kFFBounces);
             const float ts = free_flight_distance<MULTI>(A, S, ray, target, m, stack, kFFBlock);
             if (MULTI && A.rec_bits && ts != -2.0f)
                 record_hits(A, ray, ts >= 0.0f ? ts + 1e-6f : INFINITY, (uint32_t)y * A.width + (uint32_t)x, stack, kFFBlock);
@@ -555,7 +593,9 @@ __device__ __forceinline__ void ff_one_path(const RenderArgs& A, FFScratch& S, i
             const float w = (albedo * kInv4Pi) * w_ne;
             // the contribution is m * Li: L += (tp * w) * Li (integrator.h:681-687), L = w * Li (:396-399)
             const float m0 = MULTI ? tp0 * w : w, m1 = MULTI ? tp1 * w : w, m2 = MULTI ? tp2 * w : w;
-            if (!nee_queue(A, sr, dist, li, m0, m1, m2, first, last, defer)) {
+            const bool queued = nee_queue(A, sr, dist, li, m0, m1, m2, first, last, defer);
+            S.C.add(queued ? kFFNeeQueued : kFFNeeInline);
+            if (!queued) {
                 float Li0, Li1, Li2;
                 nee_radiance(A, transmittance_up_to(A, sr, dist, stack, kFFBlock), li, dist, Li0, Li1, Li2);
                 after |= first != kFFNone;
@@ -593,12 +633,16 @@ __device__ __forceinline__ void ff_one_path(const RenderArgs& A, FFScratch& S, i
 // wave that drew short paths moves on instead of idling until the launch's longest path ends.
 // Launch bounds: 4 waves/SIMD (128 VGPRs, a few spills) measured 1.14-1.44x faster than the
 // unconstrained 2 waves/SIMD (203 VGPRs) on C2/C4/C5; 5 waves/SIMD (the LDS-stack limit) is slower.
-template <bool MULTI>
-__global__ void __launch_bounds__(kFFBlock, 4) ff_path_kernel(RenderArgs A) {
+#ifndef VR_FF_WAVES
+#define VR_FF_WAVES 4  // waves per SIMD of the path kernel (launch bounds; the grid fills them)
+#endif
+// CNT: the instrumented build (vr_count_work) counts its work into A.work[0..7].
+template <bool MULTI, bool CNT = false>
+__global__ void __launch_bounds__(kFFBlock, VR_FF_WAVES) ff_path_kernel(RenderArgs A) {
     __shared__ int s_stack[kStackSize * kFFBlock];
     int* stack = s_stack + threadIdx.x;
     const uint32_t gt = blockIdx.x * kFFBlock + threadIdx.x;
-    FFScratch S{A.ff_hit + gt, A.ff_act0 + gt, A.ff_act1 + gt, A.ff_threads, 0};
+    FFScratch<CNT> S{A.ff_hit + gt, A.ff_act0 + gt, A.ff_act1 + gt, A.ff_threads, 0, {}};
     const uint32_t lane = threadIdx.x & 63u;
     for (;;) {
         unsigned long long base = 0;
@@ -606,7 +650,15 @@ __global__ void __launch_bounds__(kFFBlock, 4) ff_path_kernel(RenderArgs A) {
         base = __shfl(base, 0, 64);
         if (base >= A.ff_total) break;  // wave-uniform: every wave leaves once the work is handed out
         const unsigned long long pid = base + lane;
-        if (pid < A.ff_total) ff_one_path<MULTI>(A, S, stack, (uint32_t)(pid / kFFBlock), (uint32_t)(pid % kFFBlock), pid);
+        if (pid < A.ff_total) {
+            S.C.add(kFFPaths);
+            ff_one_path<MULTI>(A, S, stack, (uint32_t)(pid / kFFBlock), (uint32_t)(pid % kFFBlock), pid);
+        }
+    }
+    if constexpr (CNT) {
+        Ctr c{};
+        for (int i = 0; i < kFFNumCtr; ++i) c.v[i] = S.C.v[i];
+        flush_counters(A.work, c);
     }
 }
 
@@ -629,7 +681,9 @@ __device__ __forceinline__ void nee_finish(const RenderArgs& A, uint32_t id, flo
 #ifndef VR_NEE_BLOCKS
 #define VR_NEE_BLOCKS 4  // resident 256-lane blocks per CU
 #endif
+template <bool CNT = false>
 __global__ void __launch_bounds__(kFFBlock) ff_nee_kernel(RenderArgs A) {
+    FFCount<CNT> C;
     __shared__ int s_stack[kStackSize * kFFBlock];
     int* stack = s_stack + threadIdx.x;
     const uint32_t n = min(A.ff_nee_n[0], A.ff_nee_cap);
@@ -669,6 +723,7 @@ __global__ void __launch_bounds__(kFFBlock) ff_nee_kernel(RenderArgs A) {
                         sp = 0;
                         node = 0;
                         live = true;
+                        C.add(kNeeRays);
                     }
                 }
             }
@@ -680,12 +735,13 @@ __global__ void __launch_bounds__(kFFBlock) ff_nee_kernel(RenderArgs A) {
         if (live) {  // one 4-wide node step (traverse_wide's body)
             float key[4];
             int32_t kr[4];
+            C.add(kNeeNode4);
             wide_children(A, node, ix, iy, iz, oxi, oyi, ozi, [&](float tmin, float) { return tmin <= lim; }, key, kr);
             bool stop = false;
 #pragma unroll
             for (int i = 0; i < 4; ++i)  // leaves, near first
                 if (!stop && kr[i] < 0) {
-                    shadow_leaf(A, r, tmax, leaf_first(kr[i]), leaf_count(kr[i]), sum);
+                    shadow_leaf(A, r, tmax, leaf_first(kr[i]), leaf_count(kr[i]), sum, &C);
                     stop = !(sum < 104.0);
                 }
             int first = -1;
@@ -718,6 +774,11 @@ __global__ void __launch_bounds__(kFFBlock) ff_nee_kernel(RenderArgs A) {
                 live = false;
             }
         }
+    }
+    if constexpr (CNT) {  // [8..11] of the instrumented frame's counters
+        Ctr c{};
+        for (int i = 0; i < kFFNumCtr; ++i) c.v[i] = C.v[i];
+        flush_counters(A.work + 8, c);
     }
 }
 
@@ -823,24 +884,46 @@ hipError_t launch_sfd_loss_diff(const uint32_t* bits0, const uint32_t* bits1, co
     return hipGetLastError();
 }
 
+// Threads of the resident path-kernel grid on a device with `cus` CUs (the scratch row stride).
+uint32_t free_flight_threads(int cus) {
+    int per_cu = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)dev::ff_path_kernel<true, false>, dev::kFFBlock, 0) !=
+            hipSuccess ||
+        per_cu < 1)
+        per_cu = 1;
+    return (uint32_t)std::max(1, cus) * (uint32_t)per_cu * (uint32_t)dev::kFFBlock;
+}
+
 // Host launcher: one (tile chunk, sample batch) step. A.ff_* describe the step.
-hipError_t launch_free_flight(const RenderArgs& A, uint32_t chunk_tiles, hipStream_t stream) {
+hipError_t launch_free_flight(const RenderArgs& A, uint32_t chunk_tiles, hipStream_t stream, hipEvent_t* ev) {
     hipError_t e0 = hipMemsetAsync(A.ff_next, 0, sizeof(unsigned long long), stream);
     if (e0 != hipSuccess) return e0;
     if (A.ff_nee_cap > 0 && (e0 = hipMemsetAsync(A.ff_nee_n, 0, 2 * sizeof(uint32_t), stream)) != hipSuccess) return e0;
     dim3 grid(A.ff_threads / dev::kFFBlock);
-    if (A.ff_multi)
-        hipLaunchKernelGGL(dev::ff_path_kernel<true>, grid, dim3(dev::kFFBlock), 0, stream, A);
-    else
-        hipLaunchKernelGGL(dev::ff_path_kernel<false>, grid, dim3(dev::kFFBlock), 0, stream, A);
+    const bool cnt = A.work != nullptr;  // vr_count_work: the instrumented kernels
+    if ((e0 = hipEventRecord(ev[0], stream)) != hipSuccess) return e0;
+    if (A.ff_multi) {
+        if (cnt) hipLaunchKernelGGL((dev::ff_path_kernel<true, true>), grid, dim3(dev::kFFBlock), 0, stream, A);
+        else hipLaunchKernelGGL((dev::ff_path_kernel<true>), grid, dim3(dev::kFFBlock), 0, stream, A);
+    } else {
+        if (cnt) hipLaunchKernelGGL((dev::ff_path_kernel<false, true>), grid, dim3(dev::kFFBlock), 0, stream, A);
+        else hipLaunchKernelGGL((dev::ff_path_kernel<false>), grid, dim3(dev::kFFBlock), 0, stream, A);
+    }
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
+    if ((e = hipEventRecord(ev[1], stream)) != hipSuccess) return e;
     if (A.ff_nee_cap > 0) {
-        hipLaunchKernelGGL(dev::ff_nee_kernel, dim3(A.ff_threads / 1024u * VR_NEE_BLOCKS), dim3(dev::kFFBlock), 0, stream, A);
+        int dv = 0, cus = 1;
+        if (hipGetDevice(&dv) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dv);
+        const dim3 ng((unsigned)std::max(1, cus) * VR_NEE_BLOCKS);
+        if (cnt) hipLaunchKernelGGL(dev::ff_nee_kernel<true>, ng, dim3(dev::kFFBlock), 0, stream, A);
+        else hipLaunchKernelGGL(dev::ff_nee_kernel<false>, ng, dim3(dev::kFFBlock), 0, stream, A);
         if ((e = hipGetLastError()) != hipSuccess) return e;
     }
+    if ((e = hipEventRecord(ev[2], stream)) != hipSuccess) return e;
     hipLaunchKernelGGL(dev::ff_accumulate_kernel, dim3(chunk_tiles), dim3(dev::kFFBlock), 0, stream, A, chunk_tiles);
-    return hipGetLastError();
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    return hipEventRecord(ev[3], stream);
 }
 
 }  // namespace vr

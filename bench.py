@@ -67,6 +67,45 @@ def secondary_flops(sec):
             + FLOP_WEIGHTS["od"] * sec["optical_depths"])
 
 
+# Free-flight kernels (same model): a 4-wide node step 105, a child-pair node step 44 (2 slab tests),
+# a ray-Gaussian quadratic + intersect 72, an erf evaluation of the event sweep / cached entry factors /
+# distance solver 12 (fma 2 + div 4 + erf 4 + sub/mul 2), a shadow-ray optical depth 98.
+FF_FLOP_WEIGHTS = {"node4": 105, "node2": 44, "prim": 72, "erf": 12, "od": 98}
+FF_PMC_SUMMARY = "r02_ff_{cfg}_pmc_summary.json"  # rocprofv3 --pmc passes of the free-flight lines (profiles/)
+
+
+def ff_roofline(work, stage_ms, cfg):
+    """Roofline of the free-flight path kernel (dominant) with the shadow-ray kernel beside it, from
+    vr_count_work's counters of the same kernels and the per-kernel HIP-event times of the timed frames."""
+    w, p, n = FF_FLOP_WEIGHTS, work["path"], work["nee"]
+    path_fl = (w["node4"] * p["node4_steps"] + w["node2"] * p["node2_steps"] + w["prim"] * p["gaussian_tests"]
+               + w["erf"] * p["erf_evals"])
+    nee_fl = w["node4"] * n["node4_steps"] + w["prim"] * n["gaussian_tests"] + w["od"] * n["optical_depths"]
+    path_alg = w["prim"] * p["gaussian_tests"] + w["erf"] * p["erf_evals"]  # tests + integration, no tree steps
+    pm, nm = stage_ms["march"], stage_ms["secondary"]
+    roof = {"bound": "valu", "unit": "TFLOP/s", "peak": FP32_PEAK_TFLOPS, "kernel": "ff_path_kernel",
+            "kernel_ms": pm, "achieved": path_fl / (pm * 1e-3) / 1e12 if pm > 0 else None, "frac": None,
+            "alg_achieved": path_alg / (pm * 1e-3) / 1e12 if pm > 0 else None, "traffic": None,
+            "executed_flops": path_fl, "alg_flops": path_alg, "work": work, "flop_weights": w,
+            "nee_kernel": {"kernel": "ff_nee_kernel", "kernel_ms": nm, "executed_flops": nee_fl,
+                           "achieved": nee_fl / (nm * 1e-3) / 1e12 if nm > 0 else None},
+            "accumulate_ms": stage_ms["accumulate"],
+            "flops_note": "achieved: flops the timed path kernel executes (its node steps, ray-Gaussian tests and "
+                          "erf evaluations, counted by the instrumented build of the same kernels x flop_weights) "
+                          "over its HIP-event time; alg_*: the tests and erf evaluations alone (no tree steps)"}
+    if roof["achieved"] is not None:
+        roof["frac"] = roof["achieved"] / FP32_PEAK_TFLOPS
+        roof["alg_frac"] = roof["alg_achieved"] / FP32_PEAK_TFLOPS
+    pmc_path = os.path.join(ROOT, "profiles", FF_PMC_SUMMARY.format(cfg=cfg))
+    if os.path.exists(pmc_path):
+        for k, d in json.load(open(pmc_path)).items():
+            if k.startswith("vr::dev::ff_path_kernel") and "hbm_read_bytes_gfx950_corrected" in d:
+                roof["traffic"] = d["hbm_read_bytes_gfx950_corrected"] + d.get("hbm_write_bytes", 0.0)
+                roof["traffic_unit"] = "bytes per launch"
+                roof["traffic_source"] = f"profiles/{os.path.basename(pmc_path)} (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE)"
+    return roof
+
+
 def host_cores():
     """Cores this process may run on (affinity, capped by OMP_NUM_THREADS when the box sets it), the
     machine's CPU count and the CPU model."""
@@ -314,6 +353,9 @@ def main():
     if ff:
         if rank == 0:
             paths = W * H * args.spp
+            roof = None
+            if args.flops and world == 1:
+                roof = ff_roofline(dev.count_work(camera, integ.params, W, H), stage_ms, args.config)
             cpu = None
             if world == 1 and args.cpu_budget > 0:
                 cpu = cpu_baseline_ff(scene, W, H, args.integrator == "multiscatter", args.spp, args.cpu_budget,
@@ -328,6 +370,7 @@ def main():
                            "gaussians": scene.get_num_primitives(), "integrator": type(integ).__name__,
                            "spp": args.spp, "min_bounces": 5, "parallelism": f"tiles{world}",
                            "frame_kernel_ms": kernel_ms},
+                "roofline": roof,
                 "cpu_baseline": cpu}), flush=True)
         if world > 1:
             dist.destroy_process_group()

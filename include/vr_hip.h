@@ -246,7 +246,12 @@ vr_status vr_unshuffle_tiles_device(vr_ctx* ctx, const float* d_slabs, uint32_t 
  * [8] BVH node steps, [9] tree-leaf primitive tests, [10] optical-depth evaluations, [11] neighbour-
  * list primitive tests, [12] secondary rays started, [13] rays ended by the optical-depth cut-off,
  * [14] node steps of those rays, [15] node steps of the rays that ran to the end of the tree.
- * Synchronous; RayMarchingGaussians / PureRayMarching only. Used for the roofline report. */
+ * Free-flight integrators: counts[0..7], the path kernel: [0] paths, [1] free-flight distance
+ * searches (bounces), [2] 4-wide node steps and [3] child-pair node steps of the hit-collection
+ * walks, [4] ray-Gaussian quadratic + intersect evaluations, [5] erf evaluations of the event sweep,
+ * the entries' cached factors and the distance solver, [6] shadow rays traced inline, [7] shadow
+ * rays queued; counts[8..11], the shadow-ray kernel: [8] rays, [9] 4-wide node steps, [10] primitive
+ * tests, [11] optical depths. Synchronous; Gaussian scenes only. Used for the roofline reports. */
 vr_status vr_count_work(vr_ctx* ctx, const vr_camera* cam, const vr_render_params* p, uint32_t width,
                         uint32_t height, uint32_t first_tile, uint32_t tile_stride, uint32_t num_tiles,
                         uint64_t counts[16]);

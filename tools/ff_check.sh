@@ -5,5 +5,5 @@ tail -2 gpurun_out/ffc/tests.log
 for c in "c2 multiscatter 16" "c5 multiscatter 16" "c3 freeflight 4" "c4 multiscatter 1"; do
   set -- $c
   timeout -k 10 120 python3 bench.py --config $1 --integrator $2 --spp $3 --steps 3 --warmup 1 --cpu-budget 0 > gpurun_out/ffc/$1.json 2> gpurun_out/ffc/$1.log || exit 1
-  python3 -c "import json;d=json.load(open('gpurun_out/ffc/$1.json'));print('$1 $2',round(d['value'],2),'Mpaths/s',round(d['ms_per_step'],1),'ms')"
+  python3 -c "import json;d=json.load(open('gpurun_out/ffc/$1.json'));r=d.get('roofline') or {};print('$1 $2',round(d['value'],2),'Mpaths/s',round(d['ms_per_step'],1),'ms','frac',r.get('frac'),'alg',r.get('alg_frac'),'path_ms',r.get('kernel_ms'),'nee',(r.get('nee_kernel') or {}).get('kernel_ms'))"
 done
