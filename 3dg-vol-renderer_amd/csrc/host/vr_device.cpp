@@ -97,7 +97,7 @@ struct vr_ctx {
         void* p = nullptr;
         size_t bytes = 0;
     };
-    Buf px_first, px_T, rec_pos, rec_meta, rec_next, rec_act, tr, rec_alloc, rec_bloom, slowq;
+    Buf px_first, px_T, rec_pos, rec_meta, rec_next, rec_act, tr, rec_rad, rec_alloc, rec_bloom, slowq;
     Buf pcg_jump, ray_next, rec_list, rec_nlist, stack_ovf, env_order, rec_cut;
     Buf ff_scratch, ff_tail, ff_sum, ff_nee;  // free-flight integrators (vr_freeflight.hip)
     uint32_t* d_order = nullptr;      // record (leaf order) -> scene index
@@ -549,7 +549,7 @@ vr_status gauss_pipeline(vr_ctx* c, RenderArgs& A, hipStream_t s, bool stats) {
     uint64_t ovf = std::max<uint64_t>({c->ovf_hint, cap, 4096ull});
     const uint32_t S = (uint32_t)(A.num_lights + A.env_samples);
     for (int attempt = 0;; ++attempt) {
-        if (cap > 0xffffffffull / kActInline || ovf > 0xffffffffull - cap * kActInline || cap * std::max(S, 1u) >= 0xffffffffull)
+        if (cap > 0xffffffffull / kActInline || ovf > 0xffffffffull - cap * kActInline || (cap + 63) / 64 * 64 * std::max(S, 1u) >= 0xffffffffull)
             return fail(VR_ERR_UNSUPPORTED, "too many scatter records in one call (split the frame)");
         if ((st = grow(c->rec_pos, cap * 16ull, "hipMalloc(records)")) != VR_OK) return st;
         if ((st = grow(c->rec_meta, cap * 16ull, "hipMalloc(records)")) != VR_OK) return st;
@@ -581,8 +581,11 @@ vr_status gauss_pipeline(vr_ctx* c, RenderArgs& A, hipStream_t s, bool stats) {
     }
 
     // Everything below is sized by the capacity; the kernels read the live record count on the device.
-    if ((st = grow(c->tr, std::max<uint64_t>(cap * S, 1) * 4ull, "hipMalloc(secondary)")) != VR_OK) return st;
+    // Tr slots: whole 64-record chunks (tr_slot in vr_gauss.hip)
+    if ((st = grow(c->tr, std::max<uint64_t>((cap + 63) / 64 * 64 * S, 1) * 4ull, "hipMalloc(secondary)")) != VR_OK) return st;
     A.tr = (float*)c->tr.p;
+    if ((st = grow(c->rec_rad, std::max<uint64_t>(cap, 1) * 16ull, "hipMalloc(record radiance)")) != VR_OK) return st;
+    A.rec_rad = (float4*)c->rec_rad.p;
     const uint64_t nslow = cap * (uint64_t)A.num_lights;
     if ((st = grow(c->slowq, (nslow + 1) * 4ull, "hipMalloc(slow queue)")) != VR_OK) return st;
     A.slowq = (uint32_t*)c->slowq.p;
@@ -633,7 +636,7 @@ vr_status gauss_pipeline(vr_ctx* c, RenderArgs& A, hipStream_t s, bool stats) {
         A.env_order = nullptr;
         A.chunk_rec = cr;
         A.chunk_shift = shift;
-        if (A.env_samples > 0 && A.env_samples <= 256) {
+        if (A.env_samples > 0 && A.env_samples <= kEnvOrderMax) {
             const uint64_t nch = (cap + cr - 1) / cr;
             if ((st = grow(c->env_order, nch * cr * (uint64_t)A.env_samples * 2ull, "hipMalloc(environment-ray order)")) != VR_OK)
                 return st;
@@ -859,7 +862,7 @@ void vr_destroy(vr_ctx* c) {
     if (c->d_counters) (void)hipFree(c->d_counters);
     if (c->h_report) (void)hipHostFree(c->h_report);
     if (c->h_sizing) (void)hipHostFree(c->h_sizing);
-    for (vr_ctx::Buf* b : {&c->px_first, &c->px_T, &c->rec_pos, &c->rec_meta, &c->rec_next, &c->rec_act, &c->tr,
+    for (vr_ctx::Buf* b : {&c->px_first, &c->px_T, &c->rec_pos, &c->rec_meta, &c->rec_next, &c->rec_act, &c->tr, &c->rec_rad,
                            &c->rec_alloc, &c->rec_bloom, &c->slowq, &c->pcg_jump, &c->ray_next, &c->rec_list, &c->rec_nlist,
                            &c->stack_ovf, &c->env_order, &c->rec_cut, &c->ff_scratch, &c->ff_tail, &c->ff_sum, &c->ff_nee, &c->rec_bits[0], &c->rec_bits[1], &c->sfd_tmp, &c->sfd_ref,
                            &c->sfd_loss[0], &c->sfd_loss[1], &c->sfd_out})

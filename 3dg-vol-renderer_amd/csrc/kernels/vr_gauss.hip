@@ -542,6 +542,15 @@ __device__ __forceinline__ bool ray_slot(const RenderArgs& A, uint32_t chunk, ui
     return r < nrec;
 }
 
+// Result slot of a secondary ray: its position in the hand-out order (chunk-major, then the order
+// ray_slot hands the chunk's rays out). A wave takes a chunk's rays in that order and writes each Tr
+// when its ray completes, so one chunk's results fill a contiguous run of lines within a short time
+// (a [sample][record] layout scattered every chunk's 4-B stores over S rows: lines left L2 partially
+// written and were re-read — 7x write amplification). record_radiance_kernel reads a chunk back
+// whole.
+__device__ __forceinline__ uint32_t rays_per_chunk(const RenderArgs& A) {
+    return A.chunk_rec * (uint32_t)(A.num_lights + A.env_samples);
+}
 // Start ray `rem` of record chunk `chunk`. Returns false if the ray is already complete (Tr
 // written) or a padding id. norm: slab-test terms in the half nodes' scene-normalised
 // coordinates (HNode).
@@ -549,7 +558,7 @@ __device__ __forceinline__ bool sec_init(const RenderArgs& A, uint32_t nrec, uin
                                          bool norm = false) {
     uint32_t s, r;
     if (!ray_slot(A, chunk, rem, nrec, s, r)) return false;  // padding id
-    R.slot = s * A.rec_cap + r;
+    R.slot = chunk * rays_per_chunk(A) + rem;
     const float4 pos = A.rec_pos[r];
     const uint4 meta = A.rec_meta[r];
     R.rec = r;
@@ -1227,8 +1236,8 @@ __global__ __launch_bounds__(BLOCK) void secondary_slow_kernel(RenderArgs A) {
     Ctr c{};
     for (uint32_t q = blockIdx.x * BLOCK + threadIdx.x; q < n; q += gridDim.x * BLOCK) {
         const uint64_t t = A.slowq[1 + q];  // result slot s * rec_cap + r
-        const uint32_t s = (uint32_t)(t / A.rec_cap);
-        const uint32_t r = (uint32_t)(t - (uint64_t)s * A.rec_cap);
+        const uint32_t per = rays_per_chunk(A), chunk = (uint32_t)(t / per), rem = (uint32_t)(t - (uint64_t)chunk * per);
+        const uint32_t s = rem >> A.chunk_shift, r = chunk * A.chunk_rec + (rem & (A.chunk_rec - 1u));  // a light ray
         const float4 pos = A.rec_pos[r];
         const uint4 meta = A.rec_meta[r];
         ActList act{A.rec_act + meta.z, 1, (int)meta.w, A.rec_bloom[r]};
@@ -1277,6 +1286,66 @@ __global__ __launch_bounds__(256) void record_cut_kernel(RenderArgs A, float bud
         A.rec_cut[r] = fminf(kTauCut, fmaxf(0.0f, logf(1.001f * record_weight(A, A.rec_pos[r]) * rays / budget)));
 }
 
+// Per-record incident radiance Li + Le (test_integrators.h:212-275), one wave per 64-record chunk: the
+// chunk's Tr values are one contiguous run in hand-out order; they are read once, coalesced, into
+// LDS as [record][sample] (env_order tells where each environment ray went), then each lane sums its
+// record's lights and environment samples in the reference's order. Without env_order a chunk's
+// rays are sample-major ([sample][record-in-chunk]) and are read in place (coalesced).
+constexpr int kRadBlock = 64;
+template <bool ORDERED>
+__global__ __launch_bounds__(kRadBlock) void record_radiance_kernel(RenderArgs A) {
+    extern __shared__ float s_tr[];  // ORDERED: [record-in-chunk][sample]
+    const uint32_t nrec = dev_nrec(A), cr = A.chunk_rec, nl = (uint32_t)A.num_lights, ne = (uint32_t)A.env_samples;
+    const uint32_t S = nl + ne, per = rays_per_chunk(A), nch = (nrec + cr - 1u) >> A.chunk_shift;
+    for (uint32_t chunk = blockIdx.x; chunk < nch; chunk += gridDim.x) {
+        const float* tr = A.tr + (size_t)chunk * per;
+        if constexpr (ORDERED) {
+            for (uint32_t i = threadIdx.x; i < per; i += kRadBlock) {
+                uint32_t s, rl;
+                if (i < nl * cr) {
+                    s = i >> A.chunk_shift;
+                    rl = i & (cr - 1u);
+                } else {
+                    const uint32_t v = A.env_order[(size_t)chunk * (cr * ne) + (i - nl * cr)];
+                    s = nl + (v & 0xffu);
+                    rl = v >> 8;
+                }
+                s_tr[rl * S + s] = tr[i];
+            }
+            __syncthreads();
+        }
+        const uint32_t r = chunk * cr + threadIdx.x;
+        if (threadIdx.x < cr && r < nrec) {
+            auto t = [&](uint32_t s) { return ORDERED ? s_tr[threadIdx.x * S + s] : tr[s * cr + threadIdx.x]; };
+            const float4 pos = A.rec_pos[r];
+            float Li0 = 0.0f, Li1 = 0.0f, Li2 = 0.0f;
+            for (int l = 0; l < A.num_lights; ++l) {
+                const LightRecord& lr = A.lights[l];
+                float dx = lr.px - pos.x, dy = lr.py - pos.y, dz = lr.pz - pos.z;
+                float dist = sqrtf(dot3(dx, dy, dz, dx, dy, dz));
+                float Tr = t((uint32_t)l);
+                float d2 = dist * dist;
+                Li0 += __fdiv_rn(Tr * lr.ix, d2);
+                Li1 += __fdiv_rn(Tr * lr.iy, d2);
+                Li2 += __fdiv_rn(Tr * lr.iz, d2);
+            }
+            float Le0 = 0.0f, Le1 = 0.0f, Le2 = 0.0f;
+            for (uint32_t e = 0; e < ne; ++e) {
+                float Tr = t(nl + e);
+                Le0 += Tr * A.env[0];
+                Le1 += Tr * A.env[1];
+                Le2 += Tr * A.env[2];
+            }
+            const float fs = (float)A.env_samples;
+            Le0 = __fdiv_rn(Le0, fs) * k4Pi;
+            Le1 = __fdiv_rn(Le1, fs) * k4Pi;
+            Le2 = __fdiv_rn(Le2, fs) * k4Pi;
+            A.rec_rad[r] = make_float4(Li0 + Le0, Li1 + Le1, Li2 + Le2, 0.0f);
+        }
+        if constexpr (ORDERED) __syncthreads();  // s_tr is reused by the next chunk
+    }
+}
+
 __global__ __launch_bounds__(256) void accumulate_kernel(RenderArgs A) {
     const uint32_t tile_local = blockIdx.x;
     const int tid = threadIdx.x;
@@ -1287,36 +1356,14 @@ __global__ __launch_bounds__(256) void accumulate_kernel(RenderArgs A) {
         store_px(A, tile_local, lx, ly, x, y, 0.0f, 0.0f, 0.0f);
         return;
     }
-    const float fs = (float)A.env_samples;
     const float step = A.step_size;
     float L0 = 0.0f, L1 = 0.0f, L2 = 0.0f;
     for (uint32_t r = A.px_first[p]; r != kNoRecord; r = A.rec_next[r]) {  // step order
-        const float4 pos = A.rec_pos[r];
-        float Li0 = 0.0f, Li1 = 0.0f, Li2 = 0.0f;
-        for (int l = 0; l < A.num_lights; ++l) {
-            const LightRecord& lr = A.lights[l];
-            float dx = lr.px - pos.x, dy = lr.py - pos.y, dz = lr.pz - pos.z;
-            float dist = sqrtf(dot3(dx, dy, dz, dx, dy, dz));
-            float Tr = A.tr[(size_t)l * A.rec_cap + r];
-            float d2 = dist * dist;
-            Li0 += __fdiv_rn(Tr * lr.ix, d2);
-            Li1 += __fdiv_rn(Tr * lr.iy, d2);
-            Li2 += __fdiv_rn(Tr * lr.iz, d2);
-        }
-        float Le0 = 0.0f, Le1 = 0.0f, Le2 = 0.0f;
-        for (int e = 0; e < A.env_samples; ++e) {
-            float Tr = A.tr[(size_t)(A.num_lights + e) * A.rec_cap + r];
-            Le0 += Tr * A.env[0];
-            Le1 += Tr * A.env[1];
-            Le2 += Tr * A.env[2];
-        }
-        Le0 = __fdiv_rn(Le0, fs) * k4Pi;
-        Le1 = __fdiv_rn(Le1, fs) * k4Pi;
-        Le2 = __fdiv_rn(Le2, fs) * k4Pi;
-        const float Ts = pos.w;
-        L0 += ((Ts * (Li0 + Le0)) * step) * kInv4Pi;
-        L1 += ((Ts * (Li1 + Le1)) * step) * kInv4Pi;
-        L2 += ((Ts * (Li2 + Le2)) * step) * kInv4Pi;
+        const float Ts = A.rec_pos[r].w;
+        const float4 rad = A.rec_rad[r];  // Li + Le
+        L0 += ((Ts * rad.x) * step) * kInv4Pi;
+        L1 += ((Ts * rad.y) * step) * kInv4Pi;
+        L2 += ((Ts * rad.z) * step) * kInv4Pi;
     }
     const float T = A.px_T[p];
     store_px(A, tile_local, lx, ly, x, y, L0 + T * A.env[0], L1 + T * A.env[1], L2 + T * A.env[2]);
@@ -1436,6 +1483,16 @@ hipError_t gauss_record_cut(const RenderArgs& A, float budget, hipStream_t strea
 }
 
 hipError_t gauss_accumulate(const RenderArgs& A, hipStream_t stream) {
+    {  // (also with no secondary rays: Le = 0 / 0 reproduces the reference's NaN for env_samples = 0)
+        const dim3 grid(record_grid(A, A.chunk_rec, 65536));
+        if (A.env_order != nullptr)  // <= 64 KB of LDS: env_samples <= kEnvOrderMax, lights <= kMaxLights
+            hipLaunchKernelGGL(dev::record_radiance_kernel<true>, grid, dim3(dev::kRadBlock),
+                               (size_t)A.chunk_rec * (size_t)(A.num_lights + A.env_samples) * sizeof(float), stream, A);
+        else
+            hipLaunchKernelGGL(dev::record_radiance_kernel<false>, grid, dim3(dev::kRadBlock), 0, stream, A);
+        hipError_t e = hipGetLastError();
+        if (e != hipSuccess) return e;
+    }
     hipLaunchKernelGGL(dev::accumulate_kernel, dim3(A.num_tiles), dim3(256), 0, stream, A);
     return hipGetLastError();
 }

@@ -83,6 +83,7 @@ struct LightRecord {
 };
 
 constexpr int kMaxLights = 16;
+constexpr int kEnvOrderMax = 240;  // environment rays are direction-ordered up to this many samples (LDS bound)
 constexpr uint32_t kNoRecord = 0xffffffffu;
 constexpr int kActInline = 4;  // active-list slots stored with each scatter record
 
@@ -143,7 +144,8 @@ struct RenderArgs {
     uint32_t* rec_next; // per record: the pixel's next record in step order (kNoRecord: last)
     int32_t* rec_act;   // active Gaussians (leaf-order ids) of each record, sorted: kActInline slots per
                         // record, longer lists in the overflow pool after rec_cap * kActInline
-    float* tr;          // per secondary ray: transmittance, [sample][record]
+    float* tr;          // per secondary ray: transmittance, slot = chunk * rays-per-chunk + hand-out index
+    float4* rec_rad;    // per record: Li + Le (record_radiance_kernel), the radiance the accumulation weighs
     uint32_t* rec_alloc;  // [0] records allocated, [1] overflow-pool entries allocated, [2] capacity exceeded
     uint32_t rec_cap, act_ovf_cap;
     unsigned long long* rec_bloom;  // per record: 64-bit membership mask of its active list
