@@ -1116,7 +1116,16 @@ __device__ __forceinline__ void list_advance(LeafQueue& Q, int& node) {
 // Scheduling constants of the persistent kernel (tuned on C4): refill once this many
 // lanes are idle (amortises sec_init), and up to this many NODE / PRIM steps per lane per iteration
 // (amortises the per-iteration ballots and decisions).
-constexpr int kRefillMin = 24, kNodeSteps = 6, kPrimSteps = 6;
+#ifndef VR_WW_REFILL
+#define VR_WW_REFILL 24
+#endif
+#ifndef VR_WW_NODE_STEPS
+#define VR_WW_NODE_STEPS 6
+#endif
+#ifndef VR_WW_PRIM_STEPS
+#define VR_WW_PRIM_STEPS 6
+#endif
+constexpr int kRefillMin = VR_WW_REFILL, kNodeSteps = VR_WW_NODE_STEPS, kPrimSteps = VR_WW_PRIM_STEPS;
 
 // 6 waves/SIMD = 80 VGPRs: the ray state is kept small enough for that without scratch spills (a
 // spilling 6-wave build measured 9 % slower than 5 waves; this one is 5 % faster than 5 waves).

@@ -126,11 +126,13 @@ def test_odd_and_non_square_frames(W, H):
     assert nm == 0 and err < TOL
 
 
-@pytest.mark.parametrize("es", [1, 5, 37])
-def test_env_sample_counts(es):
+@pytest.mark.parametrize("es,W", [(1, 48), (5, 48), (37, 48), (240, 24), (241, 24)])
+def test_env_sample_counts(es, W):
+    # 240: the most environment samples traced in direction order (record_radiance_kernel gathers a
+    # chunk's Tr through LDS); 241: sample-major order, Tr read in place
     path = scene_path("many_gaussians.txt")
-    gpu, _ = _render_gpu_gmm(path, 48, 48, env_samples=es)
-    ref = _oracle_gmm(path, 48, 48, env_samples=es)
+    gpu, _ = _render_gpu_gmm(path, W, W, env_samples=es)
+    ref = _oracle_gmm(path, W, W, env_samples=es)
     err, nm = _linf(gpu, ref)
     assert nm == 0 and err < TOL
 
