@@ -806,6 +806,9 @@ __device__ __forceinline__ uint32_t ovf_slot(const RenderArgs& A, int sp) {
     return (uint32_t)(sp - STACK) * A.stack_ovf_lanes + blockIdx.x * BLOCK + threadIdx.x;
 }
 
+#ifndef VR_WW_NOSORT
+#define VR_WW_NOSORT 0  // 1: no near-to-far sort of a node's children (A/B)
+#endif
 // One step of the 4-wide traversal: the four children of HNode4 `node` are tested, sorted near to
 // far (misses last); leaf children go to the leaf queue in that order, the nearest inner child
 // is walked next and the other inner ones are pushed far-first (so the nearer pop first).
@@ -840,12 +843,14 @@ __device__ __forceinline__ void sec_node4(const RenderArgs& A, SecRay& R, LdsInt
         key[i] = hit ? tmin : INFINITY;
         kr[i] = hit ? ref[i] : 0;
     }
+#if !VR_WW_NOSORT
     // 4-input sorting network (5 compare-exchanges)
     cswap(key[0], kr[0], key[1], kr[1]);
     cswap(key[2], kr[2], key[3], kr[3]);
     cswap(key[0], kr[0], key[2], kr[2]);
     cswap(key[1], kr[1], key[3], kr[3]);
     cswap(key[1], kr[1], key[2], kr[2]);
+#endif
     // leaves -> queue, nearest first
     if constexpr (kQueueRing<QCAP>) {
         // Branch-free: every lane stores each child at the queue's end; a non-leaf store lands past
@@ -870,17 +875,29 @@ __device__ __forceinline__ void sec_node4(const RenderArgs& A, SecRay& R, LdsInt
     // inner children: the nearest continues, the others are pushed far-first
     int first = -1;
     int32_t next = 0;  // the nearest inner child (selects only: no dynamic register indexing)
+#if VR_WW_NOSORT
+    float best = INFINITY;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const bool b = (kr[i] > 0) & (key[i] < best);
+        best = b ? key[i] : best;
+        first = b ? i : first;
+        next = b ? kr[i] : next;
+    }
+    constexpr int kLowPush = 0;
+#else
 #pragma unroll
     for (int i = 3; i >= 0; --i) {
         first = kr[i] > 0 ? i : first;
         next = kr[i] > 0 ? kr[i] : next;
     }
+    constexpr int kLowPush = 1;  // child 0 is never pushed: if it is inner it is the nearest inner child
+#endif
     // Common case, wave-uniform: every stepping lane can take 3 pushes in LDS. Then the pushes
     // are branch-free (a lane that does not push stores above its top: dead) and the pop is LDS.
-    // (Child 0 is never pushed: if it is inner it is the nearest inner child.)
     if (__builtin_expect(__ballot(sp > STACK - 3) == 0ull, 1)) {
 #pragma unroll
-        for (int i = 3; i >= 1; --i) {
+        for (int i = 3; i >= kLowPush; --i) {
             stack[sp * BLOCK] = kr[i];
             sp += (int)((kr[i] > 0) & (i != first));
         }
