@@ -41,3 +41,24 @@ def test_primary_depths_stop_at_t_eps():
     miss = d0 < 0
     assert np.array_equal(miss, d6 < 0) and miss.any() and (~miss).any()
     assert np.all(d2[~miss] <= d6[~miss]) and np.all(d6[~miss] <= d0[~miss])
+
+
+def test_free_flight_roofline_from_work_counts():
+    """bench.ff_roofline: the path kernel's executed flops are its counted node steps, ray-Gaussian
+    tests and erf evaluations times FF_FLOP_WEIGHTS over its HIP-event time; the shadow-ray kernel is
+    reported beside it; the algorithmic part leaves out tree steps."""
+    import bench
+    work = {"path": {"paths": 10, "bounces": 20, "node4_steps": 1000, "node2_steps": 10, "gaussian_tests": 500,
+                     "erf_evals": 800, "nee_inline": 0, "nee_queued": 15},
+            "nee": {"rays": 15, "node4_steps": 300, "gaussian_tests": 200, "optical_depths": 50, "unused4": 0,
+                    "unused5": 0, "unused6": 0, "unused7": 0}}
+    stage_ms = {"march": 2.0, "sizing": 0.0, "lists": 0.0, "secondary": 1.0, "accumulate": 0.1}
+    r = bench.ff_roofline(work, stage_ms, "nonexistent-config")
+    w = bench.FF_FLOP_WEIGHTS
+    path = 1000 * w["node4"] + 10 * w["node2"] + 500 * w["prim"] + 800 * w["erf"]
+    assert r["executed_flops"] == path
+    assert r["alg_flops"] == 500 * w["prim"] + 800 * w["erf"]
+    assert abs(r["achieved"] - path / 2e-3 / 1e12) < 1e-15
+    assert abs(r["frac"] - r["achieved"] / bench.FP32_PEAK_TFLOPS) < 1e-15
+    assert r["nee_kernel"]["executed_flops"] == 300 * w["node4"] + 200 * w["prim"] + 50 * w["od"]
+    assert r["bound"] == "valu" and r["traffic"] is None
