@@ -325,8 +325,9 @@ typedef enum vr_option {
     VR_OPT_SECONDARY_BUDGET = 2, /* 1 (default): with t_eps > 0, stop secondary rays at a per-record
                                     optical depth that keeps each pixel within t_eps (DESIGN.md error
                                     budget); 0: the frame-wide cut-off ln(1/t_eps) + ln(1000) only. */
-    VR_OPT_FF_WINDOW0 = 3,       /* free-flight integrators: first hit-window capacity, 1..128 (default
-                                    8; doubles per window). Results do not depend on it. */
+    VR_OPT_FF_WINDOW0 = 3,       /* free-flight integrators: first hit-window capacity, 1..128, doubling per
+                                    window; 0 (default): derived from the uploaded scene's typical optical
+                                    depth per Gaussian (4..32). Results do not depend on it. */
     VR_OPT_RECORD_CAPACITY = 4,  /* scatter-record buffer capacity (records; the active-list pool gets the
                                     same) carried into the next frame: 0 (size it at the next frame, with one
                                     host sync) or >= 4096. The context normally sizes it from earlier frames;
