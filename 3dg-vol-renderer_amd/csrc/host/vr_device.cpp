@@ -114,6 +114,7 @@ struct vr_ctx {
     int64_t opt_secondary_budget = 1;  // VR_OPT_SECONDARY_BUDGET
     int64_t opt_ff_window0 = 0;        // VR_OPT_FF_WINDOW0 (0: auto_window0)
     int32_t auto_window0 = 8;          // first hit-window capacity derived from the uploaded scene
+    int32_t auto_nee_refill = 40;      // shadow-ray kernel refill threshold derived from the uploaded scene
     int64_t opt_ff_nee_queue = 6;      // VR_OPT_FF_NEE_QUEUE
     int64_t opt_device_bvh = 0;        // VR_OPT_DEVICE_BVH
     bool last_upload_device_bvh = false;  // the current scene's tree came from the device builder
@@ -674,6 +675,7 @@ vr_status free_flight_pipeline(vr_ctx* c, RenderArgs& A, hipStream_t s) {
     if ((st = grow(c->ff_tail, paths * sizeof(float4), "free-flight paths")) != VR_OK) return st;
     if ((st = grow(c->ff_sum, (size_t)A.num_tiles * 256 * 3 * sizeof(float), "free-flight sums")) != VR_OK) return st;
     A.ff_nee_cap = (uint32_t)std::min<uint64_t>(paths * (uint64_t)c->opt_ff_nee_queue, kFFNone);
+    A.ff_nee_refill = c->auto_nee_refill;
     if (A.ff_nee_cap > 0) {
         if ((st = grow(c->ff_nee, (size_t)A.ff_nee_cap * 3 * sizeof(float4), "free-flight shadow-ray queue")) != VR_OK) return st;
         A.ff_nee = (float4*)c->ff_nee.p;
@@ -880,15 +882,16 @@ void vr_destroy(vr_ctx* c) {
     delete c;
 }
 
-// First hit-window capacity of the free-flight sweep for a scene: a path scatters once the optical
+// Median central-chord optical depth of the scene's Gaussians and what it sets. First hit-window
+// capacity of the free-flight sweep: a path scatters once the optical
 // depth of the hits it crossed passes an Exp(1) target, so the hits a bounce needs scale like
 // 1 / (optical depth per hit). Median over (up to 4096 sampled) Gaussians of the central-chord depth
 // density * norm * sqrt(2 pi / d^T M d) along a fixed direction per Gaussian; window0 = the power of
 // two >= 64 / median, in [4, 32] (measured optima: 1000_random, median 4.5 -> 16; make_random and
 // 10k_random, median ~450 -> 4). Results do not depend on it (every window yields the same events).
-int32_t scene_window0(const HostScene& s) {
+double scene_median_chord_depth(const HostScene& s) {
     const size_t N = s.pre.size();
-    if (N == 0) return 8;
+    if (N == 0) return 0.0;
     const size_t step = std::max<size_t>(1, N / 4096);
     static const float dirs[4][3] = {{1, 0, 0}, {0, 1, 0}, {0, 0, 1}, {0.57735027f, 0.57735027f, 0.57735027f}};
     std::vector<double> tau;
@@ -900,13 +903,20 @@ int32_t scene_window0(const HostScene& s) {
                          2.0 * ((double)m[1] * d[0] * d[1] + (double)m[2] * d[0] * d[2] + (double)m[4] * d[1] * d[2]);
         if (a > 0.0 && std::isfinite(a)) tau.push_back((double)p.density * (double)p.norm * std::sqrt(2.0 * M_PI / a));
     }
-    if (tau.empty()) return 8;
+    if (tau.empty()) return 0.0;
     std::nth_element(tau.begin(), tau.begin() + tau.size() / 2, tau.end());
-    const double med = tau[tau.size() / 2];
+    return tau[tau.size() / 2];
+}
+int32_t scene_window0(double med) {
+    if (!(med > 0.0)) return 8;
     int32_t w = 4;
     while (w < 32 && (double)w * med < 64.0) w *= 2;
     return w;
 }
+// Refill threshold of the shadow-ray kernel: a refill (queue claim + ray setup) costs about a node
+// step; opaque scenes end most shadow rays after a few steps (optical depth 104 reached), so waves
+// refill in larger batches there (measured: 40-48 best for make_random, 16 for 1000_random).
+int32_t scene_nee_refill(double med) { return med >= 50.0 ? 40 : 16; }
 
 vr_status vr_upload_scene(vr_ctx* c, const vr_scene* sc) {
     if (!c || !sc) return fail(VR_ERR_INVALID, "vr_upload_scene: NULL argument");
@@ -928,7 +938,9 @@ vr_status vr_upload_scene(vr_ctx* c, const vr_scene* sc) {
     if (s.type == VR_VOLUME_GAUSSIANS) {
         const size_t N = s.pre.size();
         if (N >= (1u << 27)) return fail(VR_ERR_UNSUPPORTED, "more than 2^27 Gaussians");
-        c->auto_window0 = scene_window0(s);
+        const double med = scene_median_chord_depth(s);
+        c->auto_window0 = scene_window0(med);
+        c->auto_nee_refill = scene_nee_refill(med);
         std::vector<float> boxes(6 * N);
         for (int k = 0; k < 3; ++k) c->sig_max[k] = 0.0f;
         for (size_t i = 0; i < N; ++i) {

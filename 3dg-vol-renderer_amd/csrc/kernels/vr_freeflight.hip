@@ -665,7 +665,7 @@ __global__ void __launch_bounds__(kFFBlock, VR_FF_WAVES) ff_path_kernel(RenderAr
 // Traces the launch's queued shadow rays: the walk of transmittance_up_to (4-wide tree, near-first,
 // leaves as they are reached, the same double sum and early stop, so Tr is bit-identical to an
 // inline trace) as a persistent while-while loop: one node step per lane per iteration, and a lane
-// whose ray is done takes the next queued ray (claimed per wave once 16 lanes are idle), so a wave
+// whose ray is done takes the next queued ray (claimed per wave once ff_nee_refill lanes are idle), so a wave
 // never waits for its longest ray. Each ray's contribution m * Li replaces its weight m in place.
 __device__ __forceinline__ void nee_finish(const RenderArgs& A, uint32_t id, float tmax, float Tr) {
     float4& c = A.ff_nee[3 * (size_t)id + 2];
@@ -675,9 +675,6 @@ __device__ __forceinline__ void nee_finish(const RenderArgs& A, uint32_t id, flo
     c = make_float4(m.x * Li0, m.y * Li1, m.z * Li2, m.w);
 }
 
-#ifndef VR_NEE_REFILL
-#define VR_NEE_REFILL 40  // idle lanes that trigger a wave refill (A/B: 16-56; 40 balances C2 and C3)
-#endif
 #ifndef VR_NEE_BLOCKS
 #define VR_NEE_BLOCKS 4  // resident 256-lane blocks per CU
 #endif
@@ -696,7 +693,7 @@ __global__ void __launch_bounds__(kFFBlock) ff_nee_kernel(RenderArgs A) {
     int sp = 0, node = 0;
     for (;;) {
         const uint64_t idle = __ballot(!live);
-        if (!exhausted && (idle == ~0ull || __popcll(idle) >= VR_NEE_REFILL)) {
+        if (!exhausted && (idle == ~0ull || __popcll(idle) >= A.ff_nee_refill)) {
             uint32_t base = 0;
             if (lane == 0) base = atomicAdd(A.ff_nee_n + 1, (uint32_t)__popcll(idle));
             base = (uint32_t)__builtin_amdgcn_readfirstlane((int)base);

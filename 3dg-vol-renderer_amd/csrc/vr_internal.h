@@ -187,6 +187,7 @@ struct RenderArgs {
                              // {m0 m1 m2, light bits (-1: env)}; ff_nee_kernel overwrites m with m * Li
     uint32_t* ff_nee_n;      // [0] rays queued in the launch (may pass ff_nee_cap: those rays went inline)
     uint32_t ff_nee_cap;     // queue capacity in rays (0: every shadow ray is traced inline)
+    int32_t ff_nee_refill;   // idle lanes of a wave that trigger its refill in ff_nee_kernel
     float4* ff_tail;         // [path of the launch]: {inline radiance xyz, first queued ray | kFFTailAfter}
     const uint32_t* gauss_order;  // record (leaf order) -> scene index
     uint32_t* rec_bits;      // RECORD_PIXEL_GAUSSIANS bitset [word][pixel] (nullptr: not recording)
