@@ -34,6 +34,8 @@
 #include <algorithm>
 #include <cstdio>
 
+#include <type_traits>
+
 #include "vr_dev_common.h"
 
 namespace vr {
@@ -450,7 +452,10 @@ __device__ __forceinline__ void env_sample_dir(const RenderArgs& A, const uint4&
 
 // Direction key of an environment ray: octahedral map of the unit sphere onto [-1, 1]^2, 16 x 16
 // cells numbered in Morton order (neighbouring keys = neighbouring directions).
-constexpr int kEnvCells = 256;
+#ifndef VR_ENV_KEY_BITS
+#define VR_ENV_KEY_BITS 4  // cells per octahedral axis = 2^bits (A/B)
+#endif
+constexpr int kEnvBits = VR_ENV_KEY_BITS, kEnvSide = 1 << kEnvBits, kEnvCells = kEnvSide * kEnvSide;
 __device__ __forceinline__ uint32_t dir_key(float x, float y, float z) {
     const float n = fabsf(x) + fabsf(y) + fabsf(z);
     float u = x / n, v = y / n;
@@ -460,11 +465,11 @@ __device__ __forceinline__ uint32_t dir_key(float x, float y, float z) {
         u = uu;
         v = vv;
     }
-    const uint32_t cu = (uint32_t)min(15, max(0, (int)((u + 1.0f) * 8.0f)));
-    const uint32_t cv = (uint32_t)min(15, max(0, (int)((v + 1.0f) * 8.0f)));
+    const uint32_t cu = (uint32_t)min(kEnvSide - 1, max(0, (int)((u + 1.0f) * (0.5f * kEnvSide))));
+    const uint32_t cv = (uint32_t)min(kEnvSide - 1, max(0, (int)((v + 1.0f) * (0.5f * kEnvSide))));
     uint32_t k = 0;
 #pragma unroll
-    for (int b = 0; b < 4; ++b) k |= (((cu >> b) & 1u) << (2 * b)) | (((cv >> b) & 1u) << (2 * b + 1));
+    for (int b = 0; b < kEnvBits; ++b) k |= (((cu >> b) & 1u) << (2 * b)) | (((cv >> b) & 1u) << (2 * b + 1));
     return k;
 }
 
@@ -472,9 +477,11 @@ __device__ __forceinline__ uint32_t dir_key(float x, float y, float z) {
 // (order inside a key is arbitrary: every ray's result is independent of when it is traced).
 template <int BLOCK>
 __global__ __launch_bounds__(BLOCK) void env_order_kernel(RenderArgs A) {
-    constexpr uint32_t kKeyCap = 16384;  // keys kept in LDS (one byte each); larger chunks recompute them
+    constexpr uint32_t kKeyCap = 16384;  // keys kept in LDS; larger chunks recompute them
+    using KeyT = typename std::conditional<(kEnvCells <= 256), uint8_t, uint16_t>::type;
+    constexpr int kPer = kEnvCells / 64;  // counts per lane of the scan
     __shared__ uint32_t hist[kEnvCells];
-    __shared__ uint8_t keys[kKeyCap];
+    __shared__ KeyT keys[kKeyCap];
     const uint32_t nrec = dev_nrec(A);
     const uint32_t cr = A.chunk_rec, ne = (uint32_t)A.env_samples;
     const uint32_t n = cr * ne, nch = (nrec + cr - 1) / cr;
@@ -492,24 +499,30 @@ __global__ __launch_bounds__(BLOCK) void env_order_kernel(RenderArgs A) {
         };
         for (uint32_t i = threadIdx.x; i < n; i += BLOCK) {
             const uint32_t k = key(i);
-            if (cached) keys[i] = (uint8_t)k;
+            if (cached) keys[i] = (KeyT)k;
             atomicAdd(&hist[k], 1u);
         }
         __syncthreads();
-        if (threadIdx.x < 64) {  // exclusive scan of the 256 counts by one wave (4 per lane)
+        if (threadIdx.x < 64) {  // exclusive scan of the counts by one wave (kPer consecutive per lane)
             const uint32_t l = threadIdx.x;
-            const uint32_t a = hist[4 * l], b = hist[4 * l + 1], c = hist[4 * l + 2], d = hist[4 * l + 3];
-            uint32_t sum = a + b + c + d, incl = sum;
+            uint32_t v[kPer], sum = 0;
+#pragma unroll
+            for (int j = 0; j < kPer; ++j) {
+                v[j] = hist[kPer * l + j];
+                sum += v[j];
+            }
+            uint32_t incl = sum;
 #pragma unroll
             for (int o = 1; o < 64; o <<= 1) {
                 const uint32_t y = __shfl_up(incl, o, 64);
                 if (l >= (uint32_t)o) incl += y;
             }
-            const uint32_t ex = incl - sum;
-            hist[4 * l] = ex;
-            hist[4 * l + 1] = ex + a;
-            hist[4 * l + 2] = ex + a + b;
-            hist[4 * l + 3] = ex + a + b + c;
+            uint32_t ex = incl - sum;
+#pragma unroll
+            for (int j = 0; j < kPer; ++j) {
+                hist[kPer * l + j] = ex;
+                ex += v[j];
+            }
         }
         __syncthreads();
         uint16_t* out = A.env_order + (size_t)chunk * n;
