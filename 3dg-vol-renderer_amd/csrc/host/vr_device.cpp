@@ -547,9 +547,12 @@ vr_status gauss_pipeline(vr_ctx* c, RenderArgs& A, hipStream_t s, bool stats) {
     // exact need if it did not fit. A later frame that outgrows the buffers is reported
     // (h_report[4]) and the synchronous entry points render it again with grown buffers.
     const bool sized = c->rec_hint != 0;
-    uint64_t cap = std::max<uint64_t>({c->rec_hint, 2ull * npix, 4096ull});
-    uint64_t ovf = std::max<uint64_t>({c->ovf_hint, cap, 4096ull});
     const uint32_t S = (uint32_t)(A.num_lights + A.env_samples);
+    uint64_t cap = std::max<uint64_t>({c->rec_hint, 2ull * npix, 4096ull});
+    // secondary-ray slots are 32-bit: a hint carried over from an earlier, larger frame (or one with
+    // fewer samples per record) is clamped to what this frame's samples allow
+    cap = std::min<uint64_t>(cap, std::max<uint64_t>(4096ull, (0xfffffffeull / std::max(S, 1u)) / 64 * 64 - 64));
+    uint64_t ovf = std::max<uint64_t>({c->ovf_hint, cap, 4096ull});
     for (int attempt = 0;; ++attempt) {
         if (cap > 0xffffffffull / kActInline || ovf > 0xffffffffull - cap * kActInline || (cap + 63) / 64 * 64 * std::max(S, 1u) >= 0xffffffffull)
             return fail(VR_ERR_UNSUPPORTED, "too many scatter records in one call (split the frame)");

@@ -360,15 +360,19 @@ template <int ACT, int BLOCK, bool S, int STACK, bool H, bool W = false>
 __global__ __launch_bounds__(BLOCK) void march_kernel(RenderArgs A) {
     __shared__ int s_act[ACT * BLOCK];
     __shared__ int s_stack[STACK * BLOCK];
-    const int tid = threadIdx.x;
-    const uint32_t tile_local = xcd_tile(blockIdx.x, gridDim.x);
+    // A workgroup is one 16x16 tile (BLOCK 256) or one of its 8x8 quarters (BLOCK 64: four times as
+    // many, shorter workgroups, so the frame's last ones leave a shorter tail). Lanes never share LDS.
+    constexpr uint32_t kParts = 256u / BLOCK;
+    const uint32_t q = xcd_tile(blockIdx.x, gridDim.x);
+    const uint32_t tile_local = q / kParts;
+    const int tid = (int)((q % kParts) * BLOCK + threadIdx.x);  // lane within the tile
     const uint32_t p = tile_local * 256u + (uint32_t)tid;
     int lx, ly, x, y;
     tile_pixel(A, tile_local, tid, lx, ly, x, y);
     Ctr c{};
     int st = kOK;
     if (x < (int)A.width && y < (int)A.height) {
-        st = march<ACT, S, H, W, STACK>(A, p, x, y, s_act + tid, s_stack + tid, BLOCK, c);
+        st = march<ACT, S, H, W, STACK>(A, p, x, y, s_act + threadIdx.x, s_stack + threadIdx.x, BLOCK, c);
     } else {
         A.px_first[p] = kNoRecord;
         A.px_T[p] = 0.0f;
@@ -1176,20 +1180,28 @@ __global__ __launch_bounds__(BLOCK, WAVES) void secondary_ww_kernel(RenderArgs A
     bool counter_done = false;  // wave-uniform: the global chunk counter has passed nchunks
     const uint32_t per = A.chunk_rec * (uint32_t)(A.num_lights + A.env_samples);
     const uint32_t nrec = dev_nrec(A), nchunks = (nrec + A.chunk_rec - 1u) >> A.chunk_shift;
-    counter_done = nchunks == 0u;
+    // Claim units: a chunk's rays in hand-out order, cut into 2^split equal parts when the launch has
+    // few chunks per resident wave (a frame share of a multi-GPU split): shorter last units, a shorter
+    // tail of the persistent launch (8-way C4 share: 22.7 -> 21.7 ms). Whole chunks otherwise (record
+    // locality).
+    const uint32_t waves = gridDim.x * (BLOCK / 64u), cpw = nchunks / max(waves, 1u);
+    const uint32_t split = cpw >= 32u ? 0u : cpw >= 16u ? 1u : cpw >= 8u ? 2u : 3u;
+    const uint32_t nunits = nchunks << split;
+    counter_done = nunits == 0u;
     for (;;) {
         const uint64_t idle = __ballot(!live);
         if (__popcll(idle) >= kRefillMin) {  // refill once enough lanes are idle (amortises sec_init)
-            if (pool == pool_end && !counter_done) {  // next record chunk (all samples of its records)
+            if (pool == pool_end && !counter_done) {  // next unit of a record chunk
                 uint32_t cnext = 0;
                 if (lane == 0) cnext = (uint32_t)atomicAdd(A.ray_next, 1ull);
                 cnext = (uint32_t)__builtin_amdgcn_readfirstlane((int)cnext);  // wave-uniform: scalar register
-                if (cnext < nchunks) {
-                    chunk = cnext;
-                    pool = 0;
-                    pool_end = per;
+                if (cnext < nunits) {
+                    chunk = cnext >> split;
+                    const uint32_t part = cnext & ((1u << split) - 1u);
+                    pool = (part * per) >> split;
+                    pool_end = ((part + 1u) * per) >> split;
                 }
-                counter_done = cnext + 1u >= nchunks;
+                counter_done = cnext + 1u >= nunits;
             }
             const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(idle >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)idle, 0u));
             if (!live && pool + rank < pool_end) {
@@ -1413,7 +1425,10 @@ __global__ __launch_bounds__(256) void accumulate_kernel(RenderArgs A) {
 // ---------------------------------------------------------------------------------------------
 // Host launchers
 // ---------------------------------------------------------------------------------------------
-constexpr int kActFast = 16, kBlockFast = 256;
+#ifndef VR_MARCH_BLOCK
+#define VR_MARCH_BLOCK 64  // lanes per march workgroup: 256 (a tile) or 64 (a quarter tile; -6 % march time)
+#endif
+constexpr int kActFast = 16, kBlockFast = VR_MARCH_BLOCK;
 constexpr int kActFallback = 64, kBlockFallback = 64;
 constexpr int kBlockSecondary = 256;
 
@@ -1424,14 +1439,14 @@ static hipError_t march_pass(const RenderArgs& A, hipStream_t stream) {
     // half-precision node copy (boxes only propose candidates; every decision is the exact quadratic).
     const bool shallow = A.bvh_depth <= kShallowStack + 1;
     if (H && A.hnodes4 != nullptr)  // 4-wide tree; a query that could overflow the stack goes to the fallback
-        hipLaunchKernelGGL((dev::march_kernel<kActFast, kBlockFast, S, kShallowStack, true, true>), dim3(A.num_tiles),
+        hipLaunchKernelGGL((dev::march_kernel<kActFast, kBlockFast, S, kShallowStack, true, true>), dim3(A.num_tiles * (256 / kBlockFast)),
                            dim3(kBlockFast), 0, stream, A);
     else if (shallow)
-        hipLaunchKernelGGL((dev::march_kernel<kActFast, kBlockFast, S, kShallowStack, H>), dim3(A.num_tiles),
+        hipLaunchKernelGGL((dev::march_kernel<kActFast, kBlockFast, S, kShallowStack, H>), dim3(A.num_tiles * (256 / kBlockFast)),
                            dim3(kBlockFast), 0, stream, A);
     else
-        hipLaunchKernelGGL((dev::march_kernel<kActFast, kBlockFast, S, kStackSize, H>), dim3(A.num_tiles), dim3(kBlockFast),
-                           0, stream, A);
+        hipLaunchKernelGGL((dev::march_kernel<kActFast, kBlockFast, S, kStackSize, H>), dim3(A.num_tiles * (256 / kBlockFast)),
+                           dim3(kBlockFast), 0, stream, A);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL((dev::march_fallback_kernel<kActFallback, kBlockFallback, S, H>), dim3(1024), dim3(kBlockFallback), 0,

@@ -43,19 +43,26 @@ def main():
     out = torch.empty((nt * 256 * 3,), dtype=torch.float32, device="cuda")
     stream = torch.cuda.current_stream().cuda_stream
 
+    stages = {}
+
     def share(first, stride, count):
-        times = []
+        times, st = [], []
         for _ in range(a.reps + 1):  # the first is a warm-up (sizes the record buffers)
             dev.render_tiles_device(cam, integ.params, W, H, first, stride, count, True, out.data_ptr(), stream)
             dev.synchronize()
-            times.append(dev.stats()["kernel_ms"])
+            s = dev.stats()
+            times.append(s["kernel_ms"])
+            st.append(s["stage_ms"])
+        stages[(first, stride)] = {k: float(np.median([x[k] for x in st[1:]])) for k in st[0]}
         return float(np.median(times[1:]))
 
     full = share(0, 1, nt)
-    res = {"workload": desc, "width": W, "height": H, "tiles": nt, "full_frame_ms": full, "ranks": {}}
+    res = {"workload": desc, "width": W, "height": H, "tiles": nt, "full_frame_ms": full,
+           "full_frame_stage_ms": stages[(0, 1)], "ranks": {}}
     for R in [int(x) for x in a.ranks.split(",")]:
         t = [share(r, R, len(range(r, nt, R))) for r in range(R)]
         res["ranks"][R] = {"share_ms": t, "max_ms": max(t), "sum_ms": sum(t),
+                           "stage_ms_of_slowest": stages[(int(np.argmax(t)), R)],
                            "imbalance_max_over_mean": max(t) / (sum(t) / R),
                            "predicted_speedup": full / max(t), "predicted_efficiency": full / max(t) / R}
         print(f"[share_balance] R={R}: max {max(t):.1f} ms, mean {sum(t) / R:.1f} ms, predicted speed-up "
