@@ -918,8 +918,15 @@ int32_t scene_window0(double med) {
 }
 // Refill threshold of the shadow-ray kernel: a refill (queue claim + ray setup) costs about a node
 // step; opaque scenes end most shadow rays after a few steps (optical depth 104 reached), so waves
-// refill in larger batches there (measured: 40-48 best for make_random, 16 for 1000_random).
-int32_t scene_nee_refill(double med) { return med >= 50.0 ? 40 : 16; }
+// refill in larger batches there (while-while kernel, measured: 56 for make_random and 10k_random,
+// 16-32 alike for 1000_random).
+#ifndef VR_NEE_REFILL_OPAQUE
+#define VR_NEE_REFILL_OPAQUE 56
+#endif
+#ifndef VR_NEE_REFILL_TRANSLUCENT
+#define VR_NEE_REFILL_TRANSLUCENT 24
+#endif
+int32_t scene_nee_refill(double med) { return med >= 50.0 ? VR_NEE_REFILL_OPAQUE : VR_NEE_REFILL_TRANSLUCENT; }
 
 vr_status vr_upload_scene(vr_ctx* c, const vr_scene* sc) {
     if (!c || !sc) return fail(VR_ERR_INVALID, "vr_upload_scene: NULL argument");

@@ -662,11 +662,10 @@ __global__ void __launch_bounds__(kFFBlock, VR_FF_WAVES) ff_path_kernel(RenderAr
     }
 }
 
-// Traces the launch's queued shadow rays: the walk of transmittance_up_to (4-wide tree, near-first,
-// leaves as they are reached, the same double sum and early stop, so Tr is bit-identical to an
-// inline trace) as a persistent while-while loop: one node step per lane per iteration, and a lane
-// whose ray is done takes the next queued ray (claimed per wave once ff_nee_refill lanes are idle), so a wave
-// never waits for its longest ray. Each ray's contribution m * Li replaces its weight m in place.
+// Traces the launch's queued shadow rays (the walk of transmittance_up_to on the 4-wide tree, the
+// same double sum and early stop) as a persistent while-while kernel: a lane whose ray is done takes
+// the next queued ray, claimed per wave once ff_nee_refill lanes are idle, so a wave never waits for
+// its longest ray. Each ray's contribution m * Li replaces its weight m in place.
 __device__ __forceinline__ void nee_finish(const RenderArgs& A, uint32_t id, float tmax, float Tr) {
     float4& c = A.ff_nee[3 * (size_t)id + 2];
     const float4 m = c;
@@ -678,19 +677,28 @@ __device__ __forceinline__ void nee_finish(const RenderArgs& A, uint32_t id, flo
 #ifndef VR_NEE_BLOCKS
 #define VR_NEE_BLOCKS 4  // resident 256-lane blocks per CU
 #endif
+// A wave iteration is either a NODE iteration (lanes with room in their leaf FIFO take up to kNeeSteps 4-wide node steps, leaf
+// children queued near-first) or a PRIM iteration (lanes with queued leaves test up to kNeeSteps
+// Gaussians), whichever more lanes can use, so node and primitive work no longer split a wave. The
+// FIFO hands leaves out in the order the walk reaches them, so the double sum adds the same terms in
+// the same order as transmittance_up_to (bit-identical Tr; a sum stopped mid-leaf is >= 104 either way).
+constexpr int kNeeQueue = 8, kNeeSteps = 4;
 template <bool CNT = false>
 __global__ void __launch_bounds__(kFFBlock) ff_nee_kernel(RenderArgs A) {
     FFCount<CNT> C;
-    __shared__ int s_stack[kStackSize * kFFBlock];
+    __shared__ int s_stack[(kStackSize + kNeeQueue) * kFFBlock];
     int* stack = s_stack + threadIdx.x;
+    int* ring = stack + kStackSize * kFFBlock;
     const uint32_t n = min(A.ff_nee_n[0], A.ff_nee_cap);
     const uint32_t lane = threadIdx.x & 63u;
-    bool live = false, exhausted = false;  // exhausted: wave-uniform, the queue is handed out
+    bool live = false, exhausted = false;
     uint32_t id = 0;
     Ray r{};
     float tmax = 0.0f, lim = 0.0f, ix = 0.0f, iy = 0.0f, iz = 0.0f, oxi = 0.0f, oyi = 0.0f, ozi = 0.0f;
     double sum = 0.0;
-    int sp = 0, node = 0;
+    int sp = 0, node = -1, qh = 0, qn = 0;
+    uint32_t j = 0, end = 0;  // primitives of the leaf being tested
+    bool redo = false;        // the 4-wide stack could overflow: whole walk at the end (pair-tree fallback)
     for (;;) {
         const uint64_t idle = __ballot(!live);
         if (!exhausted && (idle == ~0ull || __popcll(idle) >= A.ff_nee_refill)) {
@@ -701,12 +709,12 @@ __global__ void __launch_bounds__(kFFBlock) ff_nee_kernel(RenderArgs A) {
             if (!live) {
                 id = base + __builtin_amdgcn_mbcnt_hi((uint32_t)(idle >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)idle, 0u));
                 if (id < n) {
-                    const float4 a = A.ff_nee[3 * (size_t)id], b = A.ff_nee[3 * (size_t)id + 1];  // b.w: link
+                    const float4 a = A.ff_nee[3 * (size_t)id], b = A.ff_nee[3 * (size_t)id + 1];
                     r = Ray{a.x, a.y, a.z, b.x, b.y, b.z};
                     tmax = a.w;
                     if (!(tmax > 0.0f)) {
                         nee_finish(A, id, tmax, 1.0f);
-                    } else {  // traverse_wide's ray setup
+                    } else {
                         float ox = r.ox, oy = r.oy, oz = r.oz;
                         node_space<true>(A, ox, oy, oz);
                         auto inv = [&](float d) {
@@ -719,6 +727,9 @@ __global__ void __launch_bounds__(kFFBlock) ff_nee_kernel(RenderArgs A) {
                         sum = 0.0;
                         sp = 0;
                         node = 0;
+                        qh = qn = 0;
+                        j = end = 0;
+                        redo = false;
                         live = true;
                         C.add(kNeeRays);
                     }
@@ -729,50 +740,68 @@ __global__ void __launch_bounds__(kFFBlock) ff_nee_kernel(RenderArgs A) {
             if (exhausted) break;
             continue;
         }
-        if (live) {  // one 4-wide node step (traverse_wide's body)
-            float key[4];
-            int32_t kr[4];
-            C.add(kNeeNode4);
-            wide_children(A, node, ix, iy, iz, oxi, oyi, ozi, [&](float tmin, float) { return tmin <= lim; }, key, kr);
-            bool stop = false;
-#pragma unroll
-            for (int i = 0; i < 4; ++i)  // leaves, near first
-                if (!stop && kr[i] < 0) {
-                    shadow_leaf(A, r, tmax, leaf_first(kr[i]), leaf_count(kr[i]), sum, &C);
-                    stop = !(sum < 104.0);
+        const bool has_prim = live && (j < end || qn > 0);
+        const bool can_node = live && node >= 0 && qn <= kNeeQueue - 4;
+        const int np = __popcll(__ballot(has_prim)), nn = __popcll(__ballot(can_node));
+        if (nn == 0 || (np > 0 && np >= nn)) {  // PRIM iteration
+            bool go = has_prim;
+            for (int k = 0; k < kNeeSteps; ++k) {
+                if (go) {
+                    if (j == end) {
+                        const int32_t ref = ring[qh * kFFBlock];
+                        qh = (qh + 1) & (kNeeQueue - 1);
+                        --qn;
+                        j = leaf_first(ref);
+                        end = j + leaf_count(ref);
+                    }
+                    shadow_leaf(A, r, tmax, j, 1u, sum, &C);
+                    ++j;
                 }
-            int first = -1;
-            int32_t next = 0;
-#pragma unroll
-            for (int i = 3; i >= 0; --i) {
-                first = kr[i] > 0 ? i : first;
-                next = kr[i] > 0 ? kr[i] : next;
+                go = go && (j < end || qn > 0) && sum < 104.0;
             }
-            bool done = stop;
-            if (!stop && sp + 3 > kStackSize) {  // the 4-wide stack could overflow: whole walk, pair-tree fallback
-                sum = -1.0;
-                done = true;
-            } else if (!stop) {
+        } else {  // NODE iteration
+            bool go = can_node;
+            for (int k = 0; k < kNeeSteps; ++k) {
+                if (go) {
+                    C.add(kNeeNode4);
+                    float key[4];
+                    int32_t kr[4];
+                    wide_children(A, node, ix, iy, iz, oxi, oyi, ozi, [&](float tmin, float) { return tmin <= lim; }, key, kr);
 #pragma unroll
-                for (int i = 3; i >= 0; --i)
-                    if (kr[i] > 0 && i != first) stack[(sp++) * kFFBlock] = kr[i];
-                if (first >= 0) {
-                    node = next;
-                } else if (sp == 0) {
-                    done = true;
-                } else {
-                    --sp;
-                    node = stack[sp * kFFBlock];
+                    for (int i = 0; i < 4; ++i)  // leaves, near first
+                        if (kr[i] < 0) {
+                            ring[((qh + qn) & (kNeeQueue - 1)) * kFFBlock] = kr[i];
+                            ++qn;
+                        }
+                    int first = -1;
+                    int32_t next = 0;
+#pragma unroll
+                    for (int i = 3; i >= 0; --i) {
+                        first = kr[i] > 0 ? i : first;
+                        next = kr[i] > 0 ? kr[i] : next;
+                    }
+                    if (sp + 3 > kStackSize) {
+                        redo = true;
+                        node = -1;
+                    } else {
+#pragma unroll
+                        for (int i = 3; i >= 0; --i)
+                            if (kr[i] > 0 && i != first) stack[(sp++) * kFFBlock] = kr[i];
+                        if (first >= 0) node = next;
+                        else if (sp > 0) node = stack[(--sp) * kFFBlock];
+                        else node = -1;
+                    }
                 }
-            }
-            if (done) {
-                const float Tr = sum < 0.0 ? transmittance_up_to(A, r, tmax, stack, kFFBlock) : expf(-(float)sum);
-                nee_finish(A, id, tmax, Tr);
-                live = false;
+                go = go && node >= 0 && qn <= kNeeQueue - 4;
             }
         }
+        if (live && (redo || !(sum < 104.0) || (node < 0 && j == end && qn == 0))) {
+            const float Tr = redo ? transmittance_up_to(A, r, tmax, stack, kFFBlock) : expf(-(float)sum);
+            nee_finish(A, id, tmax, Tr);
+            live = false;
+        }
     }
-    if constexpr (CNT) {  // [8..11] of the instrumented frame's counters
+    if constexpr (CNT) {
         Ctr c{};
         for (int i = 0; i < kFFNumCtr; ++i) c.v[i] = C.v[i];
         flush_counters(A.work + 8, c);
