@@ -341,6 +341,92 @@ __device__ void record_hits(const RenderArgs& A, const Ray& r, float lim, uint32
 // MULTI = false with a float sum, :422-498 for MULTI = true with a double sum). Returns t >= 0,
 // -1 (no scatter before the last event) or -2 (a per-thread capacity was exceeded). On return
 // with t >= 0 the active list holds the critical segment's Gaussians (count in m).
+// While-while form of the 4-wide walk for the hit collection (the shadow-ray kernel's scheme): each
+// wave iteration is a NODE iteration (up to kCollectSteps node steps per lane, leaf children into an
+// 8-entry LDS FIFO near-first) or a PRIM iteration (up to kCollectSteps Gaussians per lane), whichever
+// more of the wave's walking lanes can use. Leaves come out of the FIFO in the order the walk reaches
+// them, so ties among equal keys keep the walk order; `prune` reads the buffer's current bounds, which
+// may lag the node steps by a few primitives (it then prunes less, never more). Returns false if the
+// stack could overflow (the caller redoes the walk on the pair tree).
+constexpr int kCollectQueue = 8, kCollectSteps = 4;
+template <typename Prune, typename Prim, typename Cnt>
+__device__ __forceinline__ bool collect_walk(const RenderArgs& A, const Ray& r0, int* stack, int* ring, Prune prune,
+                                             Prim prim, Cnt* cnt) {
+    float ox = r0.ox, oy = r0.oy, oz = r0.oz;
+    node_space<true>(A, ox, oy, oz);
+    auto inv = [&](float d) {
+        d *= A.hn_scale;
+        return __frcp_rn(fabsf(d) > 1e-30f ? d : copysignf(1e-30f, d));
+    };
+    const float ix = inv(r0.dx), iy = inv(r0.dy), iz = inv(r0.dz);
+    const float oxi = ox * ix, oyi = oy * iy, ozi = oz * iz;
+    int sp = 0, node = 0, qh = 0, qn = 0;
+    uint32_t j = 0, end = 0;
+    bool ovf = false;
+    for (;;) {
+        const bool has_prim = j < end || qn > 0;
+        const bool can_node = node >= 0 && qn <= kCollectQueue - 4;
+        const uint64_t bp = __ballot(has_prim), bn = __ballot(can_node);
+        if ((bp | bn) == 0ull) break;
+        const int np = __popcll(bp), nn = __popcll(bn);
+        if (nn == 0 || (np > 0 && np >= nn)) {  // PRIM iteration
+            bool go = has_prim;
+            for (int k = 0; k < kCollectSteps; ++k) {
+                if (go) {
+                    if (j == end) {
+                        const int32_t ref = ring[qh * kFFBlock];
+                        qh = (qh + 1) & (kCollectQueue - 1);
+                        --qn;
+                        j = leaf_first(ref);
+                        end = j + leaf_count(ref);
+                    }
+                    prim(j);
+                    ++j;
+                }
+                go = go && (j < end || qn > 0);
+            }
+        } else {  // NODE iteration
+            bool go = can_node;
+            for (int k = 0; k < kCollectSteps; ++k) {
+                if (go) {
+                    if (cnt) cnt->add(kFFNode4);
+                    float key[4];
+                    int32_t kr[4];
+                    wide_children(A, node, ix, iy, iz, oxi, oyi, ozi, prune, key, kr);
+#pragma unroll
+                    for (int i = 0; i < 4; ++i)
+                        if (kr[i] < 0) {
+                            ring[((qh + qn) & (kCollectQueue - 1)) * kFFBlock] = kr[i];
+                            ++qn;
+                        }
+                    int first = -1;
+                    int32_t next = 0;
+#pragma unroll
+                    for (int i = 3; i >= 0; --i) {
+                        first = kr[i] > 0 ? i : first;
+                        next = kr[i] > 0 ? kr[i] : next;
+                    }
+                    if (sp + 3 > kStackSize) {
+                        ovf = true;
+                        node = -1;
+                        qn = 0;
+                        j = end;
+                    } else {
+#pragma unroll
+                        for (int i = 3; i >= 0; --i)
+                            if (kr[i] > 0 && i != first) stack[(sp++) * kFFBlock] = kr[i];
+                        if (first >= 0) node = next;
+                        else if (sp > 0) node = stack[(--sp) * kFFBlock];
+                        else node = -1;
+                    }
+                }
+                go = go && node >= 0 && qn <= kCollectQueue - 4;
+            }
+        }
+    }
+    return !ovf;
+}
+
 template <bool MULTI, class SC>
 __device__ float free_flight_distance(const RenderArgs& A, SC& S, const Ray& r, float target, int& m, int* stack,
                                       int stride) {
@@ -359,54 +445,58 @@ __device__ float free_flight_distance(const RenderArgs& A, SC& S, const Ray& r, 
         float t_cut = INFINITY;
         float kfull = INFINITY;  // largest kept key while the buffer is full
         bool pruned_full = false;
-        walk(
-            A, r, stack, stride,
-            [&](float tmin, float tmax) {
-                if (tmax < W0 - kTPad * (1.0f + W0)) return false;
-                const float lim = fminf(t_cut, kfull);
-                if (tmin > lim + kTPad * (1.0f + fminf(lim, 1e30f))) {
-                    pruned_full |= n == cap;
-                    return false;
+        auto prune = [&](float tmin, float tmax) {
+            if (tmax < W0 - kTPad * (1.0f + W0)) return false;
+            const float lim = fminf(t_cut, kfull);
+            if (tmin > lim + kTPad * (1.0f + fminf(lim, 1e30f))) {
+                pruned_full |= n == cap;
+                return false;
+            }
+            return true;
+        };
+        auto prim = [&](uint32_t j) {
+            S.C.add(kFFPrims);
+            GRec g = load_rec(A.gauss, (int)j);
+            float t0, t1;
+            if (!intersect(quad(g, r), t0, t1)) return;
+            if (!(t0 <= t1)) return;  // NaN distances (degenerate covariance): no event
+            if (W0 > 0.0f && !(t1 > W0)) return;
+            const float key = fmaxf(t0, W0);
+            if (key >= t_cut) return;
+            if (n == cap) {
+                if (key >= kfull) {  // would be the largest: not kept
+                    t_cut = fminf(t_cut, key);
+                    return;
                 }
-                return true;
-            },
-            [&](uint32_t first, uint32_t count) {
-                for (uint32_t j = first; j < first + count; ++j) {
-                    S.C.add(kFFPrims);
-                    GRec g = load_rec(A.gauss, (int)j);
-                    float t0, t1;
-                    if (!intersect(quad(g, r), t0, t1)) continue;
-                    if (!(t0 <= t1)) continue;  // NaN distances (degenerate covariance): no event
-                    if (W0 > 0.0f && !(t1 > W0)) continue;
-                    const float key = fmaxf(t0, W0);
-                    if (key >= t_cut) continue;
-                    if (n == cap) {
-                        if (key >= kfull) {  // would be the largest: not kept
-                            t_cut = fminf(t_cut, key);
-                            continue;
-                        }
-                        t_cut = fminf(t_cut, kfull);  // evict the largest
-                        --n;
-                    }
-                    int p = n;  // sorted insert after equal keys (walk order among ties)
-                    while (p > 0) {
-                        const float4 prev = S.H(p - 1);
-                        if (!(prev.x > key)) break;
-                        S.H(p) = prev;
-                        --p;
-                    }
-                    S.H(p) = make_float4(key, t1, __int_as_float((int)j), 0.0f);
-                    ++n;
-                    if (n == cap) kfull = S.K(n - 1);
-                }
-                return true;
-            },
-            [&]() {
-                n = 0;
-                t_cut = kfull = INFINITY;
-                pruned_full = false;
-            },
-            &S.C);
+                t_cut = fminf(t_cut, kfull);  // evict the largest
+                --n;
+            }
+            int p = n;  // sorted insert after equal keys (walk order among ties)
+            while (p > 0) {
+                const float4 prev = S.H(p - 1);
+                if (!(prev.x > key)) break;
+                S.H(p) = prev;
+                --p;
+            }
+            S.H(p) = make_float4(key, t1, __int_as_float((int)j), 0.0f);
+            ++n;
+            if (n == cap) kfull = S.K(n - 1);
+        };
+        auto leaf = [&](uint32_t first, uint32_t count) {
+            for (uint32_t j = first; j < first + count; ++j) prim(j);
+            return true;
+        };
+        auto reset = [&]() {
+            n = 0;
+            t_cut = kfull = INFINITY;
+            pruned_full = false;
+        };
+        if (A.hnodes4 == nullptr || !collect_walk(A, r, stack, stack + kStackSize * kFFBlock, prune, prim, &S.C)) {
+            reset();  // pair tree (at most one push per level; no 4-wide tree, or its stack could overflow)
+            auto on2 = [&]() { S.C.add(kFFNode2); };
+            if (A.hnodes) traverse<true>(A, r, stack, stride, prune, leaf, on2);
+            else traverse<false>(A, r, stack, stride, prune, leaf, on2);
+        }
         // skipped subtrees only hold keys beyond the (final) largest kept key
         if (pruned_full && n > 0) t_cut = fminf(t_cut, S.K(n - 1));
         while (n > 0 && S.K(n - 1) >= t_cut) --n;  // entries past the window (t_cut fell after they were kept)
@@ -639,7 +729,7 @@ __device__ __forceinline__ void ff_one_path(const RenderArgs& A, SC& S, int* sta
 // CNT: the instrumented build (vr_count_work) counts its work into A.work[0..7].
 template <bool MULTI, bool CNT = false>
 __global__ void __launch_bounds__(kFFBlock, VR_FF_WAVES) ff_path_kernel(RenderArgs A) {
-    __shared__ int s_stack[kStackSize * kFFBlock];
+    __shared__ int s_stack[(kStackSize + kCollectQueue) * kFFBlock];  // walk stack + the collection's leaf FIFO
     int* stack = s_stack + threadIdx.x;
     const uint32_t gt = blockIdx.x * kFFBlock + threadIdx.x;
     FFScratch<CNT> S{A.ff_hit + gt, A.ff_act0 + gt, A.ff_act1 + gt, A.ff_threads, 0, {}};
@@ -677,8 +767,8 @@ __device__ __forceinline__ void nee_finish(const RenderArgs& A, uint32_t id, flo
 #ifndef VR_NEE_BLOCKS
 #define VR_NEE_BLOCKS 4  // resident 256-lane blocks per CU
 #endif
-// A wave iteration is either a NODE iteration (lanes with room in their leaf FIFO take up to kNeeSteps 4-wide node steps, leaf
-// children queued near-first) or a PRIM iteration (lanes with queued leaves test up to kNeeSteps
+// A wave iteration is either a NODE iteration (lanes with room in their leaf FIFO take up to
+// kNeeSteps 4-wide node steps, leaf children queued near-first) or a PRIM iteration (lanes with queued leaves test up to kNeeSteps
 // Gaussians), whichever more lanes can use, so node and primitive work no longer split a wave. The
 // FIFO hands leaves out in the order the walk reaches them, so the double sum adds the same terms in
 // the same order as transmittance_up_to (bit-identical Tr; a sum stopped mid-leaf is >= 104 either way).
