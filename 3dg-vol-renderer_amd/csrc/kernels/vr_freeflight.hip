@@ -317,30 +317,6 @@ __device__ __forceinline__ float transmittance_up_to(const RenderArgs& A, const 
     return expf(-(float)sum);
 }
 
-// RECORD_PIXEL_GAUSSIANS (integrator.h:616-644): mark, for pixel p, every Gaussian whose events on
-// this ray lie at or before t_scatter + 1e-6 (entries t0 <= lim), or every Gaussian the ray hits
-// when it did not scatter. Bits are per original scene index: word (g >> 5) of pixel p.
-__device__ void record_hits(const RenderArgs& A, const Ray& r, float lim, uint32_t p, int* stack, int stride) {
-    walk(
-        A, r, stack, stride, [&](float tmin, float) { return tmin <= lim + kTPad * (1.0f + fminf(lim, 1e30f)); },
-        [&](uint32_t first, uint32_t count) {
-            for (uint32_t j = first; j < first + count; ++j) {
-                GRec g = load_rec(A.gauss, (int)j);
-                float t0, t1;
-                if (!intersect(quad(g, r), t0, t1)) continue;
-                if (!(t0 <= lim)) continue;
-                const uint32_t o = A.gauss_order[j];
-                atomicOr(A.rec_bits + (size_t)(o >> 5) * A.rec_npix + p, 1u << (o & 31u));
-            }
-            return true;
-        },
-        [&]() {});  // marking again is idempotent
-}
-
-// Free-flight distance along r for target optical depth `target` (integrator.h:330-360 for
-// MULTI = false with a float sum, :422-498 for MULTI = true with a double sum). Returns t >= 0,
-// -1 (no scatter before the last event) or -2 (a per-thread capacity was exceeded). On return
-// with t >= 0 the active list holds the critical segment's Gaussians (count in m).
 // While-while form of the 4-wide walk for the hit collection (the shadow-ray kernel's scheme): each
 // wave iteration is a NODE iteration (up to kCollectSteps node steps per lane, leaf children into an
 // 8-entry LDS FIFO near-first) or a PRIM iteration (up to kCollectSteps Gaussians per lane), whichever
@@ -427,6 +403,35 @@ __device__ __forceinline__ bool collect_walk(const RenderArgs& A, const Ray& r0,
     return !ovf;
 }
 
+// RECORD_PIXEL_GAUSSIANS (integrator.h:616-644): mark, for pixel p, every Gaussian whose events on
+// this ray lie at or before t_scatter + 1e-6 (entries t0 <= lim), or every Gaussian the ray hits
+// when it did not scatter. Bits are per original scene index: word (g >> 5) of pixel p.
+__device__ void record_hits(const RenderArgs& A, const Ray& r, float lim, uint32_t p, int* stack, int stride) {
+    auto prune = [&](float tmin, float) { return tmin <= lim + kTPad * (1.0f + fminf(lim, 1e30f)); };
+    auto prim = [&](uint32_t j) {
+        GRec g = load_rec(A.gauss, (int)j);
+        float t0, t1;
+        if (!intersect(quad(g, r), t0, t1)) return;
+        if (!(t0 <= lim)) return;
+        const uint32_t o = A.gauss_order[j];
+        atomicOr(A.rec_bits + (size_t)(o >> 5) * A.rec_npix + p, 1u << (o & 31u));
+    };
+    auto leaf = [&](uint32_t first, uint32_t count) {
+        for (uint32_t j = first; j < first + count; ++j) prim(j);
+        return true;
+    };
+    // while-while walk (the collection's); the pair tree redoes a walk whose stack could overflow
+    // (marking again is idempotent)
+    if (A.hnodes4 == nullptr || !collect_walk(A, r, stack, stack + kStackSize * stride, prune, prim, (FFCount<false>*)nullptr)) {
+        if (A.hnodes) traverse<true>(A, r, stack, stride, prune, leaf);
+        else traverse<false>(A, r, stack, stride, prune, leaf);
+    }
+}
+
+// Free-flight distance along r for target optical depth `target` (integrator.h:330-360 for
+// MULTI = false with a float sum, :422-498 for MULTI = true with a double sum). Returns t >= 0,
+// -1 (no scatter before the last event) or -2 (a per-thread capacity was exceeded). On return
+// with t >= 0 the active list holds the critical segment's Gaussians (count in m).
 template <bool MULTI, class SC>
 __device__ float free_flight_distance(const RenderArgs& A, SC& S, const Ray& r, float target, int& m, int* stack,
                                       int stride) {
