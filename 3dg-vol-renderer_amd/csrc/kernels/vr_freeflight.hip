@@ -324,7 +324,10 @@ __device__ __forceinline__ float transmittance_up_to(const RenderArgs& A, const 
 // them, so ties among equal keys keep the walk order; `prune` reads the buffer's current bounds, which
 // may lag the node steps by a few primitives (it then prunes less, never more). Returns false if the
 // stack could overflow (the caller redoes the walk on the pair tree).
-constexpr int kCollectQueue = 8, kCollectSteps = 4;
+#ifndef VR_COLLECT_STEPS
+#define VR_COLLECT_STEPS 4  // node steps / primitives per lane per wave iteration of the collection walk
+#endif
+constexpr int kCollectQueue = 8, kCollectSteps = VR_COLLECT_STEPS;
 template <typename Prune, typename Prim, typename Cnt>
 __device__ __forceinline__ bool collect_walk(const RenderArgs& A, const Ray& r0, int* stack, int* ring, Prune prune,
                                              Prim prim, Cnt* cnt) {
@@ -777,7 +780,10 @@ __device__ __forceinline__ void nee_finish(const RenderArgs& A, uint32_t id, flo
 // Gaussians), whichever more lanes can use, so node and primitive work no longer split a wave. The
 // FIFO hands leaves out in the order the walk reaches them, so the double sum adds the same terms in
 // the same order as transmittance_up_to (bit-identical Tr; a sum stopped mid-leaf is >= 104 either way).
-constexpr int kNeeQueue = 8, kNeeSteps = 4;
+#ifndef VR_NEE_STEPS
+#define VR_NEE_STEPS 4  // node steps / primitives per lane per wave iteration of the shadow-ray kernel
+#endif
+constexpr int kNeeQueue = 8, kNeeSteps = VR_NEE_STEPS;
 template <bool CNT = false>
 __global__ void __launch_bounds__(kFFBlock) ff_nee_kernel(RenderArgs A) {
     FFCount<CNT> C;
