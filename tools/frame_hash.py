@@ -1,0 +1,16 @@
+"""Renders the bench's C4 scene at 1024x1024 (RayMarchingGaussians, bench settings) and prints a hash
+of the frame bytes: A/B builds that must not change results (VR_LIB_PATH) print the same hash."""
+import hashlib
+import sys
+
+import numpy as np
+import torch  # noqa: F401
+
+import bench
+import vr_amd as vr
+
+scene, _, _ = bench.build_scene("c4", 2025)
+cam = vr.Pinhole_Camera(bench.CAM_POS, bench.CAM_VIEW, bench.FOV)
+img = vr.Image(1024, 1024)
+vr.RayMarchingGaussians(cam, step_size=0.01, env_samples=20, t_eps=1e-6).render(scene, img)
+print(hashlib.sha256(np.ascontiguousarray(img.pixels).tobytes()).hexdigest()[:16], float(img.pixels.mean()))
