@@ -624,134 +624,179 @@ __device__ __forceinline__ void nee_radiance(const RenderArgs& A, float Tr, int 
 }
 
 // One path: path group b = (tile b / nsb, sample si0 + b % nsb), lane_id = pixel of the tile.
-template <bool MULTI, class SC>
-__device__ __forceinline__ void ff_one_path(const RenderArgs& A, SC& S, int* stack, uint32_t b,
-                                            uint32_t lane_id, size_t out) {
+// A path between bounces: everything the bounce loop of integrator.h:560-700 carries.
+struct FFPath {
+    PCG32 rng;
+    Ray ray;
+    float tp0, tp1, tp2, L0, L1, L2;
+    uint32_t first, last;  // the path's queued shadow rays
+    uint32_t out;          // path index of the launch (its ff_tail slot)
+    uint32_t px;           // y * W + x (recording)
+    int bounce;
+    bool defer, after;
+};
+
+// Path `out` = (tile b / nsb, sample si0 + b % nsb, pixel lane_id of the tile): its camera ray
+// (integrator.h:560-570). Returns false (tail written) for a pixel outside the frame.
+__device__ __forceinline__ bool ff_start(const RenderArgs& A, uint32_t out, FFPath& P) {
+    const uint32_t b = out / kFFBlock, lane_id = out % kFFBlock;
     const uint32_t tile_local = A.ff_tile_base + b / A.ff_nsb;
     const int si = (int)(A.ff_si0 + b % A.ff_nsb);
     int lx, ly, x, y;
     tile_pixel(A, tile_local, (int)lane_id, lx, ly, x, y);
-    // L: the radiance this thread adds itself (inline NEE terms, the environment term); the path's
-    // total is its nd deferred contributions in bounce order, then L if `after` (ff_accumulate_kernel)
-    float L0 = 0.0f, L1 = 0.0f, L2 = 0.0f;
-    uint32_t first = kFFNone, last = kFFNone;  // the path's queued shadow rays
-    bool defer = A.ff_nee_cap > 0, after = false;
-    if (x < (int)A.width && y < (int)A.height) {
-        PCG32 rng(derive_path_seed(x, y, si), 1);
-        const int n = A.ff_n;
-        const int sx = si % n, sy = si / n;
-        float xi = rng.uniform();
-        float u = __fdiv_rn((float)x + __fdiv_rn((float)sx + xi, (float)n), (float)A.width);
-        xi = rng.uniform();
-        float v = __fdiv_rn((float)y + __fdiv_rn((float)sy + xi, (float)n), (float)A.height);
-        Ray ray = camera_ray(A, u, v);
-        float tp0 = 1.0f, tp1 = 1.0f, tp2 = 1.0f;
-        const int nl = A.num_lights;
-        const float w_ne = (float)(nl + 1);
-        const float p_env = __fdiv_rn(1.0f, (float)(nl + 1));
-        for (int bounce = 0;; ++bounce) {
-            int m = 0;
-            const float target = -logf(1.0f - rng.uniform());
-            S.C.add(kFFBounces);
-            const float ts = free_flight_distance<MULTI>(A, S, ray, target, m, stack, kFFBlock);
-            if (MULTI && A.rec_bits && ts != -2.0f)
-                record_hits(A, ray, ts >= 0.0f ? ts + 1e-6f : INFINITY, (uint32_t)y * A.width + (uint32_t)x, stack, kFFBlock);
-            if (ts == -2.0f || bounce >= A.ff_max_bounces) {
-                L0 = L1 = L2 = __builtin_nanf("");
-                after = true;
-                atomicAdd(A.counters, 1u);
-                break;
-            }
-            if (ts < 0.0f) {  // no event, or no scatter before the last event: environment
-                L0 += tp0 * A.env[0];
-                L1 += tp1 * A.env[1];
-                L2 += tp2 * A.env[2];
-                after |= first != kFFNone;
-                break;
-            }
-            const float px = ray.ox + ts * ray.dx, py = ray.oy + ts * ray.dy, pz = ray.oz + ts * ray.dz;
-            const float albedo = evaluate_albedo(A, S, m, px, py, pz);
-            // NEE (integrator.h:380-399 / 650-687): a light (distance-bounded) or environment shadow ray
-            const bool is_env = rng.uniform() < p_env;
-            int li = -1;
-            float dist = INFINITY;
-            Ray sr;
-            if (!is_env) {
-                li = (int)(rng.uniform() * (float)nl);
-                const LightRecord& Lt = A.lights[li];
-                float wx = Lt.px - px, wy = Lt.py - py, wz = Lt.pz - pz;
-                dist = sqrtf(dot3(wx, wy, wz, wx, wy, wz));
-                normalize3(wx, wy, wz);
-                sr = make_ray(px, py, pz, wx, wy, wz);
-            } else {
-                float wx, wy, wz;
-                sample_uniform_direction(rng, wx, wy, wz);
-                sr = make_ray(px, py, pz, wx, wy, wz);
-            }
-            const float w = (albedo * kInv4Pi) * w_ne;
-            // the contribution is m * Li: L += (tp * w) * Li (integrator.h:681-687), L = w * Li (:396-399)
-            const float m0 = MULTI ? tp0 * w : w, m1 = MULTI ? tp1 * w : w, m2 = MULTI ? tp2 * w : w;
-            const bool queued = nee_queue(A, sr, dist, li, m0, m1, m2, first, last, defer);
-            S.C.add(queued ? kFFNeeQueued : kFFNeeInline);
-            if (!queued) {
-                float Li0, Li1, Li2;
-                nee_radiance(A, transmittance_up_to(A, sr, dist, stack, kFFBlock), li, dist, Li0, Li1, Li2);
-                after |= first != kFFNone;
-                if constexpr (!MULTI) {
-                    L0 = m0 * Li0;
-                    L1 = m1 * Li1;
-                    L2 = m2 * Li2;
-                } else {
-                    L0 += m0 * Li0;
-                    L1 += m1 * Li1;
-                    L2 += m2 * Li2;
-                }
-            }
-            if constexpr (!MULTI) break;
-            tp0 *= albedo;
-            tp1 *= albedo;
-            tp2 *= albedo;
-            if (bounce >= A.ff_min_bounces) {  // integrator.h:691-695
-                float rr = fminf(fmaxf(tp0, fmaxf(tp1, tp2)), 0.9f);
-                if (rng.uniform() > rr) break;
-                tp0 = __fdiv_rn(tp0, rr);
-                tp1 = __fdiv_rn(tp1, rr);
-                tp2 = __fdiv_rn(tp2, rr);
-            }
-            float nx, ny, nz;
-            sample_uniform_direction(rng, nx, ny, nz);
-            ray = make_ray(px, py, pz, nx, ny, nz);
-        }
+    if (!(x < (int)A.width && y < (int)A.height)) {
+        A.ff_tail[out] = make_float4(0.0f, 0.0f, 0.0f, __uint_as_float(kFFNone));
+        return false;
     }
-    A.ff_tail[out] = make_float4(L0, L1, L2, __uint_as_float(first | (after ? kFFTailAfter : 0u)));
+    P.rng = PCG32(derive_path_seed(x, y, si), 1);
+    const int n = A.ff_n;
+    const int sx = si % n, sy = si / n;
+    float xi = P.rng.uniform();
+    float u = __fdiv_rn((float)x + __fdiv_rn((float)sx + xi, (float)n), (float)A.width);
+    xi = P.rng.uniform();
+    float v = __fdiv_rn((float)y + __fdiv_rn((float)sy + xi, (float)n), (float)A.height);
+    P.ray = camera_ray(A, u, v);
+    P.tp0 = P.tp1 = P.tp2 = 1.0f;
+    P.L0 = P.L1 = P.L2 = 0.0f;
+    P.first = P.last = kFFNone;
+    P.out = out;
+    P.px = (uint32_t)y * A.width + (uint32_t)x;
+    P.bounce = 0;
+    P.defer = A.ff_nee_cap > 0;
+    P.after = false;
+    return true;
 }
 
-// Persistent: a grid of resident waves; each wave claims the next 64 paths (one 8x8 pixel block
-// of one tile at one sample index) from a global counter until all ff_total paths are taken, so a
-// wave that drew short paths moves on instead of idling until the launch's longest path ends.
-// Launch bounds: 4 waves/SIMD (128 VGPRs, a few spills) measured 1.14-1.44x faster than the
-// unconstrained 2 waves/SIMD (203 VGPRs) on C2/C4/C5; 5 waves/SIMD (the LDS-stack limit) is slower.
+// One bounce of path P (integrator.h:572-700). Returns false once the path is complete (its
+// radiance written to ff_tail: the queued contributions in bounce order, then L if `after`).
+template <bool MULTI, class SC>
+__device__ __forceinline__ bool ff_bounce(const RenderArgs& A, SC& S, int* stack, FFPath& P) {
+    bool done = false;
+    int m = 0;
+    const float target = -logf(1.0f - P.rng.uniform());
+    S.C.add(kFFBounces);
+    const float ts = free_flight_distance<MULTI>(A, S, P.ray, target, m, stack, kFFBlock);
+    if (MULTI && A.rec_bits && ts != -2.0f) record_hits(A, P.ray, ts >= 0.0f ? ts + 1e-6f : INFINITY, P.px, stack, kFFBlock);
+    if (ts == -2.0f || P.bounce >= A.ff_max_bounces) {
+        P.L0 = P.L1 = P.L2 = __builtin_nanf("");
+        P.after = true;
+        atomicAdd(A.counters, 1u);
+        done = true;
+    } else if (ts < 0.0f) {  // no event, or no scatter before the last event: environment
+        P.L0 += P.tp0 * A.env[0];
+        P.L1 += P.tp1 * A.env[1];
+        P.L2 += P.tp2 * A.env[2];
+        P.after |= P.first != kFFNone;
+        done = true;
+    } else {
+        const float px = P.ray.ox + ts * P.ray.dx, py = P.ray.oy + ts * P.ray.dy, pz = P.ray.oz + ts * P.ray.dz;
+        const float albedo = evaluate_albedo(A, S, m, px, py, pz);
+        // NEE (integrator.h:380-399 / 650-687): a light (distance-bounded) or environment shadow ray
+        const int nl = A.num_lights;
+        const bool is_env = P.rng.uniform() < __fdiv_rn(1.0f, (float)(nl + 1));
+        int li = -1;
+        float dist = INFINITY;
+        Ray sr;
+        if (!is_env) {
+            li = (int)(P.rng.uniform() * (float)nl);
+            const LightRecord& Lt = A.lights[li];
+            float wx = Lt.px - px, wy = Lt.py - py, wz = Lt.pz - pz;
+            dist = sqrtf(dot3(wx, wy, wz, wx, wy, wz));
+            normalize3(wx, wy, wz);
+            sr = make_ray(px, py, pz, wx, wy, wz);
+        } else {
+            float wx, wy, wz;
+            sample_uniform_direction(P.rng, wx, wy, wz);
+            sr = make_ray(px, py, pz, wx, wy, wz);
+        }
+        const float w = (albedo * kInv4Pi) * (float)(nl + 1);
+        // the contribution is m * Li: L += (tp * w) * Li (integrator.h:681-687), L = w * Li (:396-399)
+        const float m0 = MULTI ? P.tp0 * w : w, m1 = MULTI ? P.tp1 * w : w, m2 = MULTI ? P.tp2 * w : w;
+        const bool queued = nee_queue(A, sr, dist, li, m0, m1, m2, P.first, P.last, P.defer);
+        S.C.add(queued ? kFFNeeQueued : kFFNeeInline);
+        if (!queued) {
+            float Li0, Li1, Li2;
+            nee_radiance(A, transmittance_up_to(A, sr, dist, stack, kFFBlock), li, dist, Li0, Li1, Li2);
+            P.after |= P.first != kFFNone;
+            if constexpr (!MULTI) {
+                P.L0 = m0 * Li0;
+                P.L1 = m1 * Li1;
+                P.L2 = m2 * Li2;
+            } else {
+                P.L0 += m0 * Li0;
+                P.L1 += m1 * Li1;
+                P.L2 += m2 * Li2;
+            }
+        }
+        if constexpr (!MULTI) {
+            done = true;
+        } else {
+            P.tp0 *= albedo;
+            P.tp1 *= albedo;
+            P.tp2 *= albedo;
+            if (P.bounce >= A.ff_min_bounces) {  // integrator.h:691-695
+                float rr = fminf(fmaxf(P.tp0, fmaxf(P.tp1, P.tp2)), 0.9f);
+                if (P.rng.uniform() > rr) {
+                    done = true;
+                } else {
+                    P.tp0 = __fdiv_rn(P.tp0, rr);
+                    P.tp1 = __fdiv_rn(P.tp1, rr);
+                    P.tp2 = __fdiv_rn(P.tp2, rr);
+                }
+            }
+            if (!done) {
+                float nx, ny, nz;
+                sample_uniform_direction(P.rng, nx, ny, nz);
+                P.ray = make_ray(px, py, pz, nx, ny, nz);
+                ++P.bounce;
+            }
+        }
+    }
+    if (done) A.ff_tail[P.out] = make_float4(P.L0, P.L1, P.L2, __uint_as_float(P.first | (P.after ? kFFTailAfter : 0u)));
+    return !done;
+}
+
+// Persistent: a grid of resident waves; every lane follows one path a bounce per wave iteration and,
+// once its path is complete, starts the next unclaimed path of the launch (claimed per wave when
+// kFFRefill lanes are idle), so a wave never waits for its longest path. Launch bounds: 4 waves/SIMD
+// (128 VGPRs, some spills) measured faster than 2, 3 and 5.
 #ifndef VR_FF_WAVES
 #define VR_FF_WAVES 4  // waves per SIMD of the path kernel (launch bounds; the grid fills them)
 #endif
 // CNT: the instrumented build (vr_count_work) counts its work into A.work[0..7].
+#ifndef VR_FF_REFILL
+#define VR_FF_REFILL 16  // idle lanes of a wave that trigger its path refill
+#endif
 template <bool MULTI, bool CNT = false>
 __global__ void __launch_bounds__(kFFBlock, VR_FF_WAVES) ff_path_kernel(RenderArgs A) {
-    __shared__ int s_stack[(kStackSize + kCollectQueue) * kFFBlock];  // walk stack + the collection's leaf FIFO
+    __shared__ int s_stack[(kStackSize + kCollectQueue) * kFFBlock];  // walk stack + the walks' leaf FIFO
     int* stack = s_stack + threadIdx.x;
     const uint32_t gt = blockIdx.x * kFFBlock + threadIdx.x;
     FFScratch<CNT> S{A.ff_hit + gt, A.ff_act0 + gt, A.ff_act1 + gt, A.ff_threads, 0, {}};
     const uint32_t lane = threadIdx.x & 63u;
+    FFPath P{PCG32(0, 1)};
+    bool live = false, exhausted = false;
     for (;;) {
-        unsigned long long base = 0;
-        if (lane == 0) base = atomicAdd(A.ff_next, 64ull);
-        base = __shfl(base, 0, 64);
-        if (base >= A.ff_total) break;  // wave-uniform: every wave leaves once the work is handed out
-        const unsigned long long pid = base + lane;
-        if (pid < A.ff_total) {
-            S.C.add(kFFPaths);
-            ff_one_path<MULTI>(A, S, stack, (uint32_t)(pid / kFFBlock), (uint32_t)(pid % kFFBlock), pid);
+        const uint64_t idle = __ballot(!live);
+        if (!exhausted && (idle == ~0ull || __popcll(idle) >= VR_FF_REFILL)) {
+            unsigned long long base = 0;
+            if (lane == 0) base = atomicAdd(A.ff_next, (unsigned long long)__popcll(idle));
+            base = __shfl(base, 0, 64);
+            exhausted = base + (unsigned long long)__popcll(idle) >= A.ff_total;
+            if (!live) {
+                const unsigned long long pid =
+                    base + __builtin_amdgcn_mbcnt_hi((uint32_t)(idle >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)idle, 0u));
+                if (pid < A.ff_total) {
+                    S.C.add(kFFPaths);
+                    live = ff_start(A, (uint32_t)pid, P);
+                }
+            }
         }
+        if (!__any(live)) {
+            if (exhausted) break;
+            continue;
+        }
+        if (live) live = ff_bounce<MULTI>(A, S, stack, P);
     }
     if constexpr (CNT) {
         Ctr c{};
