@@ -910,9 +910,28 @@ double scene_median_chord_depth(const HostScene& s) {
     std::nth_element(tau.begin(), tau.begin() + tau.size() / 2, tau.end());
     return tau[tau.size() / 2];
 }
-int32_t scene_window0(double med) {
+// Mean number of 3-sigma ellipsoids covering a point of the scene's bounding box.
+double scene_overlap(const HostScene& s) {
+    double vol = 0.0, lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
+    for (const GaussianPre& p : s.pre) {
+        const double a = p.cov[0], b = p.cov[1], cc = p.cov[2], d = p.cov[3], e = p.cov[4], f = p.cov[5];
+        const double det = a * (d * f - e * e) - b * (b * f - e * cc) + cc * (b * e - d * cc);
+        if (det > 0.0) vol += 4.0 / 3.0 * M_PI * 27.0 * std::sqrt(det);
+        const double ext[3] = {3.0 * std::sqrt(std::max(a, 0.0)), 3.0 * std::sqrt(std::max(d, 0.0)), 3.0 * std::sqrt(std::max(f, 0.0))};
+        for (int k = 0; k < 3; ++k) {
+            lo[k] = std::min(lo[k], (double)p.mean[k] - ext[k]);
+            hi[k] = std::max(hi[k], (double)p.mean[k] + ext[k]);
+        }
+    }
+    const double box = (hi[0] - lo[0]) * (hi[1] - lo[1]) * (hi[2] - lo[2]);
+    return box > 0.0 && std::isfinite(box) ? vol / box : 0.0;
+}
+// ... and a path starting inside a dense region first meets every Gaussian covering its start point
+// (all with entry key 0): scenes whose ellipsoids overlap >= 8-fold on average start at 8
+// (1M make_random, overlap 17: 190 vs 205 ms at 4; 100k, overlap 1.8, and 10k_random, 0.2: 4 best).
+int32_t scene_window0(double med, double overlap) {
     if (!(med > 0.0)) return 8;
-    int32_t w = 4;
+    int32_t w = overlap >= 8.0 ? 8 : 4;
     while (w < 32 && (double)w * med < 64.0) w *= 2;
     return w;
 }
@@ -949,7 +968,7 @@ vr_status vr_upload_scene(vr_ctx* c, const vr_scene* sc) {
         const size_t N = s.pre.size();
         if (N >= (1u << 27)) return fail(VR_ERR_UNSUPPORTED, "more than 2^27 Gaussians");
         const double med = scene_median_chord_depth(s);
-        c->auto_window0 = scene_window0(med);
+        c->auto_window0 = scene_window0(med, scene_overlap(s));
         c->auto_nee_refill = scene_nee_refill(med);
         std::vector<float> boxes(6 * N);
         for (int k = 0; k < 3; ++k) c->sig_max[k] = 0.0f;

@@ -17,7 +17,7 @@ for cfg, integ_name, spp in (("c2", "multiscatter", 16), ("c5", "multiscatter", 
     dev = vr.Device.get(0)
     dev.upload(scene)
     img = vr.Image(W, H)
-    for w0 in (0, 4, 8, 16):
+    for w0 in (0, 2, 4, 8, 16, 32):
         dev.set_option("ff_window0", w0)
         integ.render(scene, img)
         ts = []
