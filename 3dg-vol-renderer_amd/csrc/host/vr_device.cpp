@@ -586,7 +586,7 @@ vr_status gauss_pipeline(vr_ctx* c, RenderArgs& A, hipStream_t s, bool stats) {
     }
 
     // Everything below is sized by the capacity; the kernels read the live record count on the device.
-    // Tr slots: whole 64-record chunks (tr_slot in vr_gauss.hip)
+    // Tr slots: whole record chunks (<= 64 records; hand-out order, vr_gauss.hip)
     if ((st = grow(c->tr, std::max<uint64_t>((cap + 63) / 64 * 64 * S, 1) * 4ull, "hipMalloc(secondary)")) != VR_OK) return st;
     A.tr = (float*)c->tr.p;
     if ((st = grow(c->rec_rad, std::max<uint64_t>(cap, 1) * 16ull, "hipMalloc(record radiance)")) != VR_OK) return st;
@@ -635,9 +635,12 @@ vr_status gauss_pipeline(vr_ctx* c, RenderArgs& A, hipStream_t s, bool stats) {
     HIP_TRY(hipEventRecord(c->ev_stage[1], s), "hipEventRecord");
     HIP_TRY(gauss_lists(A, s), "neighbour lists");
     HIP_TRY(hipEventRecord(c->ev_stage[2], s), "hipEventRecord");
-    {  // environment rays traced in direction order within chunks of 64 records (see ray_slot; 128/256-record
+    {  // environment rays traced in direction order within chunks of 32 records (see ray_slot; larger
        // chunks measured 2-20 % slower: record locality is lost)
-        constexpr uint32_t cr = 64u, shift = 6u;  // entries hold record-in-chunk in 8 bits
+#ifndef VR_CHUNK_SHIFT
+#define VR_CHUNK_SHIFT 5  // 32-record chunks (A/B at C4: 8/16/32/64/128 -> 156.1/150.4/149.1/152.9/161.9 ms)
+#endif
+        constexpr uint32_t shift = VR_CHUNK_SHIFT, cr = 1u << shift;  // entries hold record-in-chunk in 8 bits
         A.env_order = nullptr;
         A.chunk_rec = cr;
         A.chunk_shift = shift;

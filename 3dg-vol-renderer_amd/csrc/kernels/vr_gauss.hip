@@ -1337,7 +1337,7 @@ __global__ __launch_bounds__(256) void record_cut_kernel(RenderArgs A, float bud
         A.rec_cut[r] = fminf(kTauCut, fmaxf(0.0f, logf(1.001f * record_weight(A, A.rec_pos[r]) * rays / budget)));
 }
 
-// Per-record incident radiance Li + Le (test_integrators.h:212-275), one wave per 64-record chunk: the
+// Per-record incident radiance Li + Le (test_integrators.h:212-275), one wave per record chunk: the
 // chunk's Tr values are one contiguous run in hand-out order; they are read once, coalesced, into
 // LDS as [record][sample] (env_order tells where each environment ray went), then each lane sums its
 // record's lights and environment samples in the reference's order. Without env_order a chunk's
