@@ -954,6 +954,30 @@ __global__ void __launch_bounds__(kFFBlock) ff_nee_kernel(RenderArgs A) {
     }
 }
 
+// Each path's radiance from its queued contributions (bounce order) and its inline part, one thread
+// per path of the launch (the chains are walked in parallel, not by the pixel's thread sample after
+// sample); written back into the path's ff_tail entry with no chain left.
+__global__ void __launch_bounds__(kFFBlock) ff_path_radiance_kernel(RenderArgs A) {
+    const size_t q = (size_t)blockIdx.x * kFFBlock + threadIdx.x;
+    if (q >= A.ff_total) return;
+    const float4 t = A.ff_tail[q];
+    const uint32_t f = __float_as_uint(t.w);
+    if ((f & ~kFFTailAfter) == kFFNone) return;
+    float p0 = 0.0f, p1 = 0.0f, p2 = 0.0f;
+    for (uint32_t e = f & ~kFFTailAfter; e != kFFNone; e = __float_as_uint(A.ff_nee[3 * (size_t)e + 1].w)) {
+        const float4 c = A.ff_nee[3 * (size_t)e + 2];
+        p0 += c.x;
+        p1 += c.y;
+        p2 += c.z;
+    }
+    if (f & kFFTailAfter) {
+        p0 += t.x;
+        p1 += t.y;
+        p2 += t.z;
+    }
+    A.ff_tail[q] = make_float4(p0, p1, p2, __uint_as_float(kFFNone));
+}
+
 // pixel_L += L_accum in sample order (integrator.h:706), then pixel_L / num_samples on the last batch.
 __global__ void __launch_bounds__(kFFBlock) ff_accumulate_kernel(RenderArgs A, uint32_t chunk_tiles) {
     const uint32_t tl = blockIdx.x;  // tile within the chunk
@@ -1093,6 +1117,11 @@ hipError_t launch_free_flight(const RenderArgs& A, uint32_t chunk_tiles, hipStre
         if ((e = hipGetLastError()) != hipSuccess) return e;
     }
     if ((e = hipEventRecord(ev[2], stream)) != hipSuccess) return e;
+    if (A.ff_nee_cap > 0) {
+        hipLaunchKernelGGL(dev::ff_path_radiance_kernel, dim3((unsigned)((A.ff_total + dev::kFFBlock - 1) / dev::kFFBlock)),
+                           dim3(dev::kFFBlock), 0, stream, A);
+        if ((e = hipGetLastError()) != hipSuccess) return e;
+    }
     hipLaunchKernelGGL(dev::ff_accumulate_kernel, dim3(chunk_tiles), dim3(dev::kFFBlock), 0, stream, A, chunk_tiles);
     if ((e = hipGetLastError()) != hipSuccess) return e;
     return hipEventRecord(ev[3], stream);
