@@ -2,6 +2,7 @@
 #pragma once
 #include <cstdint>
 #include <string>
+#include <thread>
 #include <vector>
 
 #ifndef __HIPCC__
@@ -67,6 +68,27 @@ struct vr_scene {
 // Multi-GPU group behind a vr_init_multi context (host/vr_multi.cpp).
 struct vr_group;
 namespace vr {
+// Runs fn(i) for every i in [0, n) on a host thread of its own (n == 1: on the calling thread); the
+// first failure's status wins, its message prefixed by label(i).
+template <class F, class L>
+vr_status run_parallel(int n, F fn, L label) {
+    if (n == 1) return fn(0);
+    std::vector<vr_status> st(n, VR_OK);
+    std::vector<std::string> msg(n);
+    std::vector<std::thread> th;
+    for (int i = 0; i < n; ++i)
+        th.emplace_back([&, i] {
+            st[i] = fn(i);
+            if (st[i] != VR_OK) msg[i] = vr_last_error();
+        });
+    for (auto& t : th) t.join();
+    for (int i = 0; i < n; ++i)
+        if (st[i] != VR_OK) return fail(st[i], label(i) + ": " + msg[i]);
+    return VR_OK;
+}
+// The device contexts behind a context: its group's ranks (vr_init_multi), or the context itself.
+int ctx_ranks(vr_ctx* c);
+vr_ctx* ctx_rank(vr_ctx* c, int r);
 vr_status group_create(int ndev, const int* devices, vr_group** out);
 void group_destroy(vr_group* g);
 int group_size(const vr_group* g);

@@ -123,6 +123,10 @@ struct vr_ctx {
 
 // Single-device entry points called on a multi-GPU context act on its first device.
 static inline vr_ctx* first_device(vr_ctx* c) { return (c && c->group) ? vr::group_rank(c->group, 0) : c; }
+namespace vr {
+int ctx_ranks(vr_ctx* c) { return (c && c->group) ? group_size(c->group) : 1; }
+vr_ctx* ctx_rank(vr_ctx* c, int r) { return (c && c->group) ? group_rank(c->group, r) : (r == 0 ? c : nullptr); }
+}  // namespace vr
 
 namespace {
 
@@ -1338,8 +1342,8 @@ vr_status vr_synchronize(vr_ctx* c) {
     vr_status st = collect(c);
     if (st != VR_OK || !pending) return st;
     if (frame_exceeded(c))
-        return fail(VR_ERR_OVERFLOW, "the last frame outgrew the scatter-record buffers sized from earlier frames; "
-                                     "they have been grown: render it again");
+        return fail(VR_ERR_RETRY, "the last frame outgrew the scatter-record buffers sized from earlier frames; "
+                                  "they have been grown: render it again");
     if (c->h_report[1] != 0)
         return fail(VR_ERR_OVERFLOW, std::to_string(c->h_report[1]) + " pixels / paths of the last frame exceeded a "
                                      "per-ray capacity (NaN)");

@@ -298,13 +298,22 @@ vr_status vr_sfd_optimize(vr_ctx* c, const vr_camera* cam, const vr_render_param
     const size_t N = s0.gaussians.size();
     if (s0.type != VR_VOLUME_GAUSSIANS || N == 0) return fail(VR_ERR_INVALID, "Scene has no GMM.");  // :71-74
     const size_t D = N * kPer;
-    std::vector<float> params(D), eps(D), m(D, 0.0f), v(D, 0.0f), sgn(D), plus(D), grads_f(D);
-    std::vector<double> grads(D), fdiff(N);
+    std::vector<float> params(D), eps(D), m(D, 0.0f), v(D, 0.0f), sgn(D), grads_f(D);
+    std::vector<double> grads(D);
     vr_status st;
     if ((st = vr_gmm_pack_parameters(initial, params.data(), D)) != VR_OK) return st;
     vr_gmm_default_eps(eps.data(), D);
     const uint32_t npix = W * H;
     std::vector<float> loss(npix);
+    // A multi-GPU context (vr_init_multi) spreads the perturbed renders of an iteration over its
+    // ranks: rank r renders samples r, r + R, ... after a base render of its own (every rank holds
+    // the same GMM, the render is deterministic, so each rank's base recording and losses are the
+    // ones rank 0 would make). Sample k's difference vector lands in slot k and the gradient sums
+    // them in sample order: the result does not depend on the number of ranks.
+    const int R = std::max(1, std::min(ctx_ranks(c), cfg->num_stoch_samples));
+    auto rank_label = [](int r) { return "vr_sfd_optimize rank " + std::to_string(r); };
+    std::vector<std::vector<float>> rloss(R, std::vector<float>(npix));
+    std::vector<std::vector<double>> fd((size_t)cfg->num_stoch_samples, std::vector<double>(N));
     int64_t old_bvh = 0;
     vr_get_option(c, VR_OPT_DEVICE_BVH, &old_bvh);
     if ((st = vr_set_option(c, VR_OPT_DEVICE_BVH, 1)) != VR_OK) return st;  // every re-upload builds on the device
@@ -312,47 +321,60 @@ vr_status vr_sfd_optimize(vr_ctx* c, const vr_camera* cam, const vr_render_param
         vr_set_option(c, VR_OPT_DEVICE_BVH, old_bvh);
         return r;
     };
-    if ((st = sfd_set_reference(c, I_ref, W, H)) != VR_OK) return done(st);
+    st = run_parallel(R, [&](int r) { return sfd_set_reference(ctx_rank(c, r), I_ref, W, H); }, rank_label);
+    if (st != VR_OK) return done(st);
     auto mean = [&](const std::vector<float>& l) {  // :222-225: double sum in pixel order
         double a = 0.0;
         for (float x : l) a += x;
         return a / (double)l.size();
     };
-    auto upload_params = [&](const float* p) -> vr_status {
+    auto upload_params = [&](vr_ctx* ctx, const float* p) -> vr_status {  // ctx: one rank, or the whole group
         vr_scene* sc = nullptr;
         vr_status r = vr_gmm_apply_parameters(initial, p, D, &sc);
         if (r != VR_OK) return r;
-        r = vr_upload_scene(c, sc);
+        r = vr_upload_scene(ctx, sc);
         vr_scene_destroy(sc);
         return r;
     };
     if ((st = vr_upload_scene(c, initial)) != VR_OK) return done(st);  // the initial GMM first (:84-88)
-    uint64_t draw = 0;
     for (int it = 0; it < cfg->max_iters; ++it) {
-        // 1) base render + recording, base losses (:114-122)
-        if ((st = sfd_render(c, cam, fwd, W, H, 0, 0, loss.data(), nullptr)) != VR_OK) return done(st);
-        res->loss_history[it] = mean(loss);
+        // 1) base render + recording, base losses (:114-122); 2-3) stochastic sign vectors, perturbed
+        // recorded renders, union statistic (:135-190)
+        const uint64_t draw0 = (uint64_t)it * (uint64_t)cfg->num_stoch_samples;
+        st = run_parallel(
+            R,
+            [&](int r) -> vr_status {
+                vr_ctx* cr = ctx_rank(c, r);
+                vr_status e = sfd_render(cr, cam, fwd, W, H, 0, 0, rloss[r].data(), nullptr);
+                std::vector<float> sg(D), pl(D), lplus(npix);
+                for (int k = r; e == VR_OK && k < cfg->num_stoch_samples; k += R) {
+                    sign_vector(cfg->seed, draw0 + (uint64_t)k, sg.data(), D);
+                    for (size_t i = 0; i < D; ++i) pl[i] = params[i] + sg[i] * eps[i];
+                    if ((e = upload_params(cr, pl.data())) != VR_OK) break;
+                    if ((e = sfd_render(cr, cam, fwd, W, H, 1, 1, lplus.data(), nullptr)) != VR_OK) break;
+                    e = sfd_loss_diff_device(cr, npix, fd[k].data(), N);
+                }
+                return e;
+            },
+            rank_label);
+        if (st != VR_OK) return done(st);
+        res->loss_history[it] = mean(rloss[0]);
         std::fill(grads.begin(), grads.end(), 0.0);
-        // 2-3) stochastic sign vectors, perturbed recorded renders, union statistic (:135-190)
         for (int k = 0; k < cfg->num_stoch_samples; ++k) {
-            sign_vector(cfg->seed, draw++, sgn.data(), D);
-            for (size_t i = 0; i < D; ++i) plus[i] = params[i] + sgn[i] * eps[i];
-            if ((st = upload_params(plus.data())) != VR_OK) return done(st);
-            if ((st = sfd_render(c, cam, fwd, W, H, 1, 1, loss.data(), nullptr)) != VR_OK) return done(st);
-            if ((st = sfd_loss_diff_device(c, npix, fdiff.data(), N)) != VR_OK) return done(st);
+            sign_vector(cfg->seed, draw0 + (uint64_t)k, sgn.data(), D);
             for (size_t i = 0; i < D; ++i) {
                 const double denom = (double)eps[i];
                 if (std::fabs(denom) < 1e-12) continue;
-                grads[i] += fdiff[i / kPer] * (double)sgn[i] / denom;
+                grads[i] += fd[k][i / kPer] * (double)sgn[i] / denom;
             }
         }
         for (size_t i = 0; i < D; ++i) grads_f[i] = (float)(grads[i] / (double)cfg->num_stoch_samples);
         if (res->last_grads)
             for (size_t i = 0; i < D; ++i) res->last_grads[i] = grads[i] / (double)cfg->num_stoch_samples;
-        // Adam (:201-205), then the updated GMM (:208)
+        // Adam (:201-205), then the updated GMM on every rank (:208)
         if ((st = vr_adam_step(params.data(), grads_f.data(), m.data(), v.data(), D, it + 1, cfg->lr, 0.9f, 0.999f, 1e-8f)) != VR_OK)
             return done(st);
-        if ((st = upload_params(params.data())) != VR_OK) return done(st);
+        if ((st = upload_params(c, params.data())) != VR_OK) return done(st);
         if (cfg->save_every > 0 && cfg->out_dir && cfg->out_dir[0] && it % cfg->save_every == 0) {  // :211-227
             std::vector<float> rgb((size_t)npix * 3);
             if ((st = sfd_render(c, cam, fwd, W, H, -1, 0, loss.data(), rgb.data())) != VR_OK) return done(st);

@@ -96,19 +96,9 @@ vr_status ncclf(vr_group* g, ncclResult_t r, const char* what) {
 // Runs fn(rank) on one host thread per rank; the first failure's status and message win.
 template <class F>
 vr_status each_rank_parallel(vr_group* g, F fn) {
-    const int n = (int)g->ranks.size();
-    std::vector<vr_status> st(n, VR_OK);
-    std::vector<std::string> msg(n);
-    std::vector<std::thread> th;
-    for (int r = 0; r < n; ++r)
-        th.emplace_back([&, r] {
-            st[r] = fn(r);
-            if (st[r] != VR_OK) msg[r] = vr_last_error();
-        });
-    for (auto& t : th) t.join();
-    for (int r = 0; r < n; ++r)
-        if (st[r] != VR_OK) return fail(st[r], "rank " + std::to_string(r) + " (device " + std::to_string(g->devices[r]) + "): " + msg[r]);
-    return VR_OK;
+    return run_parallel((int)g->ranks.size(), fn, [&](int r) {
+        return "rank " + std::to_string(r) + " (device " + std::to_string(g->devices[r]) + ")";
+    });
 }
 
 vr_status grow_dev(int dev, float** p, size_t* cap, size_t floats, const char* what) {
@@ -139,14 +129,15 @@ vr_status group_frame(vr_group* g, const vr_camera* cam, const vr_render_params*
     if ((st = grow_dev(g->devices[0], &g->d_recv, &g->recv_floats, slab_floats * n, "hipMalloc(gathered slabs)")) != VR_OK)
         return st;
     if ((st = grow_dev(g->devices[0], &g->d_frame, &g->frame_floats, (size_t)W * H * 3, "hipMalloc(frame)")) != VR_OK) return st;
-    // 1) every rank renders its interleaved share (asynchronous on its own stream)
-    for (int r = 0; r < n; ++r) {
+    // 1) every rank renders its interleaved share (asynchronous on its own stream), each rank's ~15
+    // launches issued from a host thread of its own so the ranks start together
+    st = each_rank_parallel(g, [&](int r) -> vr_status {
         const uint32_t count = (uint32_t)r < nt ? (nt - 1 - (uint32_t)r) / (uint32_t)n + 1 : 0;
-        if (count == 0) continue;
-        if ((st = vr_render_tiles_device(g->ranks[r], cam, p, W, H, (uint32_t)r, (uint32_t)n, count, 1, g->slab[r],
-                                         g->streams[r])) != VR_OK)
-            return st;
-    }
+        if (count == 0) return VR_OK;
+        return vr_render_tiles_device(g->ranks[r], cam, p, W, H, (uint32_t)r, (uint32_t)n, count, 1, g->slab[r],
+                                      g->streams[r]);
+    });
+    if (st != VR_OK) return st;
     // 2) gather the slabs to the root
     if (g->use_rccl) {
         ncclResult_t e = g->rccl.group_start();
@@ -189,7 +180,7 @@ vr_status group_frame(vr_group* g, const vr_camera* cam, const vr_render_params*
     for (int r = 0; r < n; ++r) {
         st = vr_synchronize(g->ranks[r]);
         if (st == VR_OK) continue;
-        if (st == VR_ERR_OVERFLOW && std::string(vr_last_error()).find("render it again") != std::string::npos) {
+        if (st == VR_ERR_RETRY) {
             *again = true;
             continue;
         }

@@ -656,11 +656,16 @@ __device__ __forceinline__ void sec_add(const RenderArgs& A, SecRay& R, const GR
         }
         return;
     }
-    if (!R.light) {
-        R.tau += FAST ? optical_depth_fast(g, q, lo, b) : optical_depth(g, q, lo, b);
+    if constexpr (FAST) {  // one optical-depth evaluation for light and environment lanes alike
+        const bool add = !R.light || b < R.lim;
+        R.needs_stop = R.needs_stop || (!add && lo < R.lim);
+        if (!R.light) R.lim = fmaxf(R.lim, b);
+        if (add) R.tau += optical_depth_chord(g, q, lo, b);  // [lo, b] lies on the 3-sigma chord
+    } else if (!R.light) {
+        R.tau += optical_depth(g, q, lo, b);
         R.lim = fmaxf(R.lim, b);
     } else if (b < R.lim) {
-        R.tau += FAST ? optical_depth_fast(g, q, lo, b) : optical_depth(g, q, lo, b);
+        R.tau += optical_depth(g, q, lo, b);
     } else if (lo < R.lim) {
         R.needs_stop = true;
     }
@@ -697,7 +702,7 @@ __device__ __forceinline__ void sec_leaf(const RenderArgs& A, SecRay& R, int32_t
 // Ray complete: write its transmittance (or hand it to the exact slow path).
 template <bool S, bool FAST, bool PURE>
 __device__ __forceinline__ void sec_finish(const RenderArgs& A, SecRay& R, Ctr& c) {
-#ifndef VR_DIAG_WAVE_UTIL
+#if !defined(VR_DIAG_WAVE_UTIL) && !defined(VR_DIAG_CYCLES) && !defined(VR_DIAG_LISTSKIP) && !defined(VR_DIAG_ORIGIN)
     if constexpr (S) {  // secondary-stage diagnostics in otherwise unused counter slots
         if (R.tau >= R.cut) {
             c.v[kCtrSteps]++;                 // rays ended by the optical-depth cut-off
@@ -859,6 +864,13 @@ __device__ __forceinline__ void sec_node4(const RenderArgs& A, SecRay& R, LdsInt
         const bool hit = (ref[i] != 0) & (tmax >= fmaxf(tmin, 0.0f)) & (tmin <= lim);
         key[i] = hit ? tmin : INFINITY;
         kr[i] = hit ? ref[i] : 0;
+#ifdef VR_DIAG_ORIGIN  // diagnostic builds only: child boxes hit that hold the ray origin (inner / leaf), inner hits
+        if constexpr (S) {
+            c.v[kCtrSteps] += (hit && ref[i] > 0 && tmin < 0.0f) ? 1u : 0u;
+            c.v[kCtrPixels] += (hit && ref[i] < 0 && tmin < 0.0f) ? 1u : 0u;
+            c.v[kCtrPrimQueries] += (hit && ref[i] > 0) ? 1u : 0u;
+        }
+#endif
     }
 #if !VR_WW_NOSORT
     // 4-input sorting network (5 compare-exchanges)
@@ -1163,7 +1175,14 @@ __device__ __forceinline__ void list_advance(LeafQueue& Q, int& node) {
 #ifndef VR_WW_PRIM_STEPS
 #define VR_WW_PRIM_STEPS 6
 #endif
+#ifndef VR_WW_PRIM_UNROLL
+#define VR_WW_PRIM_UNROLL 6  // unroll of the PRIM iteration's step loop (A/B: code size vs. scheduling)
+#endif
+#ifndef VR_WW_NODE_UNROLL
+#define VR_WW_NODE_UNROLL 1
+#endif
 constexpr int kRefillMin = VR_WW_REFILL, kNodeSteps = VR_WW_NODE_STEPS, kPrimSteps = VR_WW_PRIM_STEPS;
+constexpr int kPrimUnroll = VR_WW_PRIM_UNROLL, kNodeUnroll = VR_WW_NODE_UNROLL;
 
 // 6 waves/SIMD = 80 VGPRs: the ray state is kept small enough for that without scratch spills (a
 // spilling 6-wave build measured 9 % slower than 5 waves; this one is 5 % faster than 5 waves).
@@ -1192,6 +1211,17 @@ __global__ __launch_bounds__(BLOCK, WAVES) void secondary_ww_kernel(RenderArgs A
     const uint32_t split = cpw >= 32u ? 0u : cpw >= 16u ? 1u : cpw >= 8u ? 2u : 3u;
     const uint32_t nunits = nchunks << split;
     counter_done = nunits == 0u;
+#ifdef VR_DIAG_CYCLES  // diagnostic builds only (S = true): wave cycles per phase, lane 0's counters
+    // kCtrSteps: NODE iterations, kCtrPrimQueries: PRIM iterations, kCtrPixels: refill + completion
+    uint64_t diag_t = __builtin_amdgcn_s_memtime();
+    auto diag_lap = [&](int slot) {
+        const uint64_t now = __builtin_amdgcn_s_memtime();
+        if constexpr (S) c.v[slot] += lane == 0u ? (uint32_t)(now - diag_t) : 0u;
+        diag_t = now;
+    };
+#else
+    auto diag_lap = [](int) {};
+#endif
     for (;;) {
         const uint64_t idle = __ballot(!live);
         if (__popcll(idle) >= kRefillMin) {  // refill once enough lanes are idle (amortises sec_init)
@@ -1228,6 +1258,7 @@ __global__ __launch_bounds__(BLOCK, WAVES) void secondary_ww_kernel(RenderArgs A
 #ifdef VR_DIAG_WAVE_UTIL  // diagnostic builds only: wave iterations with a live lane, and live lanes in them
         if constexpr (S) c.v[kCtrPixels] += (lane == 0u ? 1u : 0u);
 #endif
+        diag_lap(kCtrPixels);
         const bool has_prim = live && Q.has_prim();
         constexpr int kRoom = W ? 4 : 2;  // leaves one NODE step can queue
         const bool can_node = live && node >= 0 && (QCAP == 2 ? Q.n == 0 : Q.n <= QCAP - kRoom);
@@ -1236,6 +1267,7 @@ __global__ __launch_bounds__(BLOCK, WAVES) void secondary_ww_kernel(RenderArgs A
         const bool prim_iter = nn == 0 || (np > 0 && np >= nn);
         if (prim_iter) {  // PRIM iteration: up to kPrimSteps primitive tests per lane
             bool go = has_prim;
+#pragma unroll kPrimUnroll
             for (int k = 0; k < kPrimSteps; ++k) {
 #ifdef VR_DIAG_WAVE_UTIL  // diagnostic builds only: wave-level PRIM steps (lane utilisation)
                 if constexpr (S) c.v[kCtrPrimQueries] += (__ballot(go) != 0ull && lane == 0u) ? 1u : 0u;
@@ -1246,6 +1278,15 @@ __global__ __launch_bounds__(BLOCK, WAVES) void secondary_ww_kernel(RenderArgs A
                     if constexpr (S) c.v[from_list ? kCtrMu : kCtrPrims]++;  // list members counted apart
                     const GRec g = load_rec(A.gauss, (int)j);
                     const Quad q = quad_fast(g, R.ray);
+#ifdef VR_DIAG_LISTSKIP  // diagnostic builds only: tree primitive tests of listed rays, and how many were list members
+                    if constexpr (S) {
+                        if (!from_list && R.listed) {
+                            c.v[kCtrPixels]++;
+                            if (q.Cq <= A.list_r2) c.v[kCtrSteps]++;
+                        }
+                        if (!from_list && !R.listed) c.v[kCtrPrimQueries]++;
+                    }
+#endif
                     float a, b;
                     // a tree leaf skips the record's list members (already summed)
                     if (!(R.listed && !from_list && q.Cq <= A.list_r2) && intersect_fast(q, a, b)) {
@@ -1261,8 +1302,10 @@ __global__ __launch_bounds__(BLOCK, WAVES) void secondary_ww_kernel(RenderArgs A
                 }
                 go = go && Q.has_prim() && R.tau < R.cut;
             }
+            diag_lap(kCtrPrimQueries);
         } else {  // NODE iteration: up to kNodeSteps node steps per lane
             bool go = can_node;
+#pragma unroll kNodeUnroll
             for (int k = 0; k < kNodeSteps; ++k) {
 #ifdef VR_DIAG_WAVE_UTIL  // diagnostic builds only: wave-level NODE steps (lane utilisation)
                 if constexpr (S) c.v[kCtrSteps] += (__ballot(go) != 0ull && lane == 0u) ? 1u : 0u;
@@ -1273,6 +1316,7 @@ __global__ __launch_bounds__(BLOCK, WAVES) void secondary_ww_kernel(RenderArgs A
                 }
                 go = go && node >= 0 && Q.n <= QCAP - kRoom;
             }
+            diag_lap(kCtrSteps);
         }
         if (live && (R.tau >= R.cut || (node == -1 && !Q.has_prim()))) {
             sec_finish<S, true, PURE>(A, R, c);

@@ -10,9 +10,10 @@ _PKG_ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 LIB_PATH = os.environ.get("VR_LIB_PATH") or os.path.join(_PKG_ROOT, "libvr_hip.so")  # override: A/B builds
 
 VR_OK = 0
+VR_ERR_OVERFLOW, VR_ERR_RETRY = 6, 8
 STATUS_NAMES = {
     0: "VR_OK", 1: "VR_ERR_INVALID", 2: "VR_ERR_IO", 3: "VR_ERR_PARSE", 4: "VR_ERR_HIP",
-    5: "VR_ERR_NOSCENE", 6: "VR_ERR_OVERFLOW", 7: "VR_ERR_UNSUPPORTED",
+    5: "VR_ERR_NOSCENE", 6: "VR_ERR_OVERFLOW", 7: "VR_ERR_UNSUPPORTED", 8: "VR_ERR_RETRY",
 }
 VR_VOLUME_GAUSSIANS, VR_VOLUME_SPHERES = 0, 1
 VR_CAMERA_PINHOLE, VR_CAMERA_ORTHOGRAPHIC = 0, 1

@@ -68,7 +68,7 @@ def finish_local(dev, camera, params, W, H, rank, world, slab, frame, stream_ptr
             dev.synchronize()
             return
         except L.VRError as e:
-            if attempt == retries or "render it again" not in str(e):
+            if attempt == retries or e.status != L.VR_ERR_RETRY:
                 raise
         render_local(dev, camera, params, W, H, rank, world, slab, frame, stream_ptr)
 

@@ -41,6 +41,9 @@ CONFIGS = {
     "c3": (1920, 1080, 100_000, "1920x1080, 100k Gaussians (make_random distribution)"),
     "c2": (512, 512, "1000_random.txt", "512x512, scenes/gaussians/1000_random.txt"),
     "c5": (512, 512, "10k_random.txt", "512x512, scenes/gaussians/10k_random.txt (BASELINE config 5)"),
+    # the reference driver's own default forward workload (tests/main.cpp:17-45): MultiScatterGaussians,
+    # 256 paths/pixel, 2g_altered.txt, 512x512, camera (0, 1, 6) looking at (0, 1, 0)
+    "main": (512, 512, "2g_altered.txt", "512x512, scenes/gaussians/2g_altered.txt (tests/main.cpp default render)"),
 }
 LIGHTS = [((0.0, 5.0, 0.1), (50.0, 0.0, 0.0)), ((-3.0, 3.0, 0.3), (0.0, 30.0, 0.0)),
           ((3.0, 3.0, -0.2), (0.0, 0.0, 30.0))]  # scenes/gaussians/1000_random.txt:1-3
@@ -196,6 +199,37 @@ def cpu_baseline_ff(scene, W, H, multi, spp, budget_s, threads, log):
                       f"{threads} OpenMP threads); oracle restatement of the reference integrator"}
 
 
+def render_call_times(dev, integ, scene, W, H):
+    """Wall time of the reference's own timed region, `integrator->render(scene, image)`
+    (tests/main.cpp:44-49), through the Python mirror of that call (vr_render: frame + device-to-host
+    copy of the image, scene resident in HBM), and the same call behind a fresh vr_upload_scene (host
+    precompute + BVH build + host-to-device copy: the reference builds its BVH when the scene loads,
+    outside its timed region). Untimed for the metric; one GPU."""
+    img = vr.Image(W, H)
+    integ.render(scene, img)  # host-side buffers sized
+    t0 = time.perf_counter()
+    integ.render(scene, img)
+    t_render = time.perf_counter() - t0
+    t0 = time.perf_counter()
+    dev.upload(scene, force=True)
+    t_upload = time.perf_counter() - t0
+    t0 = time.perf_counter()
+    integ.render(scene, img)
+    t_after = time.perf_counter() - t0
+    return {"render_s": t_render, "upload_s": t_upload, "upload_plus_render_s": t_upload + t_after,
+            "note": "vr_render wall time (frame + D2H copy of the W x H x 3 f32 image) with the scene resident; "
+                    "upload_s = vr_upload_scene (host precompute, BVH build, H2D)"}
+
+
+def all_core_baseline(fn, host, cores, log):
+    """The same CPU baseline on every core this process may use, when that is more than `cores`
+    (the GPU box exports OMP_NUM_THREADS = its CPU share; the machine has more cores)."""
+    if host["affinity"] <= cores:
+        return None
+    r = fn(host["affinity"])
+    return {"value": r["value"], "unit": r["unit"], "cores": host["affinity"], "sample": r["sample"]}
+
+
 def bench_sfd(args, scene, camera, W, H, t_setup):
     """Config 5: one step = one StochasticFiniteDiffInverseIntegrator iteration (inverse_integrator.h:
     115-200) of the native loop (vr_sfd_optimize): a recorded base render + num_stoch_samples (4)
@@ -256,8 +290,16 @@ def main():
     ap.add_argument("--integrator", default="raymarch", choices=["raymarch", "freeflight", "multiscatter", "sfd"],
                     help="raymarch = RayMarchingGaussians (the headline); the free-flight integrators are "
                          "secondary lines (unit Mpaths/s = pixel samples per second)")
-    ap.add_argument("--spp", type=int, default=16, help="free-flight paths per pixel")
+    ap.add_argument("--spp", type=int, default=None,
+                    help="free-flight paths per pixel (default 16; 256 with --config main, as tests/main.cpp:27)")
     args = ap.parse_args()
+    if args.config == "main":  # tests/main.cpp renders MultiScatterGaussians
+        if args.integrator == "raymarch":
+            args.integrator = "multiscatter"
+        if args.spp is None:
+            args.spp = 256
+    if args.spp is None:
+        args.spp = 16
     cores, host = host_cores()
     if args.cpu_threads <= 0:
         args.cpu_threads = cores
@@ -341,6 +383,8 @@ def main():
     elapsed = time.perf_counter() - t0
     if any(st["error_pixels"] for st in per_step):
         raise SystemExit(f"rank {rank}: pixels exceeded every capacity")
+    if any(st["record_overflow"] for st in per_step):  # a timed frame that outgrew its buffers is invalid
+        raise SystemExit(f"rank {rank}: a timed frame outgrew the scatter-record buffers (sized by the warmup)")
     kernel_ms = float(np.mean([st["kernel_ms"] for st in per_step]))
     stage_ms = {k: float(np.mean([st["stage_ms"][k] for st in per_step])) for k in vr.Device.STAGES}
     t = torch.tensor([elapsed, kernel_ms], dtype=torch.float64, device="cuda")
@@ -358,9 +402,13 @@ def main():
                 roof = ff_roofline(dev.count_work(camera, integ.params, W, H), stage_ms, args.config)
             cpu = None
             if world == 1 and args.cpu_budget > 0:
-                cpu = cpu_baseline_ff(scene, W, H, args.integrator == "multiscatter", args.spp, args.cpu_budget,
-                                      args.cpu_threads, log)
+                multi = args.integrator == "multiscatter"
+                cpu = cpu_baseline_ff(scene, W, H, multi, args.spp, args.cpu_budget, args.cpu_threads, log)
                 cpu.update(host)
+                cpu["all_cores"] = all_core_baseline(
+                    lambda n: cpu_baseline_ff(scene, W, H, multi, args.spp, args.cpu_budget / 2, n, log), host,
+                    args.cpu_threads, log)
+            call = render_call_times(dev, integ, scene, W, H) if world == 1 else None
             print(json.dumps({
                 "metric": f"Mpaths/s, {args.integrator} render", "value": paths / (ms_per_step * 1e-3) / 1e6,
                 "unit": "Mpaths/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
@@ -369,7 +417,7 @@ def main():
                 "config": {"workload": CONFIGS[args.config][3], "width": W, "height": H,
                            "gaussians": scene.get_num_primitives(), "integrator": type(integ).__name__,
                            "spp": args.spp, "min_bounces": 5, "parallelism": f"tiles{world}",
-                           "frame_kernel_ms": kernel_ms},
+                           "frame_kernel_ms": kernel_ms, "render_call": call},
                 "roofline": roof,
                 "cpu_baseline": cpu}), flush=True)
         if world > 1:
@@ -440,6 +488,10 @@ def main():
         if world == 1 and args.cpu_budget > 0:
             cpu = cpu_baseline(scene, W, H, args.env_samples, args.cpu_budget, args.cpu_threads, log)
             cpu.update(host)
+            cpu["all_cores"] = all_core_baseline(
+                lambda n: cpu_baseline(scene, W, H, args.env_samples, args.cpu_budget / 2, n, log), host,
+                args.cpu_threads, log)
+        call = render_call_times(dev, integ, scene, W, H) if world == 1 else None
         out = {
             "metric": "Mrays/s + achieved HBM GB/s, 4096² render of 1M Gaussians, 1/2/4/8 GPU",
             "value": value, "unit": "Mrays/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
@@ -448,7 +500,8 @@ def main():
             "config": {"workload": CONFIGS[args.config][3], "width": W, "height": H, "gaussians": n_g,
                        "integrator": "RayMarchingGaussians", "step_size": 0.01, "env_samples": args.env_samples,
                        "t_eps": args.t_eps, "lights": len(LIGHTS), "parallelism": f"tiles{world}",
-                       "setup_s": t_setup, "fallback_pixels": per_step[-1]["fallback_pixels"]},
+                       "setup_s": t_setup, "fallback_pixels": per_step[-1]["fallback_pixels"],
+                       "render_call": call},
             "roofline": roof,
             "cpu_baseline": cpu,
         }

@@ -23,7 +23,7 @@
 extern "C" {
 #endif
 
-#define VR_ABI_VERSION 4
+#define VR_ABI_VERSION 5
 
 typedef enum vr_status {
     VR_OK = 0,
@@ -33,7 +33,9 @@ typedef enum vr_status {
     VR_ERR_HIP = 4,         /* HIP runtime error (includes "no GPU") */
     VR_ERR_NOSCENE = 5,     /* render before vr_upload_scene */
     VR_ERR_OVERFLOW = 6,    /* a per-ray capacity (active set, stack, step table) was exceeded */
-    VR_ERR_UNSUPPORTED = 7  /* valid request the device path does not implement */
+    VR_ERR_UNSUPPORTED = 7, /* valid request the device path does not implement */
+    VR_ERR_RETRY = 8        /* vr_synchronize only: the last frame outgrew the scatter-record buffers
+                               sized from earlier frames; they have been grown, render it again */
 } vr_status;
 
 /* scene.h:18-22 Scene::VolumeType */
@@ -221,8 +223,8 @@ vr_status vr_render(vr_ctx* ctx, const vr_camera* cam, const vr_render_params* p
 /* Multi-GPU building block (asynchronous on `stream`, a hipStream_t or NULL for the default; the
  * host never waits for the device inside a frame once the context has rendered one frame of this
  * kind — the first sizes the scatter-record buffers). The frame's outcome is reported by
- * vr_synchronize (VR_ERR_OVERFLOW if pixels exceeded a per-ray capacity or the frame outgrew the
- * record buffers, which are then grown: render it again) and by vr_get_stats.
+ * vr_synchronize (VR_ERR_RETRY if the frame outgrew the record buffers, which are then grown:
+ * render it again; VR_ERR_OVERFLOW if pixels exceeded a per-ray capacity) and by vr_get_stats.
  * The frame is cut into 16x16 tiles numbered row-major; this call renders tiles
  * first_tile, first_tile + tile_stride, ... (num_tiles of them). If `packed` is non-zero the
  * output is a slab of num_tiles * 256 pixels (tile-major, row-major inside a tile, 3 floats per
@@ -347,8 +349,8 @@ typedef enum vr_option {
 } vr_option;
 vr_status vr_set_option(vr_ctx* ctx, int32_t option, int64_t value);
 vr_status vr_get_option(vr_ctx* ctx, int32_t option, int64_t* value);
-/* Waits for the context's device work; returns VR_ERR_OVERFLOW if the last frame is invalid (see
- * vr_render_tiles_device). */
+/* Waits for the context's device work; returns VR_ERR_RETRY / VR_ERR_OVERFLOW if the last frame is
+ * invalid (see vr_render_tiles_device). */
 vr_status vr_synchronize(vr_ctx* ctx);
 vr_status vr_get_stats(vr_ctx* ctx, vr_render_stats* out);
 /* Diagnostics: the pixels of the last RayMarchingGaussians / PureRayMarching frame that were re-run
