@@ -99,7 +99,9 @@ struct vr_ctx {
     };
     Buf px_first, px_T, rec_pos, rec_meta, rec_next, rec_act, tr, rec_rad, rec_alloc, rec_bloom, slowq;
     Buf pcg_jump, ray_next, rec_list, rec_nlist, stack_ovf, env_order, rec_cut;
+    Buf deep;  // march_deep_kernel: pixel queue + global active lists (vr_gauss.hip)
     Buf ff_scratch, ff_tail, ff_sum, ff_nee;  // free-flight integrators (vr_freeflight.hip)
+    Buf ff_fb;                                // ff_fallback_kernel: path queue + kFFBigCap rows
     uint32_t* d_order = nullptr;      // record (leaf order) -> scene index
     Buf rec_bits[2];                  // RECORD_PIXEL_GAUSSIANS bitsets (vr_render_record slots)
     uint32_t rec_npix[2] = {0, 0}, rec_n[2] = {0, 0};
@@ -545,6 +547,11 @@ vr_status gauss_pipeline(vr_ctx* c, RenderArgs& A, hipStream_t s, bool stats) {
         c->pcg_jump_n = n;
     }
     A.pcg_jump = (const unsigned long long*)c->pcg_jump.p;
+    if ((st = grow(c->deep, (kDeepQueue + 1) * 4ull + (uint64_t)kActDeep * kDeepThreads * 4ull, "hipMalloc(deep march)")) != VR_OK)
+        return st;
+    A.deepq = (uint32_t*)c->deep.p;
+    A.deepq_cap = kDeepQueue;
+    A.deep_act = (int32_t*)(A.deepq + kDeepQueue + 1);
 
     // Record capacity: from earlier frames of this context (hints), so the host never waits for
     // the march. A context's first frame sizes it: one host sync after the march, re-run with the
@@ -574,6 +581,7 @@ vr_status gauss_pipeline(vr_ctx* c, RenderArgs& A, hipStream_t s, bool stats) {
         A.act_ovf_cap = (uint32_t)ovf;
         HIP_TRY(hipMemsetAsync(A.rec_alloc, 0, 16, s), "hipMemsetAsync(rec_alloc)");
         HIP_TRY(hipMemsetAsync(c->d_queue, 0, sizeof(uint32_t), s), "hipMemsetAsync(queue)");
+        HIP_TRY(hipMemsetAsync(A.deepq, 0, sizeof(uint32_t), s), "hipMemsetAsync(deep queue)");
         HIP_TRY(gauss_march(A, s, stats), "march");
         if (attempt == 0) HIP_TRY(hipEventRecord(c->ev_stage[0], s), "hipEventRecord");
         if (sized) break;
@@ -670,7 +678,8 @@ vr_status gauss_pipeline(vr_ctx* c, RenderArgs& A, hipStream_t s, bool stats) {
 // sample order (vr_freeflight.hip).
 constexpr uint64_t kFFMaxPaths = 1ull << 23;
 // The active list indexes the hit buffer, so it never holds more than kFFHitCap entries: the only
-// capacity a path can exceed is kFFHitCap Gaussians overlapping one point (error path, NaN).
+// capacity a path can exceed is kFFHitCap Gaussians overlapping one point; such a path re-runs in
+// ff_fallback_kernel with kFFBigCap-entry rows (only beyond that: error path, NaN).
 constexpr int32_t kFFHitCap = 128, kFFActCap = kFFHitCap;
 vr_status free_flight_pipeline(vr_ctx* c, RenderArgs& A, hipStream_t s) {
     const uint32_t spp = (uint32_t)A.ff_samples;
@@ -689,6 +698,14 @@ vr_status free_flight_pipeline(vr_ctx* c, RenderArgs& A, hipStream_t s) {
     if (A.ff_nee_cap > 0) {
         if ((st = grow(c->ff_nee, (size_t)A.ff_nee_cap * 3 * sizeof(float4), "free-flight shadow-ray queue")) != VR_OK) return st;
         A.ff_nee = (float4*)c->ff_nee.p;
+    }
+    {  // paths over the hit-buffer capacity re-run in ff_fallback_kernel (queue + its own rows)
+        const uint64_t qcap = paths;
+        const uint64_t rows = (uint64_t)kFFBigThreads * 3ull * (uint64_t)kFFBigCap * 16ull;
+        if ((st = grow(c->ff_fb, rows + (qcap + 1) * 4ull + 64, "free-flight fallback")) != VR_OK) return st;
+        A.ff_big = (float4*)c->ff_fb.p;
+        A.ff_fbq = (uint32_t*)((char*)c->ff_fb.p + rows);
+        A.ff_fbq_cap = (uint32_t)qcap;
     }
     float4* base = (float4*)c->ff_scratch.p;
     A.ff_threads = threads;

@@ -677,6 +677,14 @@ __device__ __forceinline__ bool ff_bounce(const RenderArgs& A, SC& S, int* stack
     S.C.add(kFFBounces);
     const float ts = free_flight_distance<MULTI>(A, S, P.ray, target, m, stack, kFFBlock);
     if (MULTI && A.rec_bits && ts != -2.0f) record_hits(A, P.ray, ts >= 0.0f ? ts + 1e-6f : INFINITY, P.px, stack, kFFBlock);
+    if (ts == -2.0f && A.ff_fbq != nullptr) {  // over the hit-buffer capacity: the whole path re-runs
+        const uint32_t q = atomicAdd(A.ff_fbq, 1u);        // in ff_fallback_kernel with larger rows
+        if (q < A.ff_fbq_cap) {
+            A.ff_fbq[1 + q] = P.out;
+            A.ff_tail[P.out] = make_float4(0.0f, 0.0f, 0.0f, __uint_as_float(kFFNone));  // overwritten there
+            return false;
+        }
+    }
     if (ts == -2.0f || P.bounce >= A.ff_max_bounces) {
         P.L0 = P.L1 = P.L2 = __builtin_nanf("");
         P.after = true;
@@ -802,6 +810,33 @@ __global__ void __launch_bounds__(kFFBlock, VR_FF_WAVES) ff_path_kernel(RenderAr
         Ctr c{};
         for (int i = 0; i < kFFNumCtr; ++i) c.v[i] = S.C.v[i];
         flush_counters(A.work, c);
+    }
+}
+
+// Paths the path kernel queued because more Gaussians overlapped one point than its rows hold: each
+// re-runs from its first bounce (same seed, so the same path) with kFFBigCap-entry rows and inline
+// shadow rays, and writes its radiance as one inline sum (its earlier queued shadow rays are dropped).
+// Only a path over kFFBigCap fails (NaN, VR_ERR_OVERFLOW).
+template <bool MULTI>
+__global__ void __launch_bounds__(kFFBlock) ff_fallback_kernel(RenderArgs A) {
+    __shared__ int s_stack[(kStackSize + kCollectQueue) * kFFBlock];
+    int* stack = s_stack + threadIdx.x;
+    const uint32_t gt = blockIdx.x * kFFBlock + threadIdx.x, nt = gridDim.x * kFFBlock;
+    const uint32_t n = min(A.ff_fbq[0], A.ff_fbq_cap);
+    RenderArgs B = A;
+    B.ff_threads = nt;
+    B.ff_hit_cap = B.ff_act_cap = kFFBigCap;
+    B.ff_hit = A.ff_big;
+    B.ff_act0 = A.ff_big + (size_t)kFFBigCap * nt;
+    B.ff_act1 = A.ff_big + (size_t)2 * kFFBigCap * nt;
+    B.ff_nee_cap = 0;  // shadow rays inline
+    B.ff_fbq = nullptr;
+    FFScratch<false> S{B.ff_hit + gt, B.ff_act0 + gt, B.ff_act1 + gt, nt, 0, {}};
+    for (uint32_t q = gt; q < n; q += nt) {
+        FFPath P{PCG32(0, 1)};
+        if (!ff_start(B, A.ff_fbq[1 + q], P)) continue;
+        while (ff_bounce<MULTI>(B, S, stack, P)) {
+        }
     }
 }
 
@@ -1095,6 +1130,7 @@ hipError_t launch_free_flight(const RenderArgs& A, uint32_t chunk_tiles, hipStre
     hipError_t e0 = hipMemsetAsync(A.ff_next, 0, sizeof(unsigned long long), stream);
     if (e0 != hipSuccess) return e0;
     if (A.ff_nee_cap > 0 && (e0 = hipMemsetAsync(A.ff_nee_n, 0, 2 * sizeof(uint32_t), stream)) != hipSuccess) return e0;
+    if (A.ff_fbq != nullptr && (e0 = hipMemsetAsync(A.ff_fbq, 0, sizeof(uint32_t), stream)) != hipSuccess) return e0;
     dim3 grid(A.ff_threads / dev::kFFBlock);
     const bool cnt = A.work != nullptr;  // vr_count_work: the instrumented kernels
     if ((e0 = hipEventRecord(ev[0], stream)) != hipSuccess) return e0;
@@ -1107,6 +1143,11 @@ hipError_t launch_free_flight(const RenderArgs& A, uint32_t chunk_tiles, hipStre
     }
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
+    if (A.ff_fbq != nullptr) {  // paths over the hit-buffer capacity (usually none: the kernel exits at once)
+        if (A.ff_multi) hipLaunchKernelGGL((dev::ff_fallback_kernel<true>), dim3(kFFBigThreads / dev::kFFBlock), dim3(dev::kFFBlock), 0, stream, A);
+        else hipLaunchKernelGGL((dev::ff_fallback_kernel<false>), dim3(kFFBigThreads / dev::kFFBlock), dim3(dev::kFFBlock), 0, stream, A);
+        if ((e = hipGetLastError()) != hipSuccess) return e;
+    }
     if ((e = hipEventRecord(ev[1], stream)) != hipSuccess) return e;
     if (A.ff_nee_cap > 0) {
         int dv = 0, cus = 1;

@@ -47,6 +47,10 @@ namespace dev {
 // exponentials reaches 0 or a denormal <= 1.4e-45 at the same point.)
 constexpr float kTauCut = 104.0f;
 
+// Bit of active-list slot `slot` in a ray's 64-bit hit mask. Records with more than 64 active
+// Gaussians (march_deep_kernel) find their missed members by re-intersecting the whole list instead.
+__device__ __forceinline__ uint64_t slot_bit(int slot) { return slot < 64 ? 1ull << slot : 0ull; }
+
 // Scatter records of the frame, read on the device: the host never waits for the march (the
 // buffers are sized from the previous frame; a frame that outgrew them is reported and re-run).
 // Clamped to the capacity, so an overflowing frame stays in bounds.
@@ -78,7 +82,7 @@ __device__ float light_transmittance(const RenderArgs& A, const Ray& sr, float d
                 float lo = a;
                 if (slot >= 0) {
                     lo = 0.0f;
-                    hitmask |= 1ull << slot;
+                    hitmask |= slot_bit(slot);
                 }
                 if (b < dist) {
                     if constexpr (S) c.v[kCtrOD]++;
@@ -93,7 +97,23 @@ __device__ float light_transmittance(const RenderArgs& A, const Ray& sr, float d
     uint64_t all = act.n >= 64 ? ~0ull : ((1ull << act.n) - 1ull);
     uint64_t missed = all & ~hitmask;  // pre-activated but not intersected (rounding at the surface)
     if (tau >= kTauCut) return 0.0f;   // exp(-tau) == 0 exactly; later terms are >= 0
-    if (needs_stop || missed) {
+    // more than 64 active Gaussians: a member is missed iff the ray does not intersect it
+    auto deep_missed = [&](int s, GRec& g, Quad& q) {
+        float a, b;
+        g = load_rec(G, act.get(s));
+        q = quad(g, sr);
+        return !intersect(q, a, b);
+    };
+    bool deep_any = false;
+    if (act.n > 64) {
+        missed = 0;
+        for (int s = 0; s < act.n && !deep_any; ++s) {
+            GRec g;
+            Quad q;
+            deep_any = deep_missed(s, g, q);
+        }
+    }
+    if (needs_stop || missed || deep_any) {
         float tstop = INFINITY;  // first event at or beyond the light
         traverse<false>(
             A, sr, stack, stride,
@@ -144,6 +164,12 @@ __device__ float light_transmittance(const RenderArgs& A, const Ray& sr, float d
             if constexpr (S) c.v[kCtrOD]++;
             tau += optical_depth(g, q, 0.0f, tstop);
         }
+        if (deep_any)
+            for (int s = 0; s < act.n; ++s) {
+                GRec g;
+                Quad q;
+                if (deep_missed(s, g, q)) tau += optical_depth(g, q, 0.0f, tstop);
+            }
     }
     return expf(-tau);
 }
@@ -180,7 +206,8 @@ __device__ __forceinline__ float tail_weight(const RenderArgs& A, float x, float
 // W: BVH window queries on the 4-wide half-precision tree (CAP-entry stack; a query that could
 // overflow it sends the pixel to the fallback kernel, which walks the pair tree).
 template <int ACT, bool S, bool H, bool W = false, int CAP = kStackSize>
-__device__ int march(const RenderArgs& A, uint32_t p, int px, int py, int* act_base, int* stack, int stride, Ctr& c) {
+__device__ int march(const RenderArgs& A, uint32_t p, int px, int py, int* act_base, int* stack, int stride, Ctr& c,
+                     int act_stride = -1) {
     const Ray ray = primary_ray(A, px, py);
     const GaussianRecord* __restrict__ G = A.gauss;
     const float* __restrict__ ts = A.tsteps;
@@ -189,7 +216,7 @@ __device__ int march(const RenderArgs& A, uint32_t p, int px, int py, int* act_b
     float T = 1.0f;
     uint32_t prev = kNoRecord;  // this pixel's last record
     A.px_first[p] = kNoRecord;
-    ActList act{act_base, stride, 0, 0};
+    ActList act{act_base, act_stride < 0 ? stride : act_stride, 0, 0};
     auto walk = [&](auto prune, auto leaf) -> bool {
         if constexpr (W) {
             return traverse_wide<CAP>(A, ray, stack, stride, prune, leaf, NodeCount<S>{&c});
@@ -399,6 +426,33 @@ __global__ __launch_bounds__(BLOCK) void march_fallback_kernel(RenderArgs A) {
         tile_pixel(A, p >> 8, (int)(p & 255u), lx, ly, x, y);
         Ctr c{};
         int st = march<ACT, S, H>(A, p, x, y, s_act + tid, s_stack + tid, BLOCK, c);  // re-links px_first
+        if constexpr (S)
+            for (int i = 0; i < kNumCtr; ++i) atomicAdd(A.work + i, (unsigned long long)c.v[i]);
+        if (st == kOverflow) {  // more than ACT Gaussians active at one step: the deep pass
+            const uint32_t slot = atomicAdd(A.deepq, 1u);
+            if (slot < A.deepq_cap) A.deepq[1 + slot] = p;
+            else mark_error(A, p);
+        } else if (st != kOK) {
+            mark_error(A, p);
+        }
+    }
+}
+
+// Pixels whose active set outgrew the fallback's 64 LDS slots: the same march with the active list in
+// global memory (kActDeep slots per thread, [slot][thread] rows), a few waves for the whole frame.
+// Only an active set past kActDeep, Gaussians overlapping one point, fails (NaN, VR_ERR_OVERFLOW).
+template <bool S, bool H>
+__global__ __launch_bounds__(kDeepBlock) void march_deep_kernel(RenderArgs A) {
+    __shared__ int s_stack[kStackSize * kDeepBlock];
+    const int tid = threadIdx.x;
+    const uint32_t gt = blockIdx.x * kDeepBlock + tid, nthreads = gridDim.x * kDeepBlock;
+    const uint32_t n = min(A.deepq[0], A.deepq_cap);
+    for (uint32_t q = gt; q < n; q += nthreads) {
+        const uint32_t p = A.deepq[1 + q];
+        int lx, ly, x, y;
+        tile_pixel(A, p >> 8, (int)(p & 255u), lx, ly, x, y);
+        Ctr c{};
+        const int st = march<kActDeep, S, H>(A, p, x, y, A.deep_act + gt, s_stack + tid, kDeepBlock, c, (int)nthreads);
         if constexpr (S)
             for (int i = 0; i < kNumCtr; ++i) atomicAdd(A.work + i, (unsigned long long)c.v[i]);
         if (st != kOK) mark_error(A, p);
@@ -684,7 +738,7 @@ __device__ __forceinline__ void sec_leaf(const RenderArgs& A, SecRay& R, int32_t
         float lo = a;
         if (slot >= 0) {
             lo = 0.0f;
-            R.hitmask |= 1ull << slot;
+            R.hitmask |= slot_bit(slot);
         }
         sec_add<S, FAST, PURE>(A, R, g, q, lo, b, c);
     }
@@ -714,6 +768,30 @@ __device__ __forceinline__ void sec_finish(const RenderArgs& A, SecRay& R, Ctr& 
 #endif
     if (R.tau >= R.cut) {
         VR_TR_STORE(A, R.slot, 0.0f);
+        return;
+    }
+    if (R.act_n > 64) {  // (march_deep_kernel records) missed members: re-intersect the whole list
+        bool any = false;
+        for (uint32_t s = 0; s < R.act_n; ++s) {
+            const GRec g = load_rec(A.gauss, A.rec_act[R.act_off + s]);
+            const Quad q = FAST ? quad_fast(g, R.ray) : quad(g, R.ray);
+            float a, b;
+            if (FAST ? intersect_fast(q, a, b) : intersect(q, a, b)) continue;
+            any = true;
+            if constexpr (PURE) R.tau += marched_depth(A, g, R.ray, 0.0f, R.lim);
+            else if (!R.light) R.tau += FAST ? optical_depth_fast(g, q, 0.0f, R.lim) : optical_depth(g, q, 0.0f, R.lim);
+            else break;
+        }
+        if (!PURE && R.light && (R.needs_stop || any)) {
+            uint32_t slot = atomicAdd(A.slowq, 1u);
+            if (slot < A.slowq_cap) A.slowq[1 + slot] = R.slot;
+            else {
+                atomicAdd(A.counters, 1u);
+                A.tr[R.slot] = __builtin_nanf("");
+            }
+            return;
+        }
+        VR_TR_STORE(A, R.slot, expf(-R.tau));
         return;
     }
     const uint64_t all = R.act_n >= 64 ? ~0ull : ((1ull << R.act_n) - 1ull);
@@ -1294,7 +1372,7 @@ __global__ __launch_bounds__(BLOCK, WAVES) void secondary_ww_kernel(RenderArgs A
                         float lo = a;
                         if (slot >= 0) {
                             lo = 0.0f;
-                            R.hitmask |= 1ull << slot;
+                            R.hitmask |= slot_bit(slot);
                         }
                         sec_add<S, true, PURE>(A, R, g, q, lo, b, c);
                     }
@@ -1499,6 +1577,8 @@ static hipError_t march_pass(const RenderArgs& A, hipStream_t stream) {
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL((dev::march_fallback_kernel<kActFallback, kBlockFallback, S, H>), dim3(1024), dim3(kBlockFallback), 0,
                        stream, A);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    hipLaunchKernelGGL((dev::march_deep_kernel<S, H>), dim3(kDeepThreads / kDeepBlock), dim3(kDeepBlock), 0, stream, A);
     return hipGetLastError();
 }
 

@@ -86,6 +86,10 @@ constexpr int kMaxLights = 16;
 constexpr int kEnvOrderMax = 240;  // environment rays are direction-ordered up to this many samples (LDS bound)
 constexpr uint32_t kNoRecord = 0xffffffffu;
 constexpr int kActInline = 4;  // active-list slots stored with each scatter record
+// Ray-march pixels whose active set outgrows the 64-slot LDS fallback: a global-memory active list of
+// kActDeep slots per thread, kDeepThreads threads (march_deep_kernel), up to kDeepQueue such pixels per frame.
+constexpr int kActDeep = 2048, kDeepThreads = 256, kDeepBlock = 64;
+constexpr uint32_t kDeepQueue = 65536;
 
 // Record neighbour lists (secondary rays): every Gaussian j whose scaled Mahalanobis distance at
 // the record position satisfies q_j(pos) <= kListR2 (pos inside its 3.08-sigma ellipsoid). The
@@ -100,6 +104,8 @@ constexpr int kMaxSpheres = 64;
 constexpr uint32_t kFFNone = 0x7fffffffu;
 constexpr uint32_t kFFTailAfter = 0x80000000u;
 constexpr uint32_t kFFNeeMaxPerPath = 16;  // VR_OPT_FF_NEE_QUEUE bound (queue rays per path of a launch)
+constexpr int32_t kFFBigCap = 1024;          // ff_fallback_kernel: Gaussians overlapping one point it can sweep
+constexpr uint32_t kFFBigThreads = 1024;     // ff_fallback_kernel: threads (scratch row stride)
 
 // Kernel launch parameters (passed by value).
 struct RenderArgs {
@@ -133,6 +139,9 @@ struct RenderArgs {
     // fallback queue (active-set overflow) and error counters
     uint32_t* queue;       // [0] = count, [1..] = packed pixel ids (tile_local << 8 | lane)
     uint32_t queue_cap;
+    uint32_t* deepq;       // [0] = count, [1..] = pixels for march_deep_kernel (active set > 64)
+    uint32_t deepq_cap;
+    int32_t* deep_act;     // march_deep_kernel's active lists, [slot][thread]
     uint32_t* counters;    // [0] = error pixels
     unsigned long long* work;  // instrumented build only: [0..7] march-kernel counters, [8..15] secondary-kernel counters
 
@@ -180,6 +189,11 @@ struct RenderArgs {
     unsigned long long* ff_next;  // persistent path kernel: next unclaimed path of the launch
     unsigned long long ff_total;  // paths of the launch (tiles of the chunk x samples x 256)
     float* ff_sum;           // [tile-local pixel][3] running sum over sample batches
+    // Paths over the path kernel's hit-buffer capacity (more than ff_hit_cap Gaussians overlapping one
+    // point): queued and re-run whole by ff_fallback_kernel with kFFBigCap-entry rows (inline NEE).
+    uint32_t* ff_fbq;        // [0] count, [1..] path indices of the launch (nullptr: no fallback pass)
+    uint32_t ff_fbq_cap;
+    float4* ff_big;          // the fallback's scratch rows: hit, act0, act1, each [kFFBigCap][kFFBigThreads]
     // Deferred next-event estimation: the path kernel queues a bounce's shadow ray instead of tracing
     // it; ff_nee_kernel traces the queue and writes each contribution into its path's slot; the
     // accumulation adds a path's slots in bounce order (see vr_freeflight.hip).

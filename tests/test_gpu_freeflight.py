@@ -142,16 +142,35 @@ def test_empty_scene_free_flight_is_env():
     assert np.all(g[..., 0] == np.float32(s / np.float32(4)))
 
 
-def test_overlap_beyond_capacity_fails_loudly():
-    # 200 coincident Gaussians: more than the 128-entry per-path hit buffer overlap at one point, so
-    # the sweep cannot make progress; the render must fail (VR_ERR_OVERFLOW), not return garbage.
-    n = 200
+def _coincident_scene(n):
+    """n coincident Gaussians at (0, 1, 0) (sigma 0.2): all n overlap every point of the central rays."""
     mean = np.tile(np.float32([0.0, 1.0, 0.0]), (n, 1))
     cov6 = np.tile(np.float32([0.04, 0, 0, 0.04, 0, 0.04]), (n, 1))
-    scene = vr.Scene.from_gaussians(mean, cov6, np.full(n, 0.01, np.float32), np.full(n, 0.8, np.float32),
-                                    lights=[vr.Light((0.0, 4.0, 0.0), (30.0, 30.0, 30.0))])
+    dens = np.full(n, 0.01, np.float32)
+    alb = np.full(n, 0.8, np.float32)
+    light = ((0.0, 4.0, 0.0), (30.0, 30.0, 30.0))
+    dev = vr.Scene.from_gaussians(mean, cov6, dens, alb, lights=[vr.Light(*light)])
+    orc = O.OracleScene.from_gaussians(mean, cov6, dens, alb, [light[0]], [light[1]])
+    return dev, orc
+
+
+@pytest.mark.parametrize("multi", [False, True])
+def test_overlap_beyond_the_hit_buffer_matches_oracle(multi):
+    """200 coincident Gaussians: more than the path kernel's 128-entry rows overlap at one point. Those
+    paths re-run whole in ff_fallback_kernel (1024-entry rows, inline shadow rays); the reference's
+    event lists are unbounded (integrator.h:422-498), so the image must match the oracle."""
+    scene, orc = _coincident_scene(200)
+    g = _gpu(scene, 16, 16, multi, 4)
+    r = O.render_ff(orc, O.PINHOLE, CAM_POS, main_view_dir(), FOV, 16, 16, multi=multi, num_samples=4)
+    _check(g, r)
+
+
+def test_overlap_beyond_every_capacity_fails_loudly():
+    # more Gaussians overlapping one point than even the fallback's rows hold (kFFBigCap = 1024): the
+    # render must fail (VR_ERR_OVERFLOW), not return garbage
+    scene, _ = _coincident_scene(1100)
     with pytest.raises(vr.VRError):
-        _gpu(scene, 16, 16, True, 1)
+        _gpu(scene, 8, 8, True, 1)
 
 
 @pytest.mark.parametrize("cap0", ["1", "128"])

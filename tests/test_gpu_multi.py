@@ -59,15 +59,26 @@ def test_group_other_integrators(integ, kw):
     assert np.array_equal(got, ref)
 
 
-def test_group_overflow_fails_loudly():
-    n = 80
+def _nested(n, density):
     mean = np.tile(np.array([[0.0, 1.0, 0.0]], np.float32), (n, 1))
     sig = np.linspace(0.3, 0.4, n)
     cov = np.stack([sig ** 2, 0 * sig, 0 * sig, sig ** 2, 0 * sig, sig ** 2], 1).astype(np.float32)
-    scene = vr.Scene.from_gaussians(mean, cov, np.full(n, 1e-4, np.float32), np.full(n, 0.5, np.float32),
-                                    [vr.Light([0, 5, 0], [1, 1, 1])])
+    return vr.Scene.from_gaussians(mean, cov, np.full(n, density, np.float32), np.full(n, 0.5, np.float32),
+                                   [vr.Light([0, 5, 0], [1, 1, 1])])
+
+
+def test_group_deep_active_sets_equal_single_device():
+    # 80 nested Gaussians: the deep march pass (active sets > 64) on every rank of the group
+    scene = _nested(80, 1e-4)
+    a, _ = _render(vr.RayMarchingGaussians, scene, 16, 16, 0, env_samples=1)
+    b, st = _render(vr.RayMarchingGaussians, scene, 16, 16, (0, 0), env_samples=1)
+    assert np.array_equal(a, b) and st["error_pixels"] == 0
+
+
+def test_group_overflow_fails_loudly():
+    # more Gaussians overlapping one point than every capacity holds (kActDeep = 2048)
     with pytest.raises(vr.VRError) as e:
-        _render(vr.RayMarchingGaussians, scene, 16, 16, (0, 0), env_samples=1)
+        _render(vr.RayMarchingGaussians, _nested(2100, 1e-6), 4, 4, (0, 0), env_samples=1)
     assert e.value.status == 6
 
 

@@ -220,16 +220,42 @@ def test_dense_overlap_uses_fallback_path_and_still_matches():
     assert nm == 0 and err < TOL, err
 
 
-def test_overflow_beyond_every_capacity_fails_loudly():
-    n = 80
+def _nested_scene(n, density=1e-4):
+    """n concentric Gaussians (sigma 0.3 .. 0.4) around (0, 1, 0): all n are active at once on the
+    central rays."""
     mean = np.tile(np.array([[0.0, 1.0, 0.0]], np.float32), (n, 1))
     sig = np.linspace(0.3, 0.4, n)
     cov = np.stack([sig ** 2, 0 * sig, 0 * sig, sig ** 2, 0 * sig, sig ** 2], 1).astype(np.float32)
-    scene = vr.Scene.from_gaussians(mean, cov, np.full(n, 1e-4, np.float32), np.full(n, 0.5, np.float32),
-                                    [vr.Light([0, 5, 0], [1, 1, 1])])
+    dens = np.full(n, density, np.float32)
+    alb = np.full(n, 0.5, np.float32)
+    light = ([0.0, 5.0, 0.0], [1.0, 1.0, 1.0])
+    dev = vr.Scene.from_gaussians(mean, cov, dens, alb, [vr.Light(*light)])
+    orc = O.OracleScene.from_gaussians(mean, cov, dens, alb, [light[0]], [light[1]])
+    return dev, orc
+
+
+@pytest.mark.parametrize("n,env_samples", [(80, 1), (200, 3)])
+def test_active_sets_beyond_the_lds_capacities_match_the_oracle(n, env_samples):
+    """More Gaussians active at one step than the fallback kernel's 64 LDS slots: those pixels re-run on
+    march_deep_kernel (global-memory active lists, up to kActDeep), and their records' secondary rays
+    find missed members by re-intersecting the whole list (the 64-bit hit mask no longer covers it).
+    The reference's event lists are unbounded (gmm.h:457-515), so the frame must equal the oracle."""
+    scene, orc = _nested_scene(n)
+    img = vr.Image(16, 16)
+    integ = vr.RayMarchingGaussians(vr.Pinhole_Camera(CAM_POS, main_view_dir(), FOV), env_samples=env_samples)
+    integ.render(scene, img)
+    ref = O.render(orc, O.PINHOLE, CAM_POS, main_view_dir(), FOV, 16, 16, O.RAYMARCH_GAUSSIANS, 0.01, env_samples)
+    err, nm = _linf(img.pixels, ref)
+    assert integ.last_stats["fallback_pixels"] > 0 and integ.last_stats["error_pixels"] == 0
+    assert nm == 0 and err < TOL, err
+
+
+def test_overflow_beyond_every_capacity_fails_loudly():
+    # more Gaussians overlapping one point than even the deep pass holds (kActDeep = 2048)
+    scene, _ = _nested_scene(2100, 1e-6)
     with pytest.raises(vr.VRError) as e:
         vr.RayMarchingGaussians(vr.Pinhole_Camera(CAM_POS, main_view_dir(), FOV), env_samples=1).render(
-            scene, vr.Image(16, 16))
+            scene, vr.Image(4, 4))
     assert e.value.status == 6
 
 
