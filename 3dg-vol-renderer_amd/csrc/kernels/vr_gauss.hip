@@ -69,8 +69,18 @@ __device__ float light_transmittance(const RenderArgs& A, const Ray& sr, float d
     float tau = 0.0f;
     bool needs_stop = false;
     uint64_t hitmask = 0;
-    traverse<false>(
-        A, sr, stack, stride, [&](float tmin, float) { return tmin <= dist + kTPad * (1.0f + dist); },
+    // the 4-wide half-precision tree when the scene has one (half the dependent node fetches of the
+    // f32 pair tree; boxes only propose candidates, every decision is the exact quadratic), the pair
+    // tree when it has not or when a 4-wide walk could overflow its stack (`reset` undoes the partial walk)
+    auto walk = [&](auto prune, auto leaf, auto reset) {
+        if (A.hnodes4 != nullptr) {
+            if (traverse_wide<kStackSize>(A, sr, stack, stride, prune, leaf, NodeCount<S>{&c})) return;
+            reset();
+        }
+        traverse<false>(A, sr, stack, stride, prune, leaf, NodeCount<S>{&c});
+    };
+    walk(
+        [&](float tmin, float) { return tmin <= dist + kTPad * (1.0f + dist); },
         [&](uint32_t first, uint32_t count) {
             for (uint32_t j = first; j < first + count; ++j) {
                 if constexpr (S) c.v[kCtrPrims]++;
@@ -93,7 +103,11 @@ __device__ float light_transmittance(const RenderArgs& A, const Ray& sr, float d
             }
             return tau < kTauCut;
         },
-        NodeCount<S>{&c});
+        [&]() {
+            tau = 0.0f;
+            needs_stop = false;
+            hitmask = 0;
+        });
     uint64_t all = act.n >= 64 ? ~0ull : ((1ull << act.n) - 1ull);
     uint64_t missed = all & ~hitmask;  // pre-activated but not intersected (rounding at the surface)
     if (tau >= kTauCut) return 0.0f;   // exp(-tau) == 0 exactly; later terms are >= 0
@@ -115,8 +129,7 @@ __device__ float light_transmittance(const RenderArgs& A, const Ray& sr, float d
     }
     if (needs_stop || missed || deep_any) {
         float tstop = INFINITY;  // first event at or beyond the light
-        traverse<false>(
-            A, sr, stack, stride,
+        walk(
             [&](float tmin, float tmax) {
                 return tmax >= dist - kTPad * (1.0f + dist) && tmin <= tstop + kTPad * (1.0f + tstop);
             },
@@ -131,11 +144,11 @@ __device__ float light_transmittance(const RenderArgs& A, const Ray& sr, float d
                 }
                 return true;
             },
-            NodeCount<S>{&c});
+            [&]() { tstop = INFINITY; });
         if (tstop == INFINITY) tstop = dist;
         if (needs_stop) {
-            traverse<false>(
-                A, sr, stack, stride,
+            const float tau0 = tau;
+            walk(
                 [&](float tmin, float tmax) {
                     return tmin <= dist + kTPad * (1.0f + dist) && tmax >= dist - kTPad * (1.0f + dist);
                 },
@@ -154,7 +167,7 @@ __device__ float light_transmittance(const RenderArgs& A, const Ray& sr, float d
                     }
                     return tau < kTauCut;
                 },
-                NodeCount<S>{&c});
+                [&]() { tau = tau0; });
         }
         while (missed) {
             int s = __ffsll((unsigned long long)missed) - 1;
@@ -205,9 +218,16 @@ __device__ __forceinline__ float tail_weight(const RenderArgs& A, float x, float
 // capacity raise rec_alloc[2]; the host then grows the buffers and re-runs the march.
 // W: BVH window queries on the 4-wide half-precision tree (CAP-entry stack; a query that could
 // overflow it sends the pixel to the fallback kernel, which walks the pair tree).
-template <int ACT, bool S, bool H, bool W = false, int CAP = kStackSize>
+// COOP: the whole wave marches the same pixel (the fallback passes: a pixel whose active set
+// outgrew the fast kernel's slots marches serially for a long time). Every lane runs the same
+// queries and keeps its own identical copy of the active list; only the per-step evaluation of the
+// active list is split over the lanes (one Gaussian each), its sums and compaction then taken in
+// list order through lane broadcasts — the serial loop's operations in its order, so the result is
+// bit-identical — and lane 0 writes the records.
+template <int ACT, bool S, bool H, bool W = false, int CAP = kStackSize, bool COOP = false>
 __device__ int march(const RenderArgs& A, uint32_t p, int px, int py, int* act_base, int* stack, int stride, Ctr& c,
                      int act_stride = -1) {
+    const bool writer = !COOP || __lane_id() == 0u;  // COOP: lane 0 writes the pixel's records
     const Ray ray = primary_ray(A, px, py);
     const GaussianRecord* __restrict__ G = A.gauss;
     const float* __restrict__ ts = A.tsteps;
@@ -215,7 +235,7 @@ __device__ int march(const RenderArgs& A, uint32_t p, int px, int py, int* act_b
     const float step = A.step_size;
     float T = 1.0f;
     uint32_t prev = kNoRecord;  // this pixel's last record
-    A.px_first[p] = kNoRecord;
+    if (writer) A.px_first[p] = kNoRecord;
     ActList act{act_base, act_stride < 0 ? stride : act_stride, 0, 0};
     auto walk = [&](auto prune, auto leaf) -> bool {
         if constexpr (W) {
@@ -292,21 +312,55 @@ __device__ int march(const RenderArgs& A, uint32_t p, int px, int py, int* act_b
             const float t_k1 = t_k + step;  // `t + step_size` (test_integrators.h:286)
             float smu = 0.0f, smua = 0.0f, tau_seg = 0.0f;
             int w = 0;
-            for (int i = 0; i < act.n; ++i) {
-                int j = act.get(i);
-                GRec g = load_rec(G, j);
-                Quad q = quad(g, ray);
-                float a, b;
-                if (!intersect(q, a, b) || b <= t_k) continue;
-                act.set(w++, j);
-                float m = mu_t(g, px_, py_, pz_);
-                smu += m;
-                smua += m * g.albedo;
-                if (!A.pure) tau_seg += optical_depth(g, q, t_k, t_k1);
-                if constexpr (S) {
-                    c.v[kCtrMu]++;
-                    c.v[kCtrOD]++;
-                    c.v[kCtrPrims]++;
+            if constexpr (COOP) {
+                const int lane = (int)__lane_id();
+                for (int i0 = 0; i0 < act.n; i0 += 64) {  // (compaction writes stay below i0 + 64)
+                    const int i = i0 + lane;
+                    int j = 0;
+                    bool surv = false;
+                    float m = 0.0f, ma = 0.0f, od = 0.0f;
+                    if (i < act.n) {
+                        j = act.get(i);
+                        GRec g = load_rec(G, j);
+                        Quad q = quad(g, ray);
+                        float a, b;
+                        if (intersect(q, a, b) && b > t_k) {
+                            surv = true;
+                            m = mu_t(g, px_, py_, pz_);
+                            ma = m * g.albedo;
+                            if (!A.pure) od = optical_depth(g, q, t_k, t_k1);
+                        }
+                    }
+                    for (uint64_t sm = __ballot(surv); sm; sm &= sm - 1) {  // survivors in list order
+                        const int sl = __ffsll((unsigned long long)sm) - 1;
+                        act.set(w++, __shfl(j, sl, 64));
+                        smu += __shfl(m, sl, 64);
+                        smua += __shfl(ma, sl, 64);
+                        if (!A.pure) tau_seg += __shfl(od, sl, 64);
+                        if constexpr (S) {
+                            c.v[kCtrMu]++;
+                            c.v[kCtrOD]++;
+                            c.v[kCtrPrims]++;
+                        }
+                    }
+                }
+            } else {
+                for (int i = 0; i < act.n; ++i) {
+                    int j = act.get(i);
+                    GRec g = load_rec(G, j);
+                    Quad q = quad(g, ray);
+                    float a, b;
+                    if (!intersect(q, a, b) || b <= t_k) continue;
+                    act.set(w++, j);
+                    float m = mu_t(g, px_, py_, pz_);
+                    smu += m;
+                    smua += m * g.albedo;
+                    if (!A.pure) tau_seg += optical_depth(g, q, t_k, t_k1);
+                    if constexpr (S) {
+                        c.v[kCtrMu]++;
+                        c.v[kCtrOD]++;
+                        c.v[kCtrPrims]++;
+                    }
                 }
             }
             act.n = w;
@@ -318,35 +372,48 @@ __device__ int march(const RenderArgs& A, uint32_t p, int px, int py, int* act_b
                 sigma_s = a_mix * smu;
             }
             if (sigma_s > 0.0f) {  // scattering step -> one record
-                // lanes emitting now share one atomic (this branch is divergent: ballot = them)
-                const uint64_t m = __ballot(true);
-                const uint32_t leader = (uint32_t)__ffsll((unsigned long long)m) - 1u;
-                uint32_t base = 0;
-                if (__lane_id() == leader) base = atomicAdd(&A.rec_alloc[0], (uint32_t)__popcll(m));
-                base = (uint32_t)__builtin_amdgcn_readlane((int)base, (int)leader);
-                const uint32_t r = base + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+                uint32_t r, o = 0;
+                if constexpr (COOP) {  // one pixel per wave: lane 0 allocates
+                    uint32_t base = 0;
+                    if (writer) {
+                        base = atomicAdd(&A.rec_alloc[0], 1u);
+                        if (w > kActInline) o = atomicAdd(&A.rec_alloc[1], (uint32_t)w);
+                    }
+                    r = (uint32_t)__builtin_amdgcn_readfirstlane((int)base);
+                    o = (uint32_t)__builtin_amdgcn_readfirstlane((int)o);
+                } else {
+                    // lanes emitting now share one atomic (this branch is divergent: ballot = them)
+                    const uint64_t m = __ballot(true);
+                    const uint32_t leader = (uint32_t)__ffsll((unsigned long long)m) - 1u;
+                    uint32_t base = 0;
+                    if (__lane_id() == leader) base = atomicAdd(&A.rec_alloc[0], (uint32_t)__popcll(m));
+                    base = (uint32_t)__builtin_amdgcn_readlane((int)base, (int)leader);
+                    r = base + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+                    if (w > kActInline) o = atomicAdd(&A.rec_alloc[1], (uint32_t)w);  // rare: the overflow pool
+                }
                 uint32_t aoff = r * (uint32_t)kActInline;
                 bool fits = r < A.rec_cap;
-                if (w > kActInline) {  // rare: long active lists go to the overflow pool
-                    const uint32_t o = atomicAdd(&A.rec_alloc[1], (uint32_t)w);
+                if (w > kActInline) {  // long active lists go to the overflow pool
                     aoff = A.rec_cap * (uint32_t)kActInline + o;
                     fits = fits && o + (uint32_t)w <= A.act_ovf_cap;
                 }
                 if (fits) {
-                    A.rec_pos[r] = make_float4(px_, py_, pz_, T * sigma_s);
-                    A.rec_meta[r] = make_uint4((uint32_t)px | ((uint32_t)py << 16), (uint32_t)k, aoff, (uint32_t)w);
                     uint64_t bl = 0;
                     for (int i = 0; i < w; ++i) {
                         const int j = act.get(i);
-                        A.rec_act[aoff + i] = j;
+                        if (COOP ? (i & 63) == (int)__lane_id() : true) A.rec_act[aoff + i] = j;
                         bl |= 1ull << (j & 63);
                     }
-                    A.rec_bloom[r] = bl;
-                    A.rec_next[r] = kNoRecord;
-                    if (prev == kNoRecord) A.px_first[p] = r;
-                    else A.rec_next[prev] = r;
+                    if (writer) {
+                        A.rec_pos[r] = make_float4(px_, py_, pz_, T * sigma_s);
+                        A.rec_meta[r] = make_uint4((uint32_t)px | ((uint32_t)py << 16), (uint32_t)k, aoff, (uint32_t)w);
+                        A.rec_bloom[r] = bl;
+                        A.rec_next[r] = kNoRecord;
+                        if (prev == kNoRecord) A.px_first[p] = r;
+                        else A.rec_next[prev] = r;
+                    }
                     prev = r;
-                } else {
+                } else if (writer) {
                     A.rec_alloc[2] = 1u;  // capacity exceeded: the frame is reported and rendered again
                     if (r < A.rec_cap) {  // a slot inside [0, nrec) whose active list did not fit the pool:
                         // the later stages still read it (the host does not wait for the march), so
@@ -373,7 +440,7 @@ __device__ int march(const RenderArgs& A, uint32_t p, int px, int py, int* act_b
             if (A.t_eps > 0.0f && T * tail_weight(A, px_, py_, pz_, smu) <= A.t_eps) break;
         }
     }
-    A.px_T[p] = T;
+    if (writer) A.px_T[p] = T;
     if constexpr (S) c.v[kCtrPixels]++;
     return kOK;
 }
@@ -414,18 +481,23 @@ __global__ __launch_bounds__(BLOCK) void march_kernel(RenderArgs A) {
     }
 }
 
+// The fallback passes march one pixel per wave (march<COOP>): a pixel lands here because its active
+// set is large, and its serial march was the tail of the whole march stage (~1 ms at C4, also for a
+// 1/8 multi-GPU share). BLOCK = one wave.
 template <int ACT, int BLOCK, bool S, bool H>
 __global__ __launch_bounds__(BLOCK) void march_fallback_kernel(RenderArgs A) {
+    static_assert(BLOCK == 64, "one pixel per wave");
     __shared__ int s_act[ACT * BLOCK];
     __shared__ int s_stack[kStackSize * BLOCK];
     const int tid = threadIdx.x;
     const uint32_t n = min(A.queue[0], A.queue_cap);
-    for (uint32_t q = blockIdx.x * BLOCK + tid; q < n; q += gridDim.x * BLOCK) {
+    for (uint32_t q = blockIdx.x; q < n; q += gridDim.x) {
         const uint32_t p = A.queue[1 + q];
         int lx, ly, x, y;
         tile_pixel(A, p >> 8, (int)(p & 255u), lx, ly, x, y);
         Ctr c{};
-        int st = march<ACT, S, H>(A, p, x, y, s_act + tid, s_stack + tid, BLOCK, c);  // re-links px_first
+        int st = march<ACT, S, H, false, kStackSize, true>(A, p, x, y, s_act + tid, s_stack + tid, BLOCK, c);  // re-links px_first
+        if (tid != 0) continue;
         if constexpr (S)
             for (int i = 0; i < kNumCtr; ++i) atomicAdd(A.work + i, (unsigned long long)c.v[i]);
         if (st == kOverflow) {  // more than ACT Gaussians active at one step: the deep pass
@@ -439,20 +511,23 @@ __global__ __launch_bounds__(BLOCK) void march_fallback_kernel(RenderArgs A) {
 }
 
 // Pixels whose active set outgrew the fallback's 64 LDS slots: the same march with the active list in
-// global memory (kActDeep slots per thread, [slot][thread] rows), a few waves for the whole frame.
+// global memory (kActDeep slots per lane, [slot][thread] rows, one pixel per wave).
 // Only an active set past kActDeep, Gaussians overlapping one point, fails (NaN, VR_ERR_OVERFLOW).
 template <bool S, bool H>
 __global__ __launch_bounds__(kDeepBlock) void march_deep_kernel(RenderArgs A) {
+    static_assert(kDeepBlock == 64, "one pixel per wave");
     __shared__ int s_stack[kStackSize * kDeepBlock];
     const int tid = threadIdx.x;
     const uint32_t gt = blockIdx.x * kDeepBlock + tid, nthreads = gridDim.x * kDeepBlock;
     const uint32_t n = min(A.deepq[0], A.deepq_cap);
-    for (uint32_t q = gt; q < n; q += nthreads) {
+    for (uint32_t q = blockIdx.x; q < n; q += gridDim.x) {
         const uint32_t p = A.deepq[1 + q];
         int lx, ly, x, y;
         tile_pixel(A, p >> 8, (int)(p & 255u), lx, ly, x, y);
         Ctr c{};
-        const int st = march<kActDeep, S, H>(A, p, x, y, A.deep_act + gt, s_stack + tid, kDeepBlock, c, (int)nthreads);
+        const int st =
+            march<kActDeep, S, H, false, kStackSize, true>(A, p, x, y, A.deep_act + gt, s_stack + tid, kDeepBlock, c, (int)nthreads);
+        if (tid != 0) continue;
         if constexpr (S)
             for (int i = 0; i < kNumCtr; ++i) atomicAdd(A.work + i, (unsigned long long)c.v[i]);
         if (st != kOK) mark_error(A, p);
@@ -1592,8 +1667,14 @@ hipError_t gauss_march(const RenderArgs& A, hipStream_t stream, bool stats) {
 // 8-entry LDS ring of the 9-entry leaf queue = 26 (6 blocks of 256 lanes per CU).
 template <bool S, bool PURE, bool H, bool W>
 static hipError_t ww_launch(const RenderArgs& A, hipStream_t stream) {
-    constexpr int kStack = 18, kQueue = 9;
-    constexpr int kWaves = PURE ? 5 : 6;  // PureRayMarching's marched depth does not fit 80 VGPRs without spills
+#ifndef VR_WW_STACK
+#define VR_WW_STACK 18  // LDS traversal-stack entries per lane (deeper ones spill to the global overflow)
+#endif
+#ifndef VR_WW_WAVES
+#define VR_WW_WAVES 6  // waves per SIMD (launch bounds: 80 VGPRs at 6)
+#endif
+    constexpr int kStack = VR_WW_STACK, kQueue = 9;
+    constexpr int kWaves = PURE ? 5 : VR_WW_WAVES;  // PureRayMarching's marched depth does not fit 80 VGPRs without spills
     const void* fn = (const void*)dev::secondary_ww_kernel<kBlockSecondary, kStack, S, PURE, kWaves, kQueue, H, W>;
     int dv = 0, cus = 0, per_cu = 0;
     if (hipGetDevice(&dv) != hipSuccess) return hipErrorUnknown;

@@ -199,6 +199,18 @@ def test_dense_reference_scenes_stay_within_the_hit_capacity(name):
     _check(g, r)
 
 
+def test_reference_driver_default_render_matches_oracle():
+    """The reference driver's own forward workload (tests/main.cpp:17-45): MultiScatterGaussians on
+    2g_altered.txt at 512x512, here at 64 paths per pixel (the driver uses 256; bench.py --config main
+    times that), full frame. Every path follows the oracle's (same PCG32 stream per pixel and sample)."""
+    path = scene_path("2g_altered.txt")
+    W = H = 512
+    g = _gpu(vr.Scene.load_GMM(path), W, H, True, 64)
+    r = O.render_ff(O.OracleScene.load_gmm(path), O.PINHOLE, CAM_POS, main_view_dir(), FOV, W, H, multi=True,
+                    num_samples=64)
+    _check(g, r)
+
+
 @pytest.mark.parametrize("multi", [False, True])
 def test_deferred_shadow_rays_equal_inline(multi, device_options):
     """VR_OPT_FF_NEE_QUEUE: the path kernel queues each bounce's shadow ray for ff_nee_kernel (the same

@@ -24,6 +24,7 @@ ap.add_argument("--size", type=int, default=4096)
 ap.add_argument("--frames", type=int, default=3)
 ap.add_argument("--counts", type=int, default=1)
 ap.add_argument("--config", default="c4")
+ap.add_argument("--opt", action="append", default=[], help="name=value device option (vr_set_option)")
 args = ap.parse_args()
 
 scene, W, H = bench.build_scene(args.config, 2025)
@@ -31,6 +32,9 @@ W = H = args.size
 cam = vr.Pinhole_Camera(bench.CAM_POS, bench.CAM_VIEW, bench.FOV)
 integ = vr.RayMarchingGaussians(cam, step_size=0.01, env_samples=20, t_eps=1e-6)
 dev = vr.Device.get(0)
+for o in args.opt:
+    k, v = o.split("=")
+    dev.set_option(k, int(v))
 dev.upload(scene)
 frame = torch.empty((H, W, 3), dtype=torch.float32, device="cuda")
 sp = torch.cuda.current_stream().cuda_stream
@@ -39,7 +43,7 @@ for i in range(args.frames + 1):
     tiles.render_local(dev, cam, integ.params, W, H, 0, 1, None, frame, sp)
     if i:
         stats.append(dev.stats())
-out = {"lib": os.environ.get("VR_LIB_PATH", "product"),
+out = {"lib": os.environ.get("VR_LIB_PATH", "product"), "opt": args.opt,
        "kernel_ms": float(np.mean([s["kernel_ms"] for s in stats])),
        "stage_ms": {k: round(float(np.mean([s["stage_ms"][k] for s in stats])), 3) for k in vr.Device.STAGES},
        "mean": float(frame.mean())}
