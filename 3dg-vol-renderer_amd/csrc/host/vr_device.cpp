@@ -13,6 +13,7 @@
 #include <mutex>
 
 #include "vr_common.h"
+#include "../vr_lbvh.h"
 
 namespace vr {
 hipError_t launch_render(const RenderArgs& A, hipStream_t stream, int volume_type, int integrator);
@@ -26,17 +27,7 @@ hipError_t launch_sfd_loss_diff(const uint32_t* bits0, const uint32_t* bits1, co
                                 uint32_t n, double* out, hipStream_t stream);
 hipError_t gauss_record_cut(const RenderArgs& A, float budget, hipStream_t stream);
 hipError_t launch_pixel_losses(const float* img, const float* ref, uint32_t npix, float* out, hipStream_t stream);
-struct LbvhResult {
-    GaussianRecord* gauss = nullptr;
-    uint32_t* order = nullptr;
-    BVHNode* nodes = nullptr;
-    HNode* hnodes = nullptr;
-    HNode4* hnodes4 = nullptr;
-    size_t num_nodes = 0, num_nodes4 = 0;
-    int max_depth = 0;
-};
-hipError_t lbvh_build(const GaussianRecord* d_rec, const float* d_boxes, uint32_t n, const float cmin[3], const float cmax[3],
-                      bool half, const float hc[3], float hs, hipStream_t s, LbvhResult& R);
+
 hipError_t launch_unshuffle(const float* slabs, uint32_t nslabs, uint32_t tiles_per_slab, uint32_t tiles_x, uint32_t W,
                             uint32_t H, float* img, hipStream_t stream);
 }  // namespace vr
@@ -75,7 +66,8 @@ struct vr_ctx {
     uint32_t* d_counters = nullptr;  // [0] error pixels / paths of the frame
     // Pinned report of the last frame, copied on the render stream after its last kernel:
     // [0] fallback-queue length, [1] error pixels, [2] scatter records, [3] overflow-pool entries,
-    // [4] record capacity exceeded (the frame is invalid and must be rendered again)
+    // [4] record capacity exceeded (the frame is invalid and must be rendered again), [5] records
+    // without a neighbour list, [6] deep-pass pixels
     uint32_t* h_report = nullptr;
     bool report_gauss = false;  // the last frame ran the RayMarchingGaussians pipeline (fields [2..4])
     float* d_frame = nullptr;
@@ -781,9 +773,13 @@ vr_status launch(vr_ctx* c, RenderArgs& A, const vr_render_params* p, hipStream_
     HIP_TRY(hipEventRecord(c->ev_stop, s), "hipEventRecord");
     HIP_TRY(hipMemcpyAsync(&c->h_report[0], c->d_queue, sizeof(uint32_t), hipMemcpyDeviceToHost, s), "hipMemcpyAsync(report)");
     HIP_TRY(hipMemcpyAsync(&c->h_report[1], c->d_counters, sizeof(uint32_t), hipMemcpyDeviceToHost, s), "hipMemcpyAsync(report)");
-    if (c->report_gauss)
+    if (c->report_gauss) {
         HIP_TRY(hipMemcpyAsync(&c->h_report[2], A.rec_alloc, 3 * sizeof(uint32_t), hipMemcpyDeviceToHost, s),
                 "hipMemcpyAsync(report)");
+        HIP_TRY(hipMemcpyAsync(&c->h_report[5], c->d_counters + 2, sizeof(uint32_t), hipMemcpyDeviceToHost, s),
+                "hipMemcpyAsync(report)");
+        HIP_TRY(hipMemcpyAsync(&c->h_report[6], A.deepq, sizeof(uint32_t), hipMemcpyDeviceToHost, s), "hipMemcpyAsync(report)");
+    }
     HIP_TRY(hipEventRecord(c->ev_report, s), "hipEventRecord");
     c->stats_pending = true;
     c->last_pixels = (int64_t)A.num_tiles * 256;
@@ -1421,6 +1417,8 @@ vr_status vr_get_stats(vr_ctx* c, vr_render_stats* o) {
     o->scatter_records = c->report_gauss ? (int64_t)c->h_report[2] : 0;
     o->secondary_rays = o->scatter_records * (int64_t)c->last_secondary_per_record;
     o->record_overflow = frame_exceeded(c) ? 1 : 0;
+    o->unlisted_records = c->report_gauss ? (int64_t)c->h_report[5] : 0;
+    o->deep_pixels = c->report_gauss ? (int64_t)std::min(c->h_report[6], kDeepQueue) : 0;
     return VR_OK;
 }
 

@@ -1,4 +1,5 @@
-// Multi-GPU context (vr_init_multi): one host thread drives every GPU of the node.
+// Multi-GPU context (vr_init_multi): the GPUs of one node, each rank's launches issued from a host
+// thread of its own.
 //
 // The reference parallelises its pixel loop over CPU threads (test_integrators.h:164,
 // integrator.h:547); pixels are independent, so the frame is the data-parallel axis here too
@@ -316,6 +317,8 @@ vr_status group_stats(vr_group* g, vr_render_stats* o) {
         o->scatter_records += s.scatter_records;
         o->secondary_rays += s.secondary_rays;
         o->record_overflow |= s.record_overflow;
+        o->unlisted_records += s.unlisted_records;
+        o->deep_pixels += s.deep_pixels;
     }
     return VR_OK;
 }

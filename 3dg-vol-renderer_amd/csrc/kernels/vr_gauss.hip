@@ -700,6 +700,9 @@ __device__ __forceinline__ uint32_t rays_per_chunk(const RenderArgs& A) {
 // Start ray `rem` of record chunk `chunk`. Returns false if the ray is already complete (Tr
 // written) or a padding id. norm: slab-test terms in the half nodes' scene-normalised
 // coordinates (HNode).
+#ifndef VR_SEC_FAST_INIT
+#define VR_SEC_FAST_INIT 0
+#endif
 __device__ __forceinline__ bool sec_init(const RenderArgs& A, uint32_t nrec, uint32_t chunk, uint32_t rem, SecRay& R,
                                          bool norm = false) {
     uint32_t s, r;
@@ -720,9 +723,18 @@ __device__ __forceinline__ bool sec_init(const RenderArgs& A, uint32_t nrec, uin
     if (s < (uint32_t)A.num_lights) {
         const LightRecord& lr = A.lights[s];
         float dx = lr.px - pos.x, dy = lr.py - pos.y, dz = lr.pz - pos.z;
+#if VR_SEC_FAST_INIT
+        // a secondary ray feeds only its Tr (continuous): one hardware-rsqrt normalisation instead of
+        // the reference's two correctly rounded ones (direction within ~1 ulp)
+        const float d2 = dot3(dx, dy, dz, dx, dy, dz);
+        const float dist = sqrtf(d2);
+        const float inv = __builtin_amdgcn_rsqf(d2);
+        R.ray = Ray{pos.x, pos.y, pos.z, dx * inv, dy * inv, dz * inv};
+#else
         float dist = sqrtf(dot3(dx, dy, dz, dx, dy, dz));
         normalize3(dx, dy, dz);
         R.ray = make_ray(pos.x, pos.y, pos.z, dx, dy, dz);
+#endif
         R.light = true;
         R.lim = dist;
         if (!(dist > 0.0f)) {  // `while (t_prev < dist)` never runs
@@ -732,16 +744,26 @@ __device__ __forceinline__ bool sec_init(const RenderArgs& A, uint32_t nrec, uin
     } else {
         float wx, wy, wz;
         env_sample_dir(A, meta, s - (uint32_t)A.num_lights, wx, wy, wz);
+#if VR_SEC_FAST_INIT
+        R.ray = Ray{pos.x, pos.y, pos.z, wx, wy, wz};  // env_dir's direction is unit up to rounding
+#else
         R.ray = make_ray(pos.x, pos.y, pos.z, wx, wy, wz);
+#endif
         R.light = false;
         R.lim = 0.0f;  // last event so far
     }
     // |d| clamped away from 0: the fma slab form b/d - o/d must never see inf - inf
     const float sc = norm ? A.hn_scale : 1.0f;
     const float dx = R.ray.dx * sc, dy = R.ray.dy * sc, dz = R.ray.dz * sc;
+#if VR_SEC_FAST_INIT  // slab tests only propose candidates (boxes bound 3.15 sigma, the test is at 3)
+    R.ix = __builtin_amdgcn_rcpf(fabsf(dx) > 1e-30f ? dx : copysignf(1e-30f, dx));
+    R.iy = __builtin_amdgcn_rcpf(fabsf(dy) > 1e-30f ? dy : copysignf(1e-30f, dy));
+    R.iz = __builtin_amdgcn_rcpf(fabsf(dz) > 1e-30f ? dz : copysignf(1e-30f, dz));
+#else
     R.ix = __frcp_rn(fabsf(dx) > 1e-30f ? dx : copysignf(1e-30f, dx));
     R.iy = __frcp_rn(fabsf(dy) > 1e-30f ? dy : copysignf(1e-30f, dy));
     R.iz = __frcp_rn(fabsf(dz) > 1e-30f ? dz : copysignf(1e-30f, dz));
+#endif
     if (norm) {
         R.oxi = (R.ray.ox - A.hn_center[0]) * sc * R.ix;
         R.oyi = (R.ray.oy - A.hn_center[1]) * sc * R.iy;
@@ -1266,6 +1288,7 @@ __global__ __launch_bounds__(BLOCK) void record_list_kernel(RenderArgs A) {
             }
         }
         A.rec_nlist[r] = ovf ? 0xffffffffu : (nc | (nb << 16));
+        if (ovf) atomicAdd(A.counters + 2, 1u);  // vr_render_stats.unlisted_records
     }
 }
 

@@ -22,6 +22,7 @@
 #include <cstdio>
 
 #include "../vr_internal.h"
+#include "../vr_lbvh.h"
 
 namespace vr {
 namespace lbvh {
@@ -269,19 +270,7 @@ __global__ void gather_records_kernel(const GaussianRecord* __restrict__ src, co
 
 }  // namespace lbvh
 
-// Result of a device build (all device pointers owned by the caller afterwards).
-struct LbvhResult {
-    GaussianRecord* gauss = nullptr;  // records in leaf order
-    uint32_t* order = nullptr;        // leaf-order index -> scene index
-    BVHNode* nodes = nullptr;         // N - 1 child-pair nodes (root 0)
-    HNode* hnodes = nullptr;          // same tree at half precision (if requested)
-    HNode4* hnodes4 = nullptr;        // 4-wide tree (if requested)
-    size_t num_nodes = 0, num_nodes4 = 0;
-    int max_depth = 0;                // as BVHBuild::max_depth: root = 1, a leaf child counts as a level
-};
-
-// d_rec: records in scene order, d_boxes: 6 floats per primitive (both device, n >= 2 primitives).
-// cmin/cmax: centroid bounds; half: build the half-precision trees with normalisation (hc, hs).
+// lbvh_build (vr_lbvh.h): all device pointers of the result are owned by the caller afterwards.
 hipError_t lbvh_build(const GaussianRecord* d_rec, const float* d_boxes, uint32_t n, const float cmin[3],
                       const float cmax[3], bool half, const float hc[3], float hs, hipStream_t s, LbvhResult& R) {
     using namespace lbvh;

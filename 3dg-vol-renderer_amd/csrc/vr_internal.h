@@ -54,7 +54,7 @@ struct HNode4 {
 static_assert(sizeof(HNode4) == 64, "4-wide half node must be 64 B");
 
 #ifndef VR_LEAF_MAX
-#define VR_LEAF_MAX 3
+#define VR_LEAF_MAX 2  // A/B (round 3, every line): 2 beats 3 by 0.8-2.8 % (C4 +1.7 %), 1 and 4 lose
 #endif
 constexpr int kLeafMax = VR_LEAF_MAX;  // primitives per leaf (<= 16: leaf refs hold count - 1 in 4 bits)
 constexpr int kMaxDepth = 30;        // builder guarantees node depth <= kMaxDepth

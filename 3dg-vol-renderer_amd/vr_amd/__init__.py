@@ -359,7 +359,8 @@ class Device:
         return {"kernel_ms": s.kernel_ms, "pixels": s.pixels, "fallback_pixels": s.fallback_pixels,
                 "error_pixels": s.error_pixels, "stage_ms": dict(zip(self.STAGES, list(s.stage_ms))),
                 "scatter_records": s.scatter_records, "secondary_rays": s.secondary_rays,
-                "record_overflow": bool(s.record_overflow)}
+                "record_overflow": bool(s.record_overflow), "unlisted_records": s.unlisted_records,
+                "deep_pixels": s.deep_pixels}
 
     def fallback_pixels(self):
         """(n, 2) int array of the (x, y) pixels of the last ray-march frame that were re-run on the

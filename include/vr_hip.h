@@ -129,6 +129,10 @@ typedef struct vr_render_stats {
     int64_t record_overflow;  /* 1: the frame outgrew the scatter-record buffers sized from earlier
                                  frames (its output is invalid; the buffers have been grown, render
                                  again). vr_render does that itself. */
+    int64_t unlisted_records; /* scatter records whose neighbour-list query overflowed (more than 48
+                                 members, or its 16-entry stack): their secondary rays walk the whole
+                                 tree (exact, slower) */
+    int64_t deep_pixels;      /* pixels re-run on the global-memory active-list pass (> 64 active) */
 } vr_render_stats;
 
 typedef struct vr_scene vr_scene; /* host-side scene: primitives, lights, env colour */

@@ -1,0 +1,12 @@
+#!/bin/bash
+# Headline + free-flight lines for the product library and every build under _ab/ (timing only):
+#   tools/ab_lines.sh -> gpurun_out/ablines/<variant>_<line>.json
+cd $GRAFT_REPO_ROOT; O=gpurun_out/ablines; mkdir -p $O
+for v in base $(ls _ab 2>/dev/null); do
+  if [ $v = base ]; then unset VR_LIB_PATH; else export VR_LIB_PATH=$PWD/_ab/$v/libvr_hip.so; fi
+  for line in "c4 raymarch 3" "c2 multiscatter 5" "c5 multiscatter 5" "c3 freeflight 5"; do
+    set -- $line
+    timeout -k 10 240 python3 bench.py --config $1 --integrator $2 --steps $3 --warmup 1 --cpu-budget 0 --flops 0 > $O/${v}_$1.json 2> $O/${v}_$1.log || { echo "$v $1 failed"; tail -3 $O/${v}_$1.log; exit 1; }
+    python3 -c "import json;d=json.load(open('$O/${v}_$1.json'));print('$v','$1',round(d['value'],2),d['unit'],round(d['ms_per_step'],2),'ms')"
+  done
+done
