@@ -18,7 +18,6 @@
 namespace vr {
 hipError_t launch_render(const RenderArgs& A, hipStream_t stream, int volume_type, int integrator);
 hipError_t gauss_march(const RenderArgs& A, hipStream_t stream, bool stats);
-hipError_t gauss_lists(const RenderArgs& A, hipStream_t stream);
 hipError_t gauss_secondary(const RenderArgs& A, hipStream_t stream, bool stats);
 hipError_t gauss_accumulate(const RenderArgs& A, hipStream_t stream);
 hipError_t launch_free_flight(const RenderArgs& A, uint32_t chunk_tiles, hipStream_t stream, hipEvent_t* ev);
@@ -66,16 +65,16 @@ struct vr_ctx {
     uint32_t* d_counters = nullptr;  // [0] error pixels / paths of the frame
     // Pinned report of the last frame, copied on the render stream after its last kernel:
     // [0] fallback-queue length, [1] error pixels, [2] scatter records, [3] overflow-pool entries,
-    // [4] record capacity exceeded (the frame is invalid and must be rendered again), [5] records
-    // without a neighbour list, [6] deep-pass pixels
+    // [4] record capacity exceeded (the frame is invalid and must be rendered again), [5] deep-pass
+    // pixels
     uint32_t* h_report = nullptr;
     bool report_gauss = false;  // the last frame ran the RayMarchingGaussians pipeline (fields [2..4])
     float* d_frame = nullptr;
     size_t frame_cap = 0;
     hipEvent_t ev_start = nullptr, ev_stop = nullptr;
     hipEvent_t ev_report = nullptr;  // after the frame report's copies (collect() waits for it)
-    hipEvent_t ev_stage[4] = {nullptr, nullptr, nullptr, nullptr};  // stage boundaries of gauss_pipeline
-    bool staged = false;                                            // last launch recorded ev_stage
+    hipEvent_t ev_stage[3] = {nullptr, nullptr, nullptr};  // stage boundaries of gauss_pipeline
+    bool staged = false;                                   // last launch recorded ev_stage
     // free-flight frames: per launch, events before the path kernel, after it, after the shadow-ray
     // kernel and after the accumulation (stage_ms of vr_get_stats sums them over the frame's launches)
     std::vector<hipEvent_t> ff_ev;
@@ -90,7 +89,7 @@ struct vr_ctx {
         size_t bytes = 0;
     };
     Buf px_first, px_T, rec_pos, rec_meta, rec_next, rec_act, tr, rec_rad, rec_alloc, rec_bloom, slowq;
-    Buf pcg_jump, ray_next, rec_list, rec_nlist, stack_ovf, env_order, rec_cut;
+    Buf pcg_jump, ray_next, stack_ovf, env_order, rec_cut;
     Buf deep;  // march_deep_kernel: pixel queue + global active lists (vr_gauss.hip)
     Buf ff_scratch, ff_tail, ff_sum, ff_nee;  // free-flight integrators (vr_freeflight.hip)
     Buf ff_fb;                                // ff_fallback_kernel: path queue + kFFBigCap rows
@@ -99,7 +98,6 @@ struct vr_ctx {
     uint32_t rec_npix[2] = {0, 0}, rec_n[2] = {0, 0};
     Buf sfd_tmp;                      // vr_sfd_loss_diff: losses + output
     Buf sfd_ref, sfd_loss[2], sfd_out;  // device inverse loop (vr_sfd_optimize): I_ref, base / perturbed losses
-    bool list_ok = false;  // all covariances positive definite: neighbour lists are exact
     int pcg_jump_n = -1;
     uint32_t* h_sizing = nullptr;  // pinned copy of rec_alloc for the sizing march of a context's first frame
     uint64_t rec_hint = 0, ovf_hint = 0;  // record / overflow-pool capacities (0: not known yet)
@@ -288,20 +286,6 @@ vr_status upload_half_nodes(vr_ctx* c, const std::vector<BVHNode>& nodes) {
     return VR_OK;
 }
 
-// Neighbour lists rely on the 3.15-sigma boxes bounding {q <= kListR2}: true for positive definite
-// covariances with a finite inverse.
-bool lists_exact(const HostScene& s) {
-    for (const GaussianPre& p : s.pre) {
-        const double a = p.cov[0], b2 = p.cov[1], c2 = p.cov[2], d = p.cov[3], e = p.cov[4], f = p.cov[5];
-        const double m2 = a * d - b2 * b2;
-        const double det = a * (d * f - e * e) - b2 * (b2 * f - e * c2) + c2 * (b2 * e - d * c2);
-        bool ok = a > 0.0 && m2 > 0.0 && det > 0.0;
-        for (int k = 0; k < 6; ++k) ok = ok && std::isfinite(p.inv_cov[k]);
-        if (!ok) return false;
-    }
-    return true;
-}
-
 // Scenes at least this large may use the device builder (VR_OPT_DEVICE_BVH); smaller ones build on
 // the host in well under a millisecond.
 constexpr size_t kDeviceBvhMin = 256;
@@ -360,7 +344,6 @@ vr_status upload_device_bvh(vr_ctx* c, const HostScene& s, const std::vector<flo
     c->num_nodes = R.num_nodes;
     c->bvh_depth = R.max_depth;
     c->num_prims = (int32_t)N;
-    c->list_ok = lists_exact(s);
     c->last_upload_device_bvh = true;
     return VR_OK;
 }
@@ -513,7 +496,7 @@ vr_status grow(vr_ctx::Buf& b, size_t bytes, const char* what) {
     return VR_OK;
 }
 
-// RayMarchingGaussians: march (records) -> neighbour lists -> secondary rays -> accumulate.
+// RayMarchingGaussians: march (records) -> sizing / cut-offs -> secondary rays -> accumulate.
 vr_status gauss_pipeline(vr_ctx* c, RenderArgs& A, hipStream_t s, bool stats) {
     const uint32_t npix = A.num_tiles * 256u;
     vr_status st;
@@ -620,25 +603,7 @@ vr_status gauss_pipeline(vr_ctx* c, RenderArgs& A, hipStream_t s, bool stats) {
             HIP_TRY(gauss_record_cut(A, A.t_eps, s), "record cut-offs");
         }
     }
-    A.list_ok = c->list_ok && cap * kListCap < 0xffffffffull;
-    {  // list radius; beyond the 3.15-sigma BVH boxes the query box grows by the excess radius of the
-       // widest Gaussian on each axis (conservative: every member's box meets the query box)
-        A.list_r2 = kListR2;
-        const double excess = std::max(0.0, std::sqrt((double)kListR2) - 3.0 * 1.05);
-        for (int k = 0; k < 3; ++k) {
-            const double h = excess * c->sig_max[k];
-            A.list_h[k] = h > 0.0 ? (float)(h * (A.hnodes != nullptr ? c->hn_scale : 1.0f) * 1.001 + 1e-6) : 0.0f;
-        }
-    }
-    if (A.list_ok) {
-        if ((st = grow(c->rec_list, cap * kListCap * 4ull, "hipMalloc(record lists)")) != VR_OK) return st;
-        if ((st = grow(c->rec_nlist, cap * 4ull, "hipMalloc(record lists)")) != VR_OK) return st;
-        A.rec_list = (int32_t*)c->rec_list.p;
-        A.rec_nlist = (uint32_t*)c->rec_nlist.p;
-    }
     HIP_TRY(hipEventRecord(c->ev_stage[1], s), "hipEventRecord");
-    HIP_TRY(gauss_lists(A, s), "neighbour lists");
-    HIP_TRY(hipEventRecord(c->ev_stage[2], s), "hipEventRecord");
     {  // environment rays traced in direction order within chunks of 32 records (see ray_slot; larger
        // chunks measured 2-20 % slower: record locality is lost)
 #ifndef VR_CHUNK_SHIFT
@@ -656,7 +621,7 @@ vr_status gauss_pipeline(vr_ctx* c, RenderArgs& A, hipStream_t s, bool stats) {
         }
     }
     HIP_TRY(gauss_secondary(A, s, stats), "secondary rays");
-    HIP_TRY(hipEventRecord(c->ev_stage[3], s), "hipEventRecord");
+    HIP_TRY(hipEventRecord(c->ev_stage[2], s), "hipEventRecord");
     HIP_TRY(gauss_accumulate(A, s), "accumulate");
     c->staged = true;
     c->report_gauss = true;
@@ -776,9 +741,7 @@ vr_status launch(vr_ctx* c, RenderArgs& A, const vr_render_params* p, hipStream_
     if (c->report_gauss) {
         HIP_TRY(hipMemcpyAsync(&c->h_report[2], A.rec_alloc, 3 * sizeof(uint32_t), hipMemcpyDeviceToHost, s),
                 "hipMemcpyAsync(report)");
-        HIP_TRY(hipMemcpyAsync(&c->h_report[5], c->d_counters + 2, sizeof(uint32_t), hipMemcpyDeviceToHost, s),
-                "hipMemcpyAsync(report)");
-        HIP_TRY(hipMemcpyAsync(&c->h_report[6], A.deepq, sizeof(uint32_t), hipMemcpyDeviceToHost, s), "hipMemcpyAsync(report)");
+        HIP_TRY(hipMemcpyAsync(&c->h_report[5], A.deepq, sizeof(uint32_t), hipMemcpyDeviceToHost, s), "hipMemcpyAsync(report)");
     }
     HIP_TRY(hipEventRecord(c->ev_report, s), "hipEventRecord");
     c->stats_pending = true;
@@ -827,7 +790,7 @@ vr_status vr_init(int device, vr_ctx** out) {
         hipEventCreate(&c->ev_start) != hipSuccess || hipEventCreate(&c->ev_stop) != hipSuccess ||
         hipEventCreate(&c->ev_report) != hipSuccess ||
         hipEventCreate(&c->ev_stage[0]) != hipSuccess || hipEventCreate(&c->ev_stage[1]) != hipSuccess ||
-        hipEventCreate(&c->ev_stage[2]) != hipSuccess || hipEventCreate(&c->ev_stage[3]) != hipSuccess) {
+        hipEventCreate(&c->ev_stage[2]) != hipSuccess) {
         vr_destroy(c);
         return fail(VR_ERR_HIP, "vr_init: failed to create stream/workspace");
     }
@@ -890,7 +853,7 @@ void vr_destroy(vr_ctx* c) {
     if (c->h_report) (void)hipHostFree(c->h_report);
     if (c->h_sizing) (void)hipHostFree(c->h_sizing);
     for (vr_ctx::Buf* b : {&c->px_first, &c->px_T, &c->rec_pos, &c->rec_meta, &c->rec_next, &c->rec_act, &c->tr, &c->rec_rad,
-                           &c->rec_alloc, &c->rec_bloom, &c->slowq, &c->pcg_jump, &c->ray_next, &c->rec_list, &c->rec_nlist,
+                           &c->rec_alloc, &c->rec_bloom, &c->slowq, &c->pcg_jump, &c->ray_next,
                            &c->stack_ovf, &c->env_order, &c->rec_cut, &c->ff_scratch, &c->ff_tail, &c->ff_sum, &c->ff_nee, &c->rec_bits[0], &c->rec_bits[1], &c->sfd_tmp, &c->sfd_ref,
                            &c->sfd_loss[0], &c->sfd_loss[1], &c->sfd_out})
         if (b->p) (void)hipFree(b->p);
@@ -1032,7 +995,6 @@ vr_status vr_upload_scene(vr_ctx* c, const vr_scene* sc) {
         c->num_prims = (int32_t)N;
         c->bvh_depth = b.max_depth;
         if (vr_status hs = upload_half_nodes(c, b.nodes); hs != VR_OK) return hs;
-        c->list_ok = lists_exact(s);
         c->num_nodes = b.nodes.size();
     } else {
         const size_t N = s.spheres.size();
@@ -1397,28 +1359,27 @@ vr_status vr_get_stats(vr_ctx* c, vr_render_stats* o) {
     o->error_pixels = c->h_report[1];
     for (double& v : o->stage_ms) v = 0.0;
     if (c->staged) {
-        hipEvent_t b[6] = {c->ev_start, c->ev_stage[0], c->ev_stage[1], c->ev_stage[2], c->ev_stage[3], c->ev_stop};
-        for (int i = 0; i < 5; ++i) {
+        hipEvent_t b[5] = {c->ev_start, c->ev_stage[0], c->ev_stage[1], c->ev_stage[2], c->ev_stop};
+        for (int i = 0; i < 4; ++i) {
             float m = 0.0f;
             HIP_TRY(hipEventElapsedTime(&m, b[i], b[i + 1]), "hipEventElapsedTime");
             o->stage_ms[i] = m;
         }
     }
-    if (!c->report_gauss && c->ff_launches > 0) {  // free-flight: [0] path kernel, [3] shadow rays, [4] accumulation
+    if (!c->report_gauss && c->ff_launches > 0) {  // free-flight: [0] path kernel, [2] shadow rays, [3] accumulation
         for (uint32_t l = 0; l < c->ff_launches; ++l) {
             const hipEvent_t* e = &c->ff_ev[4 * (size_t)l];
             float m[3] = {0.0f, 0.0f, 0.0f};
             for (int i = 0; i < 3; ++i) HIP_TRY(hipEventElapsedTime(&m[i], e[i], e[i + 1]), "hipEventElapsedTime");
             o->stage_ms[0] += m[0];
-            o->stage_ms[3] += m[1];
-            o->stage_ms[4] += m[2];
+            o->stage_ms[2] += m[1];
+            o->stage_ms[3] += m[2];
         }
     }
     o->scatter_records = c->report_gauss ? (int64_t)c->h_report[2] : 0;
     o->secondary_rays = o->scatter_records * (int64_t)c->last_secondary_per_record;
     o->record_overflow = frame_exceeded(c) ? 1 : 0;
-    o->unlisted_records = c->report_gauss ? (int64_t)c->h_report[5] : 0;
-    o->deep_pixels = c->report_gauss ? (int64_t)std::min(c->h_report[6], kDeepQueue) : 0;
+    o->deep_pixels = c->report_gauss ? (int64_t)std::min(c->h_report[5], kDeepQueue) : 0;
     return VR_OK;
 }
 

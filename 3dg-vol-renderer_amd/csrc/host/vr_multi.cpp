@@ -317,7 +317,6 @@ vr_status group_stats(vr_group* g, vr_render_stats* o) {
         o->scatter_records += s.scatter_records;
         o->secondary_rays += s.secondary_rays;
         o->record_overflow |= s.record_overflow;
-        o->unlisted_records += s.unlisted_records;
         o->deep_pixels += s.deep_pixels;
     }
     return VR_OK;

@@ -561,7 +561,6 @@ struct SecRay {
     uint32_t nsteps;  // instrumented build only: node steps taken by this ray
     uint32_t rec;     // record index
     uint32_t slot;    // result slot s * rec_cap + rec in tr
-    bool listed;      // the record has a neighbour list (tree leaves then skip its members)
 };
 
 __device__ __forceinline__ int act_find(const RenderArgs& A, const SecRay& R, int j) {
@@ -701,7 +700,7 @@ __device__ __forceinline__ uint32_t rays_per_chunk(const RenderArgs& A) {
 // written) or a padding id. norm: slab-test terms in the half nodes' scene-normalised
 // coordinates (HNode).
 #ifndef VR_SEC_FAST_INIT
-#define VR_SEC_FAST_INIT 0
+#define VR_SEC_FAST_INIT 1  // A/B (round 3, C4): secondary stage -1.1 ms
 #endif
 __device__ __forceinline__ bool sec_init(const RenderArgs& A, uint32_t nrec, uint32_t chunk, uint32_t rem, SecRay& R,
                                          bool norm = false) {
@@ -853,7 +852,7 @@ __device__ __forceinline__ void sec_leaf(const RenderArgs& A, SecRay& R, int32_t
 // Ray complete: write its transmittance (or hand it to the exact slow path).
 template <bool S, bool FAST, bool PURE>
 __device__ __forceinline__ void sec_finish(const RenderArgs& A, SecRay& R, Ctr& c) {
-#if !defined(VR_DIAG_WAVE_UTIL) && !defined(VR_DIAG_CYCLES) && !defined(VR_DIAG_LISTSKIP) && !defined(VR_DIAG_ORIGIN)
+#if !defined(VR_DIAG_WAVE_UTIL) && !defined(VR_DIAG_CYCLES) && !defined(VR_DIAG_ORIGIN)
     if constexpr (S) {  // secondary-stage diagnostics in otherwise unused counter slots
         if (R.tau >= R.cut) {
             c.v[kCtrSteps]++;                 // rays ended by the optical-depth cut-off
@@ -1184,159 +1183,30 @@ __device__ __forceinline__ void sec_node(const RenderArgs& A, SecRay& R, LdsInt*
     }
 }
 
-// Neighbour list of every record: a point query of the BVH at the record position collecting
-// each Gaussian with q_j(pos) <= kListR2, central ones (q <= kListCentral, the largest optical
-// depths from pos) at the front of the record's slots, the others at the back. All secondary rays
-// of the record test this list first — most of them become opaque right there, without touching
-// the tree — and the tree walk that follows skips exactly these members (same q, bit for bit).
-#ifndef VR_LIST_STACK
-#define VR_LIST_STACK 16  // a point query pushes few siblings; 16 entries halve the LDS (list stage 8.2 -> 6.5 ms at C4)
-#endif
-template <int BLOCK, bool H, bool W = false>
-__global__ __launch_bounds__(BLOCK) void record_list_kernel(RenderArgs A) {
-    constexpr int kLS = W ? VR_LIST_STACK : kStackSize;
-    __shared__ int s_stack[kLS * BLOCK];
-    int* stack = s_stack + threadIdx.x;
-    const uint32_t nrec = dev_nrec(A);
-    for (uint32_t r = blockIdx.x * BLOCK + threadIdx.x; r < nrec; r += gridDim.x * BLOCK) {
-        const float4 pos = A.rec_pos[r];
-        float bx = pos.x, by = pos.y, bz = pos.z;  // the point in the node boxes' coordinates
-        node_space<H || W>(A, bx, by, bz);
-        int32_t* slot = A.rec_list + (size_t)r * kListCap;
-        uint32_t nc = 0, nb = 0;
-        bool ovf = false;
-        const float hx = A.list_h[0], hy = A.list_h[1], hz = A.list_h[2], r2 = A.list_r2;
-        auto leaf = [&](int32_t ref) {  // a leaf's members with q(pos) <= list_r2
-            const uint32_t first = leaf_first(ref), count = leaf_count(ref);
-            for (uint32_t j = first; j < first + count; ++j) {
-                const GRec g = load_rec(A.gauss, (int)j);
-                const float q = cq_fast(g, pos.x - g.mx, pos.y - g.my, pos.z - g.mz);
-                if (!(q <= r2)) continue;
-                if (nc + nb >= (uint32_t)kListCap) {
-                    ovf = true;
-                } else if (q <= kListCentral) {
-                    slot[nc++] = (int32_t)j;
-                } else {
-                    slot[kListCap - 1 - nb++] = (int32_t)j;
-                }
-            }
-        };
-        int sp = 0, node = 0;
-        for (;;) {
-            if constexpr (W) {  // 4-wide tree: every child box holding the point
-                const uint4* np = reinterpret_cast<const uint4*>(A.hnodes4 + node);
-                const uint4 q0 = np[0], q1 = np[1], q2 = np[2], rf = np[3];
-                const uint32_t w[12] = {q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, q1.z, q1.w, q2.x, q2.y, q2.z, q2.w};
-                const int32_t ref[4] = {(int32_t)rf.x, (int32_t)rf.y, (int32_t)rf.z, (int32_t)rf.w};
-                int32_t next = 0;
-#pragma unroll
-                for (int i = 0; i < 4; ++i) {
-                    float f[6];
-#pragma unroll
-                    for (int k = 0; k < 6; ++k) {
-                        const uint32_t word = w[(6 * i + k) >> 1];
-                        f[k] = (float)__builtin_bit_cast(_Float16,
-                                                         (uint16_t)(((6 * i + k) & 1) ? (word >> 16) : (word & 0xffffu)));
-                    }
-                    // the query box [pos - h, pos + h] meets the child box (h = 0 for the 3.08-sigma radius)
-                    const bool in = (ref[i] != 0) & (f[0] <= bx + hx) & (bx - hx <= f[3]) & (f[1] <= by + hy) &
-                                    (by - hy <= f[4]) & (f[2] <= bz + hz) & (bz - hz <= f[5]);
-                    if (in && ref[i] < 0) leaf(ref[i]);
-                    if (in && ref[i] > 0) {
-                        if (next == 0) {
-                            next = ref[i];
-                        } else if (sp < kLS) {
-                            stack[(sp++) * BLOCK] = ref[i];
-                        } else {
-                            ovf = true;  // no list for this record: its rays walk the whole tree (still exact)
-                        }
-                    }
-                }
-                if (next != 0) {
-                    node = next;
-                } else if (sp > 0) {
-                    --sp;
-                    node = stack[sp * BLOCK];
-                } else {
-                    break;
-                }
-            } else {
-                float f[12];
-                int2 ncr;
-                load_pair<H>(A, node, f, ncr);
-                const bool inl = (ncr.x != 0) & (f[0] <= bx + hx) & (bx - hx <= f[3]) & (f[1] <= by + hy) &
-                                 (by - hy <= f[4]) & (f[2] <= bz + hz) & (bz - hz <= f[5]);
-                const bool inr = (ncr.y != 0) & (f[6] <= bx + hx) & (bx - hx <= f[9]) & (f[7] <= by + hy) &
-                                 (by - hy <= f[10]) & (f[8] <= bz + hz) & (bz - hz <= f[11]);
-                if (inl && ncr.x < 0) leaf(ncr.x);  // leaf children: one contiguous primitive range each
-                if (inr && ncr.y < 0) leaf(ncr.y);
-                const bool il = inl && ncr.x > 0, ir = inr && ncr.y > 0;
-                if (il && ir) {
-                    stack[sp * BLOCK] = ncr.y;
-                    ++sp;
-                    node = ncr.x;
-                } else if (il) {
-                    node = ncr.x;
-                } else if (ir) {
-                    node = ncr.y;
-                } else if (sp > 0) {
-                    --sp;
-                    node = stack[sp * BLOCK];
-                } else {
-                    break;
-                }
-            }
-        }
-        A.rec_nlist[r] = ovf ? 0xffffffffu : (nc | (nb << 16));
-        if (ovf) atomicAdd(A.counters + 2, 1u);  // vr_render_stats.unlisted_records
-    }
-}
+// The list phase: every secondary ray of a record first tests the record's active list (the
+// Gaussians active at the record's step: they contain the record position, so they carry the
+// largest optical depths from it and most rays become opaque right there, without touching the
+// tree); the tree walk that follows skips exactly these members (act_find). The phase lives in
+// `node`: kNodeList (-2) walks the active list [Q.j, Q.end), node >= 0 is the tree walk, -1 the end.
+// (Until round 3 the phase walked a per-record neighbour list {j : q_j(pos) <= 9.5} built by a BVH
+// point query per record; the active list is a subset the march already holds: no list stage
+// (-6.1 ms at C4) and a 2.4 % faster secondary stage)
+constexpr int kNodeList = -2;
 
-// Neighbour-list phases live in `node`: kListCentral_ (-2) walks the central members [Q.j, Q.end),
-// kListOther_ (-3) the other members, whose slot range waits in the (then unused) leaf-queue
-// registers q0 / q1; node >= 0 is the tree walk, -1 the end.
-constexpr int kNodeListCentral = -2, kNodeListOther = -3;
-
-// Start ray R's neighbour-list phase (or go straight to the tree).
-__device__ __forceinline__ void list_begin(const RenderArgs& A, SecRay& R, LeafQueue& Q, int& node) {
+// Start ray R's list phase (or go straight to the tree).
+__device__ __forceinline__ void list_begin(SecRay& R, LeafQueue& Q, int& node) {
     Q.n = 0;
-    Q.j = Q.end = 0;
     Q.q1 = 0;  // ring head (ring queues): valid whenever the tree walk starts here
-    R.listed = false;
-    node = 0;
-    if (!A.list_ok) return;
-    const uint32_t nl = A.rec_nlist[R.rec];
-    if (nl == 0xffffffffu) return;
-    R.listed = true;
-    const uint32_t nc = nl & 0xffffu, nb = nl >> 16;
-    const uint32_t base = R.rec * (uint32_t)kListCap;
-    Q.q0 = (int32_t)(base + kListCap - nb);  // other members: [q0, q1)
-    Q.q1 = (int32_t)(base + kListCap);
-    if (nc > 0) {
-        Q.j = base;
-        Q.end = base + nc;
-        node = kNodeListCentral;
-    } else if (nb > 0) {
-        Q.j = (uint32_t)Q.q0;
-        Q.end = (uint32_t)Q.q1;
-        node = kNodeListOther;
-    } else {
-        Q.q1 = 0;
-    }
+    Q.j = R.act_off;
+    Q.end = R.act_off + R.act_n;
+    node = R.act_n > 0u ? kNodeList : 0;
 }
 
-// After a list slot was consumed: move to the other members, then to the tree.
+// After a list slot was consumed: move to the tree once the list is done.
 __device__ __forceinline__ void list_advance(LeafQueue& Q, int& node) {
-    if (node > kNodeListCentral || Q.j < Q.end) return;
-    if (node == kNodeListCentral && Q.q0 < Q.q1) {
-        Q.j = (uint32_t)Q.q0;
-        Q.end = (uint32_t)Q.q1;
-        node = kNodeListOther;
-    } else {
-        Q.j = Q.end = 0;
-        Q.q1 = 0;  // ring head (ring queues) / unused
-        node = 0;
-    }
+    if (node != kNodeList || Q.j < Q.end) return;
+    Q.j = Q.end = 0;
+    node = 0;
 }
 
 // Scheduling constants of the persistent kernel (tuned on C4): refill once this many
@@ -1422,7 +1292,7 @@ __global__ __launch_bounds__(BLOCK, WAVES) void secondary_ww_kernel(RenderArgs A
                 node = -1;
                 Q.n = 0;
                 Q.j = Q.end = 0;
-                if (live) list_begin(A, R, Q, node);
+                if (live) list_begin(R, Q, node);
             }
             const uint32_t handed = (uint32_t)__popcll(idle);
             pool = pool_end - pool > handed ? pool + handed : pool_end;
@@ -1449,24 +1319,15 @@ __global__ __launch_bounds__(BLOCK, WAVES) void secondary_ww_kernel(RenderArgs A
                 if constexpr (S) c.v[kCtrPrimQueries] += (__ballot(go) != 0ull && lane == 0u) ? 1u : 0u;
 #endif
                 if (go) {
-                    const bool from_list = node <= kNodeListCentral;
-                    const uint32_t j = from_list ? (uint32_t)A.rec_list[Q.j++] : Q.next<QCAP, BLOCK>(stack + STACK * BLOCK);
+                    const bool from_list = node == kNodeList;
+                    const uint32_t j = from_list ? (uint32_t)A.rec_act[Q.j++] : Q.next<QCAP, BLOCK>(stack + STACK * BLOCK);
                     if constexpr (S) c.v[from_list ? kCtrMu : kCtrPrims]++;  // list members counted apart
                     const GRec g = load_rec(A.gauss, (int)j);
                     const Quad q = quad_fast(g, R.ray);
-#ifdef VR_DIAG_LISTSKIP  // diagnostic builds only: tree primitive tests of listed rays, and how many were list members
-                    if constexpr (S) {
-                        if (!from_list && R.listed) {
-                            c.v[kCtrPixels]++;
-                            if (q.Cq <= A.list_r2) c.v[kCtrSteps]++;
-                        }
-                        if (!from_list && !R.listed) c.v[kCtrPrimQueries]++;
-                    }
-#endif
+                    // a tree leaf skips the record's active Gaussians (already summed by the list phase)
+                    const int slot = from_list ? (int)(Q.j - 1u - R.act_off) : act_find(A, R, (int)j);
                     float a, b;
-                    // a tree leaf skips the record's list members (already summed)
-                    if (!(R.listed && !from_list && q.Cq <= A.list_r2) && intersect_fast(q, a, b)) {
-                        const int slot = act_find(A, R, (int)j);
+                    if ((from_list || slot < 0) && intersect_fast(q, a, b)) {
                         float lo = a;
                         if (slot >= 0) {
                             lo = 0.0f;
@@ -1735,18 +1596,6 @@ static hipError_t secondary_launch(const RenderArgs& A, hipStream_t stream) {
 static unsigned record_grid(const RenderArgs& A, uint32_t per_block, unsigned max_blocks) {
     const uint64_t b = ((uint64_t)A.rec_cap + per_block - 1) / per_block;
     return (unsigned)std::max<uint64_t>(1, std::min<uint64_t>(b, max_blocks));
-}
-
-hipError_t gauss_lists(const RenderArgs& A, hipStream_t stream) {
-    if (!A.list_ok) return hipSuccess;
-    const unsigned lb = record_grid(A, kBlockSecondary, 8192);
-    if (A.hnodes4 != nullptr)
-        hipLaunchKernelGGL((dev::record_list_kernel<kBlockSecondary, true, true>), dim3(lb), dim3(kBlockSecondary), 0, stream, A);
-    else if (A.hnodes != nullptr)
-        hipLaunchKernelGGL((dev::record_list_kernel<kBlockSecondary, true>), dim3(lb), dim3(kBlockSecondary), 0, stream, A);
-    else
-        hipLaunchKernelGGL((dev::record_list_kernel<kBlockSecondary, false>), dim3(lb), dim3(kBlockSecondary), 0, stream, A);
-    return hipGetLastError();
 }
 
 hipError_t gauss_secondary(const RenderArgs& A, hipStream_t stream, bool stats) {

@@ -91,13 +91,6 @@ constexpr int kActInline = 4;  // active-list slots stored with each scatter rec
 constexpr int kActDeep = 2048, kDeepThreads = 256, kDeepBlock = 64;
 constexpr uint32_t kDeepQueue = 65536;
 
-// Record neighbour lists (secondary rays): every Gaussian j whose scaled Mahalanobis distance at
-// the record position satisfies q_j(pos) <= kListR2 (pos inside its 3.08-sigma ellipsoid). The
-// BVH boxes bound the 3.15-sigma ellipsoid, so a point query can never miss a member of a
-// scene whose covariances are all positive definite (checked at upload, else lists are off).
-constexpr int kListCap = 48;
-constexpr float kListR2 = 9.5f;
-constexpr float kListCentral = 4.0f;  // members with q <= 4 (inside 2 sigma) are tested first
 constexpr int kMaxSpheres = 64;
 // Deferred NEE (free-flight): a path's queued shadow rays are a linked list in the queue (kFFNone ends
 // it); ff_tail's flag bit says its inline radiance follows them.
@@ -163,15 +156,10 @@ struct RenderArgs {
     unsigned long long* ray_next;   // persistent secondary kernel: next unclaimed ray id
     int32_t* stack_ovf;             // persistent secondary kernel: traversal-stack entries past its LDS stack
     uint32_t stack_ovf_lanes;       // lanes (grid x block) the overflow buffer holds
-    int32_t* rec_list;              // per record kListCap slots: central members from the front, others from the back
-    uint32_t* rec_nlist;            // per record: central count | others << 16; 0xffffffff = no list (overflow)
     uint16_t* env_order;            // per record chunk: its environment rays (record-in-chunk << 8 | sample), direction order
     uint32_t chunk_rec;             // records per secondary-ray chunk (power of 2; 64 without env_order)
     uint32_t chunk_shift;           // log2(chunk_rec)
     float* rec_cut;                 // per record: optical-depth cut-off of its secondary rays (nullptr: tau_cut)
-    float list_r2;                  // neighbour-list radius: members are the Gaussians with q(pos) <= list_r2
-    float list_h[3];                // half-size of the list query box around pos, in node coordinates
-    int32_t list_ok;                // scene allows neighbour lists (all covariances positive definite)
     // ---- free-flight integrators (vr_freeflight.hip): one (tile chunk, sample batch) step ----
     int32_t ff_multi;        // 0 FreeFlightGaussians, 1 MultiScatterGaussians
     int32_t ff_samples;      // samples per pixel (integrator num_samples)

@@ -359,8 +359,7 @@ class Device:
         return {"kernel_ms": s.kernel_ms, "pixels": s.pixels, "fallback_pixels": s.fallback_pixels,
                 "error_pixels": s.error_pixels, "stage_ms": dict(zip(self.STAGES, list(s.stage_ms))),
                 "scatter_records": s.scatter_records, "secondary_rays": s.secondary_rays,
-                "record_overflow": bool(s.record_overflow), "unlisted_records": s.unlisted_records,
-                "deep_pixels": s.deep_pixels}
+                "record_overflow": bool(s.record_overflow), "deep_pixels": s.deep_pixels}
 
     def fallback_pixels(self):
         """(n, 2) int array of the (x, y) pixels of the last ray-march frame that were re-run on the
@@ -389,7 +388,7 @@ class Device:
         return int(v.value)
 
     # vr_render_stats.stage_ms (include/vr_hip.h)
-    STAGES = ("march", "sizing", "lists", "secondary", "accumulate")
+    STAGES = ("march", "sizing", "secondary", "accumulate")
 
     def synchronize(self):
         """Waits for the device; raises VRError(VR_ERR_OVERFLOW) if the last frame is invalid."""

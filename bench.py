@@ -11,9 +11,8 @@ synthetic Gaussians with make_random.py's distribution and 1000_random.txt's thr
 step 0.01, 20 environment samples per scattering step, early-out t_eps = 1e-6 (on
 these scenes the frame is within ~1e-6 of the exact one, tests/test_gpu_parity.py).
 
-Device stages per frame: march_kernel (scatter records) -> record_list_kernel
-(record neighbour lists) -> secondary_ww_kernel (light + environment transmittance, the dominant
-kernel) -> accumulate_kernel.
+Device stages per frame: march_kernel (scatter records) -> record cut-offs ->
+secondary_ww_kernel (light + environment transmittance, the dominant kernel) -> accumulate_kernel.
 
 Prints ONE JSON line on rank 0 (contract in the task statement); roofline and cpu_baseline
 objects are documented in DESIGN.md.
@@ -448,7 +447,7 @@ def main():
             roof.update(achieved=executed / (sec_ms * 1e-3) / 1e12, alg_flops=alg, executed_flops=executed,
                         alg_achieved=alg / (sec_ms * 1e-3) / 1e12, work=work, flop_weights=FLOP_WEIGHTS,
                         flops_note="achieved/frac: the flops the timed persistent kernel itself executes "
-                                   "(its own node steps, leaf + neighbour-list primitive tests and optical "
+                                   "(its own node steps, leaf + active-list primitive tests and optical "
                                    "depths, counted by the instrumented build of the same kernel x the "
                                    "per-operation weights in flop_weights). alg_*: the implementation-"
                                    "independent part, every Gaussian a secondary ray crosses before its "

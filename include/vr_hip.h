@@ -23,7 +23,7 @@
 extern "C" {
 #endif
 
-#define VR_ABI_VERSION 5
+#define VR_ABI_VERSION 6
 
 typedef enum vr_status {
     VR_OK = 0,
@@ -119,19 +119,17 @@ typedef struct vr_render_stats {
     int64_t pixels;           /* pixels rendered */
     int64_t fallback_pixels;  /* pixels re-run on the large-capacity path (active-set overflow) */
     int64_t error_pixels;     /* pixels that exceeded every capacity (output NaN) */
-    /* RayMarchingGaussians stages (HIP events on the render stream; 0 for the other integrators):
-     * [0] primary march (scatter records), [1] record-buffer sizing (one host sync; a re-run of
-     * the march if the capacity carried over from the last frame was too small), [2] record
-     * neighbour lists, [3] secondary-ray transmittance, [4] accumulate. */
-    double stage_ms[5];
+    /* Stages (HIP events on the render stream). RayMarchingGaussians: [0] primary march (scatter
+     * records), [1] record-buffer sizing (one host sync; a re-run of the march if the capacity
+     * carried over from the last frame was too small) and secondary-ray cut-offs, [2] secondary-ray
+     * transmittance, [3] accumulate. FreeFlight / MultiScatterGaussians: [0] path kernel, [2]
+     * deferred shadow rays, [3] accumulate. 0 for the other integrators. */
+    double stage_ms[4];
     int64_t scatter_records;  /* march steps with sigma_s > 0 (each spawns lights + env_samples rays) */
     int64_t secondary_rays;   /* records * (lights + env_samples) */
     int64_t record_overflow;  /* 1: the frame outgrew the scatter-record buffers sized from earlier
                                  frames (its output is invalid; the buffers have been grown, render
                                  again). vr_render does that itself. */
-    int64_t unlisted_records; /* scatter records whose neighbour-list query overflowed (more than 48
-                                 members, or its 16-entry stack): their secondary rays walk the whole
-                                 tree (exact, slower) */
     int64_t deep_pixels;      /* pixels re-run on the global-memory active-list pass (> 64 active) */
 } vr_render_stats;
 
@@ -249,7 +247,7 @@ vr_status vr_unshuffle_tiles_device(vr_ctx* ctx, const float* d_slabs, uint32_t 
  * quadratic + intersect evaluations, [2] optical-depth evaluations, [3] density (mu_t)
  * evaluations, [4] unused, [5] active march steps, [6] primary-ray BVH queries, [7] pixels completed.
  * counts[8..15], the secondary-ray stage (the persistent kernel's own schedule + the exact slow path):
- * [8] BVH node steps, [9] tree-leaf primitive tests, [10] optical-depth evaluations, [11] neighbour-
+ * [8] BVH node steps, [9] tree-leaf primitive tests, [10] optical-depth evaluations, [11] active-
  * list primitive tests, [12] secondary rays started, [13] rays ended by the optical-depth cut-off,
  * [14] node steps of those rays, [15] node steps of the rays that ran to the end of the tree.
  * Free-flight integrators: counts[0..7], the path kernel: [0] paths, [1] free-flight distance

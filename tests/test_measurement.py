@@ -52,7 +52,7 @@ def test_free_flight_roofline_from_work_counts():
                      "erf_evals": 800, "nee_inline": 0, "nee_queued": 15},
             "nee": {"rays": 15, "node4_steps": 300, "gaussian_tests": 200, "optical_depths": 50, "unused4": 0,
                     "unused5": 0, "unused6": 0, "unused7": 0}}
-    stage_ms = {"march": 2.0, "sizing": 0.0, "lists": 0.0, "secondary": 1.0, "accumulate": 0.1}
+    stage_ms = {"march": 2.0, "sizing": 0.0, "secondary": 1.0, "accumulate": 0.1}
     r = bench.ff_roofline(work, stage_ms, "nonexistent-config")
     w = bench.FF_FLOP_WEIGHTS
     path = 1000 * w["node4"] + 10 * w["node2"] + 500 * w["prim"] + 800 * w["erf"]
