@@ -66,7 +66,7 @@ struct vr_ctx {
     // Pinned report of the last frame, copied on the render stream after its last kernel:
     // [0] fallback-queue length, [1] error pixels, [2] scatter records, [3] overflow-pool entries,
     // [4] record capacity exceeded (the frame is invalid and must be rendered again), [5] deep-pass
-    // pixels
+    // pixels, [6] free-flight paths re-run in ff_fallback_kernel
     uint32_t* h_report = nullptr;
     bool report_gauss = false;  // the last frame ran the RayMarchingGaussians pipeline (fields [2..4])
     float* d_frame = nullptr;
@@ -743,6 +743,8 @@ vr_status launch(vr_ctx* c, RenderArgs& A, const vr_render_params* p, hipStream_
                 "hipMemcpyAsync(report)");
         HIP_TRY(hipMemcpyAsync(&c->h_report[5], A.deepq, sizeof(uint32_t), hipMemcpyDeviceToHost, s), "hipMemcpyAsync(report)");
     }
+    HIP_TRY(hipMemcpyAsync(&c->h_report[6], c->d_counters + 2, sizeof(uint32_t), hipMemcpyDeviceToHost, s),
+            "hipMemcpyAsync(report)");
     HIP_TRY(hipEventRecord(c->ev_report, s), "hipEventRecord");
     c->stats_pending = true;
     c->last_pixels = (int64_t)A.num_tiles * 256;
@@ -1355,7 +1357,7 @@ vr_status vr_get_stats(vr_ctx* c, vr_render_stats* o) {
     HIP_TRY(hipEventElapsedTime(&ms, c->ev_start, c->ev_stop), "hipEventElapsedTime");
     o->kernel_ms = ms;
     o->pixels = c->last_pixels;
-    o->fallback_pixels = c->h_report[0];
+    o->fallback_pixels = !c->report_gauss && c->ff_launches > 0 ? c->h_report[6] : c->h_report[0];
     o->error_pixels = c->h_report[1];
     for (double& v : o->stage_ms) v = 0.0;
     if (c->staged) {

@@ -679,6 +679,7 @@ __device__ __forceinline__ bool ff_bounce(const RenderArgs& A, SC& S, int* stack
     if (MULTI && A.rec_bits && ts != -2.0f) record_hits(A, P.ray, ts >= 0.0f ? ts + 1e-6f : INFINITY, P.px, stack, kFFBlock);
     if (ts == -2.0f && A.ff_fbq != nullptr) {  // over the hit-buffer capacity: the whole path re-runs
         const uint32_t q = atomicAdd(A.ff_fbq, 1u);        // in ff_fallback_kernel with larger rows
+        atomicAdd(A.counters + 2, 1u);                      // vr_render_stats.fallback_pixels (whole frame)
         if (q < A.ff_fbq_cap) {
             A.ff_fbq[1 + q] = P.out;
             A.ff_tail[P.out] = make_float4(0.0f, 0.0f, 0.0f, __uint_as_float(kFFNone));  // overwritten there

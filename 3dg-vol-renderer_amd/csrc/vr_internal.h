@@ -135,7 +135,7 @@ struct RenderArgs {
     uint32_t* deepq;       // [0] = count, [1..] = pixels for march_deep_kernel (active set > 64)
     uint32_t deepq_cap;
     int32_t* deep_act;     // march_deep_kernel's active lists, [slot][thread]
-    uint32_t* counters;    // [0] = error pixels
+    uint32_t* counters;    // [0] = error pixels / paths, [2] = free-flight paths re-run in ff_fallback_kernel
     unsigned long long* work;  // instrumented build only: [0..7] march-kernel counters, [8..15] secondary-kernel counters
 
     // ---- wavefront buffers (RayMarchingGaussians), pixel-local index p = tile_local * 256 + lane ----

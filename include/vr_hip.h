@@ -117,7 +117,9 @@ typedef struct vr_scene_info {
 typedef struct vr_render_stats {
     double kernel_ms;         /* device time of the render kernels (HIP events) */
     int64_t pixels;           /* pixels rendered */
-    int64_t fallback_pixels;  /* pixels re-run on the large-capacity path (active-set overflow) */
+    int64_t fallback_pixels;  /* pixels re-run on the large-capacity path (active-set overflow);
+                                 free-flight integrators: paths re-run with kFFBigCap-entry rows
+                                 (more than 128 Gaussians overlapping one point) */
     int64_t error_pixels;     /* pixels that exceeded every capacity (output NaN) */
     /* Stages (HIP events on the render stream). RayMarchingGaussians: [0] primary march (scatter
      * records), [1] record-buffer sizing (one host sync; a re-run of the march if the capacity

@@ -19,11 +19,13 @@ from helpers import CAM_POS, FOV, main_view_dir, scene_path
 pytestmark = pytest.mark.gpu
 
 
-def _gpu(scene, W, H, multi, spp, min_bounces=5, cam=None):
+def _gpu(scene, W, H, multi, spp, min_bounces=5, cam=None, stats=None):
     camera = cam or vr.Pinhole_Camera(CAM_POS, main_view_dir(), FOV)
     integ = vr.MultiScatterGaussians(camera, spp, min_bounces) if multi else vr.FreeFlightGaussians(camera, spp)
     img = vr.Image(W, H)
     integ.render(scene, img)
+    if stats is not None:
+        stats.update(integ.last_stats)
     return img.pixels.copy()
 
 
@@ -160,8 +162,10 @@ def test_overlap_beyond_the_hit_buffer_matches_oracle(multi):
     paths re-run whole in ff_fallback_kernel (1024-entry rows, inline shadow rays); the reference's
     event lists are unbounded (integrator.h:422-498), so the image must match the oracle."""
     scene, orc = _coincident_scene(200)
-    g = _gpu(scene, 16, 16, multi, 4)
+    st = {}
+    g = _gpu(scene, 16, 16, multi, 4, stats=st)
     r = O.render_ff(orc, O.PINHOLE, CAM_POS, main_view_dir(), FOV, 16, 16, multi=multi, num_samples=4)
+    assert st["fallback_pixels"] > 0 and st["error_pixels"] == 0  # paths re-run with the large rows
     _check(g, r)
 
 

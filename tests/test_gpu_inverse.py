@@ -92,6 +92,35 @@ def test_sfd_optimize_runs_and_is_reproducible():
     assert not np.array_equal(runs[0], p)
 
 
+def test_sfd_run_with_grown_scales_does_not_abort():
+    """An SFD run on 20k_bias.txt at 64x64 whose Gaussians start 8x wider than the scene's (log scales
+    + ln 8): ~200-500 ellipsoids overlap a point, past the path kernel's 128-entry rows, and Adam
+    moves the scales further every iteration. The reference's event lists are unbounded
+    (gmm.h:457-515, integrator.h:422-498), so the optimisation must run to the end: those paths re-run
+    in ff_fallback_kernel instead of failing the render."""
+    path = scene_path("20k_bias.txt")
+    target = vr.Scene.load_GMM(path)
+    W = 64
+    I_ref = vr.Image(W, W)
+    vr.MultiScatterGaussians(_cam(), 4).render(target, I_ref)
+    p = inv.pack_parameters(target.gaussians())
+    p[6::11] += np.float32(np.log(8.0))
+    p[7::11] += np.float32(np.log(8.0))
+    p[8::11] += np.float32(np.log(8.0))
+    start = inv.apply_params(p, target.lights, target.env_color)
+    probe = vr.MultiScatterGaussians(_cam(), 4)
+    probe.render(start, vr.Image(W, W))
+    print("paths re-run with the large rows:", probe.last_stats["fallback_pixels"])
+    assert probe.last_stats["fallback_pixels"] > 0  # the start scene already needs the large rows
+    opt = inv.StochasticFiniteDiffInverseIntegrator(_cam(), vr.MultiScatterGaussians(_cam(), 4),
+                                                    inv.SFDConfig(max_iters=4, num_stoch_samples=2, lr=0.05, seed=3,
+                                                                  final_samples=16))
+    assert opt.optimize(start, I_ref)
+    assert len(opt.history) == 4 and np.all(np.isfinite(opt.history))
+    assert np.all(np.isfinite(opt.params)) and np.isfinite(opt.final_loss)
+    assert not np.array_equal(opt.params[6::11], p[6::11])  # the scales moved
+
+
 # ---- BASELINE config 5: scenes/gaussians/10k_random.txt at 512x512 ------------------------------
 C5_W = 512
 C5_SPP = 4
