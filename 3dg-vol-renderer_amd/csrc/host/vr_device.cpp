@@ -25,6 +25,7 @@ uint32_t free_flight_threads(int cus);
 hipError_t launch_sfd_loss_diff(const uint32_t* bits0, const uint32_t* bits1, const float* lb, const float* lp, uint32_t npix,
                                 uint32_t n, double* out, hipStream_t stream);
 hipError_t gauss_record_cut(const RenderArgs& A, float budget, hipStream_t stream);
+hipError_t gauss_whiten(const GaussianRecord* rec, WRecord* out, uint32_t n, hipStream_t stream);
 hipError_t launch_pixel_losses(const float* img, const float* ref, uint32_t npix, float* out, hipStream_t stream);
 
 hipError_t launch_unshuffle(const float* slabs, uint32_t nslabs, uint32_t tiles_per_slab, uint32_t tiles_x, uint32_t W,
@@ -41,6 +42,7 @@ struct vr_ctx {
     int32_t type = VR_VOLUME_GAUSSIANS;
     int32_t num_prims = 0;
     GaussianRecord* d_gauss = nullptr;
+    WRecord* d_wrec = nullptr;  // whitened copy (secondary rays)
     BVHNode* d_nodes = nullptr;
     HNode* d_hnodes = nullptr;
     HNode4* d_hnodes4 = nullptr;
@@ -135,6 +137,8 @@ void free_scene(vr_ctx* c) {
     if (c->d_order) (void)hipFree(c->d_order);
     c->d_order = nullptr;
     if (c->d_gauss) (void)hipFree(c->d_gauss);
+    if (c->d_wrec) (void)hipFree(c->d_wrec);
+    c->d_wrec = nullptr;
     if (c->d_nodes) (void)hipFree(c->d_nodes);
     if (c->d_hnodes) (void)hipFree(c->d_hnodes);
     c->d_hnodes = nullptr;
@@ -293,6 +297,16 @@ constexpr size_t kDeviceBvhMin = 256;
 // Device BVH build (kernels/vr_lbvh.hip): records and boxes go up in scene order, the device sorts
 // them by Morton code and emits the child-pair, half-precision and 4-wide trees. VR_ERR_UNSUPPORTED:
 // the tree is deeper than the traversal stacks allow (the caller builds on the host instead).
+
+// Whitened record copy for the secondary rays (WRecord), converted on the device from d_gauss.
+static vr_status upload_whitened(vr_ctx* c, size_t N) {
+    HIP_TRY(hipMalloc(&c->d_wrec, std::max<size_t>(N, 1) * sizeof(WRecord)), "hipMalloc(whitened records)");
+    if (N == 0) return VR_OK;
+    HIP_TRY(gauss_whiten(c->d_gauss, c->d_wrec, (uint32_t)N, c->stream), "whitened records");
+    HIP_TRY(hipStreamSynchronize(c->stream), "hipStreamSynchronize(whitened records)");
+    return VR_OK;
+}
+
 vr_status upload_device_bvh(vr_ctx* c, const HostScene& s, const std::vector<float>& boxes) {
     const size_t N = s.pre.size();
     std::vector<GaussianRecord> rec(N);
@@ -337,6 +351,7 @@ vr_status upload_device_bvh(vr_ctx* c, const HostScene& s, const std::vector<flo
     if (e == hipErrorNotSupported) return fail(VR_ERR_UNSUPPORTED, "device BVH deeper than the traversal stacks");
     if (e != hipSuccess) return hip_fail(e, "device BVH build");
     c->d_gauss = R.gauss;
+    if (vr_status ws = upload_whitened(c, N); ws != VR_OK) return ws;
     c->d_order = R.order;
     c->d_nodes = R.nodes;
     c->d_hnodes = R.hnodes;
@@ -441,6 +456,7 @@ vr_status fill_args(vr_ctx* c, const vr_camera* cam, const vr_render_params* p, 
     A.height = H;
     A.tiles_x = (W + kTile - 1) / kTile;
     A.gauss = c->d_gauss;
+    A.wrec = c->d_wrec;
     A.nodes = c->d_nodes;
     A.hnodes = c->d_hnodes;
     A.hnodes4 = c->d_hnodes4;
@@ -986,6 +1002,7 @@ vr_status vr_upload_scene(vr_ctx* c, const vr_scene* sc) {
         }
         HIP_TRY(hipMalloc(&c->d_gauss, rec.size() * sizeof(GaussianRecord)), "hipMalloc(records)");
         HIP_TRY(hipMemcpy(c->d_gauss, rec.data(), rec.size() * sizeof(GaussianRecord), hipMemcpyHostToDevice), "hipMemcpy(records)");
+        if (vr_status ws = upload_whitened(c, N); ws != VR_OK) return ws;
         {
             std::vector<uint32_t> order(std::max<size_t>(N, 1), 0u);
             for (size_t j = 0; j < N; ++j) order[j] = (uint32_t)b.order[j];

@@ -555,7 +555,9 @@ struct SecRay {
     // reference's t_env_end, test_integrators.h:258-271), which bounds nothing during traversal
     float cut;         // optical depth at which the ray's transmittance counts as 0 (error budget)
     uint64_t hitmask;  // which of the record's active Gaussians the ray has met
-    uint64_t bloom;    // membership mask of the record's active list (act_find)
+    uint64_t bloom;    // membership mask of the record's active list (act_find; PureRayMarching)
+    float cmax;        // largest p.M.p (p = origin - mean) over the record's active list
+    float credit;      // RayMarchingGaussians: list members' optical depth not yet met again by the tree walk
     uint32_t act_off, act_n;  // the record's active list
     bool light, needs_stop;
     uint32_t nsteps;  // instrumented build only: node steps taken by this ray
@@ -563,10 +565,34 @@ struct SecRay {
     uint32_t slot;    // result slot s * rec_cap + rec in tr
 };
 
+// The ray's optical depth is known to have reached its cut-off. RayMarchingGaussians: tau holds what
+// the tree walk met (list members included), credit the list members' depth it has not met yet, so
+// tau + credit is a lower bound of the final depth (see wtest in secondary_ww_kernel).
+template <bool PURE>
+__device__ __forceinline__ bool cut_reached(const SecRay& R) {
+    if constexpr (PURE) return R.tau >= R.cut;
+    else return R.tau + fmaxf(R.credit, 0.0f) >= R.cut;
+}
+
+// Slot of Gaussian j in the record's active list, or -1. The list is scanned four entries per
+// round trip (independent loads), since a scan sits on the dependent chain of a primitive test.
 __device__ __forceinline__ int act_find(const RenderArgs& A, const SecRay& R, int j) {
     if (!((R.bloom >> (j & 63)) & 1ull)) return -1;
-    for (uint32_t i = 0; i < R.act_n; ++i)
-        if (A.rec_act[R.act_off + i] == j) return (int)i;
+#ifdef VR_AB_BLOOM_ONLY  // what-if A/B builds only (wrong results): the membership scan's cost
+    return -1;
+#endif
+    const int* __restrict__ p = A.rec_act + R.act_off;
+    const int n = (int)R.act_n;
+    for (int i = 0; i < n; i += 4) {
+        const int v0 = p[i];
+        const int v1 = i + 1 < n ? p[i + 1] : -1;
+        const int v2 = i + 2 < n ? p[i + 2] : -1;
+        const int v3 = i + 3 < n ? p[i + 3] : -1;
+        if (v0 == j) return i;
+        if (v1 == j) return i + 1;
+        if (v2 == j) return i + 2;
+        if (v3 == j) return i + 3;
+    }
     return -1;
 }
 
@@ -715,6 +741,8 @@ __device__ __forceinline__ bool sec_init(const RenderArgs& A, uint32_t nrec, uin
     R.act_off = meta.z;
     R.act_n = meta.w;
     R.bloom = A.rec_bloom[r];
+    R.cmax = -INFINITY;
+    R.credit = 0.0f;
     R.hitmask = 0;
     R.nsteps = 0;
     R.tau = 0.0f;
@@ -854,7 +882,7 @@ template <bool S, bool FAST, bool PURE>
 __device__ __forceinline__ void sec_finish(const RenderArgs& A, SecRay& R, Ctr& c) {
 #if !defined(VR_DIAG_WAVE_UTIL) && !defined(VR_DIAG_CYCLES) && !defined(VR_DIAG_ORIGIN)
     if constexpr (S) {  // secondary-stage diagnostics in otherwise unused counter slots
-        if (R.tau >= R.cut) {
+        if (cut_reached<PURE>(R)) {
             c.v[kCtrSteps]++;                 // rays ended by the optical-depth cut-off
             c.v[kCtrPrimQueries] += R.nsteps;  // ... and their node steps
         } else {
@@ -862,14 +890,25 @@ __device__ __forceinline__ void sec_finish(const RenderArgs& A, SecRay& R, Ctr& 
         }
     }
 #endif
-    if (R.tau >= R.cut) {
+    if (cut_reached<PURE>(R)) {
         VR_TR_STORE(A, R.slot, 0.0f);
         return;
     }
     if (R.act_n > 64) {  // (march_deep_kernel records) missed members: re-intersect the whole list
         bool any = false;
         for (uint32_t s = 0; s < R.act_n; ++s) {
-            const GRec g = load_rec(A.gauss, A.rec_act[R.act_off + s]);
+            const int j = A.rec_act[R.act_off + s];
+            if constexpr (!PURE) {  // the list phase's whitened test
+                const WRec g = load_wrec(A.wrec, j);
+                const WQuad q = wquad(g, R.ray);
+                float t0, t1, sd;
+                if (wintersect(q, t0, t1, sd)) continue;
+                any = true;
+                if (!R.light) R.tau += wod_range(g, q, 0.0f, R.lim);
+                else break;
+                continue;
+            }
+            const GRec g = load_rec(A.gauss, j);
             const Quad q = FAST ? quad_fast(g, R.ray) : quad(g, R.ray);
             float a, b;
             if (FAST ? intersect_fast(q, a, b) : intersect(q, a, b)) continue;
@@ -913,10 +952,9 @@ __device__ __forceinline__ void sec_finish(const RenderArgs& A, SecRay& R, Ctr& 
         while (missed) {  // pre-activated, missed through rounding: active up to the last event
             int s = __ffsll((unsigned long long)missed) - 1;
             missed &= missed - 1;
-            GRec g = load_rec(A.gauss, A.rec_act[R.act_off + s]);
-            Quad q = FAST ? quad_fast(g, R.ray) : quad(g, R.ray);
             if constexpr (S) c.v[kCtrOD]++;
-            R.tau += FAST ? optical_depth_fast(g, q, 0.0f, R.lim) : optical_depth(g, q, 0.0f, R.lim);
+            const WRec g = load_wrec(A.wrec, A.rec_act[R.act_off + s]);
+            R.tau += wod_range(g, wquad(g, R.ray), 0.0f, R.lim);
         }
     }
     VR_TR_STORE(A, R.slot, expf(-R.tau));
@@ -1312,6 +1350,77 @@ __global__ __launch_bounds__(BLOCK, WAVES) void secondary_ww_kernel(RenderArgs A
         // whichever kind more lanes can use; never a kind no lane can use (that would not progress)
         const bool prim_iter = nn == 0 || (np > 0 && np >= nn);
         if (prim_iter) {  // PRIM iteration: up to kPrimSteps primitive tests per lane
+            LdsInt* ext = stack + STACK * BLOCK;
+            // next primitive of the lane: a list member (ls = its slot) or a queued leaf's (ls = -1)
+            auto fetch = [&](uint32_t& j, int& ls) {
+                if (node == kNodeList) {
+                    ls = (int)(Q.j - R.act_off);
+                    j = (uint32_t)A.rec_act[Q.j++];
+                    list_advance(Q, node);
+                } else {
+                    ls = -1;
+                    j = Q.next<QCAP, BLOCK>(ext);
+                }
+            };
+            // one primitive test; ls >= 0: list member ls (pre-activated: optical depth from 0).
+            // RayMarchingGaussians: the whitened record (WRecord); PureRayMarching: the record itself
+            // (its marched depth evaluates mu_t)
+            auto wtest = [&](const WRec& g, uint32_t j, int ls) {
+                if constexpr (S) c.v[ls >= 0 ? kCtrMu : kCtrPrims]++;  // list members counted apart
+                const WQuad q = wquad(g, R.ray);
+                // The list phase sums the members' depths into `credit` (the cut-off sees them at
+                // once); the tree walk then sums every Gaussian it meets into tau, members included,
+                // so no membership lookup is needed. A member holds the origin: its p.M.p is <= cmax
+                // (the same bits the list phase took). Such a candidate is summed from t = 0, as the
+                // reference sums a pre-activated member (for a member, or any Gaussian holding the
+                // origin, that is its entry max(t0, 0) anyway), and its depth comes off the credit: the
+                // credit stays a lower bound of what the walk has still to meet.
+                if (ls >= 0) R.cmax = fmaxf(R.cmax, q.c);
+                const bool cand = ls < 0 && q.c <= R.cmax;
+                float t0, t1, sd;
+                if (!wintersect(q, t0, t1, sd)) return;
+                const bool pre = ls >= 0 || cand;  // active from t = 0
+                const float lo = pre ? 0.0f : fmaxf(t0, 0.0f);
+                const float u0 = pre ? q.hr : fmaxf(q.hr, -sd);  // erf argument x sqrt 2 at lo
+                if (ls >= 0) R.hitmask |= slot_bit(ls);
+                if constexpr (S) c.v[kCtrOD]++;
+                // sec_add's FAST rule: one optical-depth evaluation for light and environment lanes
+                const bool add = !R.light || t1 < R.lim;
+                R.needs_stop = R.needs_stop || (!add && lo < R.lim);
+                if (!R.light) R.lim = fmaxf(R.lim, t1);
+                if (add) {
+                    const float od = wod_chord(g, q, u0, sd);  // [lo, t1] lies on the 3-sigma chord
+                    if (ls >= 0) {
+                        R.credit += od;
+                    } else {
+                        R.tau += od;
+                        if (cand) R.credit -= od;
+                    }
+                }
+            };
+            auto test = [&](const GRec& g, uint32_t j, int ls) {
+                if constexpr (S) c.v[ls >= 0 ? kCtrMu : kCtrPrims]++;  // list members counted apart
+                const Quad q = quad_fast(g, R.ray);
+                int slot = ls;
+                if (ls >= 0) {
+                    R.cmax = fmaxf(R.cmax, q.Cq);
+                } else if (q.Cq <= R.cmax) {
+                    // a tree leaf skips the record's active Gaussians (already summed by the list phase).
+                    // Only a Gaussian that holds the origin as far as the members' own p.M.p values go
+                    // (the same cq_fast bits, taken by the list phase) can be one: no scan otherwise
+                    slot = act_find(A, R, (int)j);
+                    if (slot >= 0) return;
+                }
+                float a, b;
+                if (intersect_fast(q, a, b)) {
+                    float lo = a;
+                    if (slot >= 0) {
+                        lo = 0.0f;
+                        R.hitmask |= slot_bit(slot);
+                    }
+                    sec_add<S, true, PURE>(A, R, g, q, lo, b, c);
+                }
+            };
             bool go = has_prim;
 #pragma unroll kPrimUnroll
             for (int k = 0; k < kPrimSteps; ++k) {
@@ -1319,25 +1428,13 @@ __global__ __launch_bounds__(BLOCK, WAVES) void secondary_ww_kernel(RenderArgs A
                 if constexpr (S) c.v[kCtrPrimQueries] += (__ballot(go) != 0ull && lane == 0u) ? 1u : 0u;
 #endif
                 if (go) {
-                    const bool from_list = node == kNodeList;
-                    const uint32_t j = from_list ? (uint32_t)A.rec_act[Q.j++] : Q.next<QCAP, BLOCK>(stack + STACK * BLOCK);
-                    if constexpr (S) c.v[from_list ? kCtrMu : kCtrPrims]++;  // list members counted apart
-                    const GRec g = load_rec(A.gauss, (int)j);
-                    const Quad q = quad_fast(g, R.ray);
-                    // a tree leaf skips the record's active Gaussians (already summed by the list phase)
-                    const int slot = from_list ? (int)(Q.j - 1u - R.act_off) : act_find(A, R, (int)j);
-                    float a, b;
-                    if ((from_list || slot < 0) && intersect_fast(q, a, b)) {
-                        float lo = a;
-                        if (slot >= 0) {
-                            lo = 0.0f;
-                            R.hitmask |= slot_bit(slot);
-                        }
-                        sec_add<S, true, PURE>(A, R, g, q, lo, b, c);
-                    }
-                    list_advance(Q, node);
+                    uint32_t j;
+                    int ls;
+                    fetch(j, ls);
+                    if constexpr (PURE) test(load_rec(A.gauss, (int)j), j, ls);
+                    else wtest(load_wrec(A.wrec, (int)j), j, ls);
                 }
-                go = go && Q.has_prim() && R.tau < R.cut;
+                go = go && Q.has_prim() && !cut_reached<PURE>(R);
             }
             diag_lap(kCtrPrimQueries);
         } else {  // NODE iteration: up to kNodeSteps node steps per lane
@@ -1355,7 +1452,7 @@ __global__ __launch_bounds__(BLOCK, WAVES) void secondary_ww_kernel(RenderArgs A
             }
             diag_lap(kCtrSteps);
         }
-        if (live && (R.tau >= R.cut || (node == -1 && !Q.has_prim()))) {
+        if (live && (cut_reached<PURE>(R) || (node == -1 && !Q.has_prim()))) {
             sec_finish<S, true, PURE>(A, R, c);
             live = false;
         }
@@ -1387,6 +1484,24 @@ __global__ __launch_bounds__(BLOCK) void secondary_slow_kernel(RenderArgs A) {
     if constexpr (S)
         for (int i = 0; i < kNumCtr; ++i)
             if (c.v[i]) atomicAdd(A.work + kNumCtr + i, (unsigned long long)c.v[i]);
+}
+
+// WRecord of every record (vr_internal.h): Cholesky factor of M = Sigma^-1 in double. A record whose M
+// is not positive definite gets NaN factors (wintersect never reports a crossing for it).
+__global__ __launch_bounds__(256) void whiten_kernel(const GaussianRecord* __restrict__ rec, WRecord* __restrict__ out,
+                                                     uint32_t n) {
+    const uint32_t i = blockIdx.x * 256u + threadIdx.x;
+    if (i >= n) return;
+    const GaussianRecord g = rec[i];
+    const double m00 = g.m00, m01 = g.m01, m02 = g.m02, m11 = g.m11, m12 = g.m12, m22 = g.m22;
+    const double l00 = sqrt(m00), l01 = m01 / l00, l02 = m02 / l00;
+    const double l11 = sqrt(m11 - l01 * l01), l12 = (m12 - l01 * l02) / l11;
+    const double l22 = sqrt(m22 - l02 * l02 - l12 * l12);
+    const bool pd = l00 > 0.0 && l11 > 0.0 && l22 > 0.0;  // (sqrt of a negative pivot: NaN, fails too)
+    const float nan = __builtin_nanf("");
+    const float dn = (float)((double)g.density * (double)g.norm * 1.2533141373155002512);  // sqrt(pi / 2)
+    out[i] = WRecord{g.mx, g.my, g.mz, dn, pd ? (float)l00 : nan, (float)l01, (float)l02, (float)l11,
+                     (float)l12, (float)l22, 0.0f, 0.0f};
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -1609,6 +1724,11 @@ hipError_t gauss_secondary(const RenderArgs& A, hipStream_t stream, bool stats) 
     // the work this schedule really does (node steps, list and leaf primitive tests, optical depths)
     if (A.pure) return stats ? secondary_launch<true, true>(A, stream) : secondary_launch<false, true>(A, stream);
     return stats ? secondary_launch<true, false>(A, stream) : secondary_launch<false, false>(A, stream);
+}
+
+hipError_t gauss_whiten(const GaussianRecord* rec, WRecord* out, uint32_t n, hipStream_t stream) {
+    hipLaunchKernelGGL(dev::whiten_kernel, dim3((n + 255) / 256), dim3(256), 0, stream, rec, out, n);
+    return hipGetLastError();
 }
 
 hipError_t gauss_record_cut(const RenderArgs& A, float budget, hipStream_t stream) {

@@ -219,6 +219,69 @@ __device__ __forceinline__ float optical_depth_chord(const GRec& g, const Quad& 
     return pref * e * fmaxf(F1 - F0, 0.0f);  // (f32 noise can invert a tiny interval)
 }
 
+// ---- whitened secondary-ray forms (WRecord) ---------------------------------------------------
+// In the coordinates u = L (x - mean) (M = L^T L) a Gaussian's 3-sigma ellipsoid is the sphere |u| = 3
+// and a ray o + t d is u = Lp + t Ld. With a = |Ld|^2, h = Lp.Ld, c = |Lp|^2, r = a^-1/2, hr = h r:
+//   intersect_direct (gaussian.h:126-164): D = hr^2 - (c - 9) >= 0, t = r (-hr -+ sqrt(D))
+//   optical_depth (gaussian.h:208-231): dn r exp((hr^2 - c) / 2) (erf(x1) - erf(x0)),
+//     x(t) = (hr + t / r) / sqrt(2); at the exit t1, x1 = sqrt(D / 2); at the entry t0, x0 = -x1
+// (the same quantities as quad_fast / intersect_fast / optical_depth_fast in about half the VALU
+// operations and three transcendentals — rsq, sqrt, exp — instead of six).
+struct WRec {
+    float mx, my, mz, dn, l00, l01, l02, l11, l12, l22;
+};
+__device__ __forceinline__ WRec load_wrec(const WRecord* __restrict__ g, int i) {
+    const float4* p = reinterpret_cast<const float4*>(g + i);
+    const float4 a = p[0], b = p[1];
+    const float2 c = *reinterpret_cast<const float2*>(p + 2);
+    return WRec{a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w, c.x, c.y};
+}
+struct WQuad {
+    float c;   // |Lp|^2 = p.M.p (origin - mean): depends on the ray origin only
+    float r;   // |Ld|^-1
+    float hr;  // Lp.Ld / |Ld|
+    float sa;  // |Ld|
+};
+__device__ __forceinline__ WQuad wquad(const WRec& g, const Ray& ray) {
+    const float px = ray.ox - g.mx, py = ray.oy - g.my, pz = ray.oz - g.mz;
+    const float p0 = fmaf(g.l00, px, fmaf(g.l01, py, g.l02 * pz)), p1 = fmaf(g.l11, py, g.l12 * pz), p2 = g.l22 * pz;
+    const float d0 = fmaf(g.l00, ray.dx, fmaf(g.l01, ray.dy, g.l02 * ray.dz));
+    const float d1 = fmaf(g.l11, ray.dy, g.l12 * ray.dz), d2 = g.l22 * ray.dz;
+    const float a = fmaf(d0, d0, fmaf(d1, d1, d2 * d2));
+    const float h = fmaf(p0, d0, fmaf(p1, d1, p2 * d2));
+    WQuad q;
+    q.c = fmaf(p0, p0, fmaf(p1, p1, p2 * p2));
+    q.r = __builtin_amdgcn_rsqf(a);
+    q.hr = h * q.r;
+    q.sa = a * q.r;
+    return q;
+}
+// Entry / exit of the 3-sigma sphere (t0 <= t1, not clamped); s = sqrt(D). False: no crossing, or it
+// lies behind the origin (t1 < 0), as intersect_fast.
+__device__ __forceinline__ bool wintersect(const WQuad& q, float& t0, float& t1, float& s) {
+    const float D = fmaf(q.hr, q.hr, 9.0f - q.c);
+    if (!(D >= 0.0f)) return false;  // (NaN: a degenerate covariance never intersects)
+    s = __builtin_amdgcn_sqrtf(D);
+    t1 = q.r * (s - q.hr);
+    if (t1 < 0.0f) return false;
+    t0 = q.r * (-q.hr - s);
+    return true;
+}
+// Optical depth between erf arguments x0 <= x1 (times sqrt 2) on the 3-sigma chord: erf_chord.
+__device__ __forceinline__ float wod_chord(const WRec& g, const WQuad& q, float u0, float u1) {
+    constexpr float kRs2 = 0.70710678118654752f;
+    const float F1 = erf_chord(u1 * kRs2), F0 = erf_chord(u0 * kRs2);
+    const float e = __expf(0.5f * fmaf(q.hr, q.hr, -q.c));
+    return (g.dn * q.r) * e * fmaxf(F1 - F0, 0.0f);  // (f32 noise can invert a tiny interval)
+}
+// Optical depth over [t0, t1] anywhere on the ray (device erff: arguments past the chord).
+__device__ __forceinline__ float wod_range(const WRec& g, const WQuad& q, float t0, float t1) {
+    constexpr float kRs2 = 0.70710678118654752f;
+    const float F1 = erff(fmaf(q.sa, t1, q.hr) * kRs2), F0 = erff(fmaf(q.sa, t0, q.hr) * kRs2);
+    const float e = __expf(0.5f * fmaf(q.hr, q.hr, -q.c));
+    return (g.dn * q.r) * e * (F1 - F0);
+}
+
 // Gaussian::mu_t = density * evaluate(x) (gaussian.h:111-117), exponent -0.5 d^T M d with
 // Eigen's lazy-product order.
 __device__ __forceinline__ float mu_t(const GRec& g, float x, float y, float z) {

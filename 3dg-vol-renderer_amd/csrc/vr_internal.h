@@ -20,6 +20,17 @@ struct GaussianRecord {
 };
 static_assert(sizeof(GaussianRecord) == 48, "record must be 48 B");
 
+// Whitened copy of a record for the secondary rays (48 B, same leaf order): M = L^T L with L upper
+// triangular (Cholesky of the inverse covariance, in double), so a ray's quadratic is that of a unit
+// sphere in the coordinates L (x - mean): A = |L d|^2, B/2 = L p . L d, Cq = |L p|^2. dn = density *
+// norm * sqrt(pi / 2): the optical depth's prefactor density * norm * sqrt(pi / (2A)) is dn * A^-1/2.
+struct WRecord {
+    float mx, my, mz, dn;
+    float l00, l01, l02, l11;
+    float l12, l22, pad0, pad1;
+};
+static_assert(sizeof(WRecord) == 48, "whitened record must be 48 B");
+
 // ------------------------------------------------------------------------------------------
 // BVH node, child-pair layout, 64 B: one node fetch tests both children.
 //   f[0..5]  = left  child box (min xyz, max xyz)
@@ -111,6 +122,7 @@ struct RenderArgs {
     float* out;
     // scene
     const GaussianRecord* gauss;
+    const WRecord* wrec;      // whitened copy of gauss (secondary rays of RayMarchingGaussians)
     const BVHNode* nodes;
     const HNode* hnodes;      // nullptr: the scene is not suited to half-precision boxes (see vr_device.cpp)
     const HNode4* hnodes4;    // 4-wide collapse of the same tree (secondary rays); nullptr with hnodes
