@@ -267,10 +267,7 @@ vr_status upload_half_nodes(vr_ctx* c, const std::vector<BVHNode>& nodes) {
         HNode4 h{};
         for (int i = 0; i < 4; ++i) {
             if (i >= nk) {
-                for (int k = 0; k < 3; ++k) {
-                    h.h[i][k] = 0x7c00u;      // +inf
-                    h.h[i][3 + k] = 0xfc00u;  // -inf
-                }
+                for (int k = 0; k < 6; ++k) h.h[i][k] = 0x7e00u;  // NaN box: no slab test reports a hit
                 h.c[i] = 0;
                 continue;
             }

@@ -554,6 +554,7 @@ struct SecRay {
     // `lim`: a light ray's distance to the light; an environment ray's last event so far (the
     // reference's t_env_end, test_integrators.h:258-271), which bounds nothing during traversal
     float cut;         // optical depth at which the ray's transmittance counts as 0 (error budget)
+    float plim;        // node boxes entered beyond this distance hold nothing for the ray (light: past the light)
     uint64_t hitmask;  // which of the record's active Gaussians the ray has met
     uint64_t bloom;    // membership mask of the record's active list (act_find; PureRayMarching)
     float cmax;        // largest p.M.p (p = origin - mean) over the record's active list
@@ -779,6 +780,7 @@ __device__ __forceinline__ bool sec_init(const RenderArgs& A, uint32_t nrec, uin
         R.light = false;
         R.lim = 0.0f;  // last event so far
     }
+    R.plim = R.light ? R.lim + kTPad * (1.0f + R.lim) : INFINITY;
     // |d| clamped away from 0: the fma slab form b/d - o/d must never see inf - inf
     const float sc = norm ? A.hn_scale : 1.0f;
     const float dx = R.ray.dx * sc, dy = R.ray.dy * sc, dz = R.ray.dz * sc;
@@ -1057,7 +1059,7 @@ __device__ __forceinline__ void sec_node4(const RenderArgs& A, SecRay& R, LdsInt
     const uint4 q0 = np[0], q1 = np[1], q2 = np[2], rf = np[3];
     const uint32_t w[12] = {q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, q1.z, q1.w, q2.x, q2.y, q2.z, q2.w};
     const int32_t ref[4] = {(int32_t)rf.x, (int32_t)rf.y, (int32_t)rf.z, (int32_t)rf.w};
-    const float lim = R.light ? R.lim + kTPad * (1.0f + R.lim) : INFINITY;
+    const float lim = R.plim;
     float key[4];
     int32_t kr[4];
 #pragma unroll
@@ -1170,6 +1172,82 @@ __device__ __forceinline__ void sec_node4(const RenderArgs& A, SecRay& R, LdsInt
     }
 }
 
+#ifndef VR_NODE4_V2
+#define VR_NODE4_V2 1  // 1: sec_node4v (no sorting network), 0: sec_node4 (A/B)
+#endif
+// One step of the 4-wide traversal without a sorting network: the nearest inner child is walked next
+// (a min-reduction over the inner children's entry distances), the other inner children are pushed
+// and the leaf children queued in the node's child order. Empty slots carry NaN boxes, so the slab
+// test alone rejects them. Ring queues only (QCAP = 1 + 2^k).
+template <int BLOCK, bool S, int QCAP, int STACK>
+__device__ __forceinline__ void sec_node4v(const RenderArgs& A, SecRay& R, LdsInt* stack, int& sp, int& node, LeafQueue& Q,
+                                           Ctr& c) {
+    static_assert(kQueueRing<QCAP>, "sec_node4v: ring leaf queue");
+    if constexpr (S) {
+        c.v[kCtrNodes]++;
+        ++R.nsteps;
+    }
+    const uint4* np = reinterpret_cast<const uint4*>(A.hnodes4 + node);
+    const uint4 q0 = np[0], q1 = np[1], q2 = np[2], rf = np[3];
+    const uint32_t w[12] = {q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, q1.z, q1.w, q2.x, q2.y, q2.z, q2.w};
+    const int32_t ref[4] = {(int32_t)rf.x, (int32_t)rf.y, (int32_t)rf.z, (int32_t)rf.w};
+    LdsInt* ext = stack + STACK * BLOCK;
+    float best = INFINITY;
+    int32_t next = 0;  // the nearest inner child
+    bool inner[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        float f[6];
+#pragma unroll
+        for (int k = 0; k < 6; ++k) {
+            const uint32_t word = w[(6 * i + k) >> 1];
+            f[k] = (float)__builtin_bit_cast(_Float16, (uint16_t)(((6 * i + k) & 1) ? (word >> 16) : (word & 0xffffu)));
+        }
+        const float tx1 = fmaf(f[0], R.ix, -R.oxi), tx2 = fmaf(f[3], R.ix, -R.oxi);
+        const float ty1 = fmaf(f[1], R.iy, -R.oyi), ty2 = fmaf(f[4], R.iy, -R.oyi);
+        const float tz1 = fmaf(f[2], R.iz, -R.ozi), tz2 = fmaf(f[5], R.iz, -R.ozi);
+        const float tmin = fmaxf(fmaxf(fminf(tx1, tx2), fminf(ty1, ty2)), fminf(tz1, tz2));
+        const float tmax = fminf(fminf(fmaxf(tx1, tx2), fmaxf(ty1, ty2)), fmaxf(tz1, tz2));
+        // [max(tmin, 0), min(tmax, plim)] not empty; a NaN box (empty slot) fails the first compare
+        const bool hit = (tmin <= fminf(tmax, R.plim)) & (tmax >= 0.0f);
+        const bool leaf = hit & (ref[i] < 0);
+        inner[i] = hit & (ref[i] > 0);
+        // leaf -> the queue's end: branch-free, a non-leaf store lands past the last entry (never
+        // read). A NODE step starts with at most QCAP - 4 entries, so that slot is a free ring word.
+        Q.q0 = (leaf & (Q.n == 0)) ? ref[i] : Q.q0;
+        ext[((Q.q1 + Q.n - 1) & (QCAP - 2)) * BLOCK] = ref[i];
+        Q.n += (int)leaf;
+        const bool nearer = inner[i] & (tmin < best);
+        best = nearer ? tmin : best;
+        next = nearer ? ref[i] : next;
+    }
+    // the other inner children -> stack (branch-free while every stepping lane has room for 3)
+    if (__builtin_expect(__ballot(sp > STACK - 3) == 0ull, 1)) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            stack[sp * BLOCK] = ref[i];
+            sp += (int)(inner[i] & (ref[i] != next));
+        }
+    } else {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            if (inner[i] & (ref[i] != next)) {
+                if (sp < STACK) stack[sp * BLOCK] = ref[i];
+                else A.stack_ovf[ovf_slot<BLOCK, STACK>(A, sp)] = ref[i];
+                ++sp;
+            }
+        }
+    }
+    if (next != 0) {
+        node = next;
+    } else if (sp > 0) {
+        --sp;
+        node = sp < STACK ? stack[sp * BLOCK] : A.stack_ovf[ovf_slot<BLOCK, STACK>(A, sp)];
+    } else {
+        node = -1;
+    }
+}
+
 // One child-pair step of the postponed-leaf traversal: leaf children go to the queue (nearer
 // first); node < 0 afterwards means the traversal is finished. Written branch-free (bitwise
 // predicates, selects) so a wave does not split inside the step.
@@ -1193,7 +1271,7 @@ __device__ __forceinline__ void sec_node(const RenderArgs& A, SecRay& R, LdsInt*
     const float uz1 = fmaf(f[8], R.iz, -R.ozi), uz2 = fmaf(f[11], R.iz, -R.ozi);
     const float rmin = fmaxf(fmaxf(fminf(ux1, ux2), fminf(uy1, uy2)), fminf(uz1, uz2));
     const float rmax = fminf(fminf(fmaxf(ux1, ux2), fmaxf(uy1, uy2)), fmaxf(uz1, uz2));
-    const float lim = R.light ? R.lim + kTPad * (1.0f + R.lim) : INFINITY;
+    const float lim = R.plim;
     const bool hl = (nc.x != 0) & (lmax >= fmaxf(lmin, 0.0f)) & (lmin <= lim);
     const bool hr = (nc.y != 0) & (rmax >= fmaxf(rmin, 0.0f)) & (rmin <= lim);
     const bool r_near = rmin < lmin;
@@ -1265,7 +1343,15 @@ __device__ __forceinline__ void list_advance(LeafQueue& Q, int& node) {
 #ifndef VR_WW_NODE_UNROLL
 #define VR_WW_NODE_UNROLL 1
 #endif
+#ifndef VR_WW_MIN_LANES
+#define VR_WW_MIN_LANES 0  // > 0: a NODE / PRIM iteration ends once fewer lanes than this can go on (A/B)
+#endif
 constexpr int kRefillMin = VR_WW_REFILL, kNodeSteps = VR_WW_NODE_STEPS, kPrimSteps = VR_WW_PRIM_STEPS;
+constexpr int kMinLanes = VR_WW_MIN_LANES;
+#ifndef VR_WW_PRIM_BIAS
+#define VR_WW_PRIM_BIAS 100  // a PRIM iteration needs this many % of the lanes a NODE iteration could use (A/B)
+#endif
+constexpr int kPrimBias = VR_WW_PRIM_BIAS;
 constexpr int kPrimUnroll = VR_WW_PRIM_UNROLL, kNodeUnroll = VR_WW_NODE_UNROLL;
 
 // 6 waves/SIMD = 80 VGPRs: the ray state is kept small enough for that without scratch spills (a
@@ -1348,7 +1434,7 @@ __global__ __launch_bounds__(BLOCK, WAVES) void secondary_ww_kernel(RenderArgs A
         const bool can_node = live && node >= 0 && (QCAP == 2 ? Q.n == 0 : Q.n <= QCAP - kRoom);
         const int np = __popcll(__ballot(has_prim)), nn = __popcll(__ballot(can_node));
         // whichever kind more lanes can use; never a kind no lane can use (that would not progress)
-        const bool prim_iter = nn == 0 || (np > 0 && np >= nn);
+        const bool prim_iter = nn == 0 || (np > 0 && np * 100 >= nn * kPrimBias);
         if (prim_iter) {  // PRIM iteration: up to kPrimSteps primitive tests per lane
             LdsInt* ext = stack + STACK * BLOCK;
             // next primitive of the lane: a list member (ls = its slot) or a queued leaf's (ls = -1)
@@ -1435,6 +1521,8 @@ __global__ __launch_bounds__(BLOCK, WAVES) void secondary_ww_kernel(RenderArgs A
                     else wtest(load_wrec(A.wrec, (int)j), j, ls);
                 }
                 go = go && Q.has_prim() && !cut_reached<PURE>(R);
+                if constexpr (kMinLanes > 0)  // too few lanes left to fill a wave: end the iteration
+                    if (k + 1 < kPrimSteps && __popcll(__ballot(go)) < kMinLanes) break;
             }
             diag_lap(kCtrPrimQueries);
         } else {  // NODE iteration: up to kNodeSteps node steps per lane
@@ -1445,10 +1533,13 @@ __global__ __launch_bounds__(BLOCK, WAVES) void secondary_ww_kernel(RenderArgs A
                 if constexpr (S) c.v[kCtrSteps] += (__ballot(go) != 0ull && lane == 0u) ? 1u : 0u;
 #endif
                 if (go) {
-                    if constexpr (W) sec_node4<BLOCK, S, QCAP, STACK>(A, R, stack, sp, node, Q, c);
+                    if constexpr (W && VR_NODE4_V2) sec_node4v<BLOCK, S, QCAP, STACK>(A, R, stack, sp, node, Q, c);
+                    else if constexpr (W) sec_node4<BLOCK, S, QCAP, STACK>(A, R, stack, sp, node, Q, c);
                     else sec_node<BLOCK, S, QCAP, STACK, H>(A, R, stack, sp, node, Q, c);
                 }
                 go = go && node >= 0 && Q.n <= QCAP - kRoom;
+                if constexpr (kMinLanes > 0)
+                    if (k + 1 < kNodeSteps && __popcll(__ballot(go)) < kMinLanes) break;
             }
             diag_lap(kCtrSteps);
         }
@@ -1662,15 +1753,15 @@ hipError_t gauss_march(const RenderArgs& A, hipStream_t stream, bool stats) {
 }
 
 // One launch of the persistent kernel: one resident grid (every CU filled to the kernel's occupancy).
-// LDS words per lane: 18 traversal-stack entries (deeper ones overflow to global memory) + the
-// 8-entry LDS ring of the 9-entry leaf queue = 26 (6 blocks of 256 lanes per CU).
+// LDS words per lane: 14 traversal-stack entries (deeper ones overflow to global memory) + the
+// 8-entry LDS ring of the 9-entry leaf queue = 22 (7 blocks of 256 lanes per CU).
 template <bool S, bool PURE, bool H, bool W>
 static hipError_t ww_launch(const RenderArgs& A, hipStream_t stream) {
 #ifndef VR_WW_STACK
-#define VR_WW_STACK 18  // LDS traversal-stack entries per lane (deeper ones spill to the global overflow)
+#define VR_WW_STACK 14  // LDS traversal-stack entries per lane (deeper ones spill to the global overflow)
 #endif
 #ifndef VR_WW_WAVES
-#define VR_WW_WAVES 6  // waves per SIMD (launch bounds: 80 VGPRs at 6)
+#define VR_WW_WAVES 7  // waves per SIMD (launch bounds: 72 VGPRs at 7; A/B at C4: 7 + 14-entry stack 95.6 ms, 6 + 18 99.2 ms)
 #endif
     constexpr int kStack = VR_WW_STACK, kQueue = 9;
     constexpr int kWaves = PURE ? 5 : VR_WW_WAVES;  // PureRayMarching's marched depth does not fit 80 VGPRs without spills

@@ -250,10 +250,7 @@ __global__ void emit4_kernel(int n, Tree T, Emit E) {
         }
     }
     for (; m < 4; ++m) {
-        for (int k = 0; k < 3; ++k) {
-            w.h[m][k] = 0x7c00u;
-            w.h[m][3 + k] = 0xfc00u;
-        }
+        for (int k = 0; k < 6; ++k) w.h[m][k] = 0x7e00u;  // NaN box: no slab test reports a hit
         w.c[m] = 0;
     }
     E.hnodes4[T.map4[i]] = w;

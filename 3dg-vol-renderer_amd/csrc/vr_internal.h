@@ -57,7 +57,8 @@ struct HNode {
 static_assert(sizeof(HNode) == 32, "half node must be 32 B");
 
 // 4-wide half-precision node for the secondary rays: up to 4 children (boxes as in HNode, same
-// normalisation and outward rounding), collapsed from the child-pair tree. c == 0: empty slot.
+// normalisation and outward rounding), collapsed from the child-pair tree. c == 0: empty slot, whose
+// box is NaN (no slab test reports a hit for it).
 struct HNode4 {
     uint16_t h[4][6];  // child i: min xyz, max xyz
     int32_t c[4];      // > 0: HNode4 index, < 0: leaf ref, 0: empty
