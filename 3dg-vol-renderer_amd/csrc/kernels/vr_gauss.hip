@@ -568,11 +568,12 @@ struct SecRay {
 
 // The ray's optical depth is known to have reached its cut-off. RayMarchingGaussians: tau holds what
 // the tree walk met (list members included), credit the list members' depth it has not met yet, so
-// tau + credit is a lower bound of the final depth (see wtest in secondary_ww_kernel).
+// tau + credit is a lower bound of the final depth (see wtest in secondary_ww_kernel; a credit that a
+// non-member candidate drove below 0 only makes the bound lower).
 template <bool PURE>
 __device__ __forceinline__ bool cut_reached(const SecRay& R) {
     if constexpr (PURE) return R.tau >= R.cut;
-    else return R.tau + fmaxf(R.credit, 0.0f) >= R.cut;
+    else return R.tau + R.credit >= R.cut;
 }
 
 // Slot of Gaussian j in the record's active list, or -1. The list is scanned four entries per
@@ -1335,10 +1336,10 @@ __device__ __forceinline__ void list_advance(LeafQueue& Q, int& node) {
 #define VR_WW_NODE_STEPS 6
 #endif
 #ifndef VR_WW_PRIM_STEPS
-#define VR_WW_PRIM_STEPS 6
+#define VR_WW_PRIM_STEPS 5
 #endif
 #ifndef VR_WW_PRIM_UNROLL
-#define VR_WW_PRIM_UNROLL 6  // unroll of the PRIM iteration's step loop (A/B: code size vs. scheduling)
+#define VR_WW_PRIM_UNROLL 5  // unroll of the PRIM iteration's step loop (A/B: code size vs. scheduling)
 #endif
 #ifndef VR_WW_NODE_UNROLL
 #define VR_WW_NODE_UNROLL 1
@@ -1349,7 +1350,7 @@ __device__ __forceinline__ void list_advance(LeafQueue& Q, int& node) {
 constexpr int kRefillMin = VR_WW_REFILL, kNodeSteps = VR_WW_NODE_STEPS, kPrimSteps = VR_WW_PRIM_STEPS;
 constexpr int kMinLanes = VR_WW_MIN_LANES;
 #ifndef VR_WW_PRIM_BIAS
-#define VR_WW_PRIM_BIAS 100  // a PRIM iteration needs this many % of the lanes a NODE iteration could use (A/B)
+#define VR_WW_PRIM_BIAS 70  // a PRIM iteration needs this many % of the lanes a NODE iteration could use (A/B)
 #endif
 constexpr int kPrimBias = VR_WW_PRIM_BIAS;
 constexpr int kPrimUnroll = VR_WW_PRIM_UNROLL, kNodeUnroll = VR_WW_NODE_UNROLL;
