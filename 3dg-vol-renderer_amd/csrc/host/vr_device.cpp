@@ -26,6 +26,8 @@ hipError_t launch_sfd_loss_diff(const uint32_t* bits0, const uint32_t* bits1, co
                                 uint32_t n, double* out, hipStream_t stream);
 hipError_t gauss_record_cut(const RenderArgs& A, float budget, hipStream_t stream);
 hipError_t gauss_whiten(const GaussianRecord* rec, WRecord* out, uint32_t n, hipStream_t stream);
+hipError_t gauss_bin(const RenderArgs& A, bool emit, hipStream_t stream);
+hipError_t gauss_bin_scan(const uint32_t* cnt, uint32_t* off, uint32_t n, void* tmp, size_t& tmp_bytes, hipStream_t stream);
 hipError_t launch_pixel_losses(const float* img, const float* ref, uint32_t npix, float* out, hipStream_t stream);
 
 hipError_t launch_unshuffle(const float* slabs, uint32_t nslabs, uint32_t tiles_per_slab, uint32_t tiles_x, uint32_t W,
@@ -93,6 +95,7 @@ struct vr_ctx {
     Buf px_first, px_T, rec_pos, rec_meta, rec_next, rec_act, tr, rec_rad, rec_alloc, rec_bloom, slowq;
     Buf pcg_jump, ray_next, stack_ovf, env_order, rec_cut;
     Buf deep;  // march_deep_kernel: pixel queue + global active lists (vr_gauss.hip)
+    Buf bin_cnt, bin_off, bin_ent;  // tile bins of the binned march (VR_OPT_MARCH_BINNED)
     Buf ff_scratch, ff_tail, ff_sum, ff_nee;  // free-flight integrators (vr_freeflight.hip)
     Buf ff_fb;                                // ff_fallback_kernel: path queue + kFFBigCap rows
     uint32_t* d_order = nullptr;      // record (leaf order) -> scene index
@@ -111,6 +114,7 @@ struct vr_ctx {
     int32_t auto_nee_refill = 40;      // shadow-ray kernel refill threshold derived from the uploaded scene
     int64_t opt_ff_nee_queue = 6;      // VR_OPT_FF_NEE_QUEUE
     int64_t opt_device_bvh = 0;        // VR_OPT_DEVICE_BVH
+    int64_t opt_march_binned = 0;      // VR_OPT_MARCH_BINNED
     bool last_upload_device_bvh = false;  // the current scene's tree came from the device builder
     vr_group* group = nullptr;         // vr_init_multi: the devices this context drives (host/vr_multi.cpp)
 };
@@ -541,6 +545,48 @@ vr_status gauss_pipeline(vr_ctx* c, RenderArgs& A, hipStream_t s, bool stats) {
     A.deepq_cap = kDeepQueue;
     A.deep_act = (int32_t*)(A.deepq + kDeepQueue + 1);
 
+    // Tile bins of the binned march: count, scan, then (with one host sync for the entry count) emit.
+    A.bin_off = A.bin_ent = nullptr;
+    A.bin_cnt = A.bin_out = nullptr;
+    if (c->opt_march_binned && A.num_prims > 0) {
+#ifndef VR_BIN_BUCKETS
+#define VR_BIN_BUCKETS 256  // depth buckets per tile (a bucket's hits wait in a 16-entry per-lane list)
+#endif
+        const uint32_t nb = VR_BIN_BUCKETS, nbins = A.num_tiles * nb;
+        if ((st = grow(c->bin_cnt, (nbins + 1) * 4ull, "hipMalloc(bins)")) != VR_OK) return st;
+        if ((st = grow(c->bin_off, (nbins + 1) * 4ull, "hipMalloc(bins)")) != VR_OK) return st;
+        A.bin_nb = nb;
+        {  // depth buckets over [0, the farthest scene-box corner from any ray origin]
+            float r = 0.0f, far = 0.0f;
+            for (int k = 0; k < 3; ++k) r += std::fabs(A.cam_right[k]) + std::fabs(A.cam_up[k]);
+            for (int cn = 0; cn < 8; ++cn) {
+                float d2 = 0.0f;
+                for (int k = 0; k < 3; ++k) {
+                    const float v = ((cn >> k) & 1) ? c->bmax[k] : c->bmin[k];
+                    d2 += (v - A.cam_pos[k]) * (v - A.cam_pos[k]);
+                }
+                far = std::max(far, std::sqrt(d2));
+            }
+            A.bin_dz = std::max((far + r) / (float)nb, 1e-6f);
+        }
+        A.bin_cnt = (uint32_t*)c->bin_cnt.p;
+        HIP_TRY(hipMemsetAsync(A.bin_cnt, 0, (nbins + 1) * 4ull, s), "hipMemsetAsync(bins)");
+        HIP_TRY(gauss_bin(A, false, s), "bin count");
+        size_t tmp = 0;
+        HIP_TRY(gauss_bin_scan(A.bin_cnt, (uint32_t*)c->bin_off.p, nbins + 1, nullptr, tmp, s), "bin scan");
+        if ((st = grow(c->bin_ent, std::max<size_t>(tmp, 64), "hipMalloc(bin scan)")) != VR_OK) return st;
+        HIP_TRY(gauss_bin_scan(A.bin_cnt, (uint32_t*)c->bin_off.p, nbins + 1, c->bin_ent.p, tmp, s), "bin scan");
+        uint32_t total = 0;
+        HIP_TRY(hipMemcpyAsync(&total, (uint32_t*)c->bin_off.p + nbins, 4, hipMemcpyDeviceToHost, s), "bin total D2H");
+        HIP_TRY(hipStreamSynchronize(s), "bin count");
+        if ((st = grow(c->bin_ent, std::max<uint64_t>(total, 1) * 4ull, "hipMalloc(bin entries)")) != VR_OK) return st;
+        A.bin_off = (const uint32_t*)c->bin_off.p;
+        A.bin_out = (uint32_t*)c->bin_ent.p;
+        HIP_TRY(hipMemsetAsync(A.bin_cnt, 0, (nbins + 1) * 4ull, s), "hipMemsetAsync(bins)");
+        HIP_TRY(gauss_bin(A, true, s), "bin emit");
+        A.bin_ent = A.bin_out;
+    }
+
     // Record capacity: from earlier frames of this context (hints), so the host never waits for
     // the march. A context's first frame sizes it: one host sync after the march, re-run with the
     // exact need if it did not fit. A later frame that outgrows the buffers is reported
@@ -869,7 +915,7 @@ void vr_destroy(vr_ctx* c) {
     if (c->h_sizing) (void)hipHostFree(c->h_sizing);
     for (vr_ctx::Buf* b : {&c->px_first, &c->px_T, &c->rec_pos, &c->rec_meta, &c->rec_next, &c->rec_act, &c->tr, &c->rec_rad,
                            &c->rec_alloc, &c->rec_bloom, &c->slowq, &c->pcg_jump, &c->ray_next,
-                           &c->stack_ovf, &c->env_order, &c->rec_cut, &c->ff_scratch, &c->ff_tail, &c->ff_sum, &c->ff_nee, &c->rec_bits[0], &c->rec_bits[1], &c->sfd_tmp, &c->sfd_ref,
+                           &c->stack_ovf, &c->env_order, &c->rec_cut, &c->bin_cnt, &c->bin_off, &c->bin_ent, &c->ff_scratch, &c->ff_tail, &c->ff_sum, &c->ff_nee, &c->rec_bits[0], &c->rec_bits[1], &c->sfd_tmp, &c->sfd_ref,
                            &c->sfd_loss[0], &c->sfd_loss[1], &c->sfd_out})
         if (b->p) (void)hipFree(b->p);
     if (c->d_frame) (void)hipFree(c->d_frame);
@@ -1300,6 +1346,10 @@ vr_status vr_set_option(vr_ctx* c, int32_t option, int64_t value) {
             if (value != 0 && value != 1) return fail(VR_ERR_INVALID, "VR_OPT_DEVICE_BVH must be 0 or 1");
             c->opt_device_bvh = value;
             return VR_OK;
+        case VR_OPT_MARCH_BINNED:
+            if (value != 0 && value != 1) return fail(VR_ERR_INVALID, "VR_OPT_MARCH_BINNED must be 0 or 1");
+            c->opt_march_binned = value;
+            return VR_OK;
         case VR_OPT_RECORD_CAPACITY:
             if ((value != 0 && value < 4096) || value > 0x3fffffff)
                 return fail(VR_ERR_INVALID, "VR_OPT_RECORD_CAPACITY must be 0 or in [4096, 2^30)");
@@ -1320,6 +1370,7 @@ vr_status vr_get_option(vr_ctx* c, int32_t option, int64_t* value) {
         case VR_OPT_RECORD_CAPACITY: *value = (int64_t)c->rec_hint; return VR_OK;
         case VR_OPT_DEVICE_BVH: *value = c->opt_device_bvh; return VR_OK;
         case VR_OPT_FF_NEE_QUEUE: *value = c->opt_ff_nee_queue; return VR_OK;
+        case VR_OPT_MARCH_BINNED: *value = c->opt_march_binned; return VR_OK;
         default: return fail(VR_ERR_INVALID, "vr_get_option: unknown option " + std::to_string(option));
     }
 }

@@ -36,6 +36,8 @@
 
 #include <type_traits>
 
+#include <hipcub/hipcub.hpp>
+
 #include "vr_dev_common.h"
 
 namespace vr {
@@ -212,6 +214,150 @@ __device__ __forceinline__ float tail_weight(const RenderArgs& A, float x, float
     return fmaxf(fmaxf(w0, w1), w2) * (1.0f + sigma_t * A.step_size);
 }
 
+// One step k of a pixel's march once its entrants are in `act` (test_integrators.h:202-289): retire
+// the Gaussians that exited (b <= t_k), sigma at the position (gmm.h:98-126), the step's optical depth
+// (:146-157), a scatter record if sigma_s > 0, T. Returns false once the march ends (T == 0 or the
+// early-out). COOP: one pixel per wave (see march).
+template <bool S, bool COOP>
+__device__ __forceinline__ bool march_step(const RenderArgs& A, const Ray& ray, uint32_t p, int px, int py, int k, float t_k,
+                                           ActList& act, float& T, uint32_t& prev, Ctr& c, bool writer) {
+    const GaussianRecord* __restrict__ G = A.gauss;
+    const float step = A.step_size;
+    // retire (b <= t_k); sigma at pos (gmm.h:98-126); the step's optical depth (:146-157)
+    const float px_ = ray.ox + t_k * ray.dx;
+    const float py_ = ray.oy + t_k * ray.dy;
+    const float pz_ = ray.oz + t_k * ray.dz;
+    const float t_k1 = t_k + step;  // `t + step_size` (test_integrators.h:286)
+    float smu = 0.0f, smua = 0.0f, tau_seg = 0.0f;
+    int w = 0;
+    if constexpr (COOP) {
+        const int lane = (int)__lane_id();
+        for (int i0 = 0; i0 < act.n; i0 += 64) {  // (compaction writes stay below i0 + 64)
+            const int i = i0 + lane;
+            int j = 0;
+            bool surv = false;
+            float m = 0.0f, ma = 0.0f, od = 0.0f;
+            if (i < act.n) {
+                j = act.get(i);
+                GRec g = load_rec(G, j);
+                Quad q = quad(g, ray);
+                float a, b;
+                if (intersect(q, a, b) && b > t_k) {
+                    surv = true;
+                    m = mu_t(g, px_, py_, pz_);
+                    ma = m * g.albedo;
+                    if (!A.pure) od = optical_depth(g, q, t_k, t_k1);
+                }
+            }
+            for (uint64_t sm = __ballot(surv); sm; sm &= sm - 1) {  // survivors in list order
+                const int sl = __ffsll((unsigned long long)sm) - 1;
+                act.set(w++, __shfl(j, sl, 64));
+                smu += __shfl(m, sl, 64);
+                smua += __shfl(ma, sl, 64);
+                if (!A.pure) tau_seg += __shfl(od, sl, 64);
+                if constexpr (S) {
+                    c.v[kCtrMu]++;
+                    c.v[kCtrOD]++;
+                    c.v[kCtrPrims]++;
+                }
+            }
+        }
+    } else {
+        for (int i = 0; i < act.n; ++i) {
+            int j = act.get(i);
+            GRec g = load_rec(G, j);
+            Quad q = quad(g, ray);
+            float a, b;
+            if (!intersect(q, a, b) || b <= t_k) continue;
+            act.set(w++, j);
+            float m = mu_t(g, px_, py_, pz_);
+            smu += m;
+            smua += m * g.albedo;
+            if (!A.pure) tau_seg += optical_depth(g, q, t_k, t_k1);
+            if constexpr (S) {
+                c.v[kCtrMu]++;
+                c.v[kCtrOD]++;
+                c.v[kCtrPrims]++;
+            }
+        }
+    }
+    act.n = w;
+    if (w == 0) return true;
+    if constexpr (S) c.v[kCtrSteps]++;
+    float sigma_s = 0.0f;
+    if (smu > 0.0f) {
+        float a_mix = smua / smu;
+        sigma_s = a_mix * smu;
+    }
+    if (sigma_s > 0.0f) {  // scattering step -> one record
+        uint32_t r, o = 0;
+        if constexpr (COOP) {  // one pixel per wave: lane 0 allocates
+            uint32_t base = 0;
+            if (writer) {
+                base = atomicAdd(&A.rec_alloc[0], 1u);
+                if (w > kActInline) o = atomicAdd(&A.rec_alloc[1], (uint32_t)w);
+            }
+            r = (uint32_t)__builtin_amdgcn_readfirstlane((int)base);
+            o = (uint32_t)__builtin_amdgcn_readfirstlane((int)o);
+        } else {
+            // lanes emitting now share one atomic (this branch is divergent: ballot = them)
+            const uint64_t m = __ballot(true);
+            const uint32_t leader = (uint32_t)__ffsll((unsigned long long)m) - 1u;
+            uint32_t base = 0;
+            if (__lane_id() == leader) base = atomicAdd(&A.rec_alloc[0], (uint32_t)__popcll(m));
+            base = (uint32_t)__builtin_amdgcn_readlane((int)base, (int)leader);
+            r = base + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+            if (w > kActInline) o = atomicAdd(&A.rec_alloc[1], (uint32_t)w);  // rare: the overflow pool
+        }
+        uint32_t aoff = r * (uint32_t)kActInline;
+        bool fits = r < A.rec_cap;
+        if (w > kActInline) {  // long active lists go to the overflow pool
+            aoff = A.rec_cap * (uint32_t)kActInline + o;
+            fits = fits && o + (uint32_t)w <= A.act_ovf_cap;
+        }
+        if (fits) {
+            uint64_t bl = 0;
+            for (int i = 0; i < w; ++i) {
+                const int j = act.get(i);
+                if (COOP ? (i & 63) == (int)__lane_id() : true) A.rec_act[aoff + i] = j;
+                bl |= 1ull << (j & 63);
+            }
+            if (writer) {
+                A.rec_pos[r] = make_float4(px_, py_, pz_, T * sigma_s);
+                A.rec_meta[r] = make_uint4((uint32_t)px | ((uint32_t)py << 16), (uint32_t)k, aoff, (uint32_t)w);
+                A.rec_bloom[r] = bl;
+                A.rec_next[r] = kNoRecord;
+                if (prev == kNoRecord) A.px_first[p] = r;
+                else A.rec_next[prev] = r;
+            }
+            prev = r;
+        } else if (writer) {
+            A.rec_alloc[2] = 1u;  // capacity exceeded: the frame is reported and rendered again
+            if (r < A.rec_cap) {  // a slot inside [0, nrec) whose active list did not fit the pool:
+                // the later stages still read it (the host does not wait for the march), so
+                // it must be a valid record, not the previous frame's: an empty one
+                A.rec_pos[r] = make_float4(px_, py_, pz_, 0.0f);
+                A.rec_meta[r] = make_uint4((uint32_t)px | ((uint32_t)py << 16), (uint32_t)k, 0u, 0u);
+                A.rec_bloom[r] = 0ull;
+                A.rec_next[r] = kNoRecord;
+            }
+        }
+    }
+    if (A.pure) {  // integrator.h:196-198, 259: T *= exp(-sigma_t * step), sigma_t = sigma_a + sigma_s
+        float sa = 0.0f, ss = 0.0f;
+        if (smu > 0.0f) {
+            const float a_mix = smua / smu;
+            ss = a_mix * smu;
+            sa = (1.0f - a_mix) * smu;
+        }
+        T *= expf(-(sa + ss) * step);
+    } else {
+        T *= expf(-tau_seg);
+    }
+    if (T <= 0.0f) return false;  // exact: nothing after this step can add to L or to T * env
+    return !(A.t_eps > 0.0f && T * tail_weight(A, px_, py_, pz_, smu) <= A.t_eps);
+}
+
 // One pass: each scattering step allocates its record with a wave-aggregated atomic and links it
 // to the pixel's previous record (px_first / rec_next), so a pixel's records are visited in step
 // order by accumulate_kernel wherever they landed in memory. Records that do not fit the
@@ -305,139 +451,7 @@ __device__ int march(const RenderArgs& A, uint32_t p, int px, int py, int* act_b
                 });
             if (ovf || !ok) return kOverflow;
             kq = k + 1;
-            // retire (b <= t_k); sigma at pos (gmm.h:98-126); the step's optical depth (:146-157)
-            const float px_ = ray.ox + t_k * ray.dx;
-            const float py_ = ray.oy + t_k * ray.dy;
-            const float pz_ = ray.oz + t_k * ray.dz;
-            const float t_k1 = t_k + step;  // `t + step_size` (test_integrators.h:286)
-            float smu = 0.0f, smua = 0.0f, tau_seg = 0.0f;
-            int w = 0;
-            if constexpr (COOP) {
-                const int lane = (int)__lane_id();
-                for (int i0 = 0; i0 < act.n; i0 += 64) {  // (compaction writes stay below i0 + 64)
-                    const int i = i0 + lane;
-                    int j = 0;
-                    bool surv = false;
-                    float m = 0.0f, ma = 0.0f, od = 0.0f;
-                    if (i < act.n) {
-                        j = act.get(i);
-                        GRec g = load_rec(G, j);
-                        Quad q = quad(g, ray);
-                        float a, b;
-                        if (intersect(q, a, b) && b > t_k) {
-                            surv = true;
-                            m = mu_t(g, px_, py_, pz_);
-                            ma = m * g.albedo;
-                            if (!A.pure) od = optical_depth(g, q, t_k, t_k1);
-                        }
-                    }
-                    for (uint64_t sm = __ballot(surv); sm; sm &= sm - 1) {  // survivors in list order
-                        const int sl = __ffsll((unsigned long long)sm) - 1;
-                        act.set(w++, __shfl(j, sl, 64));
-                        smu += __shfl(m, sl, 64);
-                        smua += __shfl(ma, sl, 64);
-                        if (!A.pure) tau_seg += __shfl(od, sl, 64);
-                        if constexpr (S) {
-                            c.v[kCtrMu]++;
-                            c.v[kCtrOD]++;
-                            c.v[kCtrPrims]++;
-                        }
-                    }
-                }
-            } else {
-                for (int i = 0; i < act.n; ++i) {
-                    int j = act.get(i);
-                    GRec g = load_rec(G, j);
-                    Quad q = quad(g, ray);
-                    float a, b;
-                    if (!intersect(q, a, b) || b <= t_k) continue;
-                    act.set(w++, j);
-                    float m = mu_t(g, px_, py_, pz_);
-                    smu += m;
-                    smua += m * g.albedo;
-                    if (!A.pure) tau_seg += optical_depth(g, q, t_k, t_k1);
-                    if constexpr (S) {
-                        c.v[kCtrMu]++;
-                        c.v[kCtrOD]++;
-                        c.v[kCtrPrims]++;
-                    }
-                }
-            }
-            act.n = w;
-            if (w == 0) continue;
-            if constexpr (S) c.v[kCtrSteps]++;
-            float sigma_s = 0.0f;
-            if (smu > 0.0f) {
-                float a_mix = smua / smu;
-                sigma_s = a_mix * smu;
-            }
-            if (sigma_s > 0.0f) {  // scattering step -> one record
-                uint32_t r, o = 0;
-                if constexpr (COOP) {  // one pixel per wave: lane 0 allocates
-                    uint32_t base = 0;
-                    if (writer) {
-                        base = atomicAdd(&A.rec_alloc[0], 1u);
-                        if (w > kActInline) o = atomicAdd(&A.rec_alloc[1], (uint32_t)w);
-                    }
-                    r = (uint32_t)__builtin_amdgcn_readfirstlane((int)base);
-                    o = (uint32_t)__builtin_amdgcn_readfirstlane((int)o);
-                } else {
-                    // lanes emitting now share one atomic (this branch is divergent: ballot = them)
-                    const uint64_t m = __ballot(true);
-                    const uint32_t leader = (uint32_t)__ffsll((unsigned long long)m) - 1u;
-                    uint32_t base = 0;
-                    if (__lane_id() == leader) base = atomicAdd(&A.rec_alloc[0], (uint32_t)__popcll(m));
-                    base = (uint32_t)__builtin_amdgcn_readlane((int)base, (int)leader);
-                    r = base + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
-                    if (w > kActInline) o = atomicAdd(&A.rec_alloc[1], (uint32_t)w);  // rare: the overflow pool
-                }
-                uint32_t aoff = r * (uint32_t)kActInline;
-                bool fits = r < A.rec_cap;
-                if (w > kActInline) {  // long active lists go to the overflow pool
-                    aoff = A.rec_cap * (uint32_t)kActInline + o;
-                    fits = fits && o + (uint32_t)w <= A.act_ovf_cap;
-                }
-                if (fits) {
-                    uint64_t bl = 0;
-                    for (int i = 0; i < w; ++i) {
-                        const int j = act.get(i);
-                        if (COOP ? (i & 63) == (int)__lane_id() : true) A.rec_act[aoff + i] = j;
-                        bl |= 1ull << (j & 63);
-                    }
-                    if (writer) {
-                        A.rec_pos[r] = make_float4(px_, py_, pz_, T * sigma_s);
-                        A.rec_meta[r] = make_uint4((uint32_t)px | ((uint32_t)py << 16), (uint32_t)k, aoff, (uint32_t)w);
-                        A.rec_bloom[r] = bl;
-                        A.rec_next[r] = kNoRecord;
-                        if (prev == kNoRecord) A.px_first[p] = r;
-                        else A.rec_next[prev] = r;
-                    }
-                    prev = r;
-                } else if (writer) {
-                    A.rec_alloc[2] = 1u;  // capacity exceeded: the frame is reported and rendered again
-                    if (r < A.rec_cap) {  // a slot inside [0, nrec) whose active list did not fit the pool:
-                        // the later stages still read it (the host does not wait for the march), so
-                        // it must be a valid record, not the previous frame's: an empty one
-                        A.rec_pos[r] = make_float4(px_, py_, pz_, 0.0f);
-                        A.rec_meta[r] = make_uint4((uint32_t)px | ((uint32_t)py << 16), (uint32_t)k, 0u, 0u);
-                        A.rec_bloom[r] = 0ull;
-                        A.rec_next[r] = kNoRecord;
-                    }
-                }
-            }
-            if (A.pure) {  // integrator.h:196-198, 259: T *= exp(-sigma_t * step), sigma_t = sigma_a + sigma_s
-                float sa = 0.0f, ss = 0.0f;
-                if (smu > 0.0f) {
-                    const float a_mix = smua / smu;
-                    ss = a_mix * smu;
-                    sa = (1.0f - a_mix) * smu;
-                }
-                T *= expf(-(sa + ss) * step);
-            } else {
-                T *= expf(-tau_seg);
-            }
-            if (T <= 0.0f) break;  // exact: nothing after this step can add to L or to T * env
-            if (A.t_eps > 0.0f && T * tail_weight(A, px_, py_, pz_, smu) <= A.t_eps) break;
+            if (!march_step<S, COOP>(A, ray, p, px, py, k, t_k, act, T, prev, c, writer)) break;
         }
     }
     if (writer) A.px_T[p] = T;
@@ -531,6 +545,292 @@ __global__ __launch_bounds__(kDeepBlock) void march_deep_kernel(RenderArgs A) {
         if constexpr (S)
             for (int i = 0; i < kNumCtr; ++i) atomicAdd(A.work + i, (unsigned long long)c.v[i]);
         if (st != kOK) mark_error(A, p);
+    }
+}
+
+// ---------------------------------------------------------------------------------------------
+// Stage 1, binned variant (VR_OPT_MARCH_BINNED; A/B against the BVH window queries):
+// every record is binned to the 16x16 tiles its 3.15-sigma box can project onto, by a depth bucket of
+// a lower bound of the entry distance of the tile's pixel rays; a quarter-tile wave then streams its
+// tile's entries bucket by bucket (wave-uniform: scalar loads of index and record), tests each against
+// every lane's ray with the exact intersect, keeps the hits that have not entered yet in a per-lane
+// pending list sorted by entry distance, and marches every step that lies before the next bucket's
+// lower bound (no later entry can enter at or before it). The active lists, steps and records are
+// those of march(): the same intersect decides every entry, the same march_step evaluates.
+// ---------------------------------------------------------------------------------------------
+#ifndef VR_BIN_PEND
+#define VR_BIN_PEND 48
+#endif
+constexpr int kPendCap = VR_BIN_PEND;  // pending entries per lane (more: the pixel re-runs in march_fallback_kernel)
+constexpr int kBinAct = 16;      // active Gaussians per lane (as march_kernel's)
+
+// The pixel rectangle (inclusive, clamped to the frame) that the box [lo, hi] can project onto, and
+// false if it projects onto nothing; all = true when the box reaches the pinhole's side of the image
+// plane (then every tile).
+__device__ __forceinline__ bool bin_rect(const RenderArgs& A, const float* lo, const float* hi, int& x0, int& x1, int& y0,
+                                         int& y1) {
+    const float* R = A.cam_right;
+    const float* U = A.cam_up;
+    const float n0 = R[1] * U[2] - R[2] * U[1], n1 = R[2] * U[0] - R[0] * U[2], n2 = R[0] * U[1] - R[1] * U[0];
+    const float rr = R[0] * R[0] + R[1] * R[1] + R[2] * R[2], uu = U[0] * U[0] + U[1] * U[1] + U[2] * U[2];
+    float umin = INFINITY, umax = -INFINITY, vmin = INFINITY, vmax = -INFINITY;
+    bool all = false;
+    for (int c = 0; c < 8; ++c) {
+        const float X[3] = {(c & 1) ? hi[0] : lo[0], (c & 2) ? hi[1] : lo[1], (c & 4) ? hi[2] : lo[2]};
+        float o[3];
+        if (A.cam_type == 0) {  // the ray from o passes through the pinhole P: o = P + s (X - P) on the plane
+            const float* P = A.cam_pinhole;
+            const float pn = (P[0] - A.cam_pos[0]) * n0 + (P[1] - A.cam_pos[1]) * n1 + (P[2] - A.cam_pos[2]) * n2;
+            const float xn = (X[0] - P[0]) * n0 + (X[1] - P[1]) * n1 + (X[2] - P[2]) * n2;
+            if (!(xn * pn > 1e-6f * fabsf(pn) * (fabsf(pn) + fabsf(xn)))) {  // not strictly beyond the pinhole
+                all = true;
+                break;
+            }
+            const float sc = -pn / xn;
+            for (int k = 0; k < 3; ++k) o[k] = P[k] + sc * (X[k] - P[k]);
+        } else {  // orthographic: along the view direction onto the plane
+            const float* V = A.cam_view;
+            const float vn = V[0] * n0 + V[1] * n1 + V[2] * n2;
+            if (!(fabsf(vn) > 0.0f)) {
+                all = true;
+                break;
+            }
+            const float lam = ((X[0] - A.cam_pos[0]) * n0 + (X[1] - A.cam_pos[1]) * n1 + (X[2] - A.cam_pos[2]) * n2) / vn;
+            for (int k = 0; k < 3; ++k) o[k] = X[k] - lam * V[k];
+        }
+        const float d0 = o[0] - A.cam_pos[0], d1 = o[1] - A.cam_pos[1], d2 = o[2] - A.cam_pos[2];
+        const float u = (d0 * R[0] + d1 * R[1] + d2 * R[2]) / rr, v = (d0 * U[0] + d1 * U[1] + d2 * U[2]) / uu;
+        umin = fminf(umin, u);
+        umax = fmaxf(umax, u);
+        vmin = fminf(vmin, v);
+        vmax = fmaxf(vmax, v);
+    }
+    const float W = (float)A.width, H = (float)A.height;
+    float fx0, fx1, fy0, fy1;
+    if (all) {
+        fx0 = fy0 = 0.0f;
+        fx1 = W;
+        fy1 = H;
+    } else if (A.cam_type == 0) {  // u = 1 - 2 (x + .5) / W, v = 2 (y + .5) / H - 1
+        fx0 = (1.0f - umax) * 0.5f * W - 0.5f;
+        fx1 = (1.0f - umin) * 0.5f * W - 0.5f;
+        fy0 = (vmin + 1.0f) * 0.5f * H - 0.5f;
+        fy1 = (vmax + 1.0f) * 0.5f * H - 0.5f;
+    } else {  // u = 2 (x + .5) / W - 1, v = 1 - 2 (y + .5) / H
+        fx0 = (umin + 1.0f) * 0.5f * W - 0.5f;
+        fx1 = (umax + 1.0f) * 0.5f * W - 0.5f;
+        fy0 = (1.0f - vmax) * 0.5f * H - 0.5f;
+        fy1 = (1.0f - vmin) * 0.5f * H - 0.5f;
+    }
+    // two pixels of slack for rounding (directions, the box's own projection)
+    x0 = (int)fmaxf(floorf(fx0) - 2.0f, 0.0f);
+    y0 = (int)fmaxf(floorf(fy0) - 2.0f, 0.0f);
+    x1 = (int)fminf(ceilf(fx1) + 2.0f, W - 1.0f);
+    y1 = (int)fminf(ceilf(fy1) + 2.0f, H - 1.0f);
+    return fx1 + 2.0f >= 0.0f && fy1 + 2.0f >= 0.0f && fx0 - 2.0f <= W && fy0 - 2.0f <= H;
+}
+
+// 3.15-sigma box of record j (Sigma = M^-1 in double; the intersect's 3-sigma ellipsoid of the f32 M
+// lies inside with a 5 % margin, as the BVH boxes).
+__device__ __forceinline__ void bin_box(const GaussianRecord& g, float* lo, float* hi) {
+    const double m00 = g.m00, m01 = g.m01, m02 = g.m02, m11 = g.m11, m12 = g.m12, m22 = g.m22;
+    const double c00 = m11 * m22 - m12 * m12, c11 = m00 * m22 - m02 * m02, c22 = m00 * m11 - m01 * m01;
+    const double det = m00 * c00 - m01 * (m01 * m22 - m12 * m02) + m02 * (m01 * m12 - m11 * m02);
+    const double s[3] = {c00 / det, c11 / det, c22 / det};
+    const float m[3] = {g.mx, g.my, g.mz};
+    for (int k = 0; k < 3; ++k) {
+        const float e = (float)(3.15 * sqrt(fmax(s[k], 0.0)));
+        const bool ok = det > 0.0 && e == e;
+        lo[k] = ok ? m[k] - e : -INFINITY;
+        hi[k] = ok ? m[k] + e : INFINITY;
+    }
+}
+
+// Tile tile_local (of this call's strided tile set) if global tile (tx, ty) belongs to it, else -1.
+__device__ __forceinline__ int local_tile(const RenderArgs& A, uint32_t tx, uint32_t ty) {
+    const uint32_t g = ty * A.tiles_x + tx;
+    if (g < A.first_tile) return -1;
+    const uint32_t d = g - A.first_tile;
+    if (d % A.tile_stride) return -1;
+    const uint32_t t = d / A.tile_stride;
+    return t < A.num_tiles ? (int)t : -1;
+}
+
+// Lower bound of the entry distance into box [lo, hi] of every pixel ray of global tile (tx, ty): the
+// distance from the tile's central ray origin less the half diagonal of its origins (|d| = 1, so a
+// ray's t is the distance from its origin), less a relative margin for rounding.
+__device__ __forceinline__ float bin_key(const RenderArgs& A, uint32_t tx, uint32_t ty, const float* lo, const float* hi,
+                                         float hd) {
+    const float cx = (float)(tx * kTile) + 0.5f * kTile, cy = (float)(ty * kTile) + 0.5f * kTile;
+    const float uvx = cx / (float)A.width, uvy = cy / (float)A.height;
+    const float u = A.cam_type == 0 ? 1.0f - 2.0f * uvx : 2.0f * uvx - 1.0f;
+    const float v = A.cam_type == 0 ? 2.0f * uvy - 1.0f : 1.0f - 2.0f * uvy;
+    float d2 = 0.0f;
+    for (int k = 0; k < 3; ++k) {
+        const float o = A.cam_pos[k] + u * A.cam_right[k] + v * A.cam_up[k];
+        const float e = fmaxf(fmaxf(lo[k] - o, o - hi[k]), 0.0f);
+        d2 += e * e;
+    }
+    return fmaxf((sqrtf(d2) - hd) * (1.0f - 1e-4f) - 1e-4f, 0.0f);
+}
+
+__device__ __forceinline__ float bin_half_diag(const RenderArgs& A) {
+    const float* R = A.cam_right;
+    const float* U = A.cam_up;
+    const float du = 2.0f * kTile / (float)A.width * sqrtf(R[0] * R[0] + R[1] * R[1] + R[2] * R[2]);
+    const float dv = 2.0f * kTile / (float)A.height * sqrtf(U[0] * U[0] + U[1] * U[1] + U[2] * U[2]);
+    return 0.5f * sqrtf(du * du + dv * dv);
+}
+
+// EMIT = false: count the entries of every bin; true: write them at bin_off + a cursor per bin.
+template <bool EMIT>
+__global__ __launch_bounds__(256) void bin_kernel(RenderArgs A) {
+    const float hd = bin_half_diag(A);
+    const uint32_t nb = A.bin_nb;
+    for (uint32_t j = blockIdx.x * 256u + threadIdx.x; j < (uint32_t)A.num_prims; j += gridDim.x * 256u) {
+        const GaussianRecord g = A.gauss[j];
+        float lo[3], hi[3];
+        bin_box(g, lo, hi);
+        int x0, x1, y0, y1;
+        if (!bin_rect(A, lo, hi, x0, x1, y0, y1)) continue;
+        for (uint32_t ty = (uint32_t)y0 / kTile; ty <= (uint32_t)y1 / kTile; ++ty)
+            for (uint32_t tx = (uint32_t)x0 / kTile; tx <= (uint32_t)x1 / kTile; ++tx) {
+                const int t = local_tile(A, tx, ty);
+                if (t < 0) continue;
+                const uint32_t b = min(nb - 1u, (uint32_t)(bin_key(A, tx, ty, lo, hi, hd) / A.bin_dz));
+                const uint32_t bin = (uint32_t)t * nb + b;
+                if constexpr (EMIT) {
+                    const uint32_t pos = A.bin_off[bin] + atomicAdd(&A.bin_cnt[bin], 1u);
+                    A.bin_out[pos] = j;
+                } else {
+                    atomicAdd(&A.bin_cnt[bin], 1u);
+                }
+            }
+    }
+}
+
+// The binned march of one quarter tile (a wave, one lane per pixel). Returns the per-lane status.
+template <bool S>
+__global__ __launch_bounds__(64) void march_binned_kernel(RenderArgs A) {
+    __shared__ float s_pa[kPendCap * 64];  // pending entries, sorted by entry distance, largest first
+    __shared__ int s_pj[kPendCap * 64];
+    __shared__ int s_act[kBinAct * 64];
+    const uint32_t q = xcd_tile(blockIdx.x, gridDim.x);
+    const uint32_t tile_local = q >> 2;
+    const int lane = (int)threadIdx.x;
+    const int tid = (int)((q & 3u) * 64u) + lane;
+    const uint32_t p = tile_local * 256u + (uint32_t)tid;
+    int lx, ly, x, y;
+    tile_pixel(A, tile_local, tid, lx, ly, x, y);
+    Ctr c{};
+    const bool valid = x < (int)A.width && y < (int)A.height;
+    const Ray ray = primary_ray(A, x, y);
+    float* pa = s_pa + lane;
+    int* pj = s_pj + lane;
+    ActList act{s_act + lane, 64, 0, 0};
+    float T = 1.0f;
+    uint32_t prev = kNoRecord;
+    int np = 0, kq = 0, st = kOK;
+    float t_lo = -1.0f;
+    bool done = !valid;
+    if (valid) A.px_first[p] = kNoRecord;
+    const float* __restrict__ ts = A.tsteps;
+    const int nts = A.num_tsteps;
+    // every step before `bound` (no entry of a later bucket can enter at or before it)
+    auto march_to = [&](float bound) {
+        for (;;) {
+            int k;
+            if (act.n == 0) {
+                if (np == 0) return;
+                k = kfirst(ts, nts, A.step_size, pa[(np - 1) * 64]);  // the closest entry after t_lo
+            } else {
+                k = kq;
+            }
+            if (k >= nts - 1) {
+                st = kError;
+                done = true;
+                return;
+            }
+            const float t_k = ts[k];
+            if (!(t_k < bound)) return;
+            while (np > 0 && pa[(np - 1) * 64] <= t_k) {  // entrants: entered at or before t_k, still inside
+                const int j = pj[--np * 64];
+                if constexpr (S) c.v[kCtrPrims]++;
+                float a, b;
+                if (!intersect(quad(load_rec(A.gauss, j), ray), a, b) || !(b > t_k)) continue;
+                if (act.n >= kBinAct) {
+                    if constexpr (S) c.v[kCtrSecRays]++;  // (instrumented build: overflow causes)
+                    st = kOverflow;
+                    done = true;
+                    return;
+                }
+                int i = act.n;  // sorted insert (index order, gmm.h:98-126)
+                while (i > 0 && act.get(i - 1) > j) {
+                    act.set(i, act.get(i - 1));
+                    --i;
+                }
+                act.set(i, j);
+                act.n++;
+            }
+            kq = k + 1;
+            t_lo = t_k;
+            if (!march_step<S, false>(A, ray, p, x, y, k, t_k, act, T, prev, c, true)) {
+                done = true;
+                return;
+            }
+        }
+    };
+    if (A.num_prims > 0) {
+        const uint32_t nb = A.bin_nb;
+        const uint32_t* __restrict__ off = A.bin_off + tile_local * nb;
+        for (uint32_t b = 0;; ++b) {  // wave-uniform: bucket by bucket
+            while (b < nb && off[b] == off[b + 1]) ++b;  // (empty buckets)
+            // every entry of bucket b on enters at or after b * dz: march the steps before it first
+            if (!done) march_to(b < nb ? (float)b * A.bin_dz : INFINITY);
+            if (b >= nb || __ballot(!done) == 0ull) break;
+            for (uint32_t pos = off[b]; pos < off[b + 1]; ++pos) {
+                const int j = (int)A.bin_ent[pos];
+                if (!done) {
+                    if constexpr (S) c.v[kCtrPrims]++;
+                    float ta, tb;
+                    if (intersect(quad(load_rec(A.gauss, j), ray), ta, tb)) {
+                        if (!(ta > t_lo)) {  // (a key below its bound: the exact BVH march re-runs the pixel)
+                            if constexpr (S) c.v[kCtrPrimQueries]++;
+                            st = kOverflow;
+                            done = true;
+                        } else if (np >= kPendCap) {
+                            if constexpr (S) c.v[kCtrNodes]++;
+                            st = kOverflow;
+                            done = true;
+                        } else {
+                            int i = np++;  // sorted insert, largest entry distance first
+                            while (i > 0 && pa[(i - 1) * 64] < ta) {
+                                pa[i * 64] = pa[(i - 1) * 64];
+                                pj[i * 64] = pj[(i - 1) * 64];
+                                --i;
+                            }
+                            pa[i * 64] = ta;
+                            pj[i * 64] = j;
+                        }
+                    }
+                }
+            }
+        }
+    }
+    if (valid && st == kOK) A.px_T[p] = T;
+    if constexpr (S) {
+        c.v[kCtrPixels] += valid ? 1u : 0u;
+        flush_counters(A.work, c);
+    }
+    if (!valid) {
+        A.px_first[p] = kNoRecord;
+        A.px_T[p] = 0.0f;
+    } else if (st == kOverflow) {
+        uint32_t slot = atomicAdd(A.queue, 1u);
+        if (slot < A.queue_cap) A.queue[1 + slot] = p;
+        else mark_error(A, p);
+    } else if (st == kError) {
+        mark_error(A, p);
     }
 }
 
@@ -1724,13 +2024,26 @@ constexpr int kActFast = 16, kBlockFast = VR_MARCH_BLOCK;
 constexpr int kActFallback = 64, kBlockFallback = 64;
 constexpr int kBlockSecondary = 256;
 
+hipError_t gauss_bin(const RenderArgs& A, bool emit, hipStream_t stream) {
+    const unsigned grid = (unsigned)std::min<uint64_t>(((uint64_t)A.num_prims + 255) / 256, 16384);
+    if (emit) hipLaunchKernelGGL(dev::bin_kernel<true>, dim3(std::max(grid, 1u)), dim3(256), 0, stream, A);
+    else hipLaunchKernelGGL(dev::bin_kernel<false>, dim3(std::max(grid, 1u)), dim3(256), 0, stream, A);
+    return hipGetLastError();
+}
+
+hipError_t gauss_bin_scan(const uint32_t* cnt, uint32_t* off, uint32_t n, void* tmp, size_t& tmp_bytes, hipStream_t stream) {
+    return hipcub::DeviceScan::ExclusiveSum(tmp, tmp_bytes, cnt, off, (int)n, stream);
+}
+
 template <bool S, bool H>
 static hipError_t march_pass(const RenderArgs& A, hipStream_t stream) {
     // LDS per 256-lane workgroup = (active-list slots + stack entries) * 1 KiB. Shallow trees use a
     // 24-entry stack; the 16-slot active list overflows to the 64-slot fallback kernel. H: the
     // half-precision node copy (boxes only propose candidates; every decision is the exact quadratic).
     const bool shallow = A.bvh_depth <= kShallowStack + 1;
-    if (H && A.hnodes4 != nullptr)  // 4-wide tree; a query that could overflow the stack goes to the fallback
+    if (A.bin_ent != nullptr)  // binned march (its overflowing pixels re-run in the BVH fallback below)
+        hipLaunchKernelGGL((dev::march_binned_kernel<S>), dim3(A.num_tiles * 4), dim3(64), 0, stream, A);
+    else if (H && A.hnodes4 != nullptr)  // 4-wide tree; a query that could overflow the stack goes to the fallback
         hipLaunchKernelGGL((dev::march_kernel<kActFast, kBlockFast, S, kShallowStack, true, true>), dim3(A.num_tiles * (256 / kBlockFast)),
                            dim3(kBlockFast), 0, stream, A);
     else if (shallow)

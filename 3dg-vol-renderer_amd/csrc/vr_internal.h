@@ -124,6 +124,16 @@ struct RenderArgs {
     // scene
     const GaussianRecord* gauss;
     const WRecord* wrec;      // whitened copy of gauss (secondary rays of RayMarchingGaussians)
+    // tile bins of the binned march (VR_OPT_MARCH_BINNED; nullptr: the BVH march): bin (tile_local,
+    // depth bucket b) = entries bin_ent[bin_off[tile_local * bin_nb + b] ..), each a record index:
+    // the records whose 3.15-sigma box may hold a point of the tile's pixel rays at ray distance
+    // >= b * bin_dz (the bucket's lower bound of every entry distance of those rays)
+    const uint32_t* bin_off;
+    const uint32_t* bin_ent;
+    uint32_t* bin_cnt;        // binning scratch: per-bin counts, then per-bin cursors
+    uint32_t* bin_out;        // binning output (bin_ent while it is being written)
+    uint32_t bin_nb;
+    float bin_dz;
     const BVHNode* nodes;
     const HNode* hnodes;      // nullptr: the scene is not suited to half-precision boxes (see vr_device.cpp)
     const HNode4* hnodes4;    // 4-wide collapse of the same tree (secondary rays); nullptr with hnodes

@@ -373,7 +373,8 @@ class Device:
 
     OPTIONS = {"half_nodes": L.VR_OPT_HALF_NODES, "secondary_budget": L.VR_OPT_SECONDARY_BUDGET,
                "ff_window0": L.VR_OPT_FF_WINDOW0, "record_capacity": L.VR_OPT_RECORD_CAPACITY,
-               "device_bvh": L.VR_OPT_DEVICE_BVH, "ff_nee_queue": L.VR_OPT_FF_NEE_QUEUE}
+               "device_bvh": L.VR_OPT_DEVICE_BVH, "ff_nee_queue": L.VR_OPT_FF_NEE_QUEUE,
+               "march_binned": L.VR_OPT_MARCH_BINNED}
 
     def set_option(self, name, value):
         """vr_set_option (include/vr_hip.h): explicit per-context tuning (half_nodes applies at the

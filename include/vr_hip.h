@@ -344,12 +344,16 @@ typedef enum vr_option {
                                     vr_lbvh.hip) for scenes of >= 256 Gaussians — the fast path for the
                                     inverse loop's re-upload after every parameter update. Results are
                                     identical up to summation order (the event set is tree-independent). */
-    VR_OPT_FF_NEE_QUEUE = 6      /* free-flight integrators: shadow-ray queue capacity, in rays per path of a
+    VR_OPT_FF_NEE_QUEUE = 6,     /* free-flight integrators: shadow-ray queue capacity, in rays per path of a
                                     launch, 0..16 (default 6). The path kernel queues each bounce's next-event
                                     shadow ray for a separate tracing kernel; 0 traces them inline. Results
                                     are identical (the same walk and sums) except for a path that meets a full
                                     queue: its later contributions are traced inline and added after the
                                     queued ones as one partial sum (float association only). */
+    VR_OPT_MARCH_BINNED = 7      /* RayMarchingGaussians / PureRayMarching primary march: 0 (default): BVH
+                                    window queries per pixel; 1: Gaussians binned to 16x16 tiles by depth
+                                    bucket, each tile's list streamed by its waves.
+                                    Results are identical (the same exact intersect decides every entry). */
 } vr_option;
 vr_status vr_set_option(vr_ctx* ctx, int32_t option, int64_t value);
 vr_status vr_get_option(vr_ctx* ctx, int32_t option, int64_t* value);
