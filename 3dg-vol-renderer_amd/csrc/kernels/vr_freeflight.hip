@@ -30,6 +30,12 @@ namespace vr {
 namespace dev {
 
 constexpr int kFFBlock = 256;
+#ifndef VR_FF_SWEEP_UNROLL
+#define VR_FF_SWEEP_UNROLL 1  // unroll of the loops over the active list (A/B: independent row loads in flight)
+#endif
+#ifndef VR_FF_SWEEP_NOWRITE
+#define VR_FF_SWEEP_NOWRITE 0  // 1: the event sweep recomputes F at the segment start instead of writing it (A/B)
+#endif
 
 // Per-thread scratch rows (global memory, [slot][thread] so a wave's lanes touch consecutive 16-B
 // cells): every slot is one float4, so an insert shift, an entry or a cache read is ONE 16-B access
@@ -214,6 +220,7 @@ __device__ bool solve_for_t_given_tau(const GRec& g, const Ray& r, float t0, flo
 template <class SC>
 __device__ __forceinline__ float act_tau(const RenderArgs& A, const SC& S, int m, const Ray& r, float ta, float t) {
     float s = 0.0f;  // ta is the segment start t_prev, where the cached F values were taken
+#pragma unroll VR_FF_SWEEP_UNROLL
     for (int i = 0; i < m; ++i) s += S.od_to(i, t);
     return s;
 }
@@ -533,15 +540,23 @@ __device__ float free_flight_distance(const RenderArgs& A, SC& S, const Ray& r, 
             float nx = INFINITY;  // smallest t1 after the event, and its position in the list then
             int npos = -1;
             Acc seg = 0;
+#pragma unroll VR_FF_SWEEP_UNROLL
             for (int a = 0; a < m; ++a) {
                 const float4 c = S.A0(a);
                 float4& e1r = S.A1(a);
                 const float4 e1 = e1r;
                 S.C.add(kFFErf);
                 const float f1 = erff(__fdiv_rn(c.y + c.z * t_evt, c.w));
+#if VR_FF_SWEEP_NOWRITE
+                // F at the segment start recomputed (the same float operations as the cached value):
+                // the sweep writes nothing, its rows are read-only between entries
+                const float f0 = erff(__fdiv_rn(c.y + c.z * t_prev, c.w));
+                seg += (Acc)(c.x * (f1 - f0));
+#else
                 if (S.ph) e1r.x = f1;
                 else e1r.y = f1;
                 seg += (Acc)(c.x * (f1 - (S.ph ? e1.y : e1.x)));
+#endif
                 int pp = a;  // position after a swap-remove of exit_pos
                 if (!is_entry && a == m - 1) pp = exit_pos;
                 const bool gone = !is_entry && a == exit_pos;
@@ -551,12 +566,21 @@ __device__ float free_flight_distance(const RenderArgs& A, SC& S, const Ray& r, 
                 }
             }
             if (acc + seg > (Acc)target) {
+#if VR_FF_SWEEP_NOWRITE
+                S.ph = 0;  // the solver reads F at the segment start from .x
+                for (int a = 0; a < m; ++a) {
+                    const float4 c = S.A0(a);
+                    S.A1(a).x = erff(__fdiv_rn(c.y + c.z * t_prev, c.w));
+                }
+#endif
                 float rem = (float)((Acc)target - acc);
                 return solve_distance(A, S, m, r, t_prev, t_evt, rem);
             }
             acc += seg;
             t_prev = t_evt;
+#if !VR_FF_SWEEP_NOWRITE
             S.ph ^= 1;  // F at t_evt is now the segment start
+#endif
             if (window_end) break;
             if (is_entry) {
                 if (m >= A.ff_act_cap) return -2.0f;
