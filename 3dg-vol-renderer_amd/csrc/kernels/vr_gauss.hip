@@ -900,13 +900,17 @@ __device__ __forceinline__ int act_find(const RenderArgs& A, const SecRay& R, in
 
 // Direction of environment sample e of a record: PCG32 keyed by (pixel, step) as the oracle does;
 // the 2e draws of the earlier samples are skipped by LCG jump-ahead s -> M s + C (host table).
-__device__ __forceinline__ void env_sample_dir(const RenderArgs& A, const uint4& meta, uint32_t e, float& wx, float& wy,
-                                               float& wz) {
+__device__ __forceinline__ void env_sample_xi(const RenderArgs& A, const uint4& meta, uint32_t e, float& xi1, float& xi2) {
     const int px = (int)(meta.x & 0xffffu), py = (int)(meta.x >> 16);
     PCG32 rng(derive_path_seed(px, py, (int)meta.y), 1);
     rng.state = A.pcg_jump[4 * e] * rng.state + A.pcg_jump[4 * e + 1];
-    float xi1 = rng.uniform_env();
-    float xi2 = rng.uniform_env();
+    xi1 = rng.uniform_env();
+    xi2 = rng.uniform_env();
+}
+__device__ __forceinline__ void env_sample_dir(const RenderArgs& A, const uint4& meta, uint32_t e, float& wx, float& wy,
+                                               float& wz) {
+    float xi1, xi2;
+    env_sample_xi(A, meta, e, xi1, xi2);
     env_dir(xi1, xi2, wx, wy, wz);
 }
 
@@ -914,6 +918,9 @@ __device__ __forceinline__ void env_sample_dir(const RenderArgs& A, const uint4&
 // cells numbered in Morton order (neighbouring keys = neighbouring directions).
 #ifndef VR_ENV_KEY_BITS
 #define VR_ENV_KEY_BITS 4  // cells per octahedral axis = 2^bits (A/B)
+#endif
+#ifndef VR_ENV_KEY_XI
+#define VR_ENV_KEY_XI 1  // 1: direction cells of the (xi1, xi2) sample grid instead of the octahedral map (A/B)
 #endif
 constexpr int kEnvBits = VR_ENV_KEY_BITS, kEnvSide = 1 << kEnvBits, kEnvCells = kEnvSide * kEnvSide;
 __device__ __forceinline__ uint32_t dir_key(float x, float y, float z) {
@@ -953,9 +960,22 @@ __global__ __launch_bounds__(BLOCK) void env_order_kernel(RenderArgs A) {
         auto key = [&](uint32_t i) -> uint32_t {
             const uint32_t rl = i / ne, r = r0 + rl;
             if (r >= nrec) return kEnvCells - 1;  // padding records
+#if VR_ENV_KEY_XI
+            // the cell of the sample's (xi1, xi2) = (azimuth, cos polar) grid: equal-area direction
+            // cells without evaluating the direction
+            float xi1, xi2;
+            env_sample_xi(A, A.rec_meta[r], i - rl * ne, xi1, xi2);
+            const uint32_t cu = min((uint32_t)(xi1 * kEnvSide), (uint32_t)kEnvSide - 1u);
+            const uint32_t cv = min((uint32_t)(xi2 * kEnvSide), (uint32_t)kEnvSide - 1u);
+            uint32_t k = 0;
+#pragma unroll
+            for (int b = 0; b < kEnvBits; ++b) k |= (((cu >> b) & 1u) << (2 * b)) | (((cv >> b) & 1u) << (2 * b + 1));
+            return k;
+#else
             float wx, wy, wz;
             env_sample_dir(A, A.rec_meta[r], i - rl * ne, wx, wy, wz);
             return dir_key(wx, wy, wz);
+#endif
         };
         for (uint32_t i = threadIdx.x; i < n; i += BLOCK) {
             const uint32_t k = key(i);

@@ -349,7 +349,10 @@ typedef enum vr_option {
                                     shadow ray for a separate tracing kernel; 0 traces them inline. Results
                                     are identical (the same walk and sums) except for a path that meets a full
                                     queue: its later contributions are traced inline and added after the
-                                    queued ones as one partial sum (float association only). */
+                                    queued ones as one partial sum (float association only).
+                                    Memory: the queue holds value x (paths of a launch, at most 2^23) rays
+                                    of 48 B, 2.4 GB at the default 6 per path; it is grown, never shrunk,
+                                    per context (lower it for many contexts on one device). */
     VR_OPT_MARCH_BINNED = 7      /* RayMarchingGaussians / PureRayMarching primary march: 0 (default): BVH
                                     window queries per pixel; 1: Gaussians binned to 16x16 tiles by depth
                                     bucket, each tile's list streamed by its waves.

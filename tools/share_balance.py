@@ -2,7 +2,10 @@
 """Predicts the tile-split scaling on one GPU: renders each of the R interleaved
 rank shares of a frame (tiles r, r+R, r+2R, ...) on its own and times it with the library's HIP
 events (vr_get_stats kernel_ms). Predicted speed-up at R GPUs = full-frame time / slowest share
-(the gather of R slabs over xGMI, ~0.2 ms at 4096^2, not included). Prints one JSON object.
+and, with the gather modelled, full-frame time / (slowest share + gather + root unshuffle): every
+rank's slab (its tiles x 256 px x 12 B) reaches the root over its own xGMI link at --xgmi-gbs GB/s
+(the links run in parallel), then the root's unshuffle reads and writes the frame at --hbm-gbs.
+Prints one JSON object.
 
     python tools/share_balance.py [--config c4|bias20k] [--ranks 2,4,8]
 """
@@ -27,6 +30,8 @@ def main():
     ap.add_argument("--ranks", default="2,4,8")
     ap.add_argument("--t-eps", type=float, default=1e-6)
     ap.add_argument("--reps", type=int, default=2)
+    ap.add_argument("--xgmi-gbs", type=float, default=50.0, help="effective per-link xGMI rate of the gather")
+    ap.add_argument("--hbm-gbs", type=float, default=4000.0, help="effective HBM rate of the root's unshuffle")
     a = ap.parse_args()
     if a.config == "c4":
         scene, W, H = bench.build_scene("c4", 2025)
@@ -61,12 +66,20 @@ def main():
            "full_frame_stage_ms": stages[(0, 1)], "ranks": {}}
     for R in [int(x) for x in a.ranks.split(",")]:
         t = [share(r, R, len(range(r, nt, R))) for r in range(R)]
+        slab = len(range(0, nt, R)) * 256 * 12  # bytes of the largest share's slab
+        gather_ms = slab / (a.xgmi_gbs * 1e9) * 1e3
+        unshuffle_ms = 2.0 * nt * 256 * 12 / (a.hbm_gbs * 1e9) * 1e3
+        with_gather = max(t) + gather_ms + unshuffle_ms
         res["ranks"][R] = {"share_ms": t, "max_ms": max(t), "sum_ms": sum(t),
                            "stage_ms_of_slowest": stages[(int(np.argmax(t)), R)],
                            "imbalance_max_over_mean": max(t) / (sum(t) / R),
-                           "predicted_speedup": full / max(t), "predicted_efficiency": full / max(t) / R}
+                           "predicted_speedup": full / max(t), "predicted_efficiency": full / max(t) / R,
+                           "gather": {"slab_bytes": slab, "xgmi_gbs": a.xgmi_gbs, "gather_ms": gather_ms,
+                                      "unshuffle_ms": unshuffle_ms, "hbm_gbs": a.hbm_gbs},
+                           "predicted_speedup_with_gather": full / with_gather,
+                           "predicted_efficiency_with_gather": full / with_gather / R}
         print(f"[share_balance] R={R}: max {max(t):.1f} ms, mean {sum(t) / R:.1f} ms, predicted speed-up "
-              f"{full / max(t):.2f}", file=sys.stderr, flush=True)
+              f"{full / max(t):.2f} ({full / with_gather:.2f} with the gather)", file=sys.stderr, flush=True)
     print(json.dumps(res))
 
 
