@@ -51,7 +51,7 @@ CAM_VIEW = np.array([0.0, 0.0, -1.0], np.float32)
 FOV = np.float32(0.25 * np.pi)
 HBM_PEAK_GBPS = 8000.0   # MI355X_MICROARCH.md: 8.0 TB/s spec
 FP32_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md: FP32 vector peak
-PMC_SUMMARY = "r02_c4_pmc_summary.json"  # rocprofv3 --pmc passes of this command (profiles/)
+PMC_SUMMARY = "r03_c4_pmc_summary.json"  # rocprofv3 --pmc passes of this command (profiles/)
 
 # Flops per executed operation of the secondary stage (an FMA counts 2, min / max / compare 1, and
 # sqrt / rcp / div / exp / erf 4, the quarter-rate transcendental model of SURVEY §8(d)):
@@ -59,7 +59,13 @@ PMC_SUMMARY = "r02_c4_pmc_summary.json"  # rocprofv3 --pmc passes of this comman
 #          3 compares) + the 5 compare-exchanges of the near-to-far sort = 105
 #   prim:  ray-Gaussian quadratic form + 3-sigma intersection (quad_fast + intersect_fast) = 72
 #   od:    closed-form optical depth over an interval (optical_depth_fast: exp + 2 erf + sqrt + rcp) = 98
-FLOP_WEIGHTS = {"node4": 105, "prim": 72, "od": 98}
+# Flops per operation of the secondary kernel as it executes them (an FMA counts 2, as the FP32 peak
+# does; sqrt/rcp/rsq/exp/erf-polynomial terms at their issue cost, the quarter-rate model of SURVEY
+# §8(d)): a 4-wide node step 104 = 4 x (6 slab FMAs + 6 min/max + min3/max3 + prune min + 2 compares)
+# + the nearest-child selection; a primitive test 54 (the whitened quadratic a, h, c: 33, rsq, the
+# crossing D / sqrt / t0, t1: 21); an optical depth on the chord 64 (two degree-10 erf polynomials 50,
+# exp and the prefactor 14). Round 2 priced the M-form test (72) and depth (98) of vr_march.h.
+FLOP_WEIGHTS = {"node4": 104, "prim": 54, "od": 64}
 ALG_FLOPS_PER_CROSSED = FLOP_WEIGHTS["prim"] + FLOP_WEIGHTS["od"]
 
 
