@@ -1699,7 +1699,11 @@ __global__ __launch_bounds__(BLOCK, WAVES) void secondary_ww_kernel(RenderArgs A
     // tail of the persistent launch (8-way C4 share: 22.7 -> 21.7 ms). Whole chunks otherwise (record
     // locality).
     const uint32_t waves = gridDim.x * (BLOCK / 64u), cpw = nchunks / max(waves, 1u);
-    const uint32_t split = cpw >= 32u ? 0u : cpw >= 16u ? 1u : cpw >= 8u ? 2u : 3u;
+#ifndef VR_WW_SPLIT_CPW
+#define VR_WW_SPLIT_CPW 32  // chunks per resident wave below which claim units get shorter (A/B)
+#endif
+    constexpr uint32_t kSplitCpw = VR_WW_SPLIT_CPW;
+    const uint32_t split = cpw >= kSplitCpw ? 0u : cpw >= kSplitCpw / 2u ? 1u : cpw >= kSplitCpw / 4u ? 2u : 3u;
     const uint32_t nunits = nchunks << split;
     counter_done = nunits == 0u;
 #ifdef VR_DIAG_CYCLES  // diagnostic builds only (S = true): wave cycles per phase, lane 0's counters
