@@ -1208,8 +1208,6 @@ __device__ __forceinline__ void sec_finish(const RenderArgs& A, SecRay& R, Ctr& 
         if (cut_reached<PURE>(R)) {
             c.v[kCtrSteps]++;                 // rays ended by the optical-depth cut-off
             c.v[kCtrPrimQueries] += R.nsteps;  // ... and their node steps
-        } else {
-            c.v[kCtrPixels] += R.nsteps;       // node steps of rays that ran to the end of the tree
         }
     }
 #endif
@@ -1794,7 +1792,12 @@ __global__ __launch_bounds__(BLOCK, WAVES) void secondary_ww_kernel(RenderArgs A
                 const float lo = pre ? 0.0f : fmaxf(t0, 0.0f);
                 const float u0 = pre ? q.hr : fmaxf(q.hr, -sd);  // erf argument x sqrt 2 at lo
                 if (ls >= 0) R.hitmask |= slot_bit(ls);
-                if constexpr (S) c.v[kCtrOD]++;
+                if constexpr (S) {
+                    c.v[kCtrOD]++;
+#if !defined(VR_DIAG_WAVE_UTIL) && !defined(VR_DIAG_CYCLES) && !defined(VR_DIAG_ORIGIN)
+                    c.v[kCtrPixels] += cand ? 1u : 0u;  // a list member's depth again (the credit scheme)
+#endif
+                }
                 // sec_add's FAST rule: one optical-depth evaluation for light and environment lanes
                 const bool add = !R.light || t1 < R.lim;
                 R.needs_stop = R.needs_stop || (!add && lo < R.lim);

@@ -407,7 +407,7 @@ class Device:
                   "primary_queries", "pixels"),
         # secondary stage = the persistent kernel's own schedule (+ the exact slow path)
         "secondary": ("node_tests", "gaussian_tests", "optical_depths", "list_tests", "secondary_rays",
-                      "cut_rays", "cut_ray_node_steps", "full_ray_node_steps"),
+                      "cut_rays", "cut_ray_node_steps", "repeat_depths"),
         # free-flight integrators: the path kernel and the shadow-ray (deferred NEE) kernel
         "path": ("paths", "bounces", "node4_steps", "node2_steps", "gaussian_tests", "erf_evals", "nee_inline",
                  "nee_queued"),
@@ -422,8 +422,12 @@ class Device:
         check(lib().vr_count_work(self._h, ctypes.byref(camera.struct), ctypes.byref(params), width, height,
                                   first_tile, tile_stride, num_tiles, arr))
         stages = ("path", "nee") if params.integrator in (L.VR_FREE_FLIGHT, L.VR_MULTI_SCATTER) else ("march", "secondary")
-        return {stage: {k: int(arr[8 * s + i]) for i, k in enumerate(self.WORK_NAMES[stage])}
-                for s, stage in enumerate(stages)}
+        out = {stage: {k: int(arr[8 * s + i]) for i, k in enumerate(self.WORK_NAMES[stage])}
+               for s, stage in enumerate(stages)}
+        sec = out.get("secondary")
+        if sec is not None:  # node steps of the rays that ran to the end of the tree
+            sec["full_ray_node_steps"] = sec["node_tests"] - sec["cut_ray_node_steps"]
+        return out
 
     def unshuffle_tiles_device(self, slabs_ptr, nslabs, tiles_per_slab, width, height, image_ptr, stream_ptr=0):
         check(lib().vr_unshuffle_tiles_device(self._h, ctypes.c_void_p(slabs_ptr), nslabs, tiles_per_slab, width,

@@ -449,7 +449,9 @@ def main():
         if work is not None:
             sec = work["secondary"]
             executed = secondary_flops(sec)
-            alg = ALG_FLOPS_PER_CROSSED * sec["optical_depths"]
+            # crossed Gaussians: each once (the tree walk's repeat of a list member's depth is executed work,
+            # not algorithmic work)
+            alg = ALG_FLOPS_PER_CROSSED * (sec["optical_depths"] - sec.get("repeat_depths", 0))
             roof.update(achieved=executed / (sec_ms * 1e-3) / 1e12, alg_flops=alg, executed_flops=executed,
                         alg_achieved=alg / (sec_ms * 1e-3) / 1e12, work=work, flop_weights=FLOP_WEIGHTS,
                         flops_note="achieved/frac: the flops the timed persistent kernel itself executes "
