@@ -30,6 +30,9 @@ namespace vr {
 namespace dev {
 
 constexpr int kFFBlock = 256;
+#ifndef VR_FF_ALBEDO_UNROLL
+#define VR_FF_ALBEDO_UNROLL 1  // unroll of evaluate_albedo's loop over the active list (A/B)
+#endif
 #ifndef VR_FF_SWEEP_UNROLL
 #define VR_FF_SWEEP_UNROLL 1  // unroll of the loops over the active list (A/B: independent row loads in flight)
 #endif
@@ -58,7 +61,12 @@ struct FFCount {
 template <>
 struct FFCount<true> {
     uint32_t v[kFFNumCtr] = {};
-    __device__ __forceinline__ void add(int k, uint32_t n = 1) { v[k] += n; }
+    __device__ __forceinline__ void add(int k, uint32_t n = 1) {
+#ifdef VR_DIAG_FF_CYCLES  // these slots hold phase cycles in the diagnostic build (FFScratch::lap)
+        if (k == kFFErf || k == kFFNode2 || k == kFFNeeInline || k == kFFNeeQueued) return;
+#endif
+        v[k] += n;
+    }
 };
 
 template <bool CNT>
@@ -69,6 +77,19 @@ struct FFScratch {
     uint32_t stride;
     int ph;  // which of a1.x / a1.y holds F at the current segment start
     [[no_unique_address]] mutable FFCount<CNT> C;
+#ifdef VR_DIAG_FF_CYCLES  // diagnostic builds only (CNT = true): wave cycles per phase of a bounce, lane 0
+    mutable uint64_t dt = 0;
+    // (lane 0's bounces only; a lap starts at the bounce's start, so waiting for a refill is not counted)
+    __device__ __forceinline__ void lap(int k) const {
+        const uint64_t now = __builtin_amdgcn_s_memtime();
+        if constexpr (CNT) C.v[k] += (__lane_id() == 0u) ? (uint32_t)((now - dt) >> 4) : 0u;  // (16-cycle units)
+        dt = now;
+    }
+    __device__ __forceinline__ void lap_start() const { dt = __builtin_amdgcn_s_memtime(); }
+#else
+    __device__ __forceinline__ void lap(int) const {}
+    __device__ __forceinline__ void lap_start() const {}
+#endif
     __device__ __forceinline__ float4& H(int i) const { return hit[(size_t)i * stride]; }
     __device__ __forceinline__ float4& A0(int i) const { return a0[(size_t)i * stride]; }
     __device__ __forceinline__ float4& A1(int i) const { return a1[(size_t)i * stride]; }
@@ -274,6 +295,7 @@ __device__ float solve_distance(const RenderArgs& A, const SC& S, int m, const R
 template <class SC>
 __device__ float evaluate_albedo(const RenderArgs& A, const SC& S, int m, float x, float y, float z) {
     float sum = 0.0f, sum_alb = 0.0f;
+#pragma unroll VR_FF_ALBEDO_UNROLL
     for (int i = 0; i < m; ++i) {
         GRec g = load_rec(A.gauss, S.Rec(i));
         float mt = mu_t(g, x, y, z);
@@ -506,6 +528,7 @@ __device__ float free_flight_distance(const RenderArgs& A, SC& S, const Ray& r, 
             t_cut = kfull = INFINITY;
             pruned_full = false;
         };
+        S.lap(kFFErf);  // (diagnostic builds: bounce setup / window bookkeeping, with the rest of the bounce)
         if (A.hnodes4 == nullptr || !collect_walk(A, r, stack, stack + kStackSize * kFFBlock, prune, prim, &S.C)) {
             reset();  // pair tree (at most one push per level; no 4-wide tree, or its stack could overflow)
             auto on2 = [&]() { S.C.add(kFFNode2); };
@@ -513,6 +536,7 @@ __device__ float free_flight_distance(const RenderArgs& A, SC& S, const Ray& r, 
             else traverse<false>(A, r, stack, stride, prune, leaf, on2);
         }
         // skipped subtrees only hold keys beyond the (final) largest kept key
+        S.lap(kFFNode2);  // (diagnostic builds: hit collection)
         if (pruned_full && n > 0) t_cut = fminf(t_cut, S.K(n - 1));
         while (n > 0 && S.K(n - 1) >= t_cut) --n;  // entries past the window (t_cut fell after they were kept)
         if (t_cut <= W0) {  // more than cap Gaussians overlap at W0: no progress possible at this cap
@@ -535,7 +559,10 @@ __device__ float free_flight_distance(const RenderArgs& A, SC& S, const Ray& r, 
             float t_evt = fminf(next_entry, next_exit);
             const bool window_end = t_cut <= t_evt;
             if (window_end) t_evt = t_cut;
-            if (t_evt == INFINITY) return -1.0f;  // past the last event: no scatter (integrator.h:362-366)
+            if (t_evt == INFINITY) {  // past the last event: no scatter (integrator.h:362-366)
+                S.lap(kFFNeeInline);
+                return -1.0f;
+            }
             const bool is_entry = next_entry <= next_exit;
             float nx = INFINITY;  // smallest t1 after the event, and its position in the list then
             int npos = -1;
@@ -574,7 +601,10 @@ __device__ float free_flight_distance(const RenderArgs& A, SC& S, const Ray& r, 
                 }
 #endif
                 float rem = (float)((Acc)target - acc);
-                return solve_distance(A, S, m, r, t_prev, t_evt, rem);
+                S.lap(kFFNeeInline);  // (diagnostic builds: event sweep)
+                const float ts = solve_distance(A, S, m, r, t_prev, t_evt, rem);
+                S.lap(kFFNeeQueued);  // (diagnostic builds: distance solver)
+                return ts;
             }
             acc += seg;
             t_prev = t_evt;
@@ -597,6 +627,7 @@ __device__ float free_flight_distance(const RenderArgs& A, SC& S, const Ray& r, 
             next_exit = nx;
             exit_pos = npos;
         }
+        S.lap(kFFNeeInline);
         W0 = t_cut;
         cap = min(2 * cap, A.ff_hit_cap);
     }
@@ -697,6 +728,7 @@ template <bool MULTI, class SC>
 __device__ __forceinline__ bool ff_bounce(const RenderArgs& A, SC& S, int* stack, FFPath& P) {
     bool done = false;
     int m = 0;
+    S.lap_start();
     const float target = -logf(1.0f - P.rng.uniform());
     S.C.add(kFFBounces);
     const float ts = free_flight_distance<MULTI>(A, S, P.ray, target, m, stack, kFFBlock);
@@ -786,6 +818,7 @@ __device__ __forceinline__ bool ff_bounce(const RenderArgs& A, SC& S, int* stack
         }
     }
     if (done) A.ff_tail[P.out] = make_float4(P.L0, P.L1, P.L2, __uint_as_float(P.first | (P.after ? kFFTailAfter : 0u)));
+    S.lap(kFFErf);  // (diagnostic builds: the rest of the bounce — albedo, next-event ray, roulette, direction)
     return !done;
 }
 
