@@ -459,140 +459,15 @@ __device__ int march(const RenderArgs& A, uint32_t p, int px, int py, int* act_b
     return kOK;
 }
 
-// The march with a window of pending entries (march_kernel's path on the 4-wide tree). march() runs a
-// BVH query for the entrants of every step inside the Gaussians (and two per jump across empty
-// space); here one query collects the next PC entry distances at or after `cov` (the cap smallest,
-// kept sorted, as the free-flight hit collection does), and the steps take their entrants from that
-// list until it no longer covers them. Invariant: every entry a with t_lo < a < cov is in the
-// pending list [ph, np). The entrant sets, and so the records, are march()'s: the same exact
-// intersect decides every entry and the same march_step evaluates. A collection that makes no
-// progress (more than PC entries at one distance) sends the pixel to march_fallback_kernel.
-template <int ACT, bool S, int CAP, int PC>
-__device__ int march_win(const RenderArgs& A, uint32_t p, int px, int py, int* act_base, int* stack, int stride, float* pa,
-                         int* pj, Ctr& c) {
-    const Ray ray = primary_ray(A, px, py);
-    const GaussianRecord* __restrict__ G = A.gauss;
-    const float* __restrict__ ts = A.tsteps;
-    const int nts = A.num_tsteps;
-    const float step = A.step_size;
-    float T = 1.0f;
-    uint32_t prev = kNoRecord;
-    A.px_first[p] = kNoRecord;
-    ActList act{act_base, stride, 0, 0};
-    int ph = 0, np = 0;   // pending entries [ph, np), ascending entry distance
-    float cov = -1.0f;    // every entry a with t_lo < a < cov is pending
-    // Collect the next entries at or after cov into the free slots. False: no progress possible.
-    auto collect = [&]() -> bool {
-        if constexpr (S) c.v[kCtrPrimQueries]++;
-        for (int i = ph; i < np; ++i) {  // compact
-            pa[(i - ph) * stride] = pa[i * stride];
-            pj[(i - ph) * stride] = pj[i * stride];
-        }
-        np -= ph;
-        ph = 0;
-        const int n0 = np;
-        float emin = INFINITY;     // smallest entry distance seen and not kept
-        bool pruned_full = false;  // a subtree was skipped while the list was full
-        const float lo = cov;
-        const bool ok = traverse_wide<CAP>(
-            A, ray, stack, stride,
-            [&](float tmin, float tmax) {
-                if (tmax < lo - kTPad * (1.0f + fabsf(lo))) return false;
-                const float lim = fminf(emin, np == PC ? pa[(PC - 1) * stride] : INFINITY);
-                if (tmin > lim + kTPad * (1.0f + fminf(lim, 1e30f))) {
-                    pruned_full |= np == PC;
-                    return false;
-                }
-                return true;
-            },
-            [&](uint32_t first, uint32_t count) {
-                for (uint32_t j = first; j < first + count; ++j) {
-                    if constexpr (S) c.v[kCtrPrims]++;
-                    float a, b;
-                    if (!intersect(quad(load_rec(G, j), ray), a, b) || !(a >= lo) || !(a < emin)) continue;
-                    if (np == PC) {
-                        const float kmax = pa[(PC - 1) * stride];
-                        if (n0 == PC || !(a < kmax)) {  // would be the largest: not kept
-                            emin = fminf(emin, a);
-                            continue;
-                        }
-                        emin = fminf(emin, kmax);  // evict the largest
-                        --np;
-                    }
-                    int i = np++;  // sorted insert among the new entries (all >= lo > the old ones)
-                    while (i > n0 && pa[(i - 1) * stride] > a) {
-                        pa[i * stride] = pa[(i - 1) * stride];
-                        pj[i * stride] = pj[(i - 1) * stride];
-                        --i;
-                    }
-                    pa[i * stride] = a;
-                    pj[i * stride] = (int)j;
-                }
-                return true;
-            },
-            NodeCount<S>{&c});
-        if (!ok) return false;
-        if (pruned_full && np > n0) emin = fminf(emin, pa[(np - 1) * stride]);
-        while (np > n0 && !(pa[(np - 1) * stride] < emin)) --np;  // (entries tied with the cut)
-        cov = emin;
-        return np > n0 || emin == INFINITY;
-    };
-    int kq = 0;
-    if (A.num_prims > 0) {
-        for (;;) {
-            int k;
-            if (act.n == 0) {  // closest entry strictly after the last step: the pending front
-                while (ph == np && cov != INFINITY)
-                    if (!collect()) return kOverflow;
-                if (ph == np) break;
-                k = kfirst(ts, nts, step, pa[ph * stride]);
-            } else {
-                k = kq;
-            }
-            if (k >= nts - 1) return kError;  // step table too short (host sizes it from scene bounds)
-            const float t_k = ts[k];
-            while (!(cov > t_k))  // the entrants need every entry a <= t_k
-                if (!collect()) return kOverflow;
-            while (ph < np && pa[ph * stride] <= t_k) {  // entrants: a <= t_k and still inside at t_k
-                const int j = pj[ph * stride];
-                ++ph;
-                float a, b;
-                if (!intersect(quad(load_rec(G, j), ray), a, b) || !(b > t_k)) continue;
-                if (act.n >= ACT) return kOverflow;
-                int i = act.n;  // sorted insert (index order)
-                while (i > 0 && act.get(i - 1) > j) {
-                    act.set(i, act.get(i - 1));
-                    --i;
-                }
-                act.set(i, j);
-                act.n++;
-            }
-            kq = k + 1;
-            if (!march_step<S, false>(A, ray, p, px, py, k, t_k, act, T, prev, c, true)) break;
-        }
-    }
-    A.px_T[p] = T;
-    if constexpr (S) c.v[kCtrPixels]++;
-    return kOK;
-}
-
 __device__ __forceinline__ void mark_error(const RenderArgs& A, uint32_t p) {
     atomicAdd(A.counters, 1u);
     A.px_T[p] = __builtin_nanf("");
 }
 
-#ifndef VR_MARCH_WINDOW
-#define VR_MARCH_WINDOW 0  // pending entries per lane of march_win (0: march(), a BVH query per step)
-#endif
-constexpr int kMarchWin = VR_MARCH_WINDOW;
-
 template <int ACT, int BLOCK, bool S, int STACK, bool H, bool W = false>
 __global__ __launch_bounds__(BLOCK) void march_kernel(RenderArgs A) {
     __shared__ int s_act[ACT * BLOCK];
     __shared__ int s_stack[STACK * BLOCK];
-    constexpr bool kWin = W && kMarchWin > 0;
-    __shared__ float s_pa[kWin ? kMarchWin * BLOCK : 1];
-    __shared__ int s_pj[kWin ? kMarchWin * BLOCK : 1];
     // A workgroup is one 16x16 tile (BLOCK 256) or one of its 8x8 quarters (BLOCK 64: four times as
     // many, shorter workgroups, so the frame's last ones leave a shorter tail). Lanes never share LDS.
     constexpr uint32_t kParts = 256u / BLOCK;
@@ -605,11 +480,7 @@ __global__ __launch_bounds__(BLOCK) void march_kernel(RenderArgs A) {
     Ctr c{};
     int st = kOK;
     if (x < (int)A.width && y < (int)A.height) {
-        if constexpr (kWin)
-            st = march_win<ACT, S, STACK, kMarchWin>(A, p, x, y, s_act + threadIdx.x, s_stack + threadIdx.x, BLOCK,
-                                                    s_pa + threadIdx.x, s_pj + threadIdx.x, c);
-        else
-            st = march<ACT, S, H, W, STACK>(A, p, x, y, s_act + threadIdx.x, s_stack + threadIdx.x, BLOCK, c);
+        st = march<ACT, S, H, W, STACK>(A, p, x, y, s_act + threadIdx.x, s_stack + threadIdx.x, BLOCK, c);
     } else {
         A.px_first[p] = kNoRecord;
         A.px_T[p] = 0.0f;
