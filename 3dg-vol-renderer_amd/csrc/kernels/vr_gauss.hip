@@ -370,6 +370,11 @@ __device__ __forceinline__ bool march_step(const RenderArgs& A, const Ray& ray, 
 // active list is split over the lanes (one Gaussian each), its sums and compaction then taken in
 // list order through lane broadcasts — the serial loop's operations in its order, so the result is
 // bit-identical — and lane 0 writes the records.
+#ifndef VR_MARCH_UNSORTED
+#define VR_MARCH_UNSORTED 1  // 1: the march's entrant queries walk the 4-wide nodes without sorting (A/B)
+#endif
+constexpr bool kMarchUnsorted = VR_MARCH_UNSORTED;
+
 template <int ACT, bool S, bool H, bool W = false, int CAP = kStackSize, bool COOP = false>
 __device__ int march(const RenderArgs& A, uint32_t p, int px, int py, int* act_base, int* stack, int stride, Ctr& c,
                      int act_stride = -1) {
@@ -389,6 +394,15 @@ __device__ int march(const RenderArgs& A, uint32_t p, int px, int py, int* act_b
         } else {
             traverse<H>(A, ray, stack, stride, prune, leaf, NodeCount<S>{&c});
             return true;
+        }
+    };
+    // the entrants query collects every entry of (t_lo, t_k] whatever the visit order: no sorting network
+    auto walk_any = [&](auto prune, auto leaf) -> bool {
+        if constexpr (W && kMarchUnsorted) {
+            return traverse_wide<CAP, decltype(prune), decltype(leaf), NodeCount<S>, false>(A, ray, stack, stride, prune, leaf,
+                                                                                             NodeCount<S>{&c});
+        } else {
+            return walk(prune, leaf);
         }
     };
     int kq = 0;
@@ -424,7 +438,7 @@ __device__ int march(const RenderArgs& A, uint32_t p, int px, int py, int* act_b
             // entrants: t_lo < a <= t_k and still inside at t_k (b > t_k)
             if constexpr (S) c.v[kCtrPrimQueries]++;
             bool ovf = false;
-            const bool ok = walk(
+            const bool ok = walk_any(
                 [&](float tmin, float tmax) {
                     return tmax >= t_lo - kTPad * (1.0f + fabsf(t_lo)) && tmin <= t_k + kTPad * (1.0f + t_k);
                 },

@@ -483,7 +483,7 @@ __device__ __forceinline__ void cswap(float& ka, int32_t& ra, float& kb, int32_t
 
 // Slab tests of the four children of 4-wide half node `node` (HNode4) for a ray already in the
 // nodes' normalised coordinates, sorted near to far; misses (and empty slots) get key +inf, ref 0.
-template <typename Hit>
+template <typename Hit, bool SORT = true>
 __device__ __forceinline__ void wide_children(const RenderArgs& A, int node, float ix, float iy, float iz, float oxi,
                                               float oyi, float ozi, Hit hit, float* key, int32_t* kr) {
     const uint4* np = reinterpret_cast<const uint4*>(A.hnodes4 + node);
@@ -507,18 +507,22 @@ __device__ __forceinline__ void wide_children(const RenderArgs& A, int node, flo
         key[i] = h ? tmin : INFINITY;
         kr[i] = h ? ref[i] : 0;
     }
-    cswap(key[0], kr[0], key[1], kr[1]);  // 4-input sorting network
-    cswap(key[2], kr[2], key[3], kr[3]);
-    cswap(key[0], kr[0], key[2], kr[2]);
-    cswap(key[1], kr[1], key[3], kr[3]);
-    cswap(key[1], kr[1], key[2], kr[2]);
+    if constexpr (SORT) {
+        cswap(key[0], kr[0], key[1], kr[1]);  // 4-input sorting network
+        cswap(key[2], kr[2], key[3], kr[3]);
+        cswap(key[0], kr[0], key[2], kr[2]);
+        cswap(key[1], kr[1], key[3], kr[3]);
+        cswap(key[1], kr[1], key[2], kr[2]);
+    }
 }
 
 // Stack traversal of the 4-wide half-precision tree (HNode4) with the generic traverse's
 // contract (prune / leaf / on_node); leaves are handled near-first as a node's children are
 // reached, the nearest inner child is walked next and the others pushed far-first. Returns false
 // if the LDS stack (cap entries) could overflow — the caller then re-runs the work on the pair tree.
-template <int CAP, typename Prune, typename Leaf, typename OnNode = NoCount>
+// SORT = false: children in the node's order (a query whose result does not depend on the visit order,
+// e.g. a window query that collects every entry of an interval).
+template <int CAP, typename Prune, typename Leaf, typename OnNode = NoCount, bool SORT = true>
 __device__ __forceinline__ bool traverse_wide(const RenderArgs& A, const Ray& r0, int* stack, int stride, Prune prune,
                                               Leaf leaf, OnNode on_node = OnNode()) {
     float ox = r0.ox, oy = r0.oy, oz = r0.oz;
@@ -537,9 +541,9 @@ __device__ __forceinline__ bool traverse_wide(const RenderArgs& A, const Ray& r0
         on_node();
         float key[4];
         int32_t kr[4];
-        wide_children(A, node, ix, iy, iz, oxi, oyi, ozi, prune, key, kr);
+        wide_children<Prune, SORT>(A, node, ix, iy, iz, oxi, oyi, ozi, prune, key, kr);
 #pragma unroll
-        for (int i = 0; i < 4; ++i)  // leaves, near first
+        for (int i = 0; i < 4; ++i)  // leaves, near first (SORT)
             if (kr[i] < 0 && !leaf(leaf_first(kr[i]), leaf_count(kr[i]))) return true;
         int first = -1;
         int32_t next = 0;  // the nearest inner child (selects only: no dynamic register indexing)
