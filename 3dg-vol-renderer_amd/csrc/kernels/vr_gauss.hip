@@ -2118,7 +2118,10 @@ static hipError_t ww_launch(const RenderArgs& A, hipStream_t stream) {
 #ifndef VR_WW_WAVES
 #define VR_WW_WAVES 7  // waves per SIMD (launch bounds: 72 VGPRs at 7; A/B at C4: 7 + 14-entry stack 95.6 ms, 6 + 18 99.2 ms)
 #endif
-    constexpr int kStack = VR_WW_STACK, kQueue = 9;
+#ifndef VR_WW_QCAP
+#define VR_WW_QCAP 9  // leaf queue of the persistent kernel: the head entry + an LDS ring of QCAP - 1 (1 + 2^k)
+#endif
+    constexpr int kStack = VR_WW_STACK, kQueue = VR_WW_QCAP;
     constexpr int kWaves = PURE ? 5 : VR_WW_WAVES;  // PureRayMarching's marched depth does not fit 80 VGPRs without spills
     const void* fn = (const void*)dev::secondary_ww_kernel<kBlockSecondary, kStack, S, PURE, kWaves, kQueue, H, W>;
     int dv = 0, cus = 0, per_cu = 0;
