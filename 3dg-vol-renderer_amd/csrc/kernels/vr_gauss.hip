@@ -894,9 +894,6 @@ __device__ __forceinline__ bool cut_reached(const SecRay& R) {
 // round trip (independent loads), since a scan sits on the dependent chain of a primitive test.
 __device__ __forceinline__ int act_find(const RenderArgs& A, const SecRay& R, int j) {
     if (!((R.bloom >> (j & 63)) & 1ull)) return -1;
-#ifdef VR_AB_BLOOM_ONLY  // what-if A/B builds only (wrong results): the membership scan's cost
-    return -1;
-#endif
     const int* __restrict__ p = A.rec_act + R.act_off;
     const int n = (int)R.act_n;
     for (int i = 0; i < n; i += 4) {
@@ -1183,25 +1180,6 @@ __device__ __forceinline__ void sec_add(const RenderArgs& A, SecRay& R, const GR
         R.tau += optical_depth(g, q, lo, b);
     } else if (lo < R.lim) {
         R.needs_stop = true;
-    }
-}
-
-template <bool S, bool FAST, bool PURE>
-__device__ __forceinline__ void sec_leaf(const RenderArgs& A, SecRay& R, int32_t ref, Ctr& c) {
-    const uint32_t first = leaf_first(ref), count = leaf_count(ref);
-    for (uint32_t j = first; j < first + count; ++j) {
-        if constexpr (S) c.v[kCtrPrims]++;
-        GRec g = load_rec(A.gauss, j);
-        Quad q = FAST ? quad_fast(g, R.ray) : quad(g, R.ray);
-        float a, b;
-        if (!(FAST ? intersect_fast(q, a, b) : intersect(q, a, b))) continue;
-        int slot = act_find(A, R, (int)j);
-        float lo = a;
-        if (slot >= 0) {
-            lo = 0.0f;
-            R.hitmask |= slot_bit(slot);
-        }
-        sec_add<S, FAST, PURE>(A, R, g, q, lo, b, c);
     }
 }
 
