@@ -1506,6 +1506,10 @@ __device__ __forceinline__ void sec_node4v(const RenderArgs& A, SecRay& R, LdsIn
     float best = INFINITY;
     int32_t next = 0;  // the nearest inner child
     bool inner[4];
+    // ring cursor: the next leaf goes to ring slot cur & (QCAP - 2); cur == head while the queue is
+    // empty (the next leaf is the register head q0). Q.n follows from cur after the four children.
+    const int head = Q.q1 - 1;
+    int cur = head + Q.n;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
         float f[6];
@@ -1522,16 +1526,17 @@ __device__ __forceinline__ void sec_node4v(const RenderArgs& A, SecRay& R, LdsIn
         // [max(tmin, 0), min(tmax, plim)] not empty; a NaN box (empty slot) fails the first compare
         const bool hit = (tmin <= fminf(tmax, R.plim)) & (tmax >= 0.0f);
         const bool leaf = hit & (ref[i] < 0);
-        inner[i] = hit & (ref[i] > 0);
+        inner[i] = hit & !leaf;  // an empty slot (ref 0) never hits
         // leaf -> the queue's end: branch-free, a non-leaf store lands past the last entry (never
         // read). A NODE step starts with at most QCAP - 4 entries, so that slot is a free ring word.
-        Q.q0 = (leaf & (Q.n == 0)) ? ref[i] : Q.q0;
-        ext[((Q.q1 + Q.n - 1) & (QCAP - 2)) * BLOCK] = ref[i];
-        Q.n += (int)leaf;
+        Q.q0 = (leaf & (cur == head)) ? ref[i] : Q.q0;
+        ext[(cur & (QCAP - 2)) * BLOCK] = ref[i];
+        cur += (int)leaf;
         const bool nearer = inner[i] & (tmin < best);
         best = nearer ? tmin : best;
         next = nearer ? ref[i] : next;
     }
+    Q.n = cur - head;
     // the other inner children -> stack (branch-free while every stepping lane has room for 3)
     if (__builtin_expect(__ballot(sp > STACK - 3) == 0ull, 1)) {
 #pragma unroll
