@@ -1781,13 +1781,15 @@ __global__ __launch_bounds__(BLOCK, WAVES) void secondary_ww_kernel(RenderArgs A
                 // reference sums a pre-activated member (for a member, or any Gaussian holding the
                 // origin, that is its entry max(t0, 0) anyway), and its depth comes off the credit: the
                 // credit stays a lower bound of what the walk has still to meet.
-                if (ls >= 0) R.cmax = fmaxf(R.cmax, q.c);
+                // (selects rather than fmaxf where an operand is not known canonical: fmaxf would
+                // canonicalise it first, one more VALU op each; equal for every non-NaN operand)
+                R.cmax = (ls >= 0 && q.c > R.cmax) ? q.c : R.cmax;
                 const bool cand = ls < 0 && q.c <= R.cmax;
                 float t0, t1, sd;
                 if (!wintersect(q, t0, t1, sd)) return;
                 const bool pre = ls >= 0 || cand;  // active from t = 0
                 const float lo = pre ? 0.0f : fmaxf(t0, 0.0f);
-                const float u0 = pre ? q.hr : fmaxf(q.hr, -sd);  // erf argument x sqrt 2 at lo
+                const float u0 = (pre || q.hr > -sd) ? q.hr : -sd;  // erf argument x sqrt 2 at lo
                 if (ls >= 0) R.hitmask |= slot_bit(ls);
                 if constexpr (S) {
                     c.v[kCtrOD]++;
@@ -1797,8 +1799,8 @@ __global__ __launch_bounds__(BLOCK, WAVES) void secondary_ww_kernel(RenderArgs A
                 }
                 // sec_add's FAST rule: one optical-depth evaluation for light and environment lanes
                 const bool add = !R.light || t1 < R.lim;
-                R.needs_stop = R.needs_stop || (!add && lo < R.lim);
-                if (!R.light) R.lim = fmaxf(R.lim, t1);
+                R.needs_stop = R.needs_stop | (!add & (lo < R.lim));
+                R.lim = (!R.light && t1 > R.lim) ? t1 : R.lim;
                 if (add) {
                     const float od = wod_chord(g, q, u0, sd);  // [lo, t1] lies on the 3-sigma chord
                     if (ls >= 0) {
