@@ -25,7 +25,7 @@ uint32_t free_flight_threads(int cus);
 hipError_t launch_sfd_loss_diff(const uint32_t* bits0, const uint32_t* bits1, const float* lb, const float* lp, uint32_t npix,
                                 uint32_t n, double* out, hipStream_t stream);
 hipError_t gauss_record_cut(const RenderArgs& A, float budget, hipStream_t stream);
-hipError_t gauss_whiten(const GaussianRecord* rec, WRecord* out, uint32_t n, hipStream_t stream);
+hipError_t gauss_whiten(const GaussianRecord* rec, WRecord* out, uint32_t n, uint32_t* bad, hipStream_t stream);
 hipError_t gauss_bin(const RenderArgs& A, bool emit, hipStream_t stream);
 hipError_t gauss_bin_scan(const uint32_t* cnt, uint32_t* off, uint32_t n, void* tmp, size_t& tmp_bytes, hipStream_t stream);
 hipError_t launch_pixel_losses(const float* img, const float* ref, uint32_t npix, float* out, hipStream_t stream);
@@ -45,6 +45,7 @@ struct vr_ctx {
     int32_t num_prims = 0;
     GaussianRecord* d_gauss = nullptr;
     WRecord* d_wrec = nullptr;  // whitened copy (secondary rays)
+    bool wrec_pd = true;        // every record's M is positive definite (else the secondary rays use the M forms)
     BVHNode* d_nodes = nullptr;
     HNode* d_hnodes = nullptr;
     HNode4* d_hnodes4 = nullptr;
@@ -70,7 +71,8 @@ struct vr_ctx {
     // Pinned report of the last frame, copied on the render stream after its last kernel:
     // [0] fallback-queue length, [1] error pixels, [2] scatter records, [3] overflow-pool entries,
     // [4] record capacity exceeded (the frame is invalid and must be rendered again), [5] deep-pass
-    // pixels, [6] free-flight paths re-run in ff_fallback_kernel
+    // pixels, [6] free-flight paths re-run in ff_fallback_kernel, [7] free-flight: the most shadow rays
+    // one launch tried to queue
     uint32_t* h_report = nullptr;
     bool report_gauss = false;  // the last frame ran the RayMarchingGaussians pipeline (fields [2..4])
     float* d_frame = nullptr;
@@ -106,6 +108,9 @@ struct vr_ctx {
     int pcg_jump_n = -1;
     uint32_t* h_sizing = nullptr;  // pinned copy of rec_alloc for the sizing march of a context's first frame
     uint64_t rec_hint = 0, ovf_hint = 0;  // record / overflow-pool capacities (0: not known yet)
+    uint64_t nee_hint = 0;                // deferred-NEE queue capacity from earlier free-flight frames (0: not known)
+    uint32_t last_nee_cap = 0, last_nee_bound = 0;  // the last free-flight frame's queue capacity and its bound
+    bool report_ff = false;               // the last frame ran the free-flight pipeline (h_report[7])
     // vr_set_option values (explicit per-context tuning; no environment variables are read)
     int64_t opt_half_nodes = 1;        // VR_OPT_HALF_NODES
     int64_t opt_secondary_budget = 1;  // VR_OPT_SECONDARY_BUDGET
@@ -115,6 +120,7 @@ struct vr_ctx {
     int64_t opt_ff_nee_queue = 6;      // VR_OPT_FF_NEE_QUEUE
     int64_t opt_device_bvh = 0;        // VR_OPT_DEVICE_BVH
     int64_t opt_march_binned = 0;      // VR_OPT_MARCH_BINNED
+    int64_t opt_ff_solver = 0;         // VR_OPT_FF_SOLVER
     bool last_upload_device_bvh = false;  // the current scene's tree came from the device builder
     vr_group* group = nullptr;         // vr_init_multi: the devices this context drives (host/vr_multi.cpp)
 };
@@ -300,11 +306,19 @@ constexpr size_t kDeviceBvhMin = 256;
 // the tree is deeper than the traversal stacks allow (the caller builds on the host instead).
 
 // Whitened record copy for the secondary rays (WRecord), converted on the device from d_gauss.
+// A record whose f32 inverse covariance is not positive definite (a nearly singular covariance) has no
+// Cholesky factor: such a scene's secondary rays use the records' M forms instead (wrec_pd = false,
+// secondary_ww_kernel's M-form variant), as the reference's intersect_direct / optical_depth take any M.
 static vr_status upload_whitened(vr_ctx* c, size_t N) {
+    c->wrec_pd = true;
     HIP_TRY(hipMalloc(&c->d_wrec, std::max<size_t>(N, 1) * sizeof(WRecord)), "hipMalloc(whitened records)");
     if (N == 0) return VR_OK;
-    HIP_TRY(gauss_whiten(c->d_gauss, c->d_wrec, (uint32_t)N, c->stream), "whitened records");
+    HIP_TRY(hipMemsetAsync(c->d_counters, 0, sizeof(uint32_t), c->stream), "hipMemsetAsync(whitened records)");
+    HIP_TRY(gauss_whiten(c->d_gauss, c->d_wrec, (uint32_t)N, c->d_counters, c->stream), "whitened records");
+    uint32_t bad = 0;
+    HIP_TRY(hipMemcpyAsync(&bad, c->d_counters, sizeof(uint32_t), hipMemcpyDeviceToHost, c->stream), "whitened records D2H");
     HIP_TRY(hipStreamSynchronize(c->stream), "hipStreamSynchronize(whitened records)");
+    c->wrec_pd = bad == 0;
     return VR_OK;
 }
 
@@ -351,8 +365,7 @@ vr_status upload_device_bvh(vr_ctx* c, const HostScene& s, const std::vector<flo
     (void)hipFree(d_boxes);
     if (e == hipErrorNotSupported) return fail(VR_ERR_UNSUPPORTED, "device BVH deeper than the traversal stacks");
     if (e != hipSuccess) return hip_fail(e, "device BVH build");
-    c->d_gauss = R.gauss;
-    if (vr_status ws = upload_whitened(c, N); ws != VR_OK) return ws;
+    c->d_gauss = R.gauss;  // every buffer of the build belongs to the context first (free_scene frees them on error)
     c->d_order = R.order;
     c->d_nodes = R.nodes;
     c->d_hnodes = R.hnodes;
@@ -361,7 +374,7 @@ vr_status upload_device_bvh(vr_ctx* c, const HostScene& s, const std::vector<flo
     c->bvh_depth = R.max_depth;
     c->num_prims = (int32_t)N;
     c->last_upload_device_bvh = true;
-    return VR_OK;
+    return upload_whitened(c, N);
 }
 
 // Farthest distance any ray can travel before leaving the scene box: the rays of both camera
@@ -457,7 +470,7 @@ vr_status fill_args(vr_ctx* c, const vr_camera* cam, const vr_render_params* p, 
     A.height = H;
     A.tiles_x = (W + kTile - 1) / kTile;
     A.gauss = c->d_gauss;
-    A.wrec = c->d_wrec;
+    A.wrec = c->wrec_pd ? c->d_wrec : nullptr;
     A.nodes = c->d_nodes;
     A.hnodes = c->d_hnodes;
     A.hnodes4 = c->d_hnodes4;
@@ -488,6 +501,7 @@ vr_status fill_args(vr_ctx* c, const vr_camera* cam, const vr_render_params* p, 
         A.ff_n = (int32_t)std::sqrt((double)p->num_samples);  // int(std::sqrt(num_samples)), integrator.h:564
         A.ff_min_bounces = p->min_bounces;
         A.ff_max_bounces = 1 << 16;
+        A.ff_solver = (int32_t)c->opt_ff_solver;
     } else if (p->integrator != VR_TEST_HITMASK) {
         const float* d;
         int n;
@@ -709,12 +723,29 @@ vr_status free_flight_pipeline(vr_ctx* c, RenderArgs& A, hipStream_t s) {
     if (st != VR_OK) return st;
     if ((st = grow(c->ff_tail, paths * sizeof(float4), "free-flight paths")) != VR_OK) return st;
     if ((st = grow(c->ff_sum, (size_t)A.num_tiles * 256 * 3 * sizeof(float), "free-flight sums")) != VR_OK) return st;
-    A.ff_nee_cap = (uint32_t)std::min<uint64_t>(paths * (uint64_t)c->opt_ff_nee_queue, kFFNone);
-    A.ff_nee_refill = c->auto_nee_refill;
-    if (A.ff_nee_cap > 0) {
-        if ((st = grow(c->ff_nee, (size_t)A.ff_nee_cap * 3 * sizeof(float4), "free-flight shadow-ray queue")) != VR_OK) return st;
-        A.ff_nee = (float4*)c->ff_nee.p;
+    {  // Deferred-NEE queue: VR_OPT_FF_NEE_QUEUE rays per path of a launch bound it; within that bound it is
+       // sized from the need of this context's earlier frames (the most rays any launch queued, + 1/8),
+       // a first frame from the integrator (one shadow ray per bounce, min_bounces + 1 bounces before
+       // Russian roulette). A launch that outgrows it is reported and the frame rendered again with a
+       // grown queue (as the ray-march's record buffers), so frames never depend on the capacity.
+        const uint64_t bound = std::min<uint64_t>(paths * (uint64_t)c->opt_ff_nee_queue, kFFNone);
+        const uint64_t first = paths * (A.ff_multi ? (uint64_t)A.ff_min_bounces + 1ull : 1ull) + 4096ull;
+        const uint64_t cap = std::min<uint64_t>(bound, c->nee_hint ? std::max<uint64_t>(c->nee_hint, 4096ull) : first);
+        const size_t bytes = (size_t)cap * 3 * sizeof(float4);
+        if (c->ff_nee.p && c->ff_nee.bytes > 2 * bytes + (64u << 20)) {  // shrink a queue sized for a larger frame
+            (void)hipFree(c->ff_nee.p);
+            c->ff_nee.p = nullptr;
+            c->ff_nee.bytes = 0;
+        }
+        A.ff_nee_cap = (uint32_t)cap;
+        c->last_nee_cap = (uint32_t)cap;
+        c->last_nee_bound = (uint32_t)bound;
+        if (cap > 0) {
+            if ((st = grow(c->ff_nee, bytes, "free-flight shadow-ray queue")) != VR_OK) return st;
+            A.ff_nee = (float4*)c->ff_nee.p;
+        }
     }
+    A.ff_nee_refill = c->auto_nee_refill;
     {  // paths over the hit-buffer capacity re-run in ff_fallback_kernel (queue + its own rows)
         const uint64_t qcap = paths;
         const uint64_t rows = (uint64_t)kFFBigThreads * 3ull * (uint64_t)kFFBigCap * 16ull;
@@ -768,10 +799,21 @@ vr_status collect(vr_ctx* c) {
         c->rec_hint = std::max<uint64_t>(c->rec_hint, nrec + nrec / 8);
         c->ovf_hint = std::max<uint64_t>(c->ovf_hint, nact + nact / 8);
     }
+    if (c->report_ff && c->last_nee_bound > 0) {
+        // a launch that found the queue full counted its paths' first refused claim only (they then
+        // trace inline): grow at least twice over
+        const uint64_t need = c->h_report[7];
+        const bool over = need > c->last_nee_cap;
+        c->nee_hint = std::max<uint64_t>(need + need / 8, over ? 2ull * c->last_nee_cap : 0ull);
+    }
     return VR_OK;
 }
 
-bool frame_exceeded(const vr_ctx* c) { return c->report_gauss && c->h_report[4] != 0; }
+bool frame_exceeded(const vr_ctx* c) {
+    if (c->report_gauss && c->h_report[4] != 0) return true;
+    // the shadow-ray queue overflowed below its VR_OPT_FF_NEE_QUEUE bound: render again with a larger one
+    return c->report_ff && c->h_report[7] > c->last_nee_cap && c->last_nee_cap < c->last_nee_bound;
+}
 
 vr_status launch(vr_ctx* c, RenderArgs& A, const vr_render_params* p, hipStream_t s, bool stats = false) {
     vr_status st = ensure_queue(c, (uint64_t)A.num_tiles * 256u);
@@ -784,6 +826,7 @@ vr_status launch(vr_ctx* c, RenderArgs& A, const vr_render_params* p, hipStream_
     HIP_TRY(hipEventRecord(c->ev_start, s), "hipEventRecord");
     c->staged = false;
     c->report_gauss = false;
+    c->report_ff = false;
     c->ff_launches = 0;
     if (c->type == VR_VOLUME_GAUSSIANS && (p->integrator == VR_RAYMARCH_GAUSSIANS || p->integrator == VR_PURE_RAYMARCH)) {
         st = gauss_pipeline(c, A, s, stats);
@@ -791,6 +834,7 @@ vr_status launch(vr_ctx* c, RenderArgs& A, const vr_render_params* p, hipStream_
     } else if (p->integrator == VR_FREE_FLIGHT || p->integrator == VR_MULTI_SCATTER) {
         st = free_flight_pipeline(c, A, s);
         if (st != VR_OK) return st;
+        c->report_ff = true;
     } else {
         HIP_TRY(launch_render(A, s, c->type, p->integrator), "kernel launch");
     }
@@ -802,7 +846,7 @@ vr_status launch(vr_ctx* c, RenderArgs& A, const vr_render_params* p, hipStream_
                 "hipMemcpyAsync(report)");
         HIP_TRY(hipMemcpyAsync(&c->h_report[5], A.deepq, sizeof(uint32_t), hipMemcpyDeviceToHost, s), "hipMemcpyAsync(report)");
     }
-    HIP_TRY(hipMemcpyAsync(&c->h_report[6], c->d_counters + 2, sizeof(uint32_t), hipMemcpyDeviceToHost, s),
+    HIP_TRY(hipMemcpyAsync(&c->h_report[6], c->d_counters + 2, 2 * sizeof(uint32_t), hipMemcpyDeviceToHost, s),
             "hipMemcpyAsync(report)");
     HIP_TRY(hipEventRecord(c->ev_report, s), "hipEventRecord");
     c->stats_pending = true;
@@ -824,7 +868,7 @@ vr_status render_sync(vr_ctx* c, RenderArgs& A, const vr_render_params* p, bool 
         if (st != VR_OK) return st;
         if ((st = collect(c)) != VR_OK) return st;
         if (!frame_exceeded(c)) break;
-        if (attempt >= 3) return fail(VR_ERR_OVERFLOW, "scatter-record capacity could not be sized");
+        if (attempt >= 3) return fail(VR_ERR_OVERFLOW, "scatter-record / shadow-ray queue capacity could not be sized");
     }
     if (c->h_report[1] != 0)
         return fail(VR_ERR_OVERFLOW, std::to_string(c->h_report[1]) + std::string(" ") + what);
@@ -915,8 +959,9 @@ void vr_destroy(vr_ctx* c) {
     if (c->h_sizing) (void)hipHostFree(c->h_sizing);
     for (vr_ctx::Buf* b : {&c->px_first, &c->px_T, &c->rec_pos, &c->rec_meta, &c->rec_next, &c->rec_act, &c->tr, &c->rec_rad,
                            &c->rec_alloc, &c->rec_bloom, &c->slowq, &c->pcg_jump, &c->ray_next,
-                           &c->stack_ovf, &c->env_order, &c->rec_cut, &c->bin_cnt, &c->bin_off, &c->bin_ent, &c->ff_scratch, &c->ff_tail, &c->ff_sum, &c->ff_nee, &c->rec_bits[0], &c->rec_bits[1], &c->sfd_tmp, &c->sfd_ref,
-                           &c->sfd_loss[0], &c->sfd_loss[1], &c->sfd_out})
+                           &c->stack_ovf, &c->env_order, &c->rec_cut, &c->deep, &c->bin_cnt, &c->bin_off, &c->bin_ent,
+                           &c->ff_scratch, &c->ff_tail, &c->ff_sum, &c->ff_nee, &c->ff_fb, &c->rec_bits[0], &c->rec_bits[1],
+                           &c->sfd_tmp, &c->sfd_ref, &c->sfd_loss[0], &c->sfd_loss[1], &c->sfd_out})
         if (b->p) (void)hipFree(b->p);
     if (c->d_frame) (void)hipFree(c->d_frame);
     if (c->ev_start) (void)hipEventDestroy(c->ev_start);
@@ -1350,6 +1395,10 @@ vr_status vr_set_option(vr_ctx* c, int32_t option, int64_t value) {
             if (value != 0 && value != 1) return fail(VR_ERR_INVALID, "VR_OPT_MARCH_BINNED must be 0 or 1");
             c->opt_march_binned = value;
             return VR_OK;
+        case VR_OPT_FF_SOLVER:
+            if (value < 0 || value > 4) return fail(VR_ERR_INVALID, "VR_OPT_FF_SOLVER must be in [0, 4]");
+            c->opt_ff_solver = value;
+            return VR_OK;
         case VR_OPT_RECORD_CAPACITY:
             if ((value != 0 && value < 4096) || value > 0x3fffffff)
                 return fail(VR_ERR_INVALID, "VR_OPT_RECORD_CAPACITY must be 0 or in [4096, 2^30)");
@@ -1371,6 +1420,7 @@ vr_status vr_get_option(vr_ctx* c, int32_t option, int64_t* value) {
         case VR_OPT_DEVICE_BVH: *value = c->opt_device_bvh; return VR_OK;
         case VR_OPT_FF_NEE_QUEUE: *value = c->opt_ff_nee_queue; return VR_OK;
         case VR_OPT_MARCH_BINNED: *value = c->opt_march_binned; return VR_OK;
+        case VR_OPT_FF_SOLVER: *value = c->opt_ff_solver; return VR_OK;
         default: return fail(VR_ERR_INVALID, "vr_get_option: unknown option " + std::to_string(option));
     }
 }
@@ -1384,7 +1434,7 @@ vr_status vr_synchronize(vr_ctx* c) {
     vr_status st = collect(c);
     if (st != VR_OK || !pending) return st;
     if (frame_exceeded(c))
-        return fail(VR_ERR_RETRY, "the last frame outgrew the scatter-record buffers sized from earlier frames; "
+        return fail(VR_ERR_RETRY, "the last frame outgrew the scatter-record buffers / shadow-ray queue sized from earlier frames; "
                                   "they have been grown: render it again");
     if (c->h_report[1] != 0)
         return fail(VR_ERR_OVERFLOW, std::to_string(c->h_report[1]) + " pixels / paths of the last frame exceeded a "

@@ -310,7 +310,7 @@ vr_status group_stats(vr_group* g, vr_render_stats* o) {
         vr_status st = vr_get_stats(c, &s);
         if (st != VR_OK) return st;
         o->kernel_ms = std::max(o->kernel_ms, s.kernel_ms);
-        for (int i = 0; i < 5; ++i) o->stage_ms[i] = std::max(o->stage_ms[i], s.stage_ms[i]);
+        for (size_t i = 0; i < std::size(o->stage_ms); ++i) o->stage_ms[i] = std::max(o->stage_ms[i], s.stage_ms[i]);
         o->pixels += s.pixels;
         o->fallback_pixels += s.fallback_pixels;
         o->error_pixels += s.error_pixels;

@@ -281,13 +281,27 @@ __device__ float solve_newton(const RenderArgs& A, const SC& S, int m, const Ray
     return solve_bisection(A, S, m, r, ta, tb, target);
 }
 
-// distance_solvers.h:150-187, ANALYTIC_PLUS_NEWTON
+// distance_solvers.h:143-187. The reference picks its solver at compile time (ANALYTIC_PLUS_NEWTON,
+// :146); here A.ff_solver (VR_OPT_FF_SOLVER, wave-uniform) selects it per frame. UNIFORM (:132-137)
+// draws rand01() from a non-reproducible mt19937(random_device); the device draws the textbook-PCG32
+// uniform of stream 2 + bounce of the path's seed instead (the oracle does the same; documented
+// deviation), leaving the path's own stream untouched as rand01() does.
+enum { kSolverAnalyticNewton = 0, kSolverBisection = 1, kSolverNewton = 2, kSolverAnalyticBisection = 3, kSolverUniform = 4 };
 template <class SC>
-__device__ float solve_distance(const RenderArgs& A, const SC& S, int m, const Ray& r, float ta, float tb, float rem) {
+__device__ float solve_distance(const RenderArgs& A, const SC& S, int m, const Ray& r, float ta, float tb, float rem,
+                                uint64_t path_seed, int bounce) {
+    const int mode = A.ff_solver;
+    if (mode == kSolverUniform) {
+        PCG32 u(path_seed, 2u + (uint64_t)bounce);
+        return ta + u.uniform_env() * (tb - ta);
+    }
+    if (mode == kSolverBisection) return solve_bisection(A, S, m, r, ta, tb, rem);
+    if (mode == kSolverNewton) return solve_newton(A, S, m, r, ta, tb, rem);
     if (m == 1) {
         float t_an = 0.0f;
         if (solve_for_t_given_tau(load_rec(A.gauss, S.Rec(0)), r, ta, tb, rem, t_an)) return fminf(fmaxf(t_an, ta), tb);
     }
+    if (mode == kSolverAnalyticBisection) return solve_bisection(A, S, m, r, ta, tb, rem);
     return solve_newton(A, S, m, r, ta, tb, rem);
 }
 
@@ -460,13 +474,21 @@ __device__ void record_hits(const RenderArgs& A, const Ray& r, float lim, uint32
     }
 }
 
+// derive_path_seed(x, y, si) of path `out` of the launch (the numbering of ff_start).
+__device__ __forceinline__ uint64_t ff_path_seed(const RenderArgs& A, uint32_t out) {
+    const uint32_t b = out / kFFBlock, lane_id = out % kFFBlock;
+    int lx, ly, x, y;
+    tile_pixel(A, A.ff_tile_base + b / A.ff_nsb, (int)lane_id, lx, ly, x, y);
+    return derive_path_seed(x, y, (int)(A.ff_si0 + b % A.ff_nsb));
+}
+
 // Free-flight distance along r for target optical depth `target` (integrator.h:330-360 for
 // MULTI = false with a float sum, :422-498 for MULTI = true with a double sum). Returns t >= 0,
 // -1 (no scatter before the last event) or -2 (a per-thread capacity was exceeded). On return
 // with t >= 0 the active list holds the critical segment's Gaussians (count in m).
 template <bool MULTI, class SC>
 __device__ float free_flight_distance(const RenderArgs& A, SC& S, const Ray& r, float target, int& m, int* stack,
-                                      int stride) {
+                                      int stride, uint32_t path, int bounce) {
     using Acc = typename std::conditional<MULTI, double, float>::type;
     Acc acc = 0;
     float t_prev = 0.0f;
@@ -602,7 +624,8 @@ __device__ float free_flight_distance(const RenderArgs& A, SC& S, const Ray& r, 
 #endif
                 float rem = (float)((Acc)target - acc);
                 S.lap(kFFNeeInline);  // (diagnostic builds: event sweep)
-                const float ts = solve_distance(A, S, m, r, t_prev, t_evt, rem);
+                const uint64_t useed = A.ff_solver == kSolverUniform ? ff_path_seed(A, path) : 0ull;
+                const float ts = solve_distance(A, S, m, r, t_prev, t_evt, rem, useed, bounce);
                 S.lap(kFFNeeQueued);  // (diagnostic builds: distance solver)
                 return ts;
             }
@@ -731,7 +754,7 @@ __device__ __forceinline__ bool ff_bounce(const RenderArgs& A, SC& S, int* stack
     S.lap_start();
     const float target = -logf(1.0f - P.rng.uniform());
     S.C.add(kFFBounces);
-    const float ts = free_flight_distance<MULTI>(A, S, P.ray, target, m, stack, kFFBlock);
+    const float ts = free_flight_distance<MULTI>(A, S, P.ray, target, m, stack, kFFBlock, P.out, P.bounce);
     if (MULTI && A.rec_bits && ts != -2.0f) record_hits(A, P.ray, ts >= 0.0f ? ts + 1e-6f : INFINITY, P.px, stack, kFFBlock);
     if (ts == -2.0f && A.ff_fbq != nullptr) {  // over the hit-buffer capacity: the whole path re-runs
         const uint32_t q = atomicAdd(A.ff_fbq, 1u);        // in ff_fallback_kernel with larger rows
@@ -1052,6 +1075,7 @@ __global__ void __launch_bounds__(kFFBlock) ff_nee_kernel(RenderArgs A) {
 // sample); written back into the path's ff_tail entry with no chain left.
 __global__ void __launch_bounds__(kFFBlock) ff_path_radiance_kernel(RenderArgs A) {
     const size_t q = (size_t)blockIdx.x * kFFBlock + threadIdx.x;
+    if (q == 0) atomicMax(A.counters + 3, A.ff_nee_n[0]);  // the frame's largest launch queue need (host sizing)
     if (q >= A.ff_total) return;
     const float4 t = A.ff_tail[q];
     const uint32_t f = __float_as_uint(t.w);

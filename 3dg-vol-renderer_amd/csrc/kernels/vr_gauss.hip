@@ -1192,8 +1192,9 @@ __device__ __forceinline__ void sec_add(const RenderArgs& A, SecRay& R, const GR
 #define VR_TR_STORE(A, slot, v) ((A).tr[slot] = (v))
 #endif
 
-// Ray complete: write its transmittance (or hand it to the exact slow path).
-template <bool S, bool FAST, bool PURE>
+// Ray complete: write its transmittance (or hand it to the exact slow path). WH: the scene's whitened
+// records (A.wrec); false: the M forms of the records (a scene with a non-positive-definite M).
+template <bool S, bool FAST, bool PURE, bool WH = !PURE>
 __device__ __forceinline__ void sec_finish(const RenderArgs& A, SecRay& R, Ctr& c) {
 #if !defined(VR_DIAG_WAVE_UTIL) && !defined(VR_DIAG_CYCLES) && !defined(VR_DIAG_ORIGIN)
     if constexpr (S) {  // secondary-stage diagnostics in otherwise unused counter slots
@@ -1211,7 +1212,7 @@ __device__ __forceinline__ void sec_finish(const RenderArgs& A, SecRay& R, Ctr& 
         bool any = false;
         for (uint32_t s = 0; s < R.act_n; ++s) {
             const int j = A.rec_act[R.act_off + s];
-            if constexpr (!PURE) {  // the list phase's whitened test
+            if constexpr (!PURE && WH) {  // the list phase's whitened test
                 const WRec g = load_wrec(A.wrec, j);
                 const WQuad q = wquad(g, R.ray);
                 float t0, t1, sd;
@@ -1266,8 +1267,13 @@ __device__ __forceinline__ void sec_finish(const RenderArgs& A, SecRay& R, Ctr& 
             int s = __ffsll((unsigned long long)missed) - 1;
             missed &= missed - 1;
             if constexpr (S) c.v[kCtrOD]++;
-            const WRec g = load_wrec(A.wrec, A.rec_act[R.act_off + s]);
-            R.tau += wod_range(g, wquad(g, R.ray), 0.0f, R.lim);
+            if constexpr (WH) {
+                const WRec g = load_wrec(A.wrec, A.rec_act[R.act_off + s]);
+                R.tau += wod_range(g, wquad(g, R.ray), 0.0f, R.lim);
+            } else {
+                const GRec g = load_rec(A.gauss, A.rec_act[R.act_off + s]);
+                R.tau += optical_depth_fast(g, quad_fast(g, R.ray), 0.0f, R.lim);
+            }
         }
     }
     VR_TR_STORE(A, R.slot, expf(-R.tau));
@@ -1673,7 +1679,9 @@ constexpr int kPrimUnroll = VR_WW_PRIM_UNROLL, kNodeUnroll = VR_WW_NODE_UNROLL;
 // 6 waves/SIMD = 80 VGPRs: the ray state is kept small enough for that without scratch spills (a
 // spilling 6-wave build measured 9 % slower than 5 waves; this one is 5 % faster than 5 waves).
 // S = true is the instrumented build (vr_count_work): the same schedule, counting its own work.
-template <int BLOCK, int STACK, bool S, bool PURE, int WAVES, int QCAP, bool H, bool W>
+// WH: the whitened records (A.wrec); false (PureRayMarching, or a scene with a non-positive-definite M):
+// the records' M forms with the membership lookup of the record's active list.
+template <int BLOCK, int STACK, bool S, bool PURE, int WAVES, int QCAP, bool H, bool W, bool WH = !PURE>
 __global__ __launch_bounds__(BLOCK, WAVES) void secondary_ww_kernel(RenderArgs A) {
     __shared__ int s_stack[(STACK + kQueueLds<QCAP>) * BLOCK];
     LdsInt* stack = (LdsInt*)(s_stack + threadIdx.x);  // LDS-typed: stack/queue accesses are ds_* ops, never flat
@@ -1844,7 +1852,7 @@ __global__ __launch_bounds__(BLOCK, WAVES) void secondary_ww_kernel(RenderArgs A
                     uint32_t j;
                     int ls;
                     fetch(j, ls);
-                    if constexpr (PURE) test(load_rec(A.gauss, (int)j), j, ls);
+                    if constexpr (!WH) test(load_rec(A.gauss, (int)j), j, ls);
                     else wtest(load_wrec(A.wrec, (int)j), j, ls);
                 }
                 go = go && Q.has_prim() && !cut_reached<PURE>(R);
@@ -1871,7 +1879,7 @@ __global__ __launch_bounds__(BLOCK, WAVES) void secondary_ww_kernel(RenderArgs A
             diag_lap(kCtrSteps);
         }
         if (live && (cut_reached<PURE>(R) || (node == -1 && !Q.has_prim()))) {
-            sec_finish<S, true, PURE>(A, R, c);
+            sec_finish<S, true, PURE, WH>(A, R, c);
             live = false;
         }
     }
@@ -1907,7 +1915,7 @@ __global__ __launch_bounds__(BLOCK) void secondary_slow_kernel(RenderArgs A) {
 // WRecord of every record (vr_internal.h): Cholesky factor of M = Sigma^-1 in double. A record whose M
 // is not positive definite gets NaN factors (wintersect never reports a crossing for it).
 __global__ __launch_bounds__(256) void whiten_kernel(const GaussianRecord* __restrict__ rec, WRecord* __restrict__ out,
-                                                     uint32_t n) {
+                                                     uint32_t n, uint32_t* bad) {
     const uint32_t i = blockIdx.x * 256u + threadIdx.x;
     if (i >= n) return;
     const GaussianRecord g = rec[i];
@@ -1916,6 +1924,7 @@ __global__ __launch_bounds__(256) void whiten_kernel(const GaussianRecord* __res
     const double l11 = sqrt(m11 - l01 * l01), l12 = (m12 - l01 * l02) / l11;
     const double l22 = sqrt(m22 - l02 * l02 - l12 * l12);
     const bool pd = l00 > 0.0 && l11 > 0.0 && l22 > 0.0;  // (sqrt of a negative pivot: NaN, fails too)
+    if (!pd) atomicAdd(bad, 1u);  // the host then traces the scene's secondary rays with the M forms
     const float nan = __builtin_nanf("");
     const float dn = (float)((double)g.density * (double)g.norm * 1.2533141373155002512);  // sqrt(pi / 2)
     out[i] = WRecord{g.mx, g.my, g.mz, dn, pd ? (float)l00 : nan, (float)l01, (float)l02, (float)l11,
@@ -2095,7 +2104,7 @@ hipError_t gauss_march(const RenderArgs& A, hipStream_t stream, bool stats) {
 // One launch of the persistent kernel: one resident grid (every CU filled to the kernel's occupancy).
 // LDS words per lane: 14 traversal-stack entries (deeper ones overflow to global memory) + the
 // 8-entry LDS ring of the 9-entry leaf queue = 22 (7 blocks of 256 lanes per CU).
-template <bool S, bool PURE, bool H, bool W>
+template <bool S, bool PURE, bool H, bool W, bool WH = !PURE>
 static hipError_t ww_launch(const RenderArgs& A, hipStream_t stream) {
 #ifndef VR_WW_STACK
 #define VR_WW_STACK 14  // LDS traversal-stack entries per lane (deeper ones spill to the global overflow)
@@ -2107,8 +2116,8 @@ static hipError_t ww_launch(const RenderArgs& A, hipStream_t stream) {
 #define VR_WW_QCAP 9  // leaf queue of the persistent kernel: the head entry + an LDS ring of QCAP - 1 (1 + 2^k)
 #endif
     constexpr int kStack = VR_WW_STACK, kQueue = VR_WW_QCAP;
-    constexpr int kWaves = PURE ? 5 : VR_WW_WAVES;  // PureRayMarching's marched depth does not fit 80 VGPRs without spills
-    const void* fn = (const void*)dev::secondary_ww_kernel<kBlockSecondary, kStack, S, PURE, kWaves, kQueue, H, W>;
+    constexpr int kWaves = PURE ? 5 : WH ? VR_WW_WAVES : 6;  // PureRayMarching's marched depth does not fit 80 VGPRs without spills
+    const void* fn = (const void*)dev::secondary_ww_kernel<kBlockSecondary, kStack, S, PURE, kWaves, kQueue, H, W, WH>;
     int dv = 0, cus = 0, per_cu = 0;
     if (hipGetDevice(&dv) != hipSuccess) return hipErrorUnknown;
     if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dv) != hipSuccess) return hipErrorUnknown;
@@ -2119,7 +2128,7 @@ static hipError_t ww_launch(const RenderArgs& A, hipStream_t stream) {
     if (grid == 0) return hipErrorInvalidValue;
     hipError_t e = hipMemsetAsync(A.ray_next, 0, sizeof(unsigned long long), stream);
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL((dev::secondary_ww_kernel<kBlockSecondary, kStack, S, PURE, kWaves, kQueue, H, W>), dim3((unsigned)grid),
+    hipLaunchKernelGGL((dev::secondary_ww_kernel<kBlockSecondary, kStack, S, PURE, kWaves, kQueue, H, W, WH>), dim3((unsigned)grid),
                        dim3(kBlockSecondary), 0, stream, A);
     return hipGetLastError();
 }
@@ -2127,7 +2136,11 @@ static hipError_t ww_launch(const RenderArgs& A, hipStream_t stream) {
 template <bool S, bool PURE>
 static hipError_t secondary_launch(const RenderArgs& A, hipStream_t stream) {
     hipError_t e;
-    if (A.hnodes != nullptr && A.hnodes4 != nullptr)  // 4-wide half-precision tree
+    if (!PURE && A.wrec == nullptr) {  // a record without a Cholesky factor: the M forms (rare scenes)
+        if (A.hnodes != nullptr && A.hnodes4 != nullptr) e = ww_launch<S, PURE, true, true, false>(A, stream);
+        else if (A.hnodes != nullptr) e = ww_launch<S, PURE, true, false, false>(A, stream);
+        else e = ww_launch<S, PURE, false, false, false>(A, stream);
+    } else if (A.hnodes != nullptr && A.hnodes4 != nullptr)  // 4-wide half-precision tree
         e = ww_launch<S, PURE, true, true>(A, stream);
     else if (A.hnodes != nullptr)
         e = ww_launch<S, PURE, true, false>(A, stream);
@@ -2160,8 +2173,8 @@ hipError_t gauss_secondary(const RenderArgs& A, hipStream_t stream, bool stats) 
     return stats ? secondary_launch<true, false>(A, stream) : secondary_launch<false, false>(A, stream);
 }
 
-hipError_t gauss_whiten(const GaussianRecord* rec, WRecord* out, uint32_t n, hipStream_t stream) {
-    hipLaunchKernelGGL(dev::whiten_kernel, dim3((n + 255) / 256), dim3(256), 0, stream, rec, out, n);
+hipError_t gauss_whiten(const GaussianRecord* rec, WRecord* out, uint32_t n, uint32_t* bad, hipStream_t stream) {
+    hipLaunchKernelGGL(dev::whiten_kernel, dim3((n + 255) / 256), dim3(256), 0, stream, rec, out, n, bad);
     return hipGetLastError();
 }
 

@@ -158,7 +158,8 @@ struct RenderArgs {
     uint32_t* deepq;       // [0] = count, [1..] = pixels for march_deep_kernel (active set > 64)
     uint32_t deepq_cap;
     int32_t* deep_act;     // march_deep_kernel's active lists, [slot][thread]
-    uint32_t* counters;    // [0] = error pixels / paths, [2] = free-flight paths re-run in ff_fallback_kernel
+    uint32_t* counters;    // [0] = error pixels / paths, [2] = free-flight paths re-run in ff_fallback_kernel,
+                           // [3] = the most shadow rays a free-flight launch of the frame tried to queue
     unsigned long long* work;  // instrumented build only: [0..7] march-kernel counters, [8..15] secondary-kernel counters
 
     // ---- wavefront buffers (RayMarchingGaussians), pixel-local index p = tile_local * 256 + lane ----
@@ -189,6 +190,8 @@ struct RenderArgs {
     int32_t ff_n;            // int(sqrt(num_samples)): strata per axis (integrator.h:564)
     int32_t ff_min_bounces;  // MultiScatterGaussians min_scatter (Russian roulette after it)
     int32_t ff_max_bounces;  // safety bound on a path's bounces (exceeded: error path)
+    int32_t ff_solver;       // distance solver (VR_OPT_FF_SOLVER, distance_solvers.h:143-187): 0 ANALYTIC_PLUS_NEWTON,
+                             // 1 BISECTION, 2 NEWTON, 3 ANALYTIC_PLUS_BISECTION, 4 UNIFORM
     uint32_t ff_si0, ff_nsb; // first sample index of the batch, samples in the batch
     uint32_t ff_tile_base;   // first tile (tile-local index) of the chunk
     uint32_t ff_threads;     // threads of one step = row stride of the scratch arrays

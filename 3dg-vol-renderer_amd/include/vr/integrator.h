@@ -25,6 +25,7 @@ protected:
     vr_render_params params_{};
     int device_ = -1;            // >= 0: this one GPU
     std::vector<int> devices_;   // explicit device list (multi-GPU context, even for one device)
+    int solver_ = -1;            // free-flight integrators: VR_OPT_FF_SOLVER set before each render
 
 public:
     HipIntegrator(const std::shared_ptr<Camera>& camera, int integrator, float step_size, int env_samples, int dev)
@@ -50,6 +51,7 @@ public:
     void render(const Scene& scene, Image& image) override {
         vr_ctx* ctx = context();
         upload(ctx, scene);
+        apply_solver(ctx);
         vr_cpp::check(vr_render(ctx, &camera->state(), &params_, image.get_width(), image.get_height(), image.data()));
     }
     // re-upload when the scene (or the scene object) changed since the last upload to this context
@@ -62,6 +64,9 @@ public:
             vr_cpp::check(vr_upload_scene(ctx, ns));
             uploaded[ctx] = {ns, scene.native_version()};
         }
+    }
+    void apply_solver(vr_ctx* ctx) const {
+        if (solver_ >= 0) vr_cpp::check(vr_set_option(ctx, VR_OPT_FF_SOLVER, solver_));
     }
     // a context's scene was replaced behind upload()'s back (vr_sfd_optimize re-uploads): forget it
     static void forget(vr_ctx* ctx) {
@@ -94,13 +99,20 @@ public:
         : HipIntegrator(camera, VR_PURE_RAYMARCH, step_size, env_samples, dev) {}
 };
 
+// distance_solvers.h:143-147: the reference picks one of these with a #define (ANALYTIC_PLUS_NEWTON
+// compiled in); here a run-time choice per free-flight integrator (VR_OPT_FF_SOLVER). UNIFORM draws
+// from a seeded PCG32 stream instead of rand01()'s random_device (include/vr_hip.h).
+enum DistanceSolver { ANALYTIC_PLUS_NEWTON = 0, BISECTION = 1, NEWTON = 2, ANALYTIC_PLUS_BISECTION = 3, UNIFORM = 4 };
+
 // integrator.h:273-408 — FreeFlightGaussians(camera, num_samples = 256)
 class FreeFlightGaussians : public HipIntegrator {
 public:
     FreeFlightGaussians(const std::shared_ptr<Camera>& camera, int num_samples = 256, int dev = -1)
         : HipIntegrator(camera, VR_FREE_FLIGHT, 0.01f, 0, dev) {
         params_.num_samples = num_samples;
+        solver_ = ANALYTIC_PLUS_NEWTON;
     }
+    void set_distance_solver(DistanceSolver s) { solver_ = (int)s; }
 };
 
 // integrator.h:416-720 — MultiScatterGaussians(camera, samples = 16, min_bounces = 5)
@@ -110,8 +122,10 @@ public:
         : HipIntegrator(camera, VR_MULTI_SCATTER, 0.01f, 0, dev) {
         params_.num_samples = samples;
         params_.min_bounces = min_bounces;
+        solver_ = ANALYTIC_PLUS_NEWTON;
     }
     void set_num_samples(int n) { params_.num_samples = n; }  // integrator.h:719
+    void set_distance_solver(DistanceSolver s) { solver_ = (int)s; }
     using HipIntegrator::render;
     // integrator.h:532-536 with RECORD_PIXEL_GAUSSIANS: per_pixel_gaussians[y * W + x] receives the
     // sorted indices of the Gaussians recorded at that pixel (integrator.h:616-644, 700-705).
@@ -119,6 +133,7 @@ public:
         if (!per_pixel_gaussians) return render(scene, image);
         vr_ctx* ctx = context();
         upload(ctx, scene);
+        apply_solver(ctx);
         vr_cpp::check(vr_render_record(ctx, &camera->state(), &params_, image.get_width(), image.get_height(), image.data(), 0));
         const size_t npix = (size_t)image.get_width() * image.get_height(), n = scene.get_num_primitives();
         const size_t words = (n + 31) / 32;

@@ -374,7 +374,7 @@ class Device:
     OPTIONS = {"half_nodes": L.VR_OPT_HALF_NODES, "secondary_budget": L.VR_OPT_SECONDARY_BUDGET,
                "ff_window0": L.VR_OPT_FF_WINDOW0, "record_capacity": L.VR_OPT_RECORD_CAPACITY,
                "device_bvh": L.VR_OPT_DEVICE_BVH, "ff_nee_queue": L.VR_OPT_FF_NEE_QUEUE,
-               "march_binned": L.VR_OPT_MARCH_BINNED}
+               "march_binned": L.VR_OPT_MARCH_BINNED, "ff_solver": L.VR_OPT_FF_SOLVER}
 
     def set_option(self, name, value):
         """vr_set_option (include/vr_hip.h): explicit per-context tuning (half_nodes applies at the
@@ -463,9 +463,17 @@ class Integrator:
         self.device = device
         self.last_stats = None
 
-    def render(self, scene, image):
+    solver = None  # free-flight integrators: a SOLVERS key (VR_OPT_FF_SOLVER), set on the device per render
+
+    def _device(self, scene):
         dev = Device.get(self.device)
         dev.upload(scene)
+        if self.solver is not None:
+            dev.set_option("ff_solver", SOLVERS[self.solver])
+        return dev
+
+    def render(self, scene, image):
+        dev = self._device(scene)
         W, H = image.get_width(), image.get_height()
         out = np.empty((H, W, 3), np.float32)
         check(lib().vr_render(dev._h, ctypes.byref(self.camera.struct), ctypes.byref(self.params), W, H, fptr(out)))
@@ -493,15 +501,21 @@ class PureRayMarching(Integrator):
         super().__init__(camera, step_size, env_samples, t_eps, device)
 
 
+# distance_solvers.h:143-147 (compile-time #defines in the reference) -> VR_OPT_FF_SOLVER values
+SOLVERS = {"analytic_newton": 0, "bisection": 1, "newton": 2, "analytic_bisection": 3, "uniform": 4}
+
+
 class FreeFlightGaussians(Integrator):
     """integrator.h:273-408: FreeFlightGaussians(camera, num_samples=256) — single scattering by
-    free-flight sampling, one NEE sample (a light or the environment) per path."""
+    free-flight sampling, one NEE sample (a light or the environment) per path. `solver`: the
+    distance solver (SOLVERS; the reference's compiled-in ANALYTIC_PLUS_NEWTON by default)."""
 
     integrator_id = L.VR_FREE_FLIGHT
 
-    def __init__(self, camera, num_samples=256, device=0):
+    def __init__(self, camera, num_samples=256, device=0, solver="analytic_newton"):
         super().__init__(camera, 0.01, 0, 0.0, device)
         self.params.num_samples = int(num_samples)
+        self.solver = solver
 
     def set_num_samples(self, n):
         self.params.num_samples = int(n)
@@ -513,10 +527,11 @@ class MultiScatterGaussians(Integrator):
 
     integrator_id = L.VR_MULTI_SCATTER
 
-    def __init__(self, camera, samples=16, min_bounces=5, device=0):
+    def __init__(self, camera, samples=16, min_bounces=5, device=0, solver="analytic_newton"):
         super().__init__(camera, 0.01, 0, 0.0, device)
         self.params.num_samples = int(samples)
         self.params.min_bounces = int(min_bounces)
+        self.solver = solver
 
     def set_num_samples(self, n):  # integrator.h:719
         self.params.num_samples = int(n)
@@ -534,8 +549,7 @@ class MultiScatterGaussians(Integrator):
         return image
 
     def record(self, scene, image, slot=0):
-        dev = Device.get(self.device)
-        dev.upload(scene)
+        dev = self._device(scene)
         W, H = image.get_width(), image.get_height()
         out = np.empty((H, W, 3), np.float32)
         check(lib().vr_render_record(dev._h, ctypes.byref(self.camera.struct), ctypes.byref(self.params), W, H,

@@ -22,6 +22,7 @@ VR_FREE_FLIGHT, VR_MULTI_SCATTER = 4, 5
 VR_OPT_HALF_NODES, VR_OPT_SECONDARY_BUDGET, VR_OPT_FF_WINDOW0, VR_OPT_RECORD_CAPACITY, VR_OPT_DEVICE_BVH = 1, 2, 3, 4, 5
 VR_OPT_FF_NEE_QUEUE = 6
 VR_OPT_MARCH_BINNED = 7
+VR_OPT_FF_SOLVER = 8
 
 f3 = ctypes.c_float * 3
 

@@ -353,10 +353,16 @@ typedef enum vr_option {
                                     Memory: the queue holds value x (paths of a launch, at most 2^23) rays
                                     of 48 B, 2.4 GB at the default 6 per path; it is grown, never shrunk,
                                     per context (lower it for many contexts on one device). */
-    VR_OPT_MARCH_BINNED = 7      /* RayMarchingGaussians / PureRayMarching primary march: 0 (default): BVH
+    VR_OPT_MARCH_BINNED = 7,     /* RayMarchingGaussians / PureRayMarching primary march: 0 (default): BVH
                                     window queries per pixel; 1: Gaussians binned to 16x16 tiles by depth
                                     bucket, each tile's list streamed by its waves.
                                     Results are identical (the same exact intersect decides every entry). */
+    VR_OPT_FF_SOLVER = 8         /* free-flight integrators: the distance solver (distance_solvers.h:143-187, a
+                                    compile-time #define in the reference): 0 (default) ANALYTIC_PLUS_NEWTON, the
+                                    mode the reference compiles (:146); 1 BISECTION; 2 NEWTON; 3
+                                    ANALYTIC_PLUS_BISECTION; 4 UNIFORM, whose rand01() (mt19937 seeded by
+                                    random_device, not reproducible) is replaced by the textbook-PCG32 uniform of
+                                    stream 2 + bounce of the path's derive_path_seed (documented deviation). */
 } vr_option;
 vr_status vr_set_option(vr_ctx* ctx, int32_t option, int64_t value);
 vr_status vr_get_option(vr_ctx* ctx, int32_t option, int64_t* value);

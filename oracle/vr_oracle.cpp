@@ -1100,12 +1100,18 @@ static float solve_distance_newton_raphson(const Ray& ray, float ta, float tb, c
 // others for the goldens rendered with them (tests/renders/250_rand_{bisection,newton,uniform}_big).
 enum { kSolverAnalyticNewton = 0, kSolverBisection = 1, kSolverNewton = 2, kSolverAnalyticBisection = 3, kSolverUniform = 4 };
 static int g_solver = kSolverAnalyticNewton;
+// The path being solved (free_flight_pixel): UNIFORM's draw comes from its own PCG32 stream.
+static thread_local uint64_t g_uniform_seed = 0;
+static thread_local int g_uniform_bounce = 0;
 static float solve_distance(const Ray& ray, float ta, float tb, const std::vector<size_t>& act, float remaining_tau,
                             const GMM& gmm) {
-    if (g_solver == kSolverUniform) {  // :132-137: rand01() is mt19937(random_device) (rng.h:6-10); seeded here
-        static thread_local std::mt19937 gen(12345u);
-        float u = std::uniform_real_distribution<float>(0.0f, 1.0f)(gen);
-        return ta + u * (tb - ta);
+    if (g_solver == kSolverUniform) {
+        // :132-137 draws rand01() from mt19937(random_device) (rng.h:6-10): not reproducible. Documented
+        // deviation (the device does the same): the textbook-PCG32 uniform of stream 2 + bounce of the
+        // path's seed derive_path_seed(x, y, si) — unbiased like mt19937, and it leaves the path's own
+        // PCG32 stream (stream 1) untouched, as rand01() does.
+        PCG32 u(g_uniform_seed, 2u + (uint64_t)g_uniform_bounce);
+        return ta + u.uniform_env() * (tb - ta);
     }
     if (g_solver == kSolverBisection) return solve_distance_bisection(ray, ta, tb, act, remaining_tau, gmm);
     if (g_solver == kSolverNewton) return solve_distance_newton_raphson(ray, ta, tb, act, remaining_tau, gmm);
@@ -1225,12 +1231,14 @@ static V3 free_flight_pixel(const Scene& scene, const Camera& cam, int x, int y,
     const int n = int(std::sqrt(num_samples));
     for (int si = 0; si < num_samples; ++si) {
         PCG32 rng(derive_path_seed(x, y, si), 1);
+        g_uniform_seed = derive_path_seed(x, y, si);
         int sx = si % n, sy = si / n;
         float u = (x + (sx + rng.uniform()) / n) / W;
         float v = (y + (sy + rng.uniform()) / n) / H;
         Ray ray = cam.sample_ray(u, v);
         V3 throughput{1, 1, 1}, L_accum{0, 0, 0};
         for (int bounce = 0;; ++bounce) {
+            g_uniform_bounce = bounce;
             gmm.intersect_events(ray, events);
             if (events.empty()) {
                 L_accum = L_accum + V3{throughput.x * scene.env_color.x, throughput.y * scene.env_color.y,

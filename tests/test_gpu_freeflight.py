@@ -9,6 +9,8 @@ Russian roulette, light choice) lands within an ulp can diverge. Bar: at least 9
 within 1e-4 L-inf, mean |diff| < 1e-4, image means within 0.5 % (measured on MI355X: 100 % of
 pixels within 1e-4, mean |diff| ~1e-8).
 """
+import ctypes
+
 import numpy as np
 import pytest
 
@@ -233,3 +235,51 @@ def test_deferred_shadow_rays_equal_inline(multi, device_options):
         print(f"queue {q}: max|d| {d:.2e}, bitwise-equal pixels {same:.4f}")
         assert d <= 1e-6
         assert same >= (1.0 if q == 16 else 0.5)
+
+
+SOLVERS = {"analytic_newton": 0, "bisection": 1, "newton": 2, "analytic_bisection": 3, "uniform": 4}
+
+
+@pytest.mark.parametrize("solver", ["bisection", "newton", "analytic_bisection", "uniform"])
+@pytest.mark.parametrize("multi", [False, True])
+def test_distance_solver_modes_match_oracle(solver, multi):
+    """VR_OPT_FF_SOLVER: the reference's compile-time solver choice (distance_solvers.h:143-187) at run
+    time. Every mode follows the oracle's restatement of the same solver path by path; the oracle's
+    BISECTION / NEWTON / UNIFORM renders are pinned to the reference's own 250_rand_{bisection,newton,
+    uniform}_big.ppm (tests/test_oracle_freeflight.py). UNIFORM draws its rand01() from the seeded
+    PCG32 stream 2 + bounce of the path on both sides (documented deviation: the reference seeds
+    mt19937 from random_device)."""
+    L = O.lib()
+    L.orc_set_solver.argtypes = [ctypes.c_int]
+    path = scene_path("250_random.txt")
+    cam = vr.Pinhole_Camera(CAM_POS, main_view_dir(), FOV)
+    kw = {"solver": solver}
+    integ = vr.MultiScatterGaussians(cam, 4, 5, **kw) if multi else vr.FreeFlightGaussians(cam, 4, **kw)
+    img = vr.Image(40, 40)
+    try:
+        integ.render(vr.Scene.load_GMM(path), img)
+    finally:
+        vr.Device.get(0).set_option("ff_solver", 0)
+    L.orc_set_solver(SOLVERS[solver])
+    try:
+        r = O.render_ff(O.OracleScene.load_gmm(path), O.PINHOLE, CAM_POS, main_view_dir(), FOV, 40, 40, multi=multi,
+                        num_samples=4)
+    finally:
+        L.orc_set_solver(0)
+    _check(img.pixels, r)
+
+
+def test_solver_modes_change_the_frame():
+    """The modes really switch the device solver: UNIFORM (a uniform point of the critical segment)
+    renders a different frame than the default ANALYTIC_PLUS_NEWTON on the same paths."""
+    path = scene_path("250_random.txt")
+    cam = vr.Pinhole_Camera(CAM_POS, main_view_dir(), FOV)
+    frames = {}
+    try:
+        for s in ("analytic_newton", "uniform"):
+            img = vr.Image(32, 32)
+            vr.MultiScatterGaussians(cam, 4, 5, solver=s).render(vr.Scene.load_GMM(path), img)
+            frames[s] = img.pixels.copy()
+    finally:
+        vr.Device.get(0).set_option("ff_solver", 0)
+    assert not np.array_equal(frames["analytic_newton"], frames["uniform"])

@@ -230,3 +230,30 @@ def test_c5_one_sfd_iteration_matches_oracle():
     assert base_rel < 1e-4
     assert gerr <= 1e-2 * gmax
     assert np.mean(pdiff[big] <= 1e-6) >= 0.999
+
+
+def test_sfd_on_a_multi_device_context_equals_single_device():
+    """vr_sfd_optimize on a multi-device context spreads an iteration's perturbed renders over the ranks
+    (each rank uploads its own perturbed scene with the device BVH build, renders and records from a
+    host thread of its own; the base render and the union statistic on the first). The result must not
+    depend on the number of ranks: parameters, loss history and the last gradient bit-equal to the
+    single-device run with the same seed."""
+    path = scene_path("2_gaussian.txt")
+    target = vr.Scene.load_GMM(path)
+    W = 24
+    I_ref = vr.Image(W, W)
+    vr.MultiScatterGaussians(_cam(), 16).render(target, I_ref)
+    p = inv.pack_parameters(target.gaussians())
+    p[9::11] -= 0.7
+    start = inv.apply_params(p, target.lights, target.env_color)
+    runs = {}
+    for devices in (0, (0, 0), (0, 0, 0)):
+        opt = inv.StochasticFiniteDiffInverseIntegrator(
+            _cam(), vr.MultiScatterGaussians(_cam(), 4, device=devices),
+            inv.SFDConfig(max_iters=4, num_stoch_samples=3, lr=0.05, seed=5, final_samples=64))
+        assert opt.optimize(start, I_ref)
+        runs[devices] = (opt.params.copy(), np.array(opt.history), np.array(opt.last_grads))
+    base = runs[0]
+    for devices in ((0, 0), (0, 0, 0)):
+        for a, b in zip(base, runs[devices]):
+            assert np.array_equal(a, b), devices

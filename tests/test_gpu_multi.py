@@ -98,3 +98,19 @@ def test_cpp_driver_on_a_group(tmp_path, devices):
     assert f"{ndev} device(s)" in outs["group"][1]
     assert ("RCCL gather" in outs["group"][1]) == (ndev == 1)
     assert np.array_equal(outs["single"][0], outs["group"][0])
+
+
+def test_group_stats_sum_the_ranks():
+    """vr_get_stats on a group: counts are the sum over the ranks (vr_get_rank_stats), times the slowest
+    rank's, and stage_ms keeps its four stages (the group reduction once ran past the array)."""
+    scene = vr.Scene.load_GMM(scene_path("50_random.txt"))
+    devices = (0, 0, 0)
+    _, st = _render(vr.RayMarchingGaussians, scene, 100, 70, devices)
+    dev = vr.Device.get(devices)
+    ranks = [dev.rank_stats(r) for r in range(len(devices))]
+    assert len(st["stage_ms"]) == 4
+    for key in ("pixels", "scatter_records", "secondary_rays", "fallback_pixels", "error_pixels", "deep_pixels"):
+        assert st[key] == sum(r[key] for r in ranks), key
+    assert st["scatter_records"] > 0
+    for stage, ms in st["stage_ms"].items():
+        assert ms == max(r["stage_ms"][stage] for r in ranks), stage

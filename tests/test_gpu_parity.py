@@ -558,3 +558,28 @@ def test_device_bvh_full_size_c4(device_options):
               f"records {integ.last_stats['scatter_records']}")
     assert out[0][1]["scatter_records"] == out[1][1]["scatter_records"]
     assert float(np.max(np.abs(out[0][0].astype(np.float64) - out[1][0]))) < 2e-6
+
+
+def test_non_positive_definite_record_uses_the_m_forms(tmp_path):
+    """A nearly singular covariance whose f32 inverse (the reference's M, gaussian.h:53) is not positive
+    definite has no Cholesky factor, so it has no whitened record: the upload detects it and the scene's
+    secondary rays run the persistent kernel's M-form variant (quad / intersect / optical depth of M, the
+    record's active-list membership by lookup). Placed far outside the view it touches no ray, so the
+    frame must still match the oracle; this pins the M-form variant on a whole scene."""
+    cov = np.float32([0.009235004894435406, 0.06374555826187134, -0.06935998797416687, 0.5371712446212769,
+                      -0.32841256260871887, 0.7535938024520874]) * np.float32(2.0 ** -14)  # (exact scaling)
+    src = open(scene_path("50_random.txt")).read().rstrip("\n")
+    path = tmp_path / "50_random_plus_degenerate.txt"
+    # 3-sigma extent ~0.02 at distance ~30: no primary, light or environment ray of the frame meets it
+    path.write_text(src + "\ng 0.0 -30.0 0.0  " + " ".join(f"{c:.9g}" for c in cov) + "  0.3 0.7  0.1 0.1 0.1\n")
+    rec = vr.Scene.load_GMM(str(path)).records()[-1, 4:10].astype(np.float64)
+    M = np.array([[rec[0], rec[1], rec[2]], [rec[1], rec[3], rec[4]], [rec[2], rec[4], rec[5]]])
+    assert np.linalg.eigvalsh(M).min() < 0.0
+    W = H = 96
+    gpu, stats = _render_gpu_gmm(str(path), W, H, env_samples=8)
+    assert stats["error_pixels"] == 0
+    pix = _pixels(W, H, 1024)
+    ref = _oracle_gmm(str(path), W, H, env_samples=8, pixels=pix)
+    err, nan_mismatch = _linf(gpu[pix[:, 1], pix[:, 0]], ref)
+    print(f"M-form secondary rays: L-inf {err:.2e}")
+    assert nan_mismatch == 0 and err < TOL
