@@ -32,6 +32,8 @@ hipError_t launch_pixel_losses(const float* img, const float* ref, uint32_t npix
 
 hipError_t launch_unshuffle(const float* slabs, uint32_t nslabs, uint32_t tiles_per_slab, uint32_t tiles_x, uint32_t W,
                             uint32_t H, float* img, hipStream_t stream);
+hipError_t launch_unshuffle_part(const float* slabs, uint32_t first, uint32_t nslabs, uint32_t stride, uint32_t tiles_per_slab,
+                                 uint32_t tiles_x, uint32_t W, uint32_t H, float* img, hipStream_t stream);
 }  // namespace vr
 
 using namespace vr;
@@ -1225,6 +1227,18 @@ vr_status vr_unshuffle_tiles_device(vr_ctx* c, const float* d_slabs, uint32_t ns
     if (!c || !d_slabs || !d_image || nslabs == 0) return fail(VR_ERR_INVALID, "vr_unshuffle_tiles_device: bad argument");
     HIP_TRY(hipSetDevice(c->device), "hipSetDevice");
     HIP_TRY(launch_unshuffle(d_slabs, nslabs, tiles_per_slab, (W + kTile - 1) / kTile, W, H, d_image, (hipStream_t)stream),
+            "unshuffle launch");
+    return VR_OK;
+}
+
+vr_status vr_unshuffle_tiles_part_device(vr_ctx* c, const float* d_slabs, uint32_t first, uint32_t nslabs, uint32_t stride,
+                                         uint32_t tiles_per_slab, uint32_t W, uint32_t H, float* d_image, void* stream) {
+    c = first_device(c);
+    if (!c || !d_slabs || !d_image || nslabs == 0 || stride == 0 || (uint64_t)first + nslabs > stride)
+        return fail(VR_ERR_INVALID, "vr_unshuffle_tiles_part_device: bad argument");
+    HIP_TRY(hipSetDevice(c->device), "hipSetDevice");
+    HIP_TRY(launch_unshuffle_part(d_slabs, first, nslabs, stride, tiles_per_slab, (W + kTile - 1) / kTile, W, H, d_image,
+                                  (hipStream_t)stream),
             "unshuffle launch");
     return VR_OK;
 }

@@ -4,10 +4,11 @@
 // The reference parallelises its pixel loop over CPU threads (test_integrators.h:164,
 // integrator.h:547); pixels are independent, so the frame is the data-parallel axis here too
 // (SURVEY.md §8(e)). Every device holds a full scene replica; rank r renders the 16x16 tiles
-// r, r + n, r + 2n, ... of the frame (interleaving balances dense and empty regions) into a packed
-// slab on its own device; the slabs are gathered to the root device with RCCL — one
-// ncclGroupStart/End holding every rank's ncclSend and the root's ncclRecv, over xGMI — and the
-// root's unshuffle kernel writes them into the row-major frame, which is copied to the host once.
+// r, r + n, r + 2n, ... of the frame (interleaving balances dense and empty regions); the root renders
+// its tiles straight into the row-major frame, every other rank into a packed slab on its own device;
+// those slabs are gathered to the root device with RCCL — one ncclGroupStart/End holding ranks 1..n-1's
+// ncclSend and the root's ncclRecv, over xGMI — and the root's unshuffle kernel writes them into the
+// frame, which is copied to the host once.
 //
 // RCCL is loaded with dlopen at vr_init_multi, so libvr_hip.so itself needs no RCCL and a process
 // that already carries another copy (PyTorch's) does not see symbol clashes. A device listed more
@@ -29,8 +30,8 @@
 using namespace vr;
 
 namespace vr {
-hipError_t launch_unshuffle(const float* slabs, uint32_t nslabs, uint32_t tiles_per_slab, uint32_t tiles_x, uint32_t W,
-                            uint32_t H, float* img, hipStream_t stream);
+hipError_t launch_unshuffle_part(const float* slabs, uint32_t first, uint32_t nslabs, uint32_t stride, uint32_t tiles_per_slab,
+                                 uint32_t tiles_x, uint32_t W, uint32_t H, float* img, hipStream_t stream);
 }
 
 namespace {
@@ -113,8 +114,10 @@ vr_status grow_dev(int dev, float** p, size_t* cap, size_t floats, const char* w
     return VR_OK;
 }
 
-// One frame: render every rank's tiles, gather, unshuffle, copy to the host. Sets *again if a rank
-// reported that the frame outgrew its record buffers (they have been grown: render it again).
+// One frame: the root renders its own tiles straight into the row-major frame; every other rank renders
+// its tiles into a packed slab, the slabs are gathered to the root and unshuffled into the frame there,
+// which is then copied to the host once. Sets *again if a rank reported that the frame outgrew its
+// buffers (they have been grown: render it again).
 vr_status group_frame(vr_group* g, const vr_camera* cam, const vr_render_params* p, uint32_t W, uint32_t H, float* rgb,
                       bool* again) {
     const int n = (int)g->ranks.size();
@@ -122,54 +125,60 @@ vr_status group_frame(vr_group* g, const vr_camera* cam, const vr_render_params*
     const uint32_t per = (nt + n - 1) / n;
     const size_t slab_floats = (size_t)per * 256 * 3;
     vr_status st;
-    for (int r = 0; r < n; ++r) {  // every rank's slab: sized for the largest share
+    for (int r = 1; r < n; ++r) {  // every other rank's slab: sized for the largest share
         size_t cap = g->slab_floats;
         if ((st = grow_dev(g->devices[r], &g->slab[r], &cap, slab_floats, "hipMalloc(slab)")) != VR_OK) return st;
     }
     g->slab_floats = std::max(g->slab_floats, slab_floats);
-    if ((st = grow_dev(g->devices[0], &g->d_recv, &g->recv_floats, slab_floats * n, "hipMalloc(gathered slabs)")) != VR_OK)
+    if (n > 1 && (st = grow_dev(g->devices[0], &g->d_recv, &g->recv_floats, slab_floats * (n - 1), "hipMalloc(gathered slabs)")) != VR_OK)
         return st;
     if ((st = grow_dev(g->devices[0], &g->d_frame, &g->frame_floats, (size_t)W * H * 3, "hipMalloc(frame)")) != VR_OK) return st;
     // 1) every rank renders its interleaved share (asynchronous on its own stream), each rank's ~15
-    // launches issued from a host thread of its own so the ranks start together
+    // launches issued from a host thread of its own so the ranks start together; the root's tiles land
+    // in the frame itself (no copy of the root's share, no self-send)
     st = each_rank_parallel(g, [&](int r) -> vr_status {
         const uint32_t count = (uint32_t)r < nt ? (nt - 1 - (uint32_t)r) / (uint32_t)n + 1 : 0;
         if (count == 0) return VR_OK;
-        return vr_render_tiles_device(g->ranks[r], cam, p, W, H, (uint32_t)r, (uint32_t)n, count, 1, g->slab[r],
-                                      g->streams[r]);
+        return vr_render_tiles_device(g->ranks[r], cam, p, W, H, (uint32_t)r, (uint32_t)n, count, r == 0 ? 0 : 1,
+                                      r == 0 ? g->d_frame : g->slab[r], g->streams[r]);
     });
     if (st != VR_OK) return st;
-    // 2) gather the slabs to the root
-    if (g->use_rccl) {
+    // 2) gather the other ranks' slabs to the root: one group of sends / receives (the links run
+    // concurrently; each rank's send starts as soon as its own render is done)
+    if (n > 1 && g->use_rccl) {
         ncclResult_t e = g->rccl.group_start();
         if (e != ncclSuccess) return ncclf(g, e, "ncclGroupStart");
-        for (int r = 0; r < n; ++r) {
+        for (int r = 1; r < n; ++r) {
             GHIP(hipSetDevice(g->devices[r]), "hipSetDevice");
             e = g->rccl.send(g->slab[r], slab_floats, ncclFloat32, 0, g->comms[r], g->streams[r]);
             if (e != ncclSuccess) break;
         }
         if (e == ncclSuccess) {
             GHIP(hipSetDevice(g->devices[0]), "hipSetDevice");
-            for (int r = 0; r < n && e == ncclSuccess; ++r)
-                e = g->rccl.recv(g->d_recv + (size_t)r * slab_floats, slab_floats, ncclFloat32, r, g->comms[0], g->streams[0]);
+            for (int r = 1; r < n && e == ncclSuccess; ++r)
+                e = g->rccl.recv(g->d_recv + (size_t)(r - 1) * slab_floats, slab_floats, ncclFloat32, r, g->comms[0],
+                                 g->streams[0]);
         }
         ncclResult_t e2 = g->rccl.group_end();
         if (e != ncclSuccess) return ncclf(g, e, "ncclSend/ncclRecv");
         if (e2 != ncclSuccess) return ncclf(g, e2, "ncclGroupEnd");
-    } else {  // ranks sharing a GPU: device copies once every share is done
-        for (int r = 0; r < n; ++r) {
+    } else if (n > 1) {  // ranks sharing a GPU: device copies once every share is done
+        for (int r = 1; r < n; ++r) {
             GHIP(hipSetDevice(g->devices[r]), "hipSetDevice");
             GHIP(hipStreamSynchronize(g->streams[r]), "rank render");
         }
         GHIP(hipSetDevice(g->devices[0]), "hipSetDevice");
-        for (int r = 0; r < n; ++r)
-            GHIP(hipMemcpyPeerAsync(g->d_recv + (size_t)r * slab_floats, g->devices[0], g->slab[r], g->devices[r],
+        for (int r = 1; r < n; ++r)
+            GHIP(hipMemcpyPeerAsync(g->d_recv + (size_t)(r - 1) * slab_floats, g->devices[0], g->slab[r], g->devices[r],
                                     slab_floats * sizeof(float), g->streams[0]),
                  "hipMemcpyPeerAsync(slab)");
     }
-    // 3) unshuffle on the root and copy the frame out
+    // 3) unshuffle the gathered slabs (ranks 1 .. n-1) into the frame on the root and copy it out
     GHIP(hipSetDevice(g->devices[0]), "hipSetDevice");
-    GHIP(launch_unshuffle(g->d_recv, (uint32_t)n, per, (W + kTile - 1) / kTile, W, H, g->d_frame, g->streams[0]), "unshuffle");
+    if (n > 1)
+        GHIP(launch_unshuffle_part(g->d_recv, 1, (uint32_t)(n - 1), (uint32_t)n, per, (W + kTile - 1) / kTile, W, H, g->d_frame,
+                                   g->streams[0]),
+             "unshuffle");
     GHIP(hipMemcpyAsync(rgb, g->d_frame, (size_t)W * H * 3 * sizeof(float), hipMemcpyDeviceToHost, g->streams[0]),
          "hipMemcpyAsync(frame)");
     for (int r = 0; r < n; ++r) {

@@ -208,8 +208,10 @@ __global__ __launch_bounds__(BLOCK) void hitmask_kernel(RenderArgs A, int sphere
 }
 
 // Slabs (rank r holds tiles r, r + nslabs, ...) -> row-major frame.
-__global__ void unshuffle_kernel(const float* __restrict__ slabs, uint32_t nslabs, uint32_t tiles_per_slab,
-                                 uint32_t tiles_x, uint32_t W, uint32_t H, float* __restrict__ img) {
+// Slab k of `slabs` holds the tiles first + k, first + k + stride, ... (rank first + k of a stride-way
+// split); nslabs of them are scattered into the row-major frame.
+__global__ void unshuffle_kernel(const float* __restrict__ slabs, uint32_t first, uint32_t nslabs, uint32_t stride,
+                                 uint32_t tiles_per_slab, uint32_t tiles_x, uint32_t W, uint32_t H, float* __restrict__ img) {
     uint64_t gid = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     uint64_t total = (uint64_t)nslabs * tiles_per_slab * 256u;
     if (gid >= total) return;
@@ -217,7 +219,7 @@ __global__ void unshuffle_kernel(const float* __restrict__ slabs, uint32_t nslab
     uint64_t tl = gid / 256u;
     uint32_t slab = (uint32_t)(tl / tiles_per_slab);
     uint32_t i = (uint32_t)(tl % tiles_per_slab);
-    uint64_t tile = (uint64_t)slab + (uint64_t)i * nslabs;
+    uint64_t tile = (uint64_t)(first + slab) + (uint64_t)i * stride;
     uint32_t x = (uint32_t)((tile % tiles_x) * kTile) + p % kTile;
     uint32_t y = (uint32_t)((tile / tiles_x) * kTile) + p / kTile;
     if (x >= W || y >= H) return;
@@ -240,13 +242,19 @@ hipError_t launch_render(const RenderArgs& A, hipStream_t stream, int volume_typ
     return hipGetLastError();
 }
 
-hipError_t launch_unshuffle(const float* slabs, uint32_t nslabs, uint32_t tiles_per_slab, uint32_t tiles_x, uint32_t W,
-                            uint32_t H, float* img, hipStream_t stream) {
+hipError_t launch_unshuffle_part(const float* slabs, uint32_t first, uint32_t nslabs, uint32_t stride, uint32_t tiles_per_slab,
+                                 uint32_t tiles_x, uint32_t W, uint32_t H, float* img, hipStream_t stream) {
     uint64_t total = (uint64_t)nslabs * tiles_per_slab * 256u;
     if (total == 0) return hipSuccess;
     dim3 grid((unsigned)((total + 255) / 256));
-    hipLaunchKernelGGL(dev::unshuffle_kernel, grid, dim3(256), 0, stream, slabs, nslabs, tiles_per_slab, tiles_x, W, H, img);
+    hipLaunchKernelGGL(dev::unshuffle_kernel, grid, dim3(256), 0, stream, slabs, first, nslabs, stride, tiles_per_slab, tiles_x,
+                       W, H, img);
     return hipGetLastError();
+}
+
+hipError_t launch_unshuffle(const float* slabs, uint32_t nslabs, uint32_t tiles_per_slab, uint32_t tiles_x, uint32_t W,
+                            uint32_t H, float* img, hipStream_t stream) {
+    return launch_unshuffle_part(slabs, 0, nslabs, nslabs, tiles_per_slab, tiles_x, W, H, img, stream);
 }
 
 }  // namespace vr

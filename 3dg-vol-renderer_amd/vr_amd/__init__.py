@@ -191,6 +191,14 @@ class Scene:
         check(lib().vr_scene_get_spheres(self._h, arr, n))
         return np.frombuffer(arr, dtype=np.float32).reshape(max(n, 1), 6)[:n].copy()
 
+    def unshuffle_tiles_part_device(self, slabs_ptr, first, nslabs, stride, tiles_per_slab, width, height, image_ptr,
+                                    stream_ptr=0):
+        """Slabs of ranks first .. first + nslabs - 1 of a stride-way split into the frame
+        (vr_unshuffle_tiles_part_device)."""
+        check(lib().vr_unshuffle_tiles_part_device(self._h, ctypes.c_void_p(slabs_ptr), first, nslabs, stride,
+                                                   tiles_per_slab, width, height, ctypes.c_void_p(image_ptr),
+                                                   ctypes.c_void_p(stream_ptr)))
+
     def __del__(self):
         h = getattr(self, "_h", None)
         if h is not None and L._lib is not None:

@@ -132,6 +132,8 @@ SIGNATURES = {
                                     ctypes.c_uint32, ctypes.c_int32, P, P]),
     "vr_unshuffle_tiles_device": (ST, [P, P, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,
                                        P, P]),
+    "vr_unshuffle_tiles_part_device": (ST, [P, P, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,
+                                            ctypes.c_uint32, ctypes.c_uint32, P, P]),
     "vr_count_work": (ST, [P, ctypes.POINTER(vr_camera), ctypes.POINTER(vr_render_params), ctypes.c_uint32,
                            ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,
                            ctypes.POINTER(ctypes.c_uint64)]),

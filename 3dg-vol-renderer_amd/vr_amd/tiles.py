@@ -3,9 +3,11 @@
 The reference parallelises the pixel loop with OpenMP only (test_integrators.h:164); pixels are
 independent, so the frame is the data-parallel axis. The frame is cut into 16x16 tiles numbered
 row-major; rank r renders tiles r, r + R, r + 2R, ... (interleaved, which balances dense and empty
-regions of the image) into a packed slab, slabs are gathered to rank 0 with one RCCL collective
-and scattered back into the row-major frame by the device unshuffle kernel. `unshuffle_reference`
-is the host mirror of that kernel used by the CPU tests.
+regions of the image). Rank 0 renders its tiles straight into the row-major frame; every other rank
+renders into a packed slab, sends it to rank 0 (point-to-point RCCL sends in one batch, so the links
+run concurrently and nothing is sent to the root itself) and the device unshuffle kernel scatters
+those slabs into the frame. `unshuffle_reference` is the host mirror of that kernel used by the CPU
+tests.
 """
 import numpy as np
 
@@ -35,25 +37,29 @@ def tile_pixels(W, H, first, stride, count):
     return np.where(inside, x, -1).reshape(-1), np.where(inside, y, -1).reshape(-1)
 
 
-def unshuffle_reference(slabs, W, H):
-    """slabs: (R, per * 256, 3) -> (H, W, 3) frame (host mirror of vr_unshuffle_tiles_device)."""
-    R = slabs.shape[0]
+def unshuffle_reference(slabs, W, H, first=0, stride=None):
+    """slabs: (n, per * 256, 3), slab k = rank first + k of a stride-way split (stride defaults to n)
+    -> (H, W, 3) frame holding those ranks' tiles (host mirror of vr_unshuffle_tiles_part_device)."""
+    n = slabs.shape[0]
+    stride = n if stride is None else stride
     per = slabs.shape[1] // (TILE * TILE)
     img = np.zeros((H, W, 3), slabs.dtype)
-    for r in range(R):
-        x, y = tile_pixels(W, H, r, R, per)
+    for k in range(n):
+        x, y = tile_pixels(W, H, first + k, stride, per)
         m = x >= 0
-        img[y[m], x[m]] = slabs[r][m]
+        img[y[m], x[m]] = slabs[k][m]
     return img
 
 
 def render_local(dev, camera, params, W, H, rank, world, slab, frame, stream_ptr):
-    """This rank's share of one frame (device buffers are torch tensors). World 1 renders straight
-    into `frame`; otherwise the rank's interleaved tiles go into its packed `slab`. Asynchronous on
-    the stream; the frame's outcome is checked by `finish_local`."""
+    """This rank's share of one frame (device buffers are torch tensors). Rank 0 renders its tiles
+    straight into `frame` (world 1: the whole frame); every other rank into its packed `slab`.
+    Asynchronous on the stream; the frame's outcome is checked by `finish_local`."""
     first, stride, count, per = rank_tiles(W, H, rank, world)
-    if world == 1:
-        dev.render_tiles_device(camera, params, W, H, 0, 1, count, False, frame.data_ptr(), stream_ptr)
+    if count == 0:
+        return
+    if rank == 0:
+        dev.render_tiles_device(camera, params, W, H, first, stride, count, False, frame.data_ptr(), stream_ptr)
     else:
         dev.render_tiles_device(camera, params, W, H, first, stride, count, True, slab.data_ptr(), stream_ptr)
 
@@ -74,19 +80,29 @@ def finish_local(dev, camera, params, W, H, rank, world, slab, frame, stream_ptr
 
 
 def gather_frame(dev, W, H, rank, world, slab, slabs, frame, stream_ptr, dist, via_host=False):
-    """Gather every rank's slab to rank 0 (one RCCL gather over xGMI) and unshuffle there.
-    via_host: gather CPU copies instead (gloo rehearsal of the N > 1 path on one GPU)."""
+    """Ranks 1 .. world-1 send their slabs to rank 0 (one batch of point-to-point RCCL sends over xGMI:
+    the links run concurrently, the root sends nothing to itself) and rank 0 unshuffles them into the
+    frame it already holds its own tiles in. slabs (rank 0): (world - 1, per * 256 * 3).
+    via_host: the same exchange through CPU copies (gloo rehearsal of the N > 1 path on one GPU)."""
     if world == 1:
         return
-    per = slab.numel() // (TILE * TILE * 3)
+    per = (slab if rank else slabs[0]).numel() // (TILE * TILE * 3)
     if via_host:
         import torch
         torch.cuda.synchronize()
-        host = [torch.empty_like(slab, device="cpu") for _ in range(world)] if rank == 0 else None
-        dist.gather(slab.cpu(), host, dst=0)
         if rank == 0:
-            slabs.copy_(torch.stack(host).to(slabs.device))
+            for r in range(1, world):
+                host = torch.empty(slabs[r - 1].shape, dtype=slabs.dtype)
+                dist.recv(host, src=r)
+                slabs[r - 1].copy_(host.to(slabs.device))
+        else:
+            dist.send(slab.cpu(), dst=0)
     else:
-        dist.gather(slab, list(slabs.unbind(0)) if rank == 0 else None, dst=0)
+        if rank == 0:
+            ops = [dist.P2POp(dist.irecv, slabs[r - 1], r) for r in range(1, world)]
+        else:
+            ops = [dist.P2POp(dist.isend, slab, 0)]
+        for w in dist.batch_isend_irecv(ops):
+            w.wait()
     if rank == 0:
-        dev.unshuffle_tiles_device(slabs.data_ptr(), world, per, W, H, frame.data_ptr(), stream_ptr)
+        dev.unshuffle_tiles_part_device(slabs.data_ptr(), 1, world - 1, world, per, W, H, frame.data_ptr(), stream_ptr)

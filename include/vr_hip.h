@@ -23,7 +23,7 @@
 extern "C" {
 #endif
 
-#define VR_ABI_VERSION 6
+#define VR_ABI_VERSION 7
 
 typedef enum vr_status {
     VR_OK = 0,
@@ -243,6 +243,13 @@ vr_status vr_render_tiles_device(vr_ctx* ctx, const vr_camera* cam, const vr_ren
 vr_status vr_unshuffle_tiles_device(vr_ctx* ctx, const float* d_slabs, uint32_t nslabs,
                                     uint32_t tiles_per_slab, uint32_t width, uint32_t height,
                                     float* d_image, void* stream);
+/* Scatter the packed slabs of ranks first .. first + nslabs - 1 of a stride-way split (slab k = tiles
+ * first + k, first + k + stride, ...; each tiles_per_slab * 256 px) into the row-major W x H frame
+ * d_image: the gather of a split whose root rendered its own tiles straight into the frame.
+ * Asynchronous on `stream`. */
+vr_status vr_unshuffle_tiles_part_device(vr_ctx* ctx, const float* d_slabs, uint32_t first, uint32_t nslabs,
+                                         uint32_t stride, uint32_t tiles_per_slab, uint32_t width, uint32_t height,
+                                         float* d_image, void* stream);
 /* Diagnostics (untimed): render the given tiles once with the instrumented build of the same
  * kernels and return the work they executed. counts[0..7], the march kernels (both passes):
  * [0] BVH node tests (4-wide nodes, or child pairs on the fallback path), [1] ray-Gaussian

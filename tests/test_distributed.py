@@ -1,9 +1,10 @@
 """Multi-process tile sharding on CPU (torch.distributed gloo, world size 2 and 3).
 
 Each rank renders its interleaved tile share with the CPU oracle (a stand-in for the device
-renderer, which tests/test_gpu_parity.py checks bit-for-bit against the single-call frame),
-packs it into a slab exactly as vr_render_tiles_device does, the slabs are gathered to rank 0 and
-unshuffled; the reassembled frame must equal the oracle's full frame bit for bit.
+renderer, which tests/test_gpu_parity.py checks bit-for-bit against the single-call frame); rank 0
+writes its tiles straight into the frame, every other rank packs its share into a slab exactly as
+vr_render_tiles_device does and sends it to rank 0, which unshuffles them (vr_amd.tiles.gather_frame's
+exchange); the reassembled frame must equal the oracle's full frame bit for bit.
 """
 import os
 import socket
@@ -42,14 +43,22 @@ def _worker(rank, world, port, W, H, q):
         s = O.OracleScene.load_gmm(scene_path("many_gaussians.txt"))
         rgb = O.render(s, O.PINHOLE, CAM_POS, main_view_dir(), FOV, W, H, env_samples=4,
                        pixels=np.stack([x[inside], y[inside]], 1), nthreads=1)
-        slab = torch.zeros((per * 256, 3), dtype=torch.float32)
-        slab[: count * 256][torch.from_numpy(inside)] = torch.from_numpy(rgb)
-        gathered = [torch.zeros_like(slab) for _ in range(world)] if rank == 0 else None
-        dist.gather(slab, gathered, dst=0)
-        if rank == 0:
-            img = tiles.unshuffle_reference(torch.stack(gathered).numpy(), W, H)
+        if rank == 0:  # the root's tiles go straight into the frame; the others arrive as packed slabs
+            img = np.zeros((H, W, 3), np.float32)
+            img[y[inside], x[inside]] = rgb
+            slabs = torch.zeros((world - 1, per * 256, 3), dtype=torch.float32)
+            for r in range(1, world):
+                dist.recv(slabs[r - 1], src=r)
+            part = tiles.unshuffle_reference(slabs.numpy(), W, H, first=1, stride=world)
+            mine = np.zeros((H, W), bool)
+            mine[y[inside], x[inside]] = True
+            img[~mine] = part[~mine]
             full = O.render(s, O.PINHOLE, CAM_POS, main_view_dir(), FOV, W, H, env_samples=4, nthreads=1)
             q.put(bool(np.array_equal(img, full)))
+        else:
+            slab = torch.zeros((per * 256, 3), dtype=torch.float32)
+            slab[: count * 256][torch.from_numpy(inside)] = torch.from_numpy(rgb)
+            dist.send(slab, dst=0)
     finally:
         dist.destroy_process_group()
 

@@ -1,8 +1,9 @@
 """Multi-GPU context through the C ABI (vr_init_multi): the frame's 16x16 tiles are
 dealt round-robin over the ranks, gathered to the first device (RCCL ncclSend/ncclRecv when every
-rank has its own GPU, device copies when ranks share one) and unshuffled there. On the one-GPU test
-box: a one-rank group exercises the whole RCCL path (self send/receive); groups that list GPU 0
-several times exercise the split, the gather and the unshuffle. Every result must equal the
+rank has its own GPU, device copies when ranks share one) and unshuffled there; the root renders its
+own tiles straight into the frame. On the one-GPU test box groups that list GPU 0 several times
+exercise the split, the gather and the unshuffle (a one-rank group holds an RCCL communicator but,
+with no other rank, sends nothing). Every result must equal the
 single-device render bit for bit (pixels are independent; env and path RNG are keyed by pixel)."""
 import os
 import subprocess
@@ -114,3 +115,25 @@ def test_group_stats_sum_the_ranks():
     assert st["scatter_records"] > 0
     for stage, ms in st["stage_ms"].items():
         assert ms == max(r["stage_ms"][stage] for r in ranks), stage
+
+
+@pytest.mark.timeout(600)
+def test_c4_eight_way_split_equals_single_device():
+    """BASELINE config 4 at full size (4096^2, 1M make_random Gaussians, the bench settings: 20 env
+    samples, t_eps 1e-6) through vr_init_multi with eight ranks on GPU 0: every rank renders its
+    interleaved 1/8 of the 65536 tiles (the root straight into the frame, the others into packed slabs
+    gathered and unshuffled on the root). The reference's pixel loop is what the split shards
+    (test_integrators.h:164): the frame must equal the one-device frame bit for bit."""
+    scene = vr.Scene(vr.Scene.GAUSSIANS)
+    scene.add_random_gaussians(1_000_000, seed=2025, variant=0)
+    for p, i in [((0.0, 5.0, 0.1), (50.0, 0.0, 0.0)), ((-3.0, 3.0, 0.3), (0.0, 30.0, 0.0)),
+                 ((3.0, 3.0, -0.2), (0.0, 0.0, 30.0))]:
+        scene.add_light(vr.Light(p, i))
+    W = H = 4096
+    ref, st1 = _render(vr.RayMarchingGaussians, scene, W, H, 0, t_eps=1e-6)
+    devices = (0,) * 8
+    got, st8 = _render(vr.RayMarchingGaussians, scene, W, H, devices, t_eps=1e-6)
+    assert st1["error_pixels"] == 0 and st8["error_pixels"] == 0
+    assert st8["scatter_records"] == st1["scatter_records"]
+    assert np.array_equal(got, ref)
+    vr.Device._cache.pop(devices, None)  # release the eight full-size rank contexts
