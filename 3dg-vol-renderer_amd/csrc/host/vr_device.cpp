@@ -27,6 +27,7 @@ hipError_t launch_sfd_loss_diff(const uint32_t* bits0, const uint32_t* bits1, co
 hipError_t gauss_record_cut(const RenderArgs& A, float budget, hipStream_t stream);
 hipError_t gauss_whiten(const GaussianRecord* rec, WRecord* out, uint32_t n, uint32_t* bad, hipStream_t stream);
 hipError_t gauss_bin(const RenderArgs& A, bool emit, hipStream_t stream);
+hipError_t gauss_parents(const HNode4* nodes, uint32_t n, int32_t* parent, hipStream_t stream);
 hipError_t gauss_bin_scan(const uint32_t* cnt, uint32_t* off, uint32_t n, void* tmp, size_t& tmp_bytes, hipStream_t stream);
 hipError_t launch_pixel_losses(const float* img, const float* ref, uint32_t npix, float* out, hipStream_t stream);
 
@@ -51,6 +52,8 @@ struct vr_ctx {
     BVHNode* d_nodes = nullptr;
     HNode* d_hnodes = nullptr;
     HNode4* d_hnodes4 = nullptr;
+    int32_t* d_parent4 = nullptr;  // parent of every HNode4 (the secondary rays' climb out of their start subtree)
+    size_t num_nodes4 = 0;
     float hn_center[3] = {0, 0, 0}, hn_scale = 1.0f;
     float sig_max[3] = {0, 0, 0};  // largest per-axis standard deviation of any Gaussian
     SphereRecord* d_spheres = nullptr;
@@ -97,7 +100,7 @@ struct vr_ctx {
         size_t bytes = 0;
     };
     Buf px_first, px_T, rec_pos, rec_meta, rec_next, rec_act, tr, rec_rad, rec_alloc, rec_bloom, slowq;
-    Buf pcg_jump, ray_next, stack_ovf, env_order, rec_cut;
+    Buf pcg_jump, ray_next, stack_ovf, env_order, rec_cut, rec_start;
     Buf deep;  // march_deep_kernel: pixel queue + global active lists (vr_gauss.hip)
     Buf bin_cnt, bin_off, bin_ent;  // tile bins of the binned march (VR_OPT_MARCH_BINNED)
     Buf ff_scratch, ff_tail, ff_sum, ff_nee;  // free-flight integrators (vr_freeflight.hip)
@@ -123,6 +126,7 @@ struct vr_ctx {
     int64_t opt_device_bvh = 0;        // VR_OPT_DEVICE_BVH
     int64_t opt_march_binned = 0;      // VR_OPT_MARCH_BINNED
     int64_t opt_ff_solver = 0;         // VR_OPT_FF_SOLVER
+    int64_t opt_start_subtree = 1;     // VR_OPT_START_SUBTREE
     bool last_upload_device_bvh = false;  // the current scene's tree came from the device builder
     vr_group* group = nullptr;         // vr_init_multi: the devices this context drives (host/vr_multi.cpp)
 };
@@ -156,6 +160,9 @@ void free_scene(vr_ctx* c) {
     c->d_hnodes = nullptr;
     if (c->d_hnodes4) (void)hipFree(c->d_hnodes4);
     c->d_hnodes4 = nullptr;
+    if (c->d_parent4) (void)hipFree(c->d_parent4);
+    c->d_parent4 = nullptr;
+    c->num_nodes4 = 0;
     if (c->d_spheres) (void)hipFree(c->d_spheres);
     c->d_gauss = nullptr;
     c->d_nodes = nullptr;
@@ -296,6 +303,7 @@ vr_status upload_half_nodes(vr_ctx* c, const std::vector<BVHNode>& nodes) {
     }
     HIP_TRY(hipMalloc(&c->d_hnodes4, w4.size() * sizeof(HNode4)), "hipMalloc(wide nodes)");
     HIP_TRY(hipMemcpy(c->d_hnodes4, w4.data(), w4.size() * sizeof(HNode4), hipMemcpyHostToDevice), "hipMemcpy(wide nodes)");
+    c->num_nodes4 = w4.size();
     return VR_OK;
 }
 
@@ -372,11 +380,25 @@ vr_status upload_device_bvh(vr_ctx* c, const HostScene& s, const std::vector<flo
     c->d_nodes = R.nodes;
     c->d_hnodes = R.hnodes;
     c->d_hnodes4 = R.hnodes4;
+    c->num_nodes4 = R.hnodes4 ? R.num_nodes4 : 0;
     c->num_nodes = R.num_nodes;
     c->bvh_depth = R.max_depth;
     c->num_prims = (int32_t)N;
     c->last_upload_device_bvh = true;
     return upload_whitened(c, N);
+}
+
+// Parent of every 4-wide node (built on the device from the children refs): a secondary ray starts its
+// tree walk in the subtree holding its origin and climbs to the parents once that subtree is done
+// (vr_gauss.hip, record_start_kernel / sec_node4v).
+vr_status upload_parents(vr_ctx* c) {
+    if (c->d_parent4) (void)hipFree(c->d_parent4);
+    c->d_parent4 = nullptr;
+    if (!c->d_hnodes4 || c->num_nodes4 == 0) return VR_OK;
+    HIP_TRY(hipMalloc(&c->d_parent4, c->num_nodes4 * sizeof(int32_t)), "hipMalloc(wide-node parents)");
+    HIP_TRY(gauss_parents(c->d_hnodes4, (uint32_t)c->num_nodes4, c->d_parent4, c->stream), "wide-node parents");
+    HIP_TRY(hipStreamSynchronize(c->stream), "wide-node parents");
+    return VR_OK;
 }
 
 // Farthest distance any ray can travel before leaving the scene box: the rays of both camera
@@ -476,6 +498,7 @@ vr_status fill_args(vr_ctx* c, const vr_camera* cam, const vr_render_params* p, 
     A.nodes = c->d_nodes;
     A.hnodes = c->d_hnodes;
     A.hnodes4 = c->d_hnodes4;
+    A.hn4_parent = c->d_parent4;
     for (int k = 0; k < 3; ++k) A.hn_center[k] = c->hn_center[k];
     A.hn_scale = c->hn_scale;
     A.spheres = c->d_spheres;
@@ -679,6 +702,11 @@ vr_status gauss_pipeline(vr_ctx* c, RenderArgs& A, hipStream_t s, bool stats) {
         }
     }
     HIP_TRY(hipEventRecord(c->ev_stage[1], s), "hipEventRecord");
+    A.rec_start = nullptr;  // per record: the 4-wide subtree its secondary rays walk first (record_start_kernel)
+    if (A.hnodes4 != nullptr && A.hn4_parent != nullptr && c->opt_start_subtree) {
+        if ((st = grow(c->rec_start, cap * 4ull, "hipMalloc(record start nodes)")) != VR_OK) return st;
+        A.rec_start = (int32_t*)c->rec_start.p;
+    }
     {  // environment rays traced in direction order within chunks of 32 records (see ray_slot; larger
        // chunks measured 2-20 % slower: record locality is lost)
 #ifndef VR_CHUNK_SHIFT
@@ -726,7 +754,8 @@ vr_status free_flight_pipeline(vr_ctx* c, RenderArgs& A, hipStream_t s) {
     if ((st = grow(c->ff_tail, paths * sizeof(float4), "free-flight paths")) != VR_OK) return st;
     if ((st = grow(c->ff_sum, (size_t)A.num_tiles * 256 * 3 * sizeof(float), "free-flight sums")) != VR_OK) return st;
     {  // Deferred-NEE queue: VR_OPT_FF_NEE_QUEUE rays per path of a launch bound it; within that bound it is
-       // sized from the need of this context's earlier frames (the most rays any launch queued, + 1/8),
+       // sized from the need of this context's earlier frames (the most rays any launch queued, + 1/8;
+       // never shrunk, like the record buffers, so a frame that fitted before fits again),
        // a first frame from the integrator (one shadow ray per bounce, min_bounces + 1 bounces before
        // Russian roulette). A launch that outgrows it is reported and the frame rendered again with a
        // grown queue (as the ray-march's record buffers), so frames never depend on the capacity.
@@ -734,11 +763,6 @@ vr_status free_flight_pipeline(vr_ctx* c, RenderArgs& A, hipStream_t s) {
         const uint64_t first = paths * (A.ff_multi ? (uint64_t)A.ff_min_bounces + 1ull : 1ull) + 4096ull;
         const uint64_t cap = std::min<uint64_t>(bound, c->nee_hint ? std::max<uint64_t>(c->nee_hint, 4096ull) : first);
         const size_t bytes = (size_t)cap * 3 * sizeof(float4);
-        if (c->ff_nee.p && c->ff_nee.bytes > 2 * bytes + (64u << 20)) {  // shrink a queue sized for a larger frame
-            (void)hipFree(c->ff_nee.p);
-            c->ff_nee.p = nullptr;
-            c->ff_nee.bytes = 0;
-        }
         A.ff_nee_cap = (uint32_t)cap;
         c->last_nee_cap = (uint32_t)cap;
         c->last_nee_bound = (uint32_t)bound;
@@ -806,7 +830,7 @@ vr_status collect(vr_ctx* c) {
         // trace inline): grow at least twice over
         const uint64_t need = c->h_report[7];
         const bool over = need > c->last_nee_cap;
-        c->nee_hint = std::max<uint64_t>(need + need / 8, over ? 2ull * c->last_nee_cap : 0ull);
+        c->nee_hint = std::max<uint64_t>({c->nee_hint, need + need / 8, over ? 2ull * c->last_nee_cap : 0ull});
     }
     return VR_OK;
 }
@@ -961,7 +985,7 @@ void vr_destroy(vr_ctx* c) {
     if (c->h_sizing) (void)hipHostFree(c->h_sizing);
     for (vr_ctx::Buf* b : {&c->px_first, &c->px_T, &c->rec_pos, &c->rec_meta, &c->rec_next, &c->rec_act, &c->tr, &c->rec_rad,
                            &c->rec_alloc, &c->rec_bloom, &c->slowq, &c->pcg_jump, &c->ray_next,
-                           &c->stack_ovf, &c->env_order, &c->rec_cut, &c->deep, &c->bin_cnt, &c->bin_off, &c->bin_ent,
+                           &c->stack_ovf, &c->env_order, &c->rec_cut, &c->rec_start, &c->deep, &c->bin_cnt, &c->bin_off, &c->bin_ent,
                            &c->ff_scratch, &c->ff_tail, &c->ff_sum, &c->ff_nee, &c->ff_fb, &c->rec_bits[0], &c->rec_bits[1],
                            &c->sfd_tmp, &c->sfd_ref, &c->sfd_loss[0], &c->sfd_loss[1], &c->sfd_out})
         if (b->p) (void)hipFree(b->p);
@@ -1076,6 +1100,7 @@ vr_status vr_upload_scene(vr_ctx* c, const vr_scene* sc) {
         if (c->opt_device_bvh && N >= kDeviceBvhMin) {
             vr_status ds = upload_device_bvh(c, s, boxes);
             if (ds == VR_OK) {
+                if ((ds = upload_parents(c)) != VR_OK) return ds;
                 c->has_scene = true;
                 return VR_OK;
             }
@@ -1125,6 +1150,7 @@ vr_status vr_upload_scene(vr_ctx* c, const vr_scene* sc) {
     }
     if (c->num_prims == 0)
         for (int k = 0; k < 3; ++k) c->bmin[k] = c->bmax[k] = 0.0f;
+    if (vr_status ps = upload_parents(c); ps != VR_OK) return ps;
     c->has_scene = true;
     return VR_OK;
 }
@@ -1413,6 +1439,10 @@ vr_status vr_set_option(vr_ctx* c, int32_t option, int64_t value) {
             if (value < 0 || value > 4) return fail(VR_ERR_INVALID, "VR_OPT_FF_SOLVER must be in [0, 4]");
             c->opt_ff_solver = value;
             return VR_OK;
+        case VR_OPT_START_SUBTREE:
+            if (value != 0 && value != 1) return fail(VR_ERR_INVALID, "VR_OPT_START_SUBTREE must be 0 or 1");
+            c->opt_start_subtree = value;
+            return VR_OK;
         case VR_OPT_RECORD_CAPACITY:
             if ((value != 0 && value < 4096) || value > 0x3fffffff)
                 return fail(VR_ERR_INVALID, "VR_OPT_RECORD_CAPACITY must be 0 or in [4096, 2^30)");
@@ -1435,6 +1465,7 @@ vr_status vr_get_option(vr_ctx* c, int32_t option, int64_t* value) {
         case VR_OPT_FF_NEE_QUEUE: *value = c->opt_ff_nee_queue; return VR_OK;
         case VR_OPT_MARCH_BINNED: *value = c->opt_march_binned; return VR_OK;
         case VR_OPT_FF_SOLVER: *value = c->opt_ff_solver; return VR_OK;
+        case VR_OPT_START_SUBTREE: *value = c->opt_start_subtree; return VR_OK;
         default: return fail(VR_ERR_INVALID, "vr_get_option: unknown option " + std::to_string(option));
     }
 }

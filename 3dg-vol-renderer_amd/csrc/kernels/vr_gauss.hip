@@ -861,6 +861,9 @@ __global__ __launch_bounds__(64) void march_binned_kernel(RenderArgs A) {
 // through rounding) are rare; they go to a queue served by secondary_slow_kernel's exact
 // three-pass light_transmittance.
 // ---------------------------------------------------------------------------------------------
+// A 4-wide node index (< 2^27 nodes) in the walk's `node`; bits 28-30 may carry a child slot to skip.
+constexpr int32_t kNodeIndexMask = 0x0fffffff;
+
 struct SecRay {
     Ray ray;
     float ix, iy, iz, oxi, oyi, ozi;  // 1/d and o/d for the slab test
@@ -876,6 +879,7 @@ struct SecRay {
     uint32_t act_off, act_n;  // the record's active list
     bool light, needs_stop;
     uint32_t nsteps;  // instrumented build only: node steps taken by this ray
+    int32_t from;     // 4-wide walk: root of the subtree the ray walks / has finished (climbs from the record's start subtree)
     uint32_t rec;     // record index
     uint32_t slot;    // result slot s * rec_cap + rec in tr
 };
@@ -1078,6 +1082,7 @@ __device__ __forceinline__ bool sec_init(const RenderArgs& A, uint32_t nrec, uin
     R.credit = 0.0f;
     R.hitmask = 0;
     R.nsteps = 0;
+    R.from = 0;
     R.tau = 0.0f;
     R.needs_stop = false;
     if (s < (uint32_t)A.num_lights) {
@@ -1504,7 +1509,8 @@ __device__ __forceinline__ void sec_node4v(const RenderArgs& A, SecRay& R, LdsIn
         c.v[kCtrNodes]++;
         ++R.nsteps;
     }
-    const uint4* np = reinterpret_cast<const uint4*>(A.hnodes4 + node);
+    const int skip = node >> 28;  // a climb's node: the finished child's slot + 1 (0: none)
+    const uint4* np = reinterpret_cast<const uint4*>(A.hnodes4 + (node & kNodeIndexMask));
     const uint4 q0 = np[0], q1 = np[1], q2 = np[2], rf = np[3];
     const uint32_t w[12] = {q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, q1.z, q1.w, q2.x, q2.y, q2.z, q2.w};
     const int32_t ref[4] = {(int32_t)rf.x, (int32_t)rf.y, (int32_t)rf.z, (int32_t)rf.w};
@@ -1529,8 +1535,9 @@ __device__ __forceinline__ void sec_node4v(const RenderArgs& A, SecRay& R, LdsIn
         const float tz1 = fmaf(f[2], R.iz, -R.ozi), tz2 = fmaf(f[5], R.iz, -R.ozi);
         const float tmin = fmaxf(fmaxf(fminf(tx1, tx2), fminf(ty1, ty2)), fminf(tz1, tz2));
         const float tmax = fminf(fminf(fmaxf(tx1, tx2), fmaxf(ty1, ty2)), fmaxf(tz1, tz2));
-        // [max(tmin, 0), min(tmax, plim)] not empty; a NaN box (empty slot) fails the first compare
-        const bool hit = (tmin <= fminf(tmax, R.plim)) & (tmax >= 0.0f);
+        // [max(tmin, 0), min(tmax, plim)] not empty; a NaN box (empty slot) fails the first compare; the
+        // subtree the ray has just finished (child slot skip - 1, right after a climb) is skipped
+        const bool hit = (tmin <= fminf(tmax, R.plim)) & (tmax >= 0.0f) & (skip != i + 1);
         const bool leaf = hit & (ref[i] < 0);
         inner[i] = hit & !leaf;  // an empty slot (ref 0) never hits
         // leaf -> the queue's end: branch-free, a non-leaf store lands past the last entry (never
@@ -1565,6 +1572,13 @@ __device__ __forceinline__ void sec_node4v(const RenderArgs& A, SecRay& R, LdsIn
     } else if (sp > 0) {
         --sp;
         node = sp < STACK ? stack[sp * BLOCK] : A.stack_ovf[ovf_slot<BLOCK, STACK>(A, sp)];
+    } else if (R.from > 0) {
+        // the subtree rooted at R.from is done: its parent next, without that child (every node is still
+        // visited at most once: the walk from the record's start subtree up to the root covers the tree).
+        // The parent entry carries the child's slot in bits 28-30 (slot + 1), which the next step skips.
+        const int32_t up = A.hn4_parent[R.from];
+        R.from = up & kNodeIndexMask;
+        node = up;
     } else {
         node = -1;
     }
@@ -1637,14 +1651,14 @@ __device__ __forceinline__ void list_begin(SecRay& R, LeafQueue& Q, int& node) {
     Q.q1 = 0;  // ring head (ring queues): valid whenever the tree walk starts here
     Q.j = R.act_off;
     Q.end = R.act_off + R.act_n;
-    node = R.act_n > 0u ? kNodeList : 0;
+    node = R.act_n > 0u ? kNodeList : R.from;
 }
 
-// After a list slot was consumed: move to the tree once the list is done.
-__device__ __forceinline__ void list_advance(LeafQueue& Q, int& node) {
+// After a list slot was consumed: move to the tree (its start subtree) once the list is done.
+__device__ __forceinline__ void list_advance(LeafQueue& Q, int& node, int start) {
     if (node != kNodeList || Q.j < Q.end) return;
     Q.j = Q.end = 0;
-    node = 0;
+    node = start;
 }
 
 // Scheduling constants of the persistent kernel (tuned on C4): refill once this many
@@ -1744,7 +1758,11 @@ __global__ __launch_bounds__(BLOCK, WAVES) void secondary_ww_kernel(RenderArgs A
                 node = -1;
                 Q.n = 0;
                 Q.j = Q.end = 0;
-                if (live) list_begin(R, Q, node);
+                if (live) {
+                    if constexpr (W && VR_NODE4_V2)  // the tree walk starts in the record's start subtree
+                        if (A.rec_start != nullptr) R.from = A.rec_start[R.rec];
+                    list_begin(R, Q, node);
+                }
             }
             const uint32_t handed = (uint32_t)__popcll(idle);
             pool = pool_end - pool > handed ? pool + handed : pool_end;
@@ -1770,7 +1788,7 @@ __global__ __launch_bounds__(BLOCK, WAVES) void secondary_ww_kernel(RenderArgs A
                 if (node == kNodeList) {
                     ls = (int)(Q.j - R.act_off);
                     j = (uint32_t)A.rec_act[Q.j++];
-                    list_advance(Q, node);
+                    list_advance(Q, node, R.from);
                 } else {
                     ls = -1;
                     j = Q.next<QCAP, BLOCK>(ext);
@@ -1910,6 +1928,63 @@ __global__ __launch_bounds__(BLOCK) void secondary_slow_kernel(RenderArgs A) {
     if constexpr (S)
         for (int i = 0; i < kNumCtr; ++i)
             if (c.v[i]) atomicAdd(A.work + kNumCtr + i, (unsigned long long)c.v[i]);
+}
+
+// Parent of every 4-wide node with the node's slot in it: parent | (slot + 1) << 28 (root: -1).
+__global__ __launch_bounds__(256) void parents_kernel(const HNode4* __restrict__ nodes, uint32_t n, int32_t* __restrict__ parent) {
+    const uint32_t i = blockIdx.x * 256u + threadIdx.x;
+    if (i >= n) return;
+    if (i == 0) parent[0] = -1;
+    const int4 c = reinterpret_cast<const int4*>(nodes + i)[3];
+    if (c.x > 0) parent[c.x] = (int32_t)(i | (1u << 28));
+    if (c.y > 0) parent[c.y] = (int32_t)(i | (2u << 28));
+    if (c.z > 0) parent[c.z] = (int32_t)(i | (3u << 28));
+    if (c.w > 0) parent[c.w] = (int32_t)(i | (4u << 28));
+}
+
+// Start subtree of a record's secondary rays: the deepest 4-wide node whose box holds the record position
+// with `margin` (scene-normalised units) to spare, taking at every level the inner child with the most
+// room. The rays walk that subtree first and then climb to its parents (sec_node4v), so every node is
+// still visited at most once, and a ray whose optical-depth cut-off is reached near its origin — most of
+// them: the record sits inside an opaque blob's neighbours — skips the descent from the root.
+#ifndef VR_START_MARGIN
+#define VR_START_MARGIN 0.0f  // room (world units) the start subtree's box keeps around the record position (A/B)
+#endif
+__global__ __launch_bounds__(256) void record_start_kernel(RenderArgs A) {
+    const uint32_t nrec = dev_nrec(A);
+    const float margin = VR_START_MARGIN * A.hn_scale;
+    for (uint32_t r = blockIdx.x * 256u + threadIdx.x; r < nrec; r += gridDim.x * 256u) {
+        const float4 pos = A.rec_pos[r];
+        float p[3] = {pos.x, pos.y, pos.z};
+        node_space<true>(A, p[0], p[1], p[2]);
+        int32_t node = 0;
+        for (int depth = 0; depth < kWideStackMax; ++depth) {
+            const uint4* np = reinterpret_cast<const uint4*>(A.hnodes4 + node);
+            const uint4 q0 = np[0], q1 = np[1], q2 = np[2], rf = np[3];
+            const uint32_t w[12] = {q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, q1.z, q1.w, q2.x, q2.y, q2.z, q2.w};
+            const int32_t ref[4] = {(int32_t)rf.x, (int32_t)rf.y, (int32_t)rf.z, (int32_t)rf.w};
+            float best = margin;
+            int32_t next = -1;
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                float room = INFINITY;
+#pragma unroll
+                for (int k = 0; k < 3; ++k) {
+                    const uint32_t wl = w[(6 * i + k) >> 1], wh = w[(6 * i + 3 + k) >> 1];
+                    const float lo = (float)__builtin_bit_cast(_Float16, (uint16_t)(((6 * i + k) & 1) ? (wl >> 16) : (wl & 0xffffu)));
+                    const float hi =
+                        (float)__builtin_bit_cast(_Float16, (uint16_t)(((6 * i + 3 + k) & 1) ? (wh >> 16) : (wh & 0xffffu)));
+                    room = fminf(room, fminf(p[k] - lo, hi - p[k]));
+                }
+                const bool take = (ref[i] > 0) & (room >= best);  // (a NaN box never has room)
+                best = take ? room : best;
+                next = take ? ref[i] : next;
+            }
+            if (next < 0) break;
+            node = next;
+        }
+        A.rec_start[r] = node;
+    }
 }
 
 // WRecord of every record (vr_internal.h): Cholesky factor of M = Sigma^-1 in double. A record whose M
@@ -2162,6 +2237,11 @@ static unsigned record_grid(const RenderArgs& A, uint32_t per_block, unsigned ma
 
 hipError_t gauss_secondary(const RenderArgs& A, hipStream_t stream, bool stats) {
     if (A.num_lights + A.env_samples == 0) return hipSuccess;
+    if (A.rec_start != nullptr) {  // every record's start subtree (the 4-wide walk with parents only)
+        hipLaunchKernelGGL(dev::record_start_kernel, dim3(record_grid(A, 256, 16384)), dim3(256), 0, stream, A);
+        hipError_t e = hipGetLastError();
+        if (e != hipSuccess) return e;
+    }
     if (A.env_order != nullptr) {
         hipLaunchKernelGGL(dev::env_order_kernel<256>, dim3(record_grid(A, A.chunk_rec, 4096)), dim3(256), 0, stream, A);
         hipError_t e = hipGetLastError();
@@ -2171,6 +2251,11 @@ hipError_t gauss_secondary(const RenderArgs& A, hipStream_t stream, bool stats) 
     // the work this schedule really does (node steps, list and leaf primitive tests, optical depths)
     if (A.pure) return stats ? secondary_launch<true, true>(A, stream) : secondary_launch<false, true>(A, stream);
     return stats ? secondary_launch<true, false>(A, stream) : secondary_launch<false, false>(A, stream);
+}
+
+hipError_t gauss_parents(const HNode4* nodes, uint32_t n, int32_t* parent, hipStream_t stream) {
+    hipLaunchKernelGGL(dev::parents_kernel, dim3((n + 255) / 256), dim3(256), 0, stream, nodes, n, parent);
+    return hipGetLastError();
 }
 
 hipError_t gauss_whiten(const GaussianRecord* rec, WRecord* out, uint32_t n, uint32_t* bad, hipStream_t stream) {

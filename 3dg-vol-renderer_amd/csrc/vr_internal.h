@@ -137,6 +137,7 @@ struct RenderArgs {
     const BVHNode* nodes;
     const HNode* hnodes;      // nullptr: the scene is not suited to half-precision boxes (see vr_device.cpp)
     const HNode4* hnodes4;    // 4-wide collapse of the same tree (secondary rays); nullptr with hnodes
+    const int32_t* hn4_parent;  // parent of every HNode4 (root: -1); nullptr: secondary rays start at the root
     float hn_center[3], hn_scale;
     const SphereRecord* spheres;
     int32_t num_prims;
@@ -184,6 +185,7 @@ struct RenderArgs {
     uint32_t chunk_rec;             // records per secondary-ray chunk (power of 2; 64 without env_order)
     uint32_t chunk_shift;           // log2(chunk_rec)
     float* rec_cut;                 // per record: optical-depth cut-off of its secondary rays (nullptr: tau_cut)
+    int32_t* rec_start;             // per record: the HNode4 subtree its secondary rays walk first (nullptr: the root)
     // ---- free-flight integrators (vr_freeflight.hip): one (tile chunk, sample batch) step ----
     int32_t ff_multi;        // 0 FreeFlightGaussians, 1 MultiScatterGaussians
     int32_t ff_samples;      // samples per pixel (integrator num_samples)

@@ -340,10 +340,10 @@ class Device:
         return bool(lib().vr_ctx_uses_rccl(self._h))
 
     def rank_stats(self, rank):
+        """vr_get_rank_stats: one rank's statistics of the last frame (same keys as stats())."""
         s = L.vr_render_stats()
         check(lib().vr_get_rank_stats(self._h, int(rank), ctypes.byref(s)))
-        return {"kernel_ms": s.kernel_ms, "pixels": s.pixels, "fallback_pixels": s.fallback_pixels,
-                "error_pixels": s.error_pixels, "scatter_records": s.scatter_records}
+        return self._stats_dict(s)
 
     @classmethod
     def get(cls, device=0):
@@ -364,6 +364,9 @@ class Device:
     def stats(self):
         s = L.vr_render_stats()
         check(lib().vr_get_stats(self._h, ctypes.byref(s)))
+        return self._stats_dict(s)
+
+    def _stats_dict(self, s):
         return {"kernel_ms": s.kernel_ms, "pixels": s.pixels, "fallback_pixels": s.fallback_pixels,
                 "error_pixels": s.error_pixels, "stage_ms": dict(zip(self.STAGES, list(s.stage_ms))),
                 "scatter_records": s.scatter_records, "secondary_rays": s.secondary_rays,
@@ -382,7 +385,8 @@ class Device:
     OPTIONS = {"half_nodes": L.VR_OPT_HALF_NODES, "secondary_budget": L.VR_OPT_SECONDARY_BUDGET,
                "ff_window0": L.VR_OPT_FF_WINDOW0, "record_capacity": L.VR_OPT_RECORD_CAPACITY,
                "device_bvh": L.VR_OPT_DEVICE_BVH, "ff_nee_queue": L.VR_OPT_FF_NEE_QUEUE,
-               "march_binned": L.VR_OPT_MARCH_BINNED, "ff_solver": L.VR_OPT_FF_SOLVER}
+               "march_binned": L.VR_OPT_MARCH_BINNED, "ff_solver": L.VR_OPT_FF_SOLVER,
+               "start_subtree": L.VR_OPT_START_SUBTREE}
 
     def set_option(self, name, value):
         """vr_set_option (include/vr_hip.h): explicit per-context tuning (half_nodes applies at the

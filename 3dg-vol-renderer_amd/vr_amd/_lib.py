@@ -23,6 +23,7 @@ VR_OPT_HALF_NODES, VR_OPT_SECONDARY_BUDGET, VR_OPT_FF_WINDOW0, VR_OPT_RECORD_CAP
 VR_OPT_FF_NEE_QUEUE = 6
 VR_OPT_MARCH_BINNED = 7
 VR_OPT_FF_SOLVER = 8
+VR_OPT_START_SUBTREE = 9
 
 f3 = ctypes.c_float * 3
 

@@ -364,12 +364,17 @@ typedef enum vr_option {
                                     window queries per pixel; 1: Gaussians binned to 16x16 tiles by depth
                                     bucket, each tile's list streamed by its waves.
                                     Results are identical (the same exact intersect decides every entry). */
-    VR_OPT_FF_SOLVER = 8         /* free-flight integrators: the distance solver (distance_solvers.h:143-187, a
+    VR_OPT_FF_SOLVER = 8,        /* free-flight integrators: the distance solver (distance_solvers.h:143-187, a
                                     compile-time #define in the reference): 0 (default) ANALYTIC_PLUS_NEWTON, the
                                     mode the reference compiles (:146); 1 BISECTION; 2 NEWTON; 3
                                     ANALYTIC_PLUS_BISECTION; 4 UNIFORM, whose rand01() (mt19937 seeded by
                                     random_device, not reproducible) is replaced by the textbook-PCG32 uniform of
                                     stream 2 + bounce of the path's derive_path_seed (documented deviation). */
+    VR_OPT_START_SUBTREE = 9     /* RayMarchingGaussians / PureRayMarching secondary rays (4-wide tree): 1 (default):
+                                    a ray walks the deepest subtree holding its record's position first, then
+                                    climbs to the root (no descent from the root for rays cut near their origin);
+                                    0: every walk starts at the root. Same Gaussians, same decisions; only the
+                                    order of the optical-depth sum differs (float association). */
 } vr_option;
 vr_status vr_set_option(vr_ctx* ctx, int32_t option, int64_t value);
 vr_status vr_get_option(vr_ctx* ctx, int32_t option, int64_t* value);
