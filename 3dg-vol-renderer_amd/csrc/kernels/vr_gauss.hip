@@ -863,6 +863,12 @@ __global__ __launch_bounds__(64) void march_binned_kernel(RenderArgs A) {
 // ---------------------------------------------------------------------------------------------
 // A 4-wide node index (< 2^27 nodes) in the walk's `node`; bits 28-30 may carry a child slot to skip.
 constexpr int32_t kNodeIndexMask = 0x0fffffff;
+#ifdef VR_DIAG_LEVELS
+// Diagnostic builds only: VR_DIAG_LEVELS = 1 counts the node steps of the rays that end uncut, 2 those of
+// the rays that reach their cut-off, by tree depth (secondary counters [8 + b]: depths 2b, 2b + 1; b = 7:
+// deeper). Depths of the 4-wide nodes from their parents (depth_kernel, before the secondary stage).
+__device__ uint8_t g_diag_depth[1u << 23];
+#endif
 
 struct SecRay {
     Ray ray;
@@ -880,6 +886,9 @@ struct SecRay {
     bool light, needs_stop;
     uint32_t nsteps;  // instrumented build only: node steps taken by this ray
     int32_t from;     // 4-wide walk: root of the subtree the ray walks / has finished (climbs from the record's start subtree)
+#ifdef VR_DIAG_LEVELS  // diagnostic builds only: this ray's node steps per tree depth (2 levels per bucket)
+    uint32_t lv[8];
+#endif
     uint32_t rec;     // record index
     uint32_t slot;    // result slot s * rec_cap + rec in tr
 };
@@ -1083,6 +1092,9 @@ __device__ __forceinline__ bool sec_init(const RenderArgs& A, uint32_t nrec, uin
     R.hitmask = 0;
     R.nsteps = 0;
     R.from = 0;
+#ifdef VR_DIAG_LEVELS
+    for (int b = 0; b < 8; ++b) R.lv[b] = 0;
+#endif
     R.tau = 0.0f;
     R.needs_stop = false;
     if (s < (uint32_t)A.num_lights) {
@@ -1201,7 +1213,12 @@ __device__ __forceinline__ void sec_add(const RenderArgs& A, SecRay& R, const GR
 // records (A.wrec); false: the M forms of the records (a scene with a non-positive-definite M).
 template <bool S, bool FAST, bool PURE, bool WH = !PURE>
 __device__ __forceinline__ void sec_finish(const RenderArgs& A, SecRay& R, Ctr& c) {
-#if !defined(VR_DIAG_WAVE_UTIL) && !defined(VR_DIAG_CYCLES) && !defined(VR_DIAG_ORIGIN)
+#ifdef VR_DIAG_LEVELS
+    if constexpr (S)
+        if ((VR_DIAG_LEVELS == 2) == cut_reached<PURE>(R))
+            for (int b = 0; b < 8; ++b)
+                if (R.lv[b]) atomicAdd(A.work + kNumCtr + b, (unsigned long long)R.lv[b]);
+#elif !defined(VR_DIAG_WAVE_UTIL) && !defined(VR_DIAG_CYCLES) && !defined(VR_DIAG_ORIGIN)
     if constexpr (S) {  // secondary-stage diagnostics in otherwise unused counter slots
         if (cut_reached<PURE>(R)) {
             c.v[kCtrSteps]++;                 // rays ended by the optical-depth cut-off
@@ -1510,6 +1527,9 @@ __device__ __forceinline__ void sec_node4v(const RenderArgs& A, SecRay& R, LdsIn
         ++R.nsteps;
     }
     const int skip = node >> 28;  // a climb's node: the finished child's slot + 1 (0: none)
+#ifdef VR_DIAG_LEVELS
+    R.lv[min((int)g_diag_depth[node & kNodeIndexMask] >> 1, 7)]++;
+#endif
     const uint4* np = reinterpret_cast<const uint4*>(A.hnodes4 + (node & kNodeIndexMask));
     const uint4 q0 = np[0], q1 = np[1], q2 = np[2], rf = np[3];
     const uint32_t w[12] = {q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, q1.z, q1.w, q2.x, q2.y, q2.z, q2.w};
@@ -1901,7 +1921,9 @@ __global__ __launch_bounds__(BLOCK, WAVES) void secondary_ww_kernel(RenderArgs A
             live = false;
         }
     }
+#ifndef VR_DIAG_LEVELS
     if constexpr (S) flush_counters(A.work + kNumCtr, c);
+#endif
 }
 
 // Exact three-pass light transmittance for the queued rays (see light_transmittance).
@@ -1929,6 +1951,16 @@ __global__ __launch_bounds__(BLOCK) void secondary_slow_kernel(RenderArgs A) {
         for (int i = 0; i < kNumCtr; ++i)
             if (c.v[i]) atomicAdd(A.work + kNumCtr + i, (unsigned long long)c.v[i]);
 }
+
+#ifdef VR_DIAG_LEVELS
+__global__ __launch_bounds__(256) void depth_kernel(const int32_t* __restrict__ parent, uint32_t n) {
+    const uint32_t i = blockIdx.x * 256u + threadIdx.x;
+    if (i >= n || i >= (1u << 23)) return;
+    uint32_t d = 0;
+    for (int32_t x = (int32_t)i; x > 0; x = parent[x] & kNodeIndexMask) ++d;
+    g_diag_depth[i] = (uint8_t)min(d, 255u);
+}
+#endif
 
 // Parent of every 4-wide node with the node's slot in it: parent | (slot + 1) << 28 (root: -1).
 __global__ __launch_bounds__(256) void parents_kernel(const HNode4* __restrict__ nodes, uint32_t n, int32_t* __restrict__ parent) {
@@ -2237,6 +2269,10 @@ static unsigned record_grid(const RenderArgs& A, uint32_t per_block, unsigned ma
 
 hipError_t gauss_secondary(const RenderArgs& A, hipStream_t stream, bool stats) {
     if (A.num_lights + A.env_samples == 0) return hipSuccess;
+#ifdef VR_DIAG_LEVELS
+    if (A.hn4_parent != nullptr && A.num_nodes4 > 0)
+        hipLaunchKernelGGL(dev::depth_kernel, dim3((A.num_nodes4 + 255) / 256), dim3(256), 0, stream, A.hn4_parent, A.num_nodes4);
+#endif
     if (A.rec_start != nullptr) {  // every record's start subtree (the 4-wide walk with parents only)
         hipLaunchKernelGGL(dev::record_start_kernel, dim3(record_grid(A, 256, 16384)), dim3(256), 0, stream, A);
         hipError_t e = hipGetLastError();

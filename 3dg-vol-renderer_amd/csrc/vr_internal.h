@@ -1,6 +1,7 @@
 // Internal layouts shared by the host side (scene prep, BVH build, launch) and the HIP kernels.
 // Everything here is plain data: it is the HBM image of a scene.
 #pragma once
+#include <hip/hip_runtime_api.h>
 #include <hip/hip_vector_types.h>
 #include <stdint.h>
 
@@ -112,6 +113,13 @@ constexpr uint32_t kFFNeeMaxPerPath = 16;  // VR_OPT_FF_NEE_QUEUE bound (queue r
 constexpr int32_t kFFBigCap = 1024;          // ff_fallback_kernel: Gaussians overlapping one point it can sweep
 constexpr uint32_t kFFBigThreads = 1024;     // ff_fallback_kernel: threads (scratch row stride)
 
+// Host-side polling of the staged free-flight pipeline (vr_freeflight.hip ffs_run): two pinned words
+// and their events.
+struct FFPoll {
+    uint32_t* host;
+    hipEvent_t ev[2];
+};
+
 // Kernel launch parameters (passed by value).
 struct RenderArgs {
     // camera
@@ -137,7 +145,8 @@ struct RenderArgs {
     const BVHNode* nodes;
     const HNode* hnodes;      // nullptr: the scene is not suited to half-precision boxes (see vr_device.cpp)
     const HNode4* hnodes4;    // 4-wide collapse of the same tree (secondary rays); nullptr with hnodes
-    const int32_t* hn4_parent;  // parent of every HNode4 (root: -1); nullptr: secondary rays start at the root
+    const int32_t* hn4_parent;  // parent of every HNode4 | (its slot + 1) << 28 (root: -1); nullptr: walks start at the root
+    uint32_t num_nodes4;        // HNode4 count
     float hn_center[3], hn_scale;
     const SphereRecord* spheres;
     int32_t num_prims;
@@ -219,6 +228,22 @@ struct RenderArgs {
     uint32_t ff_nee_cap;     // queue capacity in rays (0: every shadow ray is traced inline)
     int32_t ff_nee_refill;   // idle lanes of a wave that trigger its refill in ff_nee_kernel
     float4* ff_tail;         // [path of the launch]: {inline radiance xyz, first queued ray | kFFTailAfter}
+    // Staged free-flight pipeline (vr_freeflight.hip ffs_* kernels): ff_pool path slots step through a
+    // hit-collection, an event-sweep and a shading kernel per iteration, queued between them; the scratch
+    // rows above are indexed by slot (ff_threads = ff_pool). ff_pool == 0: the persistent path kernel.
+    uint32_t ff_pool;
+    float4* fs_ray0;         // per slot: {origin, target optical depth of the bounce}
+    float4* fs_ray1;         // {direction, W0: start of the hit window}
+    float4* fs_tp;           // {throughput, t_prev: the sweep's segment start}
+    float4* fs_L;            // {inline radiance, t_cut: end of the collected window}
+    float4* fs_out;          // {t_scatter (-1: no scatter, -2: over capacity), albedo, -, -}
+    double* fs_acc;          // optical depth accumulated before the window (FreeFlightGaussians: a float)
+    unsigned long long* fs_rng;  // PCG32 state (stream 1)
+    uint4* fs_meta;          // {path index of the launch, first / last queued shadow ray, bounce}
+    uint4* fs_meta2;         // {flags (1: defer NEE, 2: inline radiance after the queued), window capacity, hits, -}
+    uint32_t* fs_q;          // slot queues, ff_pool entries each: collect[0], collect[1], sweep, shade
+    uint32_t* fs_cnt;        // [0], [1] collect queue lengths, [2] sweep, [3] shade, [4], [5] claim counters
+    uint32_t fs_cur;         // the collect queue this iteration consumes
     const uint32_t* gauss_order;  // record (leaf order) -> scene index
     uint32_t* rec_bits;      // RECORD_PIXEL_GAUSSIANS bitset [word][pixel] (nullptr: not recording)
     uint32_t rec_npix;       // W * H

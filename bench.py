@@ -324,6 +324,8 @@ def main():
                          "secondary lines (unit Mpaths/s = pixel samples per second)")
     ap.add_argument("--spp", type=int, default=None,
                     help="free-flight paths per pixel (default 16; 256 with --config main, as tests/main.cpp:27)")
+    ap.add_argument("--opt", action="append", default=[],
+                    help="name=value device option (vr_set_option, e.g. ff_staged=0) for A/B runs")
     args = ap.parse_args()
     if args.config == "main":  # tests/main.cpp renders MultiScatterGaussians
         if args.integrator == "raymarch":
@@ -367,6 +369,9 @@ def main():
         integ = vr.RayMarchingGaussians(camera, step_size=0.01, env_samples=args.env_samples, t_eps=args.t_eps,
                                         device=local)
     dev = vr.Device.get(local)
+    for o in args.opt:
+        k, v = o.split("=")
+        dev.set_option(k, int(v))
     dev.upload(scene)
     t_setup = time.perf_counter() - t_setup
 

@@ -370,11 +370,15 @@ typedef enum vr_option {
                                     ANALYTIC_PLUS_BISECTION; 4 UNIFORM, whose rand01() (mt19937 seeded by
                                     random_device, not reproducible) is replaced by the textbook-PCG32 uniform of
                                     stream 2 + bounce of the path's derive_path_seed (documented deviation). */
-    VR_OPT_START_SUBTREE = 9     /* RayMarchingGaussians / PureRayMarching secondary rays (4-wide tree): 1 (default):
+    VR_OPT_START_SUBTREE = 9,    /* RayMarchingGaussians / PureRayMarching secondary rays (4-wide tree): 1 (default):
                                     a ray walks the deepest subtree holding its record's position first, then
                                     climbs to the root (no descent from the root for rays cut near their origin);
                                     0: every walk starts at the root. Same Gaussians, same decisions; only the
                                     order of the optical-depth sum differs (float association). */
+    VR_OPT_FF_STAGED = 10        /* free-flight integrators: 1 (default): the staged pipeline (a pool of path slots
+                                    stepping through hit-collection, event-sweep and shading kernels, queued
+                                    between them, each with per-lane refill); 0: the persistent path kernel
+                                    (a whole bounce per lane and wave iteration). Frames are identical. */
 } vr_option;
 vr_status vr_set_option(vr_ctx* ctx, int32_t option, int64_t value);
 vr_status vr_get_option(vr_ctx* ctx, int32_t option, int64_t* value);

@@ -283,3 +283,32 @@ def test_solver_modes_change_the_frame():
     finally:
         vr.Device.get(0).set_option("ff_solver", 0)
     assert not np.array_equal(frames["analytic_newton"], frames["uniform"])
+
+
+@pytest.mark.parametrize("multi", [False, True])
+@pytest.mark.parametrize("name,W,spp", [("50_random.txt", 40, 8), ("many_gaussians.txt", 32, 8), ("god_ray.txt", 32, 4)])
+def test_staged_pipeline_equals_persistent_kernel(name, W, spp, multi, device_options):
+    """VR_OPT_FF_STAGED: the staged pipeline (path slots stepping through the hit-collection, event-sweep and
+    shading kernels) runs every path's operations in the persistent path kernel's order, so the two
+    frames are equal bit for bit."""
+    scene = vr.Scene.load_GMM(scene_path(name))
+    frames = {}
+    for staged in (0, 1):
+        device_options("ff_staged", staged)
+        frames[staged] = _gpu(scene, W, W, multi, spp)
+    assert np.array_equal(frames[0], frames[1])
+
+
+def test_staged_pipeline_windows_and_fallback_equal_persistent(device_options):
+    """The staged pipeline's window continuations (hit windows of capacity 1 force a new collection per
+    event) and its capacity fallback (more Gaussians overlapping one point than the rows hold) equal the
+    persistent kernel's frames."""
+    scene = vr.Scene.load_GMM(scene_path("50_random.txt"))
+    coinc, _ = _coincident_scene(200)
+    out = {}
+    for staged in (0, 1):
+        device_options("ff_staged", staged)
+        device_options("ff_window0", 1)
+        out[staged] = (_gpu(scene, 24, 24, True, 4), _gpu(coinc, 16, 16, True, 4))
+    assert np.array_equal(out[0][0], out[1][0])
+    assert np.array_equal(out[0][1], out[1][1])
