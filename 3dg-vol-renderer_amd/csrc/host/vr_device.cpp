@@ -27,7 +27,7 @@ hipError_t launch_sfd_loss_diff(const uint32_t* bits0, const uint32_t* bits1, co
 hipError_t gauss_record_cut(const RenderArgs& A, float budget, hipStream_t stream);
 hipError_t gauss_whiten(const GaussianRecord* rec, WRecord* out, uint32_t n, uint32_t* bad, hipStream_t stream);
 hipError_t gauss_bin(const RenderArgs& A, bool emit, hipStream_t stream);
-hipError_t gauss_parents(const HNode4* nodes, uint32_t n, int32_t* parent, hipStream_t stream);
+hipError_t gauss_parents(const HNode4* nodes, uint32_t n, int32_t* parent, uint4* sib, hipStream_t stream);
 hipError_t gauss_bin_scan(const uint32_t* cnt, uint32_t* off, uint32_t n, void* tmp, size_t& tmp_bytes, hipStream_t stream);
 hipError_t launch_pixel_losses(const float* img, const float* ref, uint32_t npix, float* out, hipStream_t stream);
 
@@ -53,6 +53,7 @@ struct vr_ctx {
     HNode* d_hnodes = nullptr;
     HNode4* d_hnodes4 = nullptr;
     int32_t* d_parent4 = nullptr;  // parent of every HNode4 (the secondary rays' climb out of their start subtree)
+    uint4* d_sib4 = nullptr;       // union box of every HNode4's siblings (the climb's skip test)
     size_t num_nodes4 = 0;
     float hn_center[3] = {0, 0, 0}, hn_scale = 1.0f;
     float sig_max[3] = {0, 0, 0};  // largest per-axis standard deviation of any Gaussian
@@ -166,6 +167,8 @@ void free_scene(vr_ctx* c) {
     c->d_hnodes4 = nullptr;
     if (c->d_parent4) (void)hipFree(c->d_parent4);
     c->d_parent4 = nullptr;
+    if (c->d_sib4) (void)hipFree(c->d_sib4);
+    c->d_sib4 = nullptr;
     c->num_nodes4 = 0;
     if (c->d_spheres) (void)hipFree(c->d_spheres);
     c->d_gauss = nullptr;
@@ -398,9 +401,12 @@ vr_status upload_device_bvh(vr_ctx* c, const HostScene& s, const std::vector<flo
 vr_status upload_parents(vr_ctx* c) {
     if (c->d_parent4) (void)hipFree(c->d_parent4);
     c->d_parent4 = nullptr;
+    if (c->d_sib4) (void)hipFree(c->d_sib4);
+    c->d_sib4 = nullptr;
     if (!c->d_hnodes4 || c->num_nodes4 == 0) return VR_OK;
     HIP_TRY(hipMalloc(&c->d_parent4, c->num_nodes4 * sizeof(int32_t)), "hipMalloc(wide-node parents)");
-    HIP_TRY(gauss_parents(c->d_hnodes4, (uint32_t)c->num_nodes4, c->d_parent4, c->stream), "wide-node parents");
+    HIP_TRY(hipMalloc(&c->d_sib4, c->num_nodes4 * sizeof(uint4)), "hipMalloc(wide-node siblings)");
+    HIP_TRY(gauss_parents(c->d_hnodes4, (uint32_t)c->num_nodes4, c->d_parent4, c->d_sib4, c->stream), "wide-node parents");
     HIP_TRY(hipStreamSynchronize(c->stream), "wide-node parents");
     return VR_OK;
 }
@@ -504,6 +510,7 @@ vr_status fill_args(vr_ctx* c, const vr_camera* cam, const vr_render_params* p, 
     A.hnodes4 = c->d_hnodes4;
     A.hn4_parent = c->d_parent4;
     A.num_nodes4 = (uint32_t)c->num_nodes4;
+    A.hn4_sib = c->d_sib4;
     for (int k = 0; k < 3; ++k) A.hn_center[k] = c->hn_center[k];
     A.hn_scale = c->hn_scale;
     A.spheres = c->d_spheres;

@@ -374,6 +374,10 @@ __device__ __forceinline__ bool march_step(const RenderArgs& A, const Ray& ray, 
 #define VR_MARCH_UNSORTED 1  // 1: the march's entrant queries walk the 4-wide nodes without sorting (A/B)
 #endif
 constexpr bool kMarchUnsorted = VR_MARCH_UNSORTED;
+#ifndef VR_MARCH_PRETEST
+#define VR_MARCH_PRETEST 1  // 1: the march's BVH queries skip certain misses with the fast forms (fast_reject_*)
+#endif
+constexpr bool kMarchPretest = VR_MARCH_PRETEST;
 
 template <int ACT, bool S, bool H, bool W = false, int CAP = kStackSize, bool COOP = false>
 __device__ int march(const RenderArgs& A, uint32_t p, int px, int py, int* act_base, int* stack, int stride, Ctr& c,
@@ -421,6 +425,7 @@ __device__ int march(const RenderArgs& A, uint32_t p, int px, int py, int* act_b
                         for (uint32_t j = first; j < first + count; ++j) {
                             if constexpr (S) c.v[kCtrPrims]++;
                             GRec g = load_rec(G, j);
+                            if (kMarchPretest && fast_reject_closest(g, ray, t_lo, best)) continue;
                             Quad q = quad(g, ray);
                             float a, b;
                             if (intersect(q, a, b) && a > t_lo && a < best) best = a;
@@ -446,6 +451,7 @@ __device__ int march(const RenderArgs& A, uint32_t p, int px, int py, int* act_b
                     for (uint32_t j = first; j < first + count; ++j) {
                         if constexpr (S) c.v[kCtrPrims]++;
                         GRec g = load_rec(G, j);
+                        if (kMarchPretest && fast_reject_window(g, ray, t_lo, t_k)) continue;
                         Quad q = quad(g, ray);
                         float a, b;
                         if (!intersect(q, a, b) || !(a > t_lo) || !(a <= t_k) || !(b > t_k)) continue;
@@ -863,6 +869,10 @@ __global__ __launch_bounds__(64) void march_binned_kernel(RenderArgs A) {
 // ---------------------------------------------------------------------------------------------
 // A 4-wide node index (< 2^27 nodes) in the walk's `node`; bits 28-30 may carry a child slot to skip.
 constexpr int32_t kNodeIndexMask = 0x0fffffff;
+#ifndef VR_CLIMB_SKIP
+#define VR_CLIMB_SKIP 0  // 1: a climbing ray tests its finished subtree's siblings' union box first (A/B)
+#endif
+constexpr bool kClimbSkip = VR_CLIMB_SKIP;
 #ifdef VR_DIAG_LEVELS
 // Diagnostic builds only: VR_DIAG_LEVELS = 1 counts the node steps of the rays that end uncut, 2 those of
 // the rays that reach their cut-off, by tree depth (secondary counters [8 + b]: depths 2b, 2b + 1; b = 7:
@@ -1511,6 +1521,20 @@ __device__ __forceinline__ void sec_node4(const RenderArgs& A, SecRay& R, LdsInt
     }
 }
 
+// The ray's slab test against a sibling-union box (siblings_kernel's layout: 6 f16 in the first 12 B).
+__device__ __forceinline__ bool sibling_hit(const RenderArgs& A, const SecRay& R, const uint4& b) {
+    const uint32_t w[3] = {b.x, b.y, b.z};
+    float f[6];
+#pragma unroll
+    for (int k = 0; k < 6; ++k) f[k] = (float)__builtin_bit_cast(_Float16, (uint16_t)((k & 1) ? (w[k >> 1] >> 16) : (w[k >> 1] & 0xffffu)));
+    const float tx1 = fmaf(f[0], R.ix, -R.oxi), tx2 = fmaf(f[3], R.ix, -R.oxi);
+    const float ty1 = fmaf(f[1], R.iy, -R.oyi), ty2 = fmaf(f[4], R.iy, -R.oyi);
+    const float tz1 = fmaf(f[2], R.iz, -R.ozi), tz2 = fmaf(f[5], R.iz, -R.ozi);
+    const float tmin = fmaxf(fmaxf(fminf(tx1, tx2), fminf(ty1, ty2)), fminf(tz1, tz2));
+    const float tmax = fminf(fminf(fmaxf(tx1, tx2), fmaxf(ty1, ty2)), fmaxf(tz1, tz2));
+    return (tmin <= fminf(tmax, R.plim)) & (tmax >= 0.0f);
+}
+
 #ifndef VR_NODE4_V2
 #define VR_NODE4_V2 1  // 1: sec_node4v (no sorting network), 0: sec_node4 (A/B)
 #endif
@@ -1596,9 +1620,15 @@ __device__ __forceinline__ void sec_node4v(const RenderArgs& A, SecRay& R, LdsIn
         // the subtree rooted at R.from is done: its parent next, without that child (every node is still
         // visited at most once: the walk from the record's start subtree up to the root covers the tree).
         // The parent entry carries the child's slot in bits 28-30 (slot + 1), which the next step skips.
-        const int32_t up = A.hn4_parent[R.from];
+        int32_t up = A.hn4_parent[R.from];
+        if constexpr (kClimbSkip) {  // parents whose other children the ray misses are passed over
+            while (up > 0 && !sibling_hit(A, R, A.hn4_sib[R.from])) {
+                R.from = up & kNodeIndexMask;
+                up = A.hn4_parent[R.from];
+            }
+        }
         R.from = up & kNodeIndexMask;
-        node = up;
+        node = up;  // (-1: the root's subtree is done)
     } else {
         node = -1;
     }
@@ -1974,6 +2004,39 @@ __global__ __launch_bounds__(256) void parents_kernel(const HNode4* __restrict__
     if (c.w > 0) parent[c.w] = (int32_t)(i | (4u << 28));
 }
 
+// Box (f16, scene-normalised, as the node's) of the union of every node's siblings: the children of its
+// parent other than itself (leaves included, empty slots not). A ray climbing out of a finished subtree
+// that misses its siblings' box has nothing to do at the parent (VR_CLIMB_SKIP).
+__global__ __launch_bounds__(256) void siblings_kernel(const HNode4* __restrict__ nodes, uint32_t n, uint4* __restrict__ sib) {
+    const uint32_t p = blockIdx.x * 256u + threadIdx.x;
+    if (p >= n) return;
+    const HNode4 h = nodes[p];
+    float lo[4][3], hi[4][3];
+    for (int i = 0; i < 4; ++i)
+        for (int k = 0; k < 3; ++k) {
+            lo[i][k] = (float)__builtin_bit_cast(_Float16, h.h[i][k]);
+            hi[i][k] = (float)__builtin_bit_cast(_Float16, h.h[i][3 + k]);
+        }
+    for (int i = 0; i < 4; ++i) {
+        if (h.c[i] <= 0) continue;
+        float ul[3] = {INFINITY, INFINITY, INFINITY}, uh[3] = {-INFINITY, -INFINITY, -INFINITY};
+        for (int j = 0; j < 4; ++j) {
+            if (j == i || h.c[j] == 0) continue;
+            for (int k = 0; k < 3; ++k) {
+                ul[k] = fminf(ul[k], lo[j][k]);
+                uh[k] = fmaxf(uh[k], hi[j][k]);
+            }
+        }
+        uint16_t b[8];
+        for (int k = 0; k < 3; ++k) {  // (f16 values: the conversions are exact; no sibling: an inverted box)
+            b[k] = __builtin_bit_cast(uint16_t, (_Float16)ul[k]);
+            b[3 + k] = __builtin_bit_cast(uint16_t, (_Float16)uh[k]);
+        }
+        b[6] = b[7] = 0;
+        sib[h.c[i]] = make_uint4(b[0] | ((uint32_t)b[1] << 16), b[2] | ((uint32_t)b[3] << 16), b[4] | ((uint32_t)b[5] << 16), 0u);
+    }
+}
+
 // Start subtree of a record's secondary rays: the deepest 4-wide node whose box holds the record position
 // with `margin` (scene-normalised units) to spare, taking at every level the inner child with the most
 // room. The rays walk that subtree first and then climb to its parents (sec_node4v), so every node is
@@ -2289,8 +2352,9 @@ hipError_t gauss_secondary(const RenderArgs& A, hipStream_t stream, bool stats) 
     return stats ? secondary_launch<true, false>(A, stream) : secondary_launch<false, false>(A, stream);
 }
 
-hipError_t gauss_parents(const HNode4* nodes, uint32_t n, int32_t* parent, hipStream_t stream) {
+hipError_t gauss_parents(const HNode4* nodes, uint32_t n, int32_t* parent, uint4* sib, hipStream_t stream) {
     hipLaunchKernelGGL(dev::parents_kernel, dim3((n + 255) / 256), dim3(256), 0, stream, nodes, n, parent);
+    hipLaunchKernelGGL(dev::siblings_kernel, dim3((n + 255) / 256), dim3(256), 0, stream, nodes, n, sib);
     return hipGetLastError();
 }
 

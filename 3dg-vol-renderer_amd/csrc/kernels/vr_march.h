@@ -172,6 +172,46 @@ __device__ __forceinline__ bool intersect_fast(const Quad& q, float& t_enter, fl
     return true;
 }
 
+// Conservative pre-test for the primary march's exact decisions (intersect() + an interval condition):
+// the same crossing in the FMA-contracted / hardware-rcp forms with a margin that bounds the difference
+// to the exact forms many times over (discriminant: 1e-3 of its terms' magnitude, distances: 1 % of the
+// chord + 1e-4 (1 + |t|)). Returns the crossing [t0, t1] of the fast forms and false when the exact test
+// could go either way — grazing rays, a degenerate or non-positive-definite M, NaN — so only Gaussians
+// the exact test would certainly reject are ever skipped: every accepted Gaussian, and every decision,
+// stays the exact test's (bit-identical march).
+__device__ __forceinline__ bool fast_crossing(const GRec& g, const Ray& r, float& t0, float& t1, float& tol) {
+    const Quad f = quad_fast(g, r);
+    if (!(f.A > 0.0f)) return false;
+    const float c4 = 4.0f * f.A * (f.Cq - 9.0f);
+    const float disc = fmaf(f.B, f.B, -c4), scale = fmaf(f.B, f.B, fabsf(c4));
+    if (disc < -1e-3f * scale) {  // certainly no crossing
+        t0 = t1 = INFINITY;
+        tol = 0.0f;
+        return true;
+    }
+    if (!(disc > 1e-3f * scale)) return false;  // grazing (or NaN): the exact test decides
+    const float sd = __builtin_amdgcn_sqrtf(disc), inv = __builtin_amdgcn_rcpf(2.0f * f.A);
+    t0 = (-f.B - sd) * inv;
+    t1 = (-f.B + sd) * inv;
+    tol = 1e-2f * (t1 - t0) + 1e-4f * (1.0f + fabsf(t0) + fabsf(t1));
+    return true;
+}
+// True if the exact test certainly rejects Gaussian g as an entrant of the window (t_lo, t_k]: the exact
+// condition is intersect(q, a, b) && a > t_lo && a <= t_k && b > t_k with a = max(t0, 0), b = t1.
+__device__ __forceinline__ bool fast_reject_window(const GRec& g, const Ray& r, float t_lo, float t_k) {
+    float t0, t1, tol;
+    if (!fast_crossing(g, r, t0, t1, tol)) return false;
+    if (t0 == INFINITY) return true;
+    return (t1 + tol <= t_k) || (fmaxf(t0 - tol, 0.0f) > t_k) || (fmaxf(t0 + tol, 0.0f) <= t_lo);
+}
+// ... as the closest entry after t_lo below `best`: intersect(q, a, b) && a > t_lo && a < best.
+__device__ __forceinline__ bool fast_reject_closest(const GRec& g, const Ray& r, float t_lo, float best) {
+    float t0, t1, tol;
+    if (!fast_crossing(g, r, t0, t1, tol)) return false;
+    if (t0 == INFINITY) return true;
+    return (t1 + tol < 0.0f) || (fmaxf(t0 + tol, 0.0f) <= t_lo) || (fmaxf(t0 - tol, 0.0f) >= best);
+}
+
 __device__ __forceinline__ float optical_depth_fast(const GRec& g, const Quad& q, float t0, float t1) {
     const float twoA = 2.0f * q.A;
     const float r2A = __builtin_amdgcn_rcpf(twoA);

@@ -147,6 +147,7 @@ struct RenderArgs {
     const HNode4* hnodes4;    // 4-wide collapse of the same tree (secondary rays); nullptr with hnodes
     const int32_t* hn4_parent;  // parent of every HNode4 | (its slot + 1) << 28 (root: -1); nullptr: walks start at the root
     uint32_t num_nodes4;        // HNode4 count
+    const uint4* hn4_sib;       // per HNode4: f16 box of the union of its siblings (the climb's skip test)
     float hn_center[3], hn_scale;
     const SphereRecord* spheres;
     int32_t num_prims;
