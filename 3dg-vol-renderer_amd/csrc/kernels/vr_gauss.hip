@@ -374,6 +374,10 @@ __device__ __forceinline__ bool march_step(const RenderArgs& A, const Ray& ray, 
 #define VR_MARCH_UNSORTED 1  // 1: the march's entrant queries walk the 4-wide nodes without sorting (A/B)
 #endif
 constexpr bool kMarchUnsorted = VR_MARCH_UNSORTED;
+#ifndef VR_MARCH_LOCAL
+#define VR_MARCH_LOCAL 1  // 1: the march's queries start in the subtree holding their window and climb (A/B)
+#endif
+constexpr bool kMarchLocal = VR_MARCH_LOCAL;
 #ifndef VR_MARCH_PRETEST
 #define VR_MARCH_PRETEST 1  // 1: the march's BVH queries skip certain misses with the fast forms (fast_reject_*)
 #endif
@@ -400,6 +404,17 @@ __device__ int march(const RenderArgs& A, uint32_t p, int px, int py, int* act_b
             return true;
         }
     };
+    // Queries local to a point of the ray start in the deepest subtree holding it (and the window's other
+    // end) and climb (traverse_wide_climb): a window query of one step then walks a few local nodes and
+    // one sibling-box test per ancestor instead of the descent from the root.
+    auto walk_local = [&](float ta, float tb, auto prune, auto leaf) -> bool {
+        float p[3] = {ray.ox + ta * ray.dx, ray.oy + ta * ray.dy, ray.oz + ta * ray.dz};
+        float q[3] = {ray.ox + tb * ray.dx, ray.oy + tb * ray.dy, ray.oz + tb * ray.dz};
+        node_space<true>(A, p[0], p[1], p[2]);
+        node_space<true>(A, q[0], q[1], q[2]);
+        return traverse_wide_climb<CAP>(A, ray, wide_start_node(A, p, q), stack, stride, prune, leaf, NodeCount<S>{&c});
+    };
+    const bool local = W && kMarchLocal && A.hn4_parent != nullptr && A.hn4_sib != nullptr;
     // the entrants query collects every entry of (t_lo, t_k] whatever the visit order: no sorting network
     auto walk_any = [&](auto prune, auto leaf) -> bool {
         if constexpr (W && kMarchUnsorted) {
@@ -417,21 +432,22 @@ __device__ int march(const RenderArgs& A, uint32_t p, int px, int py, int* act_b
             if (act.n == 0) {  // closest entry strictly after t_lo
                 if constexpr (S) c.v[kCtrPrimQueries]++;
                 float best = INFINITY;
-                const bool ok = walk(
-                    [&](float tmin, float tmax) {
-                        return tmax >= t_lo - kTPad * (1.0f + fabsf(t_lo)) && tmin <= best + kTPad * (1.0f + best);
-                    },
-                    [&](uint32_t first, uint32_t count) {
-                        for (uint32_t j = first; j < first + count; ++j) {
-                            if constexpr (S) c.v[kCtrPrims]++;
-                            GRec g = load_rec(G, j);
-                            if (kMarchPretest && fast_reject_closest(g, ray, t_lo, best)) continue;
-                            Quad q = quad(g, ray);
-                            float a, b;
-                            if (intersect(q, a, b) && a > t_lo && a < best) best = a;
-                        }
-                        return true;
-                    });
+                auto prune_c = [&](float tmin, float tmax) {
+                    return tmax >= t_lo - kTPad * (1.0f + fabsf(t_lo)) && tmin <= best + kTPad * (1.0f + best);
+                };
+                auto leaf_c = [&](uint32_t first, uint32_t count) {
+                    for (uint32_t j = first; j < first + count; ++j) {
+                        if constexpr (S) c.v[kCtrPrims]++;
+                        GRec g = load_rec(G, j);
+                        if (kMarchPretest && fast_reject_closest(g, ray, t_lo, best)) continue;
+                        Quad q = quad(g, ray);
+                        float a, b;
+                        if (intersect(q, a, b) && a > t_lo && a < best) best = a;
+                    }
+                    return true;
+                };
+                // (the closest entry after t_lo: local from the ray's point at t_lo once the march is past 0)
+                const bool ok = (local && t_lo >= 0.0f) ? walk_local(t_lo, t_lo, prune_c, leaf_c) : walk(prune_c, leaf_c);
                 if (!ok) return kOverflow;
                 if (best == INFINITY) break;
                 k = kfirst(ts, nts, step, best);
@@ -443,10 +459,14 @@ __device__ int march(const RenderArgs& A, uint32_t p, int px, int py, int* act_b
             // entrants: t_lo < a <= t_k and still inside at t_k (b > t_k)
             if constexpr (S) c.v[kCtrPrimQueries]++;
             bool ovf = false;
-            const bool ok = walk_any(
-                [&](float tmin, float tmax) {
-                    return tmax >= t_lo - kTPad * (1.0f + fabsf(t_lo)) && tmin <= t_k + kTPad * (1.0f + t_k);
-                },
+            auto prune_w = [&](float tmin, float tmax) {
+                return tmax >= t_lo - kTPad * (1.0f + fabsf(t_lo)) && tmin <= t_k + kTPad * (1.0f + t_k);
+            };
+            auto walk_w = [&](auto prune, auto leaf) -> bool {  // a window of one step: local; from 0: the root
+                return (local && t_lo >= 0.0f) ? walk_local(t_lo, t_k, prune, leaf) : walk_any(prune, leaf);
+            };
+            const bool ok = walk_w(
+                prune_w,
                 [&](uint32_t first, uint32_t count) {
                     for (uint32_t j = first; j < first + count; ++j) {
                         if constexpr (S) c.v[kCtrPrims]++;

@@ -5,7 +5,7 @@ oracle's restatement (oracle/vr_oracle.cpp free_flight_pixel).
 Both sides follow each path (pixel, sample) with the same PCG32 stream, bit-identical camera rays
 and ellipsoid distances, and the same solver; libm (log, erf, acos, sin, cos) differs from the
 device library by a few ulp, so a path whose discrete decision (scatter-or-not in a segment,
-Russian roulette, light choice) lands within an ulp can diverge. Bar: at least 99 % of pixels
+Russian roulette, light choice) lands within an ulp can diverge. Bar: at least 99.9 % of pixels
 within 1e-4 L-inf, mean |diff| < 1e-4, image means within 0.5 % (measured on MI355X: 100 % of
 pixels within 1e-4, mean |diff| ~1e-8).
 """
@@ -31,7 +31,7 @@ def _gpu(scene, W, H, multi, spp, min_bounces=5, cam=None, stats=None):
     return img.pixels.copy()
 
 
-def _check(g, r, frac_min=0.99, mean_max=1e-4):
+def _check(g, r, frac_min=0.999, mean_max=1e-4):
     g = np.asarray(g, np.float64)
     r = np.asarray(r, np.float64)
     assert not np.isnan(g).any()

@@ -8,7 +8,7 @@ rc=$?; tail -4 $O/tests.log; [ $rc -ne 0 ] && exit $rc
 for line in "c2 multiscatter 16" "c3 freeflight 4" "c5 multiscatter 16" "main multiscatter 256" "c4 multiscatter 1"; do
   set -- $line
   for st in 1 0; do
-    timeout -k 10 300 python3 bench.py --config $1 --integrator $2 --spp $3 --steps 5 --warmup 1 --cpu-budget 0 --flops 0 --opt ff_staged=$st > $O/$1_$st.json 2> $O/$1_$st.log || { echo "$1 staged=$st failed"; tail -5 $O/$1_$st.log; exit 1; }
+    timeout -k 10 300 python3 bench.py --config $1 --integrator $2 --spp $3 --steps 3 --warmup 1 --cpu-budget 0 --flops 0 --opt ff_staged=$st > $O/$1_$st.json 2> $O/$1_$st.log || { echo "$1 staged=$st failed"; tail -5 $O/$1_$st.log; exit 1; }
     python3 -c "import json;d=json.load(open('$O/$1_$st.json'));print('$1 staged=$st', round(d['value'],2), d['unit'], round(d['ms_per_step'],2), 'ms')"
   done
 done
