@@ -1335,6 +1335,10 @@ __global__ void __launch_bounds__(kFFBlock) ffs_collect_kernel(RenderArgs A) {
 // (per-lane refill). Outcomes: the segment holding the scatter ({t_prev, t_evt, target left, m | ph <<
 // 16}, to the shading queue), the window's end (the next window's collection, next iteration), no
 // scatter (-1) or a capacity exceeded (-2), both to the shading queue ({ts, -, -, -1}).
+#ifndef VR_FFS_EVENT_BUDGET
+#define VR_FFS_EVENT_BUDGET 0  // active-entry evaluations a lane may spend on events per wave iteration (0: one event)
+#endif
+constexpr int kFFSEventBudget = VR_FFS_EVENT_BUDGET;
 #ifndef VR_FFS_SWEEP_WAVES
 #define VR_FFS_SWEEP_WAVES 6  // waves per SIMD of the sweep kernel (launch bounds)
 #endif
@@ -1404,7 +1408,11 @@ __global__ void __launch_bounds__(kFFBlock, VR_FFS_SWEEP_WAVES) ffs_sweep_kernel
             if (exhausted) break;
             continue;
         }
-        if (live) {  // one event of the window (free_flight_distance's sweep, term for term)
+        // One event per lane (free_flight_distance's sweep, term for term); with an event budget, a lane
+        // whose events are cheap (few active entries) takes several in one wave iteration.
+        int budget = kFFSEventBudget;
+        while (live) {
+            budget -= max(m, 1);
             const float next_entry = i < n ? S.K(i) : INFINITY;
             float t_evt = fminf(next_entry, next_exit);
             const bool window_end = t_cut <= t_evt;
@@ -1474,6 +1482,7 @@ __global__ void __launch_bounds__(kFFBlock, VR_FFS_SWEEP_WAVES) ffs_sweep_kernel
                     exit_pos = npos;
                 }
             }
+            if (budget <= 0) break;
         }
         ffs_push(A, 3, s, to_shade);
         ffs_push(A, nxt, s, to_collect);

@@ -12,3 +12,11 @@ for line in "c2 multiscatter 16" "c3 freeflight 4" "c5 multiscatter 16" "main mu
     python3 -c "import json;d=json.load(open('$O/$1_$st.json'));print('$1 staged=$st', round(d['value'],2), d['unit'], round(d['ms_per_step'],2), 'ms')"
   done
 done
+for v in evb16; do
+  [ -f _ab/$v/libvr_hip.so ] || continue
+  for line in "c2 multiscatter 16" "c5 multiscatter 16"; do
+    set -- $line
+    VR_LIB_PATH=$PWD/_ab/$v/libvr_hip.so timeout -k 10 300 python3 bench.py --config $1 --integrator $2 --spp $3 --steps 3 --warmup 1 --cpu-budget 0 --flops 0 > $O/$1_$v.json 2> $O/$1_$v.log || { echo "$1 $v failed"; tail -5 $O/$1_$v.log; exit 1; }
+    python3 -c "import json;d=json.load(open('$O/$1_$v.json'));print('$1 $v', round(d['value'],2), d['unit'], round(d['ms_per_step'],2), 'ms')"
+  done
+done
