@@ -81,7 +81,10 @@ BVHBuild build_bvh(const std::vector<float>& boxes) {
         work.push_back({0, 1});
     }
     uint32_t* ord = out.order.data();
-    constexpr int kBins = 16;            // SAH bins per axis
+#ifndef VR_BVH_BINS
+#define VR_BVH_BINS 16
+#endif
+    constexpr int kBins = VR_BVH_BINS;   // SAH bins per axis (<= 64)
     constexpr uint32_t leaf_max = kLeafMax;
     // Depth budget: SAH may go kSlack levels deeper than a perfectly balanced tree, but never past
     // kMaxDepth. Shallow trees let the march kernel use a 24-entry LDS stack (more waves per CU);

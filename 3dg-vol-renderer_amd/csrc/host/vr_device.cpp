@@ -28,6 +28,9 @@ hipError_t gauss_record_cut(const RenderArgs& A, float budget, hipStream_t strea
 hipError_t gauss_whiten(const GaussianRecord* rec, WRecord* out, uint32_t n, uint32_t* bad, hipStream_t stream);
 hipError_t gauss_bin(const RenderArgs& A, bool emit, hipStream_t stream);
 hipError_t gauss_parents(const HNode4* nodes, uint32_t n, int32_t* parent, uint4* sib, hipStream_t stream);
+hipError_t gauss_refit_secondary(const HNode4* src, HNode4* dst, uint32_t n, const GaussianRecord* rec, const int32_t* parent,
+                                 uint8_t* depth, float* nbox, uint32_t* maxd, const float hc[3], float hs, float diag,
+                                 hipStream_t stream);
 hipError_t gauss_bin_scan(const uint32_t* cnt, uint32_t* off, uint32_t n, void* tmp, size_t& tmp_bytes, hipStream_t stream);
 hipError_t launch_pixel_losses(const float* img, const float* ref, uint32_t npix, float* out, hipStream_t stream);
 
@@ -52,6 +55,7 @@ struct vr_ctx {
     BVHNode* d_nodes = nullptr;
     HNode* d_hnodes = nullptr;
     HNode4* d_hnodes4 = nullptr;
+    HNode4* d_hnodes4s = nullptr;  // the secondary rays' copy with tight boxes (VR_OPT_SEC_TIGHT)
     int32_t* d_parent4 = nullptr;  // parent of every HNode4 (the secondary rays' climb out of their start subtree)
     uint4* d_sib4 = nullptr;       // union box of every HNode4's siblings (the climb's skip test)
     size_t num_nodes4 = 0;
@@ -131,7 +135,8 @@ struct vr_ctx {
     int64_t opt_march_binned = 0;      // VR_OPT_MARCH_BINNED
     int64_t opt_ff_solver = 0;         // VR_OPT_FF_SOLVER
     int64_t opt_start_subtree = 1;     // VR_OPT_START_SUBTREE
-    int64_t opt_ff_staged = 1;         // VR_OPT_FF_STAGED
+    int64_t opt_ff_staged = 0;         // VR_OPT_FF_STAGED
+    int64_t opt_sec_tight = 1;         // VR_OPT_SEC_TIGHT (next upload)
     bool last_upload_device_bvh = false;  // the current scene's tree came from the device builder
     vr_group* group = nullptr;         // vr_init_multi: the devices this context drives (host/vr_multi.cpp)
 };
@@ -165,6 +170,8 @@ void free_scene(vr_ctx* c) {
     c->d_hnodes = nullptr;
     if (c->d_hnodes4) (void)hipFree(c->d_hnodes4);
     c->d_hnodes4 = nullptr;
+    if (c->d_hnodes4s) (void)hipFree(c->d_hnodes4s);
+    c->d_hnodes4s = nullptr;
     if (c->d_parent4) (void)hipFree(c->d_parent4);
     c->d_parent4 = nullptr;
     if (c->d_sib4) (void)hipFree(c->d_sib4);
@@ -212,6 +219,8 @@ vr_status upload_half_nodes(vr_ctx* c, const std::vector<BVHNode>& nodes) {
     c->d_hnodes = nullptr;
     if (c->d_hnodes4) (void)hipFree(c->d_hnodes4);
     c->d_hnodes4 = nullptr;
+    if (c->d_hnodes4s) (void)hipFree(c->d_hnodes4s);
+    c->d_hnodes4s = nullptr;
     if (!c->opt_half_nodes) return VR_OK;
     double half = 0.0;
     for (int k = 0; k < 3; ++k) {
@@ -395,6 +404,38 @@ vr_status upload_device_bvh(vr_ctx* c, const HostScene& s, const std::vector<flo
     return upload_whitened(c, N);
 }
 
+// The secondary rays' 4-wide tree: the shared tree's nodes refit with the records' tight boxes on the
+// device (vr_gauss.hip, refit_kernel; whitened scenes only: the M forms keep the padded boxes).
+vr_status upload_secondary_tree(vr_ctx* c) {
+    if (c->d_hnodes4s) (void)hipFree(c->d_hnodes4s);
+    c->d_hnodes4s = nullptr;
+    if (!c->opt_sec_tight || !c->wrec_pd || !c->d_wrec || !c->d_hnodes4 || !c->d_parent4 || !c->d_gauss || c->num_nodes4 == 0)
+        return VR_OK;
+    const size_t n = c->num_nodes4;
+    double d2 = 0.0;  // the scene box's diagonal: no ray origin is farther than that from a record
+    for (int k = 0; k < 3; ++k) d2 += ((double)c->bmax[k] - c->bmin[k]) * ((double)c->bmax[k] - c->bmin[k]);
+    uint8_t* depth = nullptr;
+    float* nbox = nullptr;
+    uint32_t* maxd = nullptr;
+    hipError_t e = hipMalloc(&c->d_hnodes4s, n * sizeof(HNode4));
+    if (e == hipSuccess) e = hipMalloc(&depth, n);
+    if (e == hipSuccess) e = hipMalloc(&nbox, n * 6 * sizeof(float));
+    if (e == hipSuccess) e = hipMalloc(&maxd, sizeof(uint32_t));
+    if (e == hipSuccess)
+        e = gauss_refit_secondary(c->d_hnodes4, c->d_hnodes4s, (uint32_t)n, c->d_gauss, c->d_parent4, depth, nbox, maxd,
+                                  c->hn_center, c->hn_scale, (float)std::sqrt(d2), c->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+    for (void* p : {(void*)depth, (void*)nbox, (void*)maxd})
+        if (p) (void)hipFree(p);
+    if (e == hipErrorNotSupported) {  // a tree deeper than 255 levels: the shared boxes
+        (void)hipFree(c->d_hnodes4s);
+        c->d_hnodes4s = nullptr;
+        return VR_OK;
+    }
+    if (e != hipSuccess) return hip_fail(e, "secondary-ray tree");
+    return VR_OK;
+}
+
 // Parent of every 4-wide node (built on the device from the children refs): a secondary ray starts its
 // tree walk in the subtree holding its origin and climbs to the parents once that subtree is done
 // (vr_gauss.hip, record_start_kernel / sec_node4v).
@@ -408,7 +449,7 @@ vr_status upload_parents(vr_ctx* c) {
     HIP_TRY(hipMalloc(&c->d_sib4, c->num_nodes4 * sizeof(uint4)), "hipMalloc(wide-node siblings)");
     HIP_TRY(gauss_parents(c->d_hnodes4, (uint32_t)c->num_nodes4, c->d_parent4, c->d_sib4, c->stream), "wide-node parents");
     HIP_TRY(hipStreamSynchronize(c->stream), "wide-node parents");
-    return VR_OK;
+    return upload_secondary_tree(c);
 }
 
 // Farthest distance any ray can travel before leaving the scene box: the rays of both camera
@@ -508,6 +549,7 @@ vr_status fill_args(vr_ctx* c, const vr_camera* cam, const vr_render_params* p, 
     A.nodes = c->d_nodes;
     A.hnodes = c->d_hnodes;
     A.hnodes4 = c->d_hnodes4;
+    A.hnodes4s = c->d_hnodes4s ? c->d_hnodes4s : c->d_hnodes4;
     A.hn4_parent = c->d_parent4;
     A.num_nodes4 = (uint32_t)c->num_nodes4;
     A.hn4_sib = c->d_sib4;
@@ -1495,6 +1537,10 @@ vr_status vr_set_option(vr_ctx* c, int32_t option, int64_t value) {
             if (value != 0 && value != 1) return fail(VR_ERR_INVALID, "VR_OPT_FF_STAGED must be 0 or 1");
             c->opt_ff_staged = value;
             return VR_OK;
+        case VR_OPT_SEC_TIGHT:
+            if (value != 0 && value != 1) return fail(VR_ERR_INVALID, "VR_OPT_SEC_TIGHT must be 0 or 1");
+            c->opt_sec_tight = value;
+            return VR_OK;
         case VR_OPT_RECORD_CAPACITY:
             if ((value != 0 && value < 4096) || value > 0x3fffffff)
                 return fail(VR_ERR_INVALID, "VR_OPT_RECORD_CAPACITY must be 0 or in [4096, 2^30)");
@@ -1519,6 +1565,7 @@ vr_status vr_get_option(vr_ctx* c, int32_t option, int64_t* value) {
         case VR_OPT_FF_SOLVER: *value = c->opt_ff_solver; return VR_OK;
         case VR_OPT_START_SUBTREE: *value = c->opt_start_subtree; return VR_OK;
         case VR_OPT_FF_STAGED: *value = c->opt_ff_staged; return VR_OK;
+        case VR_OPT_SEC_TIGHT: *value = c->opt_sec_tight; return VR_OK;
         default: return fail(VR_ERR_INVALID, "vr_get_option: unknown option " + std::to_string(option));
     }
 }

@@ -375,11 +375,11 @@ __device__ __forceinline__ bool march_step(const RenderArgs& A, const Ray& ray, 
 #endif
 constexpr bool kMarchUnsorted = VR_MARCH_UNSORTED;
 #ifndef VR_MARCH_LOCAL
-#define VR_MARCH_LOCAL 1  // 1: the march's queries start in the subtree holding their window and climb (A/B)
+#define VR_MARCH_LOCAL 0  // 1: the march's queries start in the subtree holding their window and climb (A/B: C4 march 14.0 -> 14.9 ms)
 #endif
 constexpr bool kMarchLocal = VR_MARCH_LOCAL;
 #ifndef VR_MARCH_PRETEST
-#define VR_MARCH_PRETEST 1  // 1: the march's BVH queries skip certain misses with the fast forms (fast_reject_*)
+#define VR_MARCH_PRETEST 0  // 1: the march's BVH queries skip certain misses with the fast forms (fast_reject_*; A/B: C4 14.0 -> 16.4 ms)
 #endif
 constexpr bool kMarchPretest = VR_MARCH_PRETEST;
 
@@ -1424,7 +1424,7 @@ __device__ __forceinline__ void sec_node4(const RenderArgs& A, SecRay& R, LdsInt
         c.v[kCtrNodes]++;
         ++R.nsteps;
     }
-    const uint4* np = reinterpret_cast<const uint4*>(A.hnodes4 + node);
+    const uint4* np = reinterpret_cast<const uint4*>(A.hnodes4s + node);
     const uint4 q0 = np[0], q1 = np[1], q2 = np[2], rf = np[3];
     const uint32_t w[12] = {q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, q1.z, q1.w, q2.x, q2.y, q2.z, q2.w};
     const int32_t ref[4] = {(int32_t)rf.x, (int32_t)rf.y, (int32_t)rf.z, (int32_t)rf.w};
@@ -1574,7 +1574,7 @@ __device__ __forceinline__ void sec_node4v(const RenderArgs& A, SecRay& R, LdsIn
 #ifdef VR_DIAG_LEVELS
     R.lv[min((int)g_diag_depth[node & kNodeIndexMask] >> 1, 7)]++;
 #endif
-    const uint4* np = reinterpret_cast<const uint4*>(A.hnodes4 + (node & kNodeIndexMask));
+    const uint4* np = reinterpret_cast<const uint4*>(A.hnodes4s + (node & kNodeIndexMask));
     const uint4 q0 = np[0], q1 = np[1], q2 = np[2], rf = np[3];
     const uint32_t w[12] = {q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, q1.z, q1.w, q2.x, q2.y, q2.z, q2.w};
     const int32_t ref[4] = {(int32_t)rf.x, (int32_t)rf.y, (int32_t)rf.z, (int32_t)rf.w};
@@ -2057,6 +2057,106 @@ __global__ __launch_bounds__(256) void siblings_kernel(const HNode4* __restrict_
     }
 }
 
+// ---- the secondary rays' own 4-wide tree: the same nodes with tight boxes (round 4) -------------------
+// The shared tree's boxes are the primitives' 3-sigma boxes padded by 5 % (gaussian_bounds): the exact
+// M-form quadratic of the primary and free-flight rays, evaluated from a camera several units away,
+// accepts points a few percent outside the ellipsoid, and their boxes must hold those. The secondary
+// rays' whitened test takes the distance from the chord to the centre directly (wquad: |Lp - (h/a) Ld|^2,
+// error linear in the origin's whitened distance instead of quadratic), so what it accepts lies within
+// ~1e-5 of the ellipsoid, and their tree gets the exact box of {x : x^T M x <= 9}: half extent
+// 3 sqrt((M^-1)_kk) from the record's M in double, outward rounding, and a relative pad of
+// 2e-4 + 3.2e-7 rw, rw = diag sqrt(trace M) >= the whitened distance of any origin in the scene box
+// (diagonal diag): the chord distance's f32 error is ~1.4e-6 rw in e2, i.e. ~8e-8 rw of the radius, so
+// the pad keeps a factor >= 4 at any scene scale (C4: 2e-4 .. 6e-4). C4: 9.5 % fewer node steps and 19 %
+// fewer primitive tests.
+__device__ __forceinline__ uint16_t f16_out(double v, bool up) {  // smallest half >= v (up) / largest <= v
+    uint16_t h = __builtin_bit_cast(uint16_t, (_Float16)(float)v);
+    for (int it = 0; it < 4; ++it) {
+        const double hv = (double)__builtin_bit_cast(_Float16, h);
+        if (up ? hv >= v : hv <= v) break;
+        const bool neg = (h & 0x8000u) != 0;
+        if ((h & 0x7fffu) == 0) h = up ? 0x0001u : 0x8001u;
+        else h = (uint16_t)((neg != up) ? h + 1 : h - 1);
+    }
+    return h;
+}
+// Tight box of record j (f32, rounded outward); a record whose M is not positive definite keeps an
+// infinite box (the secondary kernel then runs the M forms on the shared tree anyway).
+__device__ __forceinline__ void tight_box(const GaussianRecord& g, float diag, float lo[3], float hi[3]) {
+    const double m0 = g.m00, m1 = g.m01, m2 = g.m02, m3 = g.m11, m4 = g.m12, m5 = g.m22;
+    const double c00 = m3 * m5 - m4 * m4, c11 = m0 * m5 - m2 * m2, c22 = m0 * m3 - m1 * m1;
+    const double c01 = m2 * m4 - m1 * m5, c02 = m1 * m4 - m2 * m3;
+    const double det = m0 * c00 + m1 * c01 + m2 * c02;
+    const double s[3] = {c00 / det, c11 / det, c22 / det};
+    const double mean[3] = {g.mx, g.my, g.mz};
+    const bool pd = m0 > 0.0 && c22 > 0.0 && det > 0.0 && s[0] > 0.0 && s[1] > 0.0 && s[2] > 0.0;
+    const double pad = 1.0 + 2e-4 + 3.2e-7 * (double)diag * sqrt(m0 + m3 + m5);
+    for (int k = 0; k < 3; ++k) {
+        const double h = pd ? 3.0 * sqrt(s[k]) * pad + 1e-6 : INFINITY;
+        lo[k] = __double2float_rd(mean[k] - h);
+        hi[k] = __double2float_ru(mean[k] + h);
+    }
+}
+// Depth of every 4-wide node (from the parents) and the deepest.
+__global__ __launch_bounds__(256) void node_depth_kernel(const int32_t* __restrict__ parent, uint32_t n, uint8_t* __restrict__ depth,
+                                                         uint32_t* __restrict__ maxd) {
+    const uint32_t i = blockIdx.x * 256u + threadIdx.x;
+    if (i >= n) return;
+    uint32_t d = 0;
+    for (int32_t x = (int32_t)i; x > 0 && d < 255u; x = parent[x] & kNodeIndexMask) ++d;
+    depth[i] = (uint8_t)d;
+    atomicMax(maxd, d);
+}
+// One level of the refit, deepest first: every node at `level` gets its children's tight boxes (a leaf:
+// the union of its records' boxes; an inner child: the union its own refit left in nbox) as outward
+// rounded f16 in the shared tree's normalisation, and leaves the union of them in nbox for its parent.
+__global__ __launch_bounds__(256) void refit_kernel(const HNode4* __restrict__ src, HNode4* __restrict__ dst,
+                                                    const GaussianRecord* __restrict__ rec, const uint8_t* __restrict__ depth,
+                                                    uint32_t level, uint32_t n, float* __restrict__ nbox, float3 hc, float hs,
+                                                    float diag) {
+    const uint32_t i = blockIdx.x * 256u + threadIdx.x;
+    if (i >= n || depth[i] != level) return;
+    HNode4 h = src[i];
+    float ul[3] = {INFINITY, INFINITY, INFINITY}, uh[3] = {-INFINITY, -INFINITY, -INFINITY};
+    const double c[3] = {hc.x, hc.y, hc.z};
+    for (int s = 0; s < 4; ++s) {
+        const int32_t r = h.c[s];
+        if (r == 0) continue;  // empty slot: its NaN box stays
+        float lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
+        if (r < 0) {
+            const uint32_t first = leaf_first(r), cnt = leaf_count(r);
+            for (uint32_t j = first; j < first + cnt; ++j) {
+                float a[3], b[3];
+                tight_box(rec[j], diag, a, b);
+                for (int k = 0; k < 3; ++k) {
+                    lo[k] = fminf(lo[k], a[k]);
+                    hi[k] = fmaxf(hi[k], b[k]);
+                }
+            }
+        } else {
+            for (int k = 0; k < 3; ++k) {
+                lo[k] = nbox[6 * (size_t)r + k];
+                hi[k] = nbox[6 * (size_t)r + 3 + k];
+            }
+        }
+        for (int k = 0; k < 3; ++k) {
+            ul[k] = fminf(ul[k], lo[k]);
+            uh[k] = fmaxf(uh[k], hi[k]);
+            // never wider than the shared tree's box (both hold the child; the tighter one is kept)
+            const uint16_t a = f16_out(((double)lo[k] - c[k]) * (double)hs, false);
+            const uint16_t b = f16_out(((double)hi[k] - c[k]) * (double)hs, true);
+            const float sa = (float)__builtin_bit_cast(_Float16, h.h[s][k]), sb = (float)__builtin_bit_cast(_Float16, h.h[s][3 + k]);
+            if ((float)__builtin_bit_cast(_Float16, a) > sa) h.h[s][k] = a;
+            if ((float)__builtin_bit_cast(_Float16, b) < sb) h.h[s][3 + k] = b;
+        }
+    }
+    dst[i] = h;
+    for (int k = 0; k < 3; ++k) {
+        nbox[6 * (size_t)i + k] = ul[k];
+        nbox[6 * (size_t)i + 3 + k] = uh[k];
+    }
+}
+
 // Start subtree of a record's secondary rays: the deepest 4-wide node whose box holds the record position
 // with `margin` (scene-normalised units) to spare, taking at every level the inner child with the most
 // room. The rays walk that subtree first and then climb to its parents (sec_node4v), so every node is
@@ -2074,7 +2174,7 @@ __global__ __launch_bounds__(256) void record_start_kernel(RenderArgs A) {
         node_space<true>(A, p[0], p[1], p[2]);
         int32_t node = 0;
         for (int depth = 0; depth < kWideStackMax; ++depth) {
-            const uint4* np = reinterpret_cast<const uint4*>(A.hnodes4 + node);
+            const uint4* np = reinterpret_cast<const uint4*>(A.hnodes4s + node);
             const uint4 q0 = np[0], q1 = np[1], q2 = np[2], rf = np[3];
             const uint32_t w[12] = {q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, q1.z, q1.w, q2.x, q2.y, q2.z, q2.w};
             const int32_t ref[4] = {(int32_t)rf.x, (int32_t)rf.y, (int32_t)rf.z, (int32_t)rf.w};
@@ -2318,8 +2418,10 @@ static hipError_t ww_launch(const RenderArgs& A, hipStream_t stream) {
     if (grid == 0) return hipErrorInvalidValue;
     hipError_t e = hipMemsetAsync(A.ray_next, 0, sizeof(unsigned long long), stream);
     if (e != hipSuccess) return e;
+    RenderArgs B = A;  // the tight tree only under the whitened test (the M forms: the shared tree's padded boxes)
+    if (PURE || !WH) B.hnodes4s = A.hnodes4;
     hipLaunchKernelGGL((dev::secondary_ww_kernel<kBlockSecondary, kStack, S, PURE, kWaves, kQueue, H, W, WH>), dim3((unsigned)grid),
-                       dim3(kBlockSecondary), 0, stream, A);
+                       dim3(kBlockSecondary), 0, stream, B);
     return hipGetLastError();
 }
 
@@ -2376,6 +2478,29 @@ hipError_t gauss_parents(const HNode4* nodes, uint32_t n, int32_t* parent, uint4
     hipLaunchKernelGGL(dev::parents_kernel, dim3((n + 255) / 256), dim3(256), 0, stream, nodes, n, parent);
     hipLaunchKernelGGL(dev::siblings_kernel, dim3((n + 255) / 256), dim3(256), 0, stream, nodes, n, sib);
     return hipGetLastError();
+}
+
+// The secondary rays' tree (refit_kernel): nodes 0..n-1 of `src` with tight boxes into `dst`. Scratch:
+// depth (n B), nbox (24 n B), maxd (one word, device) and host_maxd (pinned or pageable host word).
+hipError_t gauss_refit_secondary(const HNode4* src, HNode4* dst, uint32_t n, const GaussianRecord* rec, const int32_t* parent,
+                                 uint8_t* depth, float* nbox, uint32_t* maxd, const float hc[3], float hs, float diag,
+                                 hipStream_t stream) {
+    if (n == 0) return hipSuccess;
+    hipError_t e = hipMemsetAsync(maxd, 0, sizeof(uint32_t), stream);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(dev::node_depth_kernel, dim3((n + 255) / 256), dim3(256), 0, stream, parent, n, depth, maxd);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    uint32_t md = 0;
+    if ((e = hipMemcpyAsync(&md, maxd, sizeof(uint32_t), hipMemcpyDeviceToHost, stream)) != hipSuccess) return e;
+    if ((e = hipStreamSynchronize(stream)) != hipSuccess) return e;
+    if (md >= 255u) return hipErrorNotSupported;
+    const float3 c = make_float3(hc[0], hc[1], hc[2]);
+    for (int level = (int)md; level >= 0; --level) {
+        hipLaunchKernelGGL(dev::refit_kernel, dim3((n + 255) / 256), dim3(256), 0, stream, src, dst, rec, depth, (uint32_t)level, n,
+                           nbox, c, hs, diag);
+        if ((e = hipGetLastError()) != hipSuccess) return e;
+    }
+    return hipSuccess;
 }
 
 hipError_t gauss_whiten(const GaussianRecord* rec, WRecord* out, uint32_t n, uint32_t* bad, hipStream_t stream) {

@@ -262,8 +262,8 @@ __device__ __forceinline__ float optical_depth_chord(const GRec& g, const Quad& 
 // ---- whitened secondary-ray forms (WRecord) ---------------------------------------------------
 // In the coordinates u = L (x - mean) (M = L^T L) a Gaussian's 3-sigma ellipsoid is the sphere |u| = 3
 // and a ray o + t d is u = Lp + t Ld. With a = |Ld|^2, h = Lp.Ld, c = |Lp|^2, r = a^-1/2, hr = h r:
-//   intersect_direct (gaussian.h:126-164): D = hr^2 - (c - 9) >= 0, t = r (-hr -+ sqrt(D))
-//   optical_depth (gaussian.h:208-231): dn r exp((hr^2 - c) / 2) (erf(x1) - erf(x0)),
+//   intersect_direct (gaussian.h:126-164): D = hr^2 - (c - 9) = 9 - e2 >= 0, t = r (-hr -+ sqrt(D))
+//   optical_depth (gaussian.h:208-231): dn r exp((hr^2 - c) / 2) (erf(x1) - erf(x0)) = dn r exp(-e2 / 2) (..),
 //     x(t) = (hr + t / r) / sqrt(2); at the exit t1, x1 = sqrt(D / 2); at the entry t0, x0 = -x1
 // (the same quantities as quad_fast / intersect_fast / optical_depth_fast in about half the VALU
 // operations and three transcendentals — rsq, sqrt, exp — instead of six).
@@ -281,6 +281,8 @@ struct WQuad {
     float r;   // |Ld|^-1
     float hr;  // Lp.Ld / |Ld|
     float sa;  // |Ld|
+    float e2;  // |Lp - (h / a) Ld|^2: the chord's squared distance from the centre (c - hr^2, without the
+               // cancellation: its error grows with the origin's whitened distance, not with its square)
 };
 __device__ __forceinline__ WQuad wquad(const WRec& g, const Ray& ray) {
     const float px = ray.ox - g.mx, py = ray.oy - g.my, pz = ray.oz - g.mz;
@@ -294,12 +296,15 @@ __device__ __forceinline__ WQuad wquad(const WRec& g, const Ray& ray) {
     q.r = __builtin_amdgcn_rsqf(a);
     q.hr = h * q.r;
     q.sa = a * q.r;
+    const float k = -q.hr * q.r;  // -h / a
+    const float e0 = fmaf(k, d0, p0), e1 = fmaf(k, d1, p1), e2 = fmaf(k, d2, p2);
+    q.e2 = fmaf(e0, e0, fmaf(e1, e1, e2 * e2));
     return q;
 }
 // Entry / exit of the 3-sigma sphere (t0 <= t1, not clamped); s = sqrt(D). False: no crossing, or it
 // lies behind the origin (t1 < 0), as intersect_fast.
 __device__ __forceinline__ bool wintersect(const WQuad& q, float& t0, float& t1, float& s) {
-    const float D = fmaf(q.hr, q.hr, 9.0f - q.c);
+    const float D = 9.0f - q.e2;
     if (!(D >= 0.0f)) return false;  // (NaN: a degenerate covariance never intersects)
     s = __builtin_amdgcn_sqrtf(D);
     t1 = q.r * (s - q.hr);
@@ -311,14 +316,14 @@ __device__ __forceinline__ bool wintersect(const WQuad& q, float& t0, float& t1,
 __device__ __forceinline__ float wod_chord(const WRec& g, const WQuad& q, float u0, float u1) {
     constexpr float kRs2 = 0.70710678118654752f;
     const float F1 = erf_chord(u1 * kRs2), F0 = erf_chord(u0 * kRs2);
-    const float e = __expf(0.5f * fmaf(q.hr, q.hr, -q.c));
+    const float e = __expf(-0.5f * q.e2);
     return (g.dn * q.r) * e * fmaxf(F1 - F0, 0.0f);  // (f32 noise can invert a tiny interval)
 }
 // Optical depth over [t0, t1] anywhere on the ray (device erff: arguments past the chord).
 __device__ __forceinline__ float wod_range(const WRec& g, const WQuad& q, float t0, float t1) {
     constexpr float kRs2 = 0.70710678118654752f;
     const float F1 = erff(fmaf(q.sa, t1, q.hr) * kRs2), F0 = erff(fmaf(q.sa, t0, q.hr) * kRs2);
-    const float e = __expf(0.5f * fmaf(q.hr, q.hr, -q.c));
+    const float e = __expf(-0.5f * q.e2);
     return (g.dn * q.r) * e * (F1 - F0);
 }
 

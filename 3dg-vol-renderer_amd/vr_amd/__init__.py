@@ -386,13 +386,14 @@ class Device:
                "ff_window0": L.VR_OPT_FF_WINDOW0, "record_capacity": L.VR_OPT_RECORD_CAPACITY,
                "device_bvh": L.VR_OPT_DEVICE_BVH, "ff_nee_queue": L.VR_OPT_FF_NEE_QUEUE,
                "march_binned": L.VR_OPT_MARCH_BINNED, "ff_solver": L.VR_OPT_FF_SOLVER,
-               "start_subtree": L.VR_OPT_START_SUBTREE, "ff_staged": L.VR_OPT_FF_STAGED}
+               "start_subtree": L.VR_OPT_START_SUBTREE, "ff_staged": L.VR_OPT_FF_STAGED,
+               "sec_tight": L.VR_OPT_SEC_TIGHT}
 
     def set_option(self, name, value):
         """vr_set_option (include/vr_hip.h): explicit per-context tuning (half_nodes applies at the
         next upload, so the scene is re-uploaded)."""
         check(lib().vr_set_option(self._h, self.OPTIONS[name], int(value)))
-        if name in ("half_nodes", "device_bvh"):
+        if name in ("half_nodes", "device_bvh", "sec_tight"):
             self._scene_key = None
 
     def get_option(self, name):

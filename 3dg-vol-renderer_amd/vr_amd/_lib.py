@@ -25,6 +25,7 @@ VR_OPT_MARCH_BINNED = 7
 VR_OPT_FF_SOLVER = 8
 VR_OPT_START_SUBTREE = 9
 VR_OPT_FF_STAGED = 10
+VR_OPT_SEC_TIGHT = 11
 
 f3 = ctypes.c_float * 3
 

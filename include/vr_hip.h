@@ -375,10 +375,16 @@ typedef enum vr_option {
                                     climbs to the root (no descent from the root for rays cut near their origin);
                                     0: every walk starts at the root. Same Gaussians, same decisions; only the
                                     order of the optical-depth sum differs (float association). */
-    VR_OPT_FF_STAGED = 10        /* free-flight integrators: 1 (default): the staged pipeline (a pool of path slots
-                                    stepping through hit-collection, event-sweep and shading kernels, queued
-                                    between them, each with per-lane refill); 0: the persistent path kernel
-                                    (a whole bounce per lane and wave iteration). Frames are identical. */
+    VR_OPT_FF_STAGED = 10,       /* free-flight integrators: 0 (default): the persistent path kernel (a whole
+                                    bounce per lane and wave iteration); 1: the staged pipeline (a pool of path
+                                    slots stepping through hit-collection, event-sweep and shading kernels,
+                                    queued between them, each with per-lane refill; slower).
+                                    Frames are identical. */
+    VR_OPT_SEC_TIGHT = 11        /* RayMarchingGaussians secondary rays, applied at the next upload: 1 (default):
+                                    their own copy of the 4-wide tree with the exact boxes of the ellipsoids the
+                                    whitened test accepts (the shared tree's boxes are padded by 5 % for the
+                                    camera rays' M-form test); 0: the shared tree. Same Gaussians, same
+                                    decisions; only the order of the optical-depth sum differs. */
 } vr_option;
 vr_status vr_set_option(vr_ctx* ctx, int32_t option, int64_t value);
 vr_status vr_get_option(vr_ctx* ctx, int32_t option, int64_t* value);

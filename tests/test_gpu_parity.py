@@ -560,6 +560,35 @@ def test_device_bvh_full_size_c4(device_options):
     assert float(np.max(np.abs(out[0][0].astype(np.float64) - out[1][0]))) < 2e-6
 
 
+@pytest.mark.timeout(600)
+def test_secondary_tight_tree_same_frame_fewer_steps(device_options):
+    """The secondary rays' own 4-wide tree (VR_OPT_SEC_TIGHT, tight boxes of the ellipsoids the whitened
+    test accepts) finds the same Gaussians as the shared tree with its 5 %-padded boxes: same scatter
+    records, frames within float association (2e-6, as the host / device trees), on the host- and the
+    device-built tree, with fewer node steps and primitive tests."""
+    scene, _ = _synthetic_scene(100_000)
+    cam = vr.Pinhole_Camera(CAM_POS, main_view_dir(), FOV)
+    dev = vr.Device.get(0)
+    W = 1024
+    for bvh in (0, 1):
+        device_options("device_bvh", bvh)
+        out = {}
+        for tight in (0, 1):
+            device_options("sec_tight", tight)
+            dev.upload(scene, force=True)
+            img = vr.Image(W, W)
+            integ = vr.RayMarchingGaussians(cam, t_eps=1e-6)
+            integ.render(scene, img)
+            work = dev.count_work(cam, integ.params, W, W)["secondary"]
+            out[tight] = (img.pixels.copy(), integ.last_stats, work)
+            print(f"device_bvh={bvh} sec_tight={tight}: node steps {work['node_tests']}, "
+                  f"primitive tests {work['gaussian_tests']}, frame {integ.last_stats['kernel_ms']:.2f} ms")
+        assert out[0][1]["scatter_records"] == out[1][1]["scatter_records"]
+        assert float(np.max(np.abs(out[0][0].astype(np.float64) - out[1][0]))) < 2e-6
+        assert out[1][2]["node_tests"] < out[0][2]["node_tests"]
+        assert out[1][2]["gaussian_tests"] < out[0][2]["gaussian_tests"]
+
+
 def test_non_positive_definite_record_uses_the_m_forms(tmp_path):
     """A nearly singular covariance whose f32 inverse (the reference's M, gaussian.h:53) is not positive
     definite has no Cholesky factor, so it has no whitened record: the upload detects it and the scene's

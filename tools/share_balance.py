@@ -2,9 +2,10 @@
 """Predicts the tile-split scaling on one GPU: renders each of the R interleaved
 rank shares of a frame (tiles r, r+R, r+2R, ...) on its own and times it with the library's HIP
 events (vr_get_stats kernel_ms). Predicted speed-up at R GPUs = full-frame time / slowest share
-and, with the gather modelled, full-frame time / (slowest share + gather + root unshuffle): every
-rank's slab (its tiles x 256 px x 12 B) reaches the root over its own xGMI link at --xgmi-gbs GB/s
-(the links run in parallel), then the root's unshuffle reads and writes the frame at --hbm-gbs.
+and, with the gather modelled, full-frame time / (slowest share + gather + root unshuffle): the root
+renders its own tiles straight into the frame; every other rank's slab (its tiles x 256 px x 12 B)
+reaches the root over its own xGMI link at --xgmi-gbs GB/s (the links run in parallel), then the root's
+unshuffle reads and writes the other ranks' (R - 1) / R of the frame at --hbm-gbs.
 Prints one JSON object.
 
     python tools/share_balance.py [--config c4|bias20k] [--ranks 2,4,8]
@@ -68,7 +69,7 @@ def main():
         t = [share(r, R, len(range(r, nt, R))) for r in range(R)]
         slab = len(range(0, nt, R)) * 256 * 12  # bytes of the largest share's slab
         gather_ms = slab / (a.xgmi_gbs * 1e9) * 1e3
-        unshuffle_ms = 2.0 * nt * 256 * 12 / (a.hbm_gbs * 1e9) * 1e3
+        unshuffle_ms = 2.0 * (nt - len(range(0, nt, R))) * 256 * 12 / (a.hbm_gbs * 1e9) * 1e3
         with_gather = max(t) + gather_ms + unshuffle_ms
         res["ranks"][R] = {"share_ms": t, "max_ms": max(t), "sum_ms": sum(t),
                            "stage_ms_of_slowest": stages[(int(np.argmax(t)), R)],
