@@ -52,7 +52,7 @@ CAM_VIEW = np.array([0.0, 0.0, -1.0], np.float32)
 FOV = np.float32(0.25 * np.pi)
 HBM_PEAK_GBPS = 8000.0   # MI355X_MICROARCH.md: 8.0 TB/s spec
 FP32_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md: FP32 vector peak
-PMC_SUMMARY = "r03_c4_pmc_summary.json"  # rocprofv3 --pmc passes of this command (profiles/)
+PMC_SUMMARY = "r04_c4_pmc_summary.json"  # rocprofv3 --pmc passes of this command (profiles/)
 
 # Flops per executed operation of the secondary stage (an FMA counts 2, min / max / compare 1, and
 # sqrt / rcp / div / exp / erf 4, the quarter-rate transcendental model of SURVEY §8(d)):
