@@ -84,7 +84,7 @@ def secondary_flops(sec):
 # a ray-Gaussian quadratic + intersect 72, an erf evaluation of the event sweep / cached entry factors /
 # distance solver 12 (fma 2 + div 4 + erf 4 + sub/mul 2), a shadow-ray optical depth 98.
 FF_FLOP_WEIGHTS = {"node4": 105, "node2": 44, "prim": 72, "erf": 12, "od": 98}
-FF_PMC_SUMMARY = "r03_ff_{cfg}_pmc_summary.json"  # rocprofv3 --pmc passes of the free-flight lines (profiles/)
+FF_PMC_SUMMARY = "r04_ff_{cfg}_pmc_summary.json"  # rocprofv3 --pmc passes of the free-flight lines (profiles/)
 
 
 def ff_roofline(work, stage_ms, cfg):
