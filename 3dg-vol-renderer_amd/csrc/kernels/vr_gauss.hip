@@ -1779,6 +1779,7 @@ __global__ __launch_bounds__(BLOCK, WAVES) void secondary_ww_kernel(RenderArgs A
     // wave-uniform: the record chunk being handed out and its rays [pool, pool_end) not yet handed out
     uint32_t chunk = 0, pool = 0, pool_end = 0;
     bool counter_done = false;  // wave-uniform: the global chunk counter has passed nchunks
+    bool fin = false;           // the lane's ray is complete and its Tr not yet written (VR_WW_BATCH_FINISH)
     const uint32_t per = A.chunk_rec * (uint32_t)(A.num_lights + A.env_samples);
     const uint32_t nrec = dev_nrec(A), nchunks = (nrec + A.chunk_rec - 1u) >> A.chunk_shift;
     // Claim units: a chunk's rays in hand-out order, cut into 2^split equal parts when the launch has
@@ -1786,6 +1787,9 @@ __global__ __launch_bounds__(BLOCK, WAVES) void secondary_ww_kernel(RenderArgs A
     // tail of the persistent launch (8-way C4 share: 22.7 -> 21.7 ms). Whole chunks otherwise (record
     // locality).
     const uint32_t waves = gridDim.x * (BLOCK / 64u), cpw = nchunks / max(waves, 1u);
+#ifndef VR_WW_BATCH_FINISH
+#define VR_WW_BATCH_FINISH 1  // 1: completed rays write their Tr at the next refill, all in one pass (A/B)
+#endif
 #ifndef VR_WW_SPLIT_CPW
 #define VR_WW_SPLIT_CPW 32  // chunks per resident wave below which claim units get shorter (A/B)
 #endif
@@ -1807,6 +1811,12 @@ __global__ __launch_bounds__(BLOCK, WAVES) void secondary_ww_kernel(RenderArgs A
     for (;;) {
         const uint64_t idle = __ballot(!live);
         if (__popcll(idle) >= kRefillMin) {  // refill once enough lanes are idle (amortises sec_init)
+#if VR_WW_BATCH_FINISH
+            if (fin) {  // the completions since the last refill, in one pass
+                sec_finish<S, true, PURE, WH>(A, R, c);
+                fin = false;
+            }
+#endif
             if (pool == pool_end && !counter_done) {  // next unit of a record chunk
                 uint32_t cnext = 0;
                 if (lane == 0) cnext = (uint32_t)atomicAdd(A.ray_next, 1ull);
@@ -1838,6 +1848,12 @@ __global__ __launch_bounds__(BLOCK, WAVES) void secondary_ww_kernel(RenderArgs A
             pool = pool_end - pool > handed ? pool + handed : pool_end;
         }
         if (!__any(live)) {
+#if VR_WW_BATCH_FINISH
+            if (fin) {  // (only if the refill threshold exceeded the wave: every lane idle refills above)
+                sec_finish<S, true, PURE, WH>(A, R, c);
+                fin = false;
+            }
+#endif
             if (counter_done && pool == pool_end) break;
             continue;
         }
@@ -1967,7 +1983,11 @@ __global__ __launch_bounds__(BLOCK, WAVES) void secondary_ww_kernel(RenderArgs A
             diag_lap(kCtrSteps);
         }
         if (live && (cut_reached<PURE>(R) || (node == -1 && !Q.has_prim()))) {
+#if VR_WW_BATCH_FINISH
+            fin = true;  // written at the next refill (the lane idles until then anyway)
+#else
             sec_finish<S, true, PURE, WH>(A, R, c);
+#endif
             live = false;
         }
     }
