@@ -382,6 +382,17 @@ constexpr bool kMarchLocal = VR_MARCH_LOCAL;
 #define VR_MARCH_PRETEST 0  // 1: the march's BVH queries skip certain misses with the fast forms (fast_reject_*; A/B: C4 14.0 -> 16.4 ms)
 #endif
 constexpr bool kMarchPretest = VR_MARCH_PRETEST;
+// Look-ahead windows: one entrant query covers this many steps; the entrants of the later steps wait in
+// up to kMarchPending register slots (j, entry, exit) and join the active list at their step. The
+// entrant set of every step is the one its own query would return, so the march is unchanged bit for
+// bit; a window with more later entrants than slots keeps only its first step's (the next step queries).
+#ifndef VR_MARCH_LOOKAHEAD
+#define VR_MARCH_LOOKAHEAD 1  // steps per entrant query (1: one query per step; A/B at C4: 2 steps 14.4 ms, 3 17.8, 4 21.5 vs 14.0)
+#endif
+#ifndef VR_MARCH_PENDING
+#define VR_MARCH_PENDING 4  // register slots for the later steps' entrants
+#endif
+constexpr int kMarchLook = VR_MARCH_LOOKAHEAD, kMarchPend = VR_MARCH_PENDING;
 
 template <int ACT, bool S, bool H, bool W = false, int CAP = kStackSize, bool COOP = false>
 __device__ int march(const RenderArgs& A, uint32_t p, int px, int py, int* act_base, int* stack, int stride, Ctr& c,
@@ -425,11 +436,29 @@ __device__ int march(const RenderArgs& A, uint32_t p, int px, int py, int* act_b
         }
     };
     int kq = 0;
+    // look-ahead (W, not COOP): pend_k = the last step the pending slots are complete for (-1: none);
+    // a consumed or empty slot has pa = +inf
+    constexpr bool kLook = W && !COOP && kMarchLook > 1;
+    int pend_k = -1;
+    int pj[kMarchPend];
+    float pa[kMarchPend], pb[kMarchPend];
+#pragma unroll
+    for (int i = 0; i < kMarchPend; ++i) {
+        pj[i] = 0;
+        pa[i] = pb[i] = INFINITY;
+    }
     if (A.num_prims > 0) {
         for (;;) {
             const float t_lo = (kq == 0) ? -1.0f : ts[kq - 1];
             int k;
-            if (act.n == 0) {  // closest entry strictly after t_lo
+            float pmin = INFINITY;  // the earliest pending entry (pending: every entry of (t_lo, ts[pend_k]])
+            if constexpr (kLook) {
+#pragma unroll
+                for (int i = 0; i < kMarchPend; ++i) pmin = fminf(pmin, pa[i]);
+            }
+            if (kLook && act.n == 0 && pmin < INFINITY) {  // the closest entry after t_lo is pending
+                k = kfirst(ts, nts, step, pmin);
+            } else if (act.n == 0) {  // closest entry strictly after t_lo
                 if constexpr (S) c.v[kCtrPrimQueries]++;
                 float best = INFINITY;
                 auto prune_c = [&](float tmin, float tmax) {
@@ -456,14 +485,48 @@ __device__ int march(const RenderArgs& A, uint32_t p, int px, int py, int* act_b
             }
             if (k >= nts - 1) return kError;  // step table too short (host sizes it from scene bounds)
             const float t_k = ts[k];
-            // entrants: t_lo < a <= t_k and still inside at t_k (b > t_k)
-            if constexpr (S) c.v[kCtrPrimQueries]++;
             bool ovf = false;
+            if (kLook && k <= pend_k) {  // this step's entrants wait in the pending slots
+#pragma unroll
+                for (int i = 0; i < kMarchPend; ++i) {
+                    if (!(pa[i] <= t_k)) continue;  // a later step's (or an empty slot)
+                    const int j = pj[i];
+                    const bool inside = pb[i] > t_k;
+                    pa[i] = INFINITY;
+                    if (!inside) continue;
+                    if (act.n >= ACT) {
+                        ovf = true;
+                        continue;
+                    }
+                    int q = act.n;  // sorted insert, as the query's
+                    while (q > 0 && act.get(q - 1) > j) {
+                        act.set(q, act.get(q - 1));
+                        --q;
+                    }
+                    act.set(q, j);
+                    act.n++;
+                }
+                if (ovf) return kOverflow;
+                kq = k + 1;
+                if (!march_step<S, COOP>(A, ray, p, px, py, k, t_k, act, T, prev, c, writer)) break;
+                continue;
+            }
+            // entrants: t_lo < a <= t_k and still inside at t_k (b > t_k); with look-ahead the window
+            // runs on to t_end and the later steps' entrants go to the pending slots
+            const int k_end = kLook ? min(k + kMarchLook - 1, nts - 2) : k;
+            const float t_end = ts[k_end];
+            int pn = 0;
+            bool pend_ovf = false;
+            if constexpr (kLook) {
+#pragma unroll
+                for (int i = 0; i < kMarchPend; ++i) pa[i] = INFINITY;
+            }
+            if constexpr (S) c.v[kCtrPrimQueries]++;
             auto prune_w = [&](float tmin, float tmax) {
-                return tmax >= t_lo - kTPad * (1.0f + fabsf(t_lo)) && tmin <= t_k + kTPad * (1.0f + t_k);
+                return tmax >= t_lo - kTPad * (1.0f + fabsf(t_lo)) && tmin <= t_end + kTPad * (1.0f + t_end);
             };
             auto walk_w = [&](auto prune, auto leaf) -> bool {  // a window of one step: local; from 0: the root
-                return (local && t_lo >= 0.0f) ? walk_local(t_lo, t_k, prune, leaf) : walk_any(prune, leaf);
+                return (local && t_lo >= 0.0f) ? walk_local(t_lo, t_end, prune, leaf) : walk_any(prune, leaf);
             };
             const bool ok = walk_w(
                 prune_w,
@@ -474,7 +537,20 @@ __device__ int march(const RenderArgs& A, uint32_t p, int px, int py, int* act_b
                         if (kMarchPretest && fast_reject_window(g, ray, t_lo, t_k)) continue;
                         Quad q = quad(g, ray);
                         float a, b;
-                        if (!intersect(q, a, b) || !(a > t_lo) || !(a <= t_k) || !(b > t_k)) continue;
+                        if (!intersect(q, a, b) || !(a > t_lo) || !(a <= t_end)) continue;
+                        if (kLook && !(a <= t_k)) {  // a later step's entrant
+#pragma unroll
+                            for (int i = 0; i < kMarchPend; ++i)
+                                if (i == pn) {
+                                    pj[i] = (int)j;
+                                    pa[i] = a;
+                                    pb[i] = b;
+                                }
+                            pend_ovf = pend_ovf || pn == kMarchPend;
+                            pn = min(pn + 1, kMarchPend);
+                            continue;
+                        }
+                        if (!(b > t_k)) continue;
                         if (act.n >= ACT) {
                             ovf = true;
                             continue;
@@ -490,6 +566,14 @@ __device__ int march(const RenderArgs& A, uint32_t p, int px, int py, int* act_b
                     return true;
                 });
             if (ovf || !ok) return kOverflow;
+            if constexpr (kLook) {
+                pend_k = k_end;
+                if (pend_ovf) {  // more later entrants than slots: only this step's are complete
+                    pend_k = k;
+#pragma unroll
+                    for (int i = 0; i < kMarchPend; ++i) pa[i] = INFINITY;
+                }
+            }
             kq = k + 1;
             if (!march_step<S, COOP>(A, ray, p, px, py, k, t_k, act, T, prev, c, writer)) break;
         }
