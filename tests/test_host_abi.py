@@ -170,6 +170,19 @@ def test_device_entry_points_fail_loudly_without_scene_or_gpu():
     assert st == 5
 
 
+def test_option_table_mirrors_the_header():
+    """Every vr_option of include/vr_hip.h has the same value in vr_amd._lib and a Device.set_option name
+    (the Python mirror cannot drift from the ABI's option numbers)."""
+    header = open(os.path.join(ROOT, "include", "vr_hip.h")).read()
+    enum = header[header.index("typedef enum vr_option"):]
+    enum = enum[:enum.index("} vr_option;")]
+    declared = {m.group(1): int(m.group(2)) for m in re.finditer(r"(VR_OPT_[A-Z0-9_]+)\s*=\s*(\d+)", enum)}
+    assert len(declared) >= 11
+    for name, value in declared.items():
+        assert getattr(L, name) == value, name
+    assert sorted(vr.Device.OPTIONS.values()) == sorted(declared.values())
+
+
 def test_num_tiles():
     assert vr.num_tiles(16, 16) == 1
     assert vr.num_tiles(17, 16) == 2
