@@ -1825,7 +1825,7 @@ __device__ __forceinline__ void list_advance(LeafQueue& Q, int& node, int start)
 #define VR_WW_NODE_STEPS 6
 #endif
 #ifndef VR_WW_PRIM_STEPS
-#define VR_WW_PRIM_STEPS 5
+#define VR_WW_PRIM_STEPS 4  // A/B round 4 (tight tree, C4 secondary): 3: 77.1, 4: 77.1-77.3, 5: 77.6-78.0, 7: 85.7 ms
 #endif
 #ifndef VR_WW_PRIM_UNROLL
 #define VR_WW_PRIM_UNROLL 5  // unroll of the PRIM iteration's step loop (A/B: code size vs. scheduling)
