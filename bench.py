@@ -503,7 +503,9 @@ def main():
         # HBM traffic of the dominant kernel: rocprofv3 PMC passes of this same command (FETCH_SIZE x 2,
         # the gfx950 correction of MI355X_MICROARCH.md, + WRITE_SIZE), committed under profiles/
         pmc_path = os.path.join(ROOT, "profiles", PMC_SUMMARY)
-        if args.config == "c4" and world == 1 and os.path.exists(pmc_path):
+        # (only for the command those passes profiled: C4 at its default settings)
+        if (args.config == "c4" and world == 1 and args.env_samples == 20 and args.t_eps == 1e-6
+                and os.path.exists(pmc_path)):
             pmc = json.load(open(pmc_path))
             for k, d in pmc.items():
                 if k.startswith("vr::dev::secondary_ww_kernel") and "hbm_read_bytes_gfx950_corrected" in d:

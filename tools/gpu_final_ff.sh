@@ -12,6 +12,7 @@ run() {  # name, args...
   timeout -k 10 300 python3 bench.py "$@" > $O/$n.json 2> $O/$n.log || { echo "$n failed"; tail -5 $O/$n.log; exit 1; }
   python3 -c "import json;d=json.load(open('$O/$n.json'));r=d.get('roofline') or {};print('$n', round(d['value'],3), d['unit'], round(d['ms_per_step'],2), 'ms', 'frac', r.get('frac'), 'traffic', r.get('traffic'))"
 }
+run c4_env1 --env-samples 1 --steps 5
 run ff_c2 --config c2 --integrator multiscatter --spp 16 --steps 5
 run ff_c3 --config c3 --integrator freeflight --spp 4 --steps 5
 run ff_c4 --config c4 --integrator multiscatter --spp 1 --steps 3
