@@ -137,6 +137,7 @@ struct vr_ctx {
     int64_t opt_start_subtree = 1;     // VR_OPT_START_SUBTREE
     int64_t opt_ff_staged = 0;         // VR_OPT_FF_STAGED
     int64_t opt_sec_tight = 1;         // VR_OPT_SEC_TIGHT (next upload)
+    int64_t opt_march_wide_min = 2048;  // VR_OPT_MARCH_WIDE_MIN
     bool last_upload_device_bvh = false;  // the current scene's tree came from the device builder
     vr_group* group = nullptr;         // vr_init_multi: the devices this context drives (host/vr_multi.cpp)
 };
@@ -632,11 +633,14 @@ vr_status gauss_pipeline(vr_ctx* c, RenderArgs& A, hipStream_t s, bool stats) {
         c->pcg_jump_n = n;
     }
     A.pcg_jump = (const unsigned long long*)c->pcg_jump.p;
-    if ((st = grow(c->deep, (kDeepQueue + 1) * 4ull + (uint64_t)kActDeep * kDeepThreads * 4ull, "hipMalloc(deep march)")) != VR_OK)
+    if ((st = grow(c->deep, (kDeepQueue + 1) * 4ull + (uint64_t)kActDeep * kDeepThreads * 4ull + (uint64_t)kActWide * kWideThreads * 4ull,
+                   "hipMalloc(deep march)")) != VR_OK)
         return st;
     A.deepq = (uint32_t*)c->deep.p;
     A.deepq_cap = kDeepQueue;
     A.deep_act = (int32_t*)(A.deepq + kDeepQueue + 1);
+    A.wide_act = A.deep_act + (size_t)kActDeep * kDeepThreads;
+    A.wide_min = (uint32_t)c->opt_march_wide_min;
 
     // Tile bins of the binned march: count, scan, then (with one host sync for the entry count) emit.
     A.bin_off = A.bin_ent = nullptr;
@@ -1541,6 +1545,10 @@ vr_status vr_set_option(vr_ctx* c, int32_t option, int64_t value) {
             if (value != 0 && value != 1) return fail(VR_ERR_INVALID, "VR_OPT_SEC_TIGHT must be 0 or 1");
             c->opt_sec_tight = value;
             return VR_OK;
+        case VR_OPT_MARCH_WIDE_MIN:
+            if (value < 0 || value > 0xffffffffll) return fail(VR_ERR_INVALID, "VR_OPT_MARCH_WIDE_MIN must be in [0, 2^32)");
+            c->opt_march_wide_min = value;
+            return VR_OK;
         case VR_OPT_RECORD_CAPACITY:
             if ((value != 0 && value < 4096) || value > 0x3fffffff)
                 return fail(VR_ERR_INVALID, "VR_OPT_RECORD_CAPACITY must be 0 or in [4096, 2^30)");
@@ -1566,6 +1574,7 @@ vr_status vr_get_option(vr_ctx* c, int32_t option, int64_t* value) {
         case VR_OPT_START_SUBTREE: *value = c->opt_start_subtree; return VR_OK;
         case VR_OPT_FF_STAGED: *value = c->opt_ff_staged; return VR_OK;
         case VR_OPT_SEC_TIGHT: *value = c->opt_sec_tight; return VR_OK;
+        case VR_OPT_MARCH_WIDE_MIN: *value = c->opt_march_wide_min; return VR_OK;
         default: return fail(VR_ERR_INVALID, "vr_get_option: unknown option " + std::to_string(option));
     }
 }

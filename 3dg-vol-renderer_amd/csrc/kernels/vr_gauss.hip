@@ -629,6 +629,7 @@ __global__ __launch_bounds__(BLOCK) void march_fallback_kernel(RenderArgs A) {
     __shared__ int s_stack[kStackSize * BLOCK];
     const int tid = threadIdx.x;
     const uint32_t n = min(A.queue[0], A.queue_cap);
+    if (n >= A.wide_min) return;  // a long queue: march_wide_kernel takes it (one pixel per lane)
     for (uint32_t q = blockIdx.x; q < n; q += gridDim.x) {
         const uint32_t p = A.queue[1 + q];
         int lx, ly, x, y;
@@ -646,6 +647,37 @@ __global__ __launch_bounds__(BLOCK) void march_fallback_kernel(RenderArgs A) {
             mark_error(A, p);
         }
     }
+}
+
+// A long fallback queue (translucent scenes with many overlapping Gaussians: C2 sends most pixels here)
+// one pixel per lane: the main kernel's march with kActWide active-list slots per lane in global memory
+// ([slot][thread] rows, coalesced over a wave's lanes) instead of 16 in LDS. One wave per pixel
+// (march_fallback_kernel) shortens a single pixel's march but runs the queue 64x narrower; it keeps
+// queues shorter than A.wide_min (C4: 833 pixels). Same march<> operations as every other pass, so
+// a pixel's records do not depend on which pass marched it. Overflow (more than kActWide active, or a
+// 4-wide walk past its stack): the deep pass.
+template <bool S, bool H, bool W>
+__global__ __launch_bounds__(kWideBlock) void march_wide_kernel(RenderArgs A) {
+    __shared__ int s_stack[kStackSize * kWideBlock];
+    const int tid = threadIdx.x;
+    const uint32_t gt = blockIdx.x * kWideBlock + tid, nthreads = gridDim.x * kWideBlock;
+    const uint32_t n = min(A.queue[0], A.queue_cap);
+    if (n < A.wide_min) return;
+    Ctr c{};
+    for (uint32_t q = gt; q < n; q += nthreads) {
+        const uint32_t p = A.queue[1 + q];
+        int lx, ly, x, y;
+        tile_pixel(A, p >> 8, (int)(p & 255u), lx, ly, x, y);
+        const int st = march<kActWide, S, H, W, kStackSize>(A, p, x, y, A.wide_act + gt, s_stack + tid, kWideBlock, c, (int)nthreads);
+        if (st == kOverflow) {
+            const uint32_t slot = atomicAdd(A.deepq, 1u);
+            if (slot < A.deepq_cap) A.deepq[1 + slot] = p;
+            else mark_error(A, p);
+        } else if (st != kOK) {
+            mark_error(A, p);
+        }
+    }
+    if constexpr (S) flush_counters(A.work, c);
 }
 
 // Pixels whose active set outgrew the fallback's 64 LDS slots: the same march with the active list in
@@ -2485,6 +2517,11 @@ static hipError_t march_pass(const RenderArgs& A, hipStream_t stream) {
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL((dev::march_fallback_kernel<kActFallback, kBlockFallback, S, H>), dim3(1024), dim3(kBlockFallback), 0,
                        stream, A);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    if (H && A.hnodes4 != nullptr)  // (exactly one of the two passes takes the queue, by its length)
+        hipLaunchKernelGGL((dev::march_wide_kernel<S, H, true>), dim3(kWideThreads / kWideBlock), dim3(kWideBlock), 0, stream, A);
+    else
+        hipLaunchKernelGGL((dev::march_wide_kernel<S, H, false>), dim3(kWideThreads / kWideBlock), dim3(kWideBlock), 0, stream, A);
     if ((e = hipGetLastError()) != hipSuccess) return e;
     hipLaunchKernelGGL((dev::march_deep_kernel<S, H>), dim3(kDeepThreads / kDeepBlock), dim3(kDeepBlock), 0, stream, A);
     return hipGetLastError();

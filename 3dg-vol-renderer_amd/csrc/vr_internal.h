@@ -103,6 +103,9 @@ constexpr int kActInline = 4;  // active-list slots stored with each scatter rec
 // kActDeep slots per thread, kDeepThreads threads (march_deep_kernel), up to kDeepQueue such pixels per frame.
 constexpr int kActDeep = 2048, kDeepThreads = 256, kDeepBlock = 64;
 constexpr uint32_t kDeepQueue = 65536;
+// march_wide_kernel: the fallback queue one pixel per lane, kActWide active-list slots per lane in global
+// memory ([slot][thread] rows), kWideThreads lanes; used when the queue holds at least A.wide_min pixels.
+constexpr int kActWide = 64, kWideThreads = 65536, kWideBlock = 64;
 
 constexpr int kMaxSpheres = 64;
 // Deferred NEE (free-flight): a path's queued shadow rays are a linked list in the queue (kFFNone ends
@@ -170,6 +173,8 @@ struct RenderArgs {
     uint32_t* deepq;       // [0] = count, [1..] = pixels for march_deep_kernel (active set > 64)
     uint32_t deepq_cap;
     int32_t* deep_act;     // march_deep_kernel's active lists, [slot][thread]
+    int32_t* wide_act;     // march_wide_kernel's active lists, [slot][thread]
+    uint32_t wide_min;     // fallback pixels from which the per-lane wide pass takes the queue (VR_OPT_MARCH_WIDE_MIN)
     uint32_t* counters;    // [0] = error pixels / paths, [2] = free-flight paths re-run in ff_fallback_kernel,
                            // [3] = the most shadow rays a free-flight launch of the frame tried to queue
     unsigned long long* work;  // instrumented build only: [0..7] march-kernel counters, [8..15] secondary-kernel counters

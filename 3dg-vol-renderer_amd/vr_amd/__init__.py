@@ -387,7 +387,7 @@ class Device:
                "device_bvh": L.VR_OPT_DEVICE_BVH, "ff_nee_queue": L.VR_OPT_FF_NEE_QUEUE,
                "march_binned": L.VR_OPT_MARCH_BINNED, "ff_solver": L.VR_OPT_FF_SOLVER,
                "start_subtree": L.VR_OPT_START_SUBTREE, "ff_staged": L.VR_OPT_FF_STAGED,
-               "sec_tight": L.VR_OPT_SEC_TIGHT}
+               "sec_tight": L.VR_OPT_SEC_TIGHT, "march_wide_min": L.VR_OPT_MARCH_WIDE_MIN}
 
     def set_option(self, name, value):
         """vr_set_option (include/vr_hip.h): explicit per-context tuning (half_nodes applies at the

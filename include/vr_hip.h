@@ -380,11 +380,16 @@ typedef enum vr_option {
                                     slots stepping through hit-collection, event-sweep and shading kernels,
                                     queued between them, each with per-lane refill; slower).
                                     Frames are identical. */
-    VR_OPT_SEC_TIGHT = 11        /* RayMarchingGaussians secondary rays, applied at the next upload: 1 (default):
+    VR_OPT_SEC_TIGHT = 11,       /* RayMarchingGaussians secondary rays, applied at the next upload: 1 (default):
                                     their own copy of the 4-wide tree with the exact boxes of the ellipsoids the
                                     whitened test accepts (the shared tree's boxes are padded by 5 % for the
                                     camera rays' M-form test); 0: the shared tree. Same Gaussians, same
                                     decisions; only the order of the optical-depth sum differs. */
+    VR_OPT_MARCH_WIDE_MIN = 12   /* RayMarchingGaussians / PureRayMarching: pixels whose active set outgrew the
+                                    primary march's 16 LDS slots are marched again; a queue of at least this
+                                    many pixels (default 2048) goes one pixel per lane with 64 slots in
+                                    global memory, a shorter one one pixel per wave (64 LDS slots). Same
+                                    operations either way: frames are identical. */
 } vr_option;
 vr_status vr_set_option(vr_ctx* ctx, int32_t option, int64_t value);
 vr_status vr_get_option(vr_ctx* ctx, int32_t option, int64_t* value);

@@ -266,6 +266,40 @@ def test_records_with_long_active_lists_match_the_oracle():
     assert nm == 0 and err < TOL, err
 
 
+@pytest.mark.parametrize("case", ["nested60", "nested80", "c2_1000_random"])
+def test_wide_fallback_pass_equals_the_wave_pass(case, device_options):
+    """VR_OPT_MARCH_WIDE_MIN: the fallback queue marched one pixel per lane (64 global-memory slots,
+    march_wide_kernel) or one pixel per wave (64 LDS slots, march_fallback_kernel) runs the same march
+    operations: identical frames and statistics, past 64 active Gaussians too (both hand those pixels to
+    the deep pass). C2's 1000_random (the translucent BASELINE config 2 scene) sends most of its pixels
+    there; its frame also matches the oracle on a tile-stratified sample."""
+    if case == "c2_1000_random":
+        scene = vr.Scene.load_GMM(scene_path("1000_random.txt"))
+        W = H = 128
+        cam = vr.Pinhole_Camera(CAM_POS, main_view_dir(), FOV)
+    else:
+        scene, _ = _nested_scene(int(case[6:]))
+        W = H = 16
+        cam = vr.Pinhole_Camera(CAM_POS, main_view_dir(), FOV)
+    out = {}
+    for wide_min in (0, 1 << 31):
+        device_options("march_wide_min", wide_min)
+        img = vr.Image(W, H)
+        integ = vr.RayMarchingGaussians(cam, env_samples=3)
+        integ.render(scene, img)
+        out[wide_min] = (img.pixels.copy(), dict(integ.last_stats))
+    a, b = out[0], out[1 << 31]
+    assert a[1]["fallback_pixels"] > 0 and a[1]["error_pixels"] == 0
+    for k in ("fallback_pixels", "deep_pixels", "scatter_records", "secondary_rays"):
+        assert a[1][k] == b[1][k], k
+    assert np.array_equal(a[0].view(np.uint32), b[0].view(np.uint32))
+    if case == "c2_1000_random":
+        pix = _tile_stratified(W, H, 1, seed=3)[:48]
+        ref = _oracle_gmm(scene_path("1000_random.txt"), W, H, env_samples=3, pixels=pix)
+        err, nm = _linf(a[0][pix[:, 1], pix[:, 0]], ref)
+        assert nm == 0 and err < TOL, err
+
+
 def test_overflow_beyond_every_capacity_fails_loudly():
     # more Gaussians overlapping one point than even the deep pass holds (kActDeep = 2048)
     scene, _ = _nested_scene(2100, 1e-6)
