@@ -27,7 +27,7 @@ hipError_t launch_sfd_loss_diff(const uint32_t* bits0, const uint32_t* bits1, co
 hipError_t gauss_record_cut(const RenderArgs& A, float budget, hipStream_t stream);
 hipError_t gauss_whiten(const GaussianRecord* rec, WRecord* out, uint32_t n, uint32_t* bad, hipStream_t stream);
 hipError_t gauss_bin(const RenderArgs& A, bool emit, hipStream_t stream);
-hipError_t gauss_parents(const HNode4* nodes, uint32_t n, int32_t* parent, uint4* sib, hipStream_t stream);
+hipError_t gauss_parents(const HNode4* nodes, uint32_t n, int32_t* parent, uint4* sib, int32_t* prim_node, hipStream_t stream);
 hipError_t gauss_refit_secondary(const HNode4* src, HNode4* dst, uint32_t n, const GaussianRecord* rec, const int32_t* parent,
                                  uint8_t* depth, float* nbox, uint32_t* maxd, const float hc[3], float hs, float diag,
                                  hipStream_t stream);
@@ -58,6 +58,7 @@ struct vr_ctx {
     HNode4* d_hnodes4s = nullptr;  // the secondary rays' copy with tight boxes (VR_OPT_SEC_TIGHT)
     int32_t* d_parent4 = nullptr;  // parent of every HNode4 (the secondary rays' climb out of their start subtree)
     uint4* d_sib4 = nullptr;       // union box of every HNode4's siblings (the climb's skip test)
+    int32_t* d_prim_node4 = nullptr;  // the HNode4 whose child is each record's leaf (record starts)
     size_t num_nodes4 = 0;
     float hn_center[3] = {0, 0, 0}, hn_scale = 1.0f;
     float sig_max[3] = {0, 0, 0};  // largest per-axis standard deviation of any Gaussian
@@ -177,6 +178,8 @@ void free_scene(vr_ctx* c) {
     c->d_parent4 = nullptr;
     if (c->d_sib4) (void)hipFree(c->d_sib4);
     c->d_sib4 = nullptr;
+    if (c->d_prim_node4) (void)hipFree(c->d_prim_node4);
+    c->d_prim_node4 = nullptr;
     c->num_nodes4 = 0;
     if (c->d_spheres) (void)hipFree(c->d_spheres);
     c->d_gauss = nullptr;
@@ -445,10 +448,15 @@ vr_status upload_parents(vr_ctx* c) {
     c->d_parent4 = nullptr;
     if (c->d_sib4) (void)hipFree(c->d_sib4);
     c->d_sib4 = nullptr;
+    if (c->d_prim_node4) (void)hipFree(c->d_prim_node4);
+    c->d_prim_node4 = nullptr;
     if (!c->d_hnodes4 || c->num_nodes4 == 0) return VR_OK;
     HIP_TRY(hipMalloc(&c->d_parent4, c->num_nodes4 * sizeof(int32_t)), "hipMalloc(wide-node parents)");
     HIP_TRY(hipMalloc(&c->d_sib4, c->num_nodes4 * sizeof(uint4)), "hipMalloc(wide-node siblings)");
-    HIP_TRY(gauss_parents(c->d_hnodes4, (uint32_t)c->num_nodes4, c->d_parent4, c->d_sib4, c->stream), "wide-node parents");
+    if (c->num_prims > 0)
+        HIP_TRY(hipMalloc(&c->d_prim_node4, (size_t)c->num_prims * sizeof(int32_t)), "hipMalloc(record leaf nodes)");
+    HIP_TRY(gauss_parents(c->d_hnodes4, (uint32_t)c->num_nodes4, c->d_parent4, c->d_sib4, c->d_prim_node4, c->stream),
+            "wide-node parents");
     HIP_TRY(hipStreamSynchronize(c->stream), "wide-node parents");
     return upload_secondary_tree(c);
 }
@@ -552,6 +560,7 @@ vr_status fill_args(vr_ctx* c, const vr_camera* cam, const vr_render_params* p, 
     A.hnodes4 = c->d_hnodes4;
     A.hnodes4s = c->d_hnodes4s ? c->d_hnodes4s : c->d_hnodes4;
     A.hn4_parent = c->d_parent4;
+    A.prim_node4 = c->d_prim_node4;
     A.num_nodes4 = (uint32_t)c->num_nodes4;
     A.hn4_sib = c->d_sib4;
     for (int k = 0; k < 3; ++k) A.hn_center[k] = c->hn_center[k];

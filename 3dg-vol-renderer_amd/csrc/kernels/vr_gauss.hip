@@ -2301,10 +2301,32 @@ __global__ __launch_bounds__(256) void refit_kernel(const HNode4* __restrict__ s
 #ifndef VR_START_MARGIN
 #define VR_START_MARGIN 0.0f  // room (world units) the start subtree's box keeps around the record position (A/B)
 #endif
+#ifndef VR_START_FROM_MEMBER
+#define VR_START_FROM_MEMBER 1  // 1: a record with an active Gaussian starts at the node holding that Gaussian's leaf (A/B)
+#endif
+// Every record has an active Gaussian (a step scatters only with sigma_s > 0): the 4-wide node whose
+// child is that Gaussian's leaf is a leaf-level node near the record (the Gaussian holds the position),
+// found with two loads instead of a descent from the root.
+__global__ __launch_bounds__(256) void prim_node_kernel(const HNode4* __restrict__ nodes, uint32_t n, int32_t* __restrict__ map) {
+    const uint32_t i = blockIdx.x * 256u + threadIdx.x;
+    if (i >= n) return;
+    const int4 c = reinterpret_cast<const int4*>(nodes + i)[3];
+    const int32_t ref[4] = {c.x, c.y, c.z, c.w};
+    for (int s = 0; s < 4; ++s)
+        if (ref[s] < 0)
+            for (uint32_t j = leaf_first(ref[s]); j < leaf_first(ref[s]) + leaf_count(ref[s]); ++j) map[j] = (int32_t)i;
+}
 __global__ __launch_bounds__(256) void record_start_kernel(RenderArgs A) {
     const uint32_t nrec = dev_nrec(A);
     const float margin = VR_START_MARGIN * A.hn_scale;
     for (uint32_t r = blockIdx.x * 256u + threadIdx.x; r < nrec; r += gridDim.x * 256u) {
+        if (VR_START_FROM_MEMBER && A.prim_node4 != nullptr) {
+            const uint4 meta = A.rec_meta[r];
+            if (meta.w > 0u) {
+                A.rec_start[r] = A.prim_node4[A.rec_act[meta.z]];
+                continue;
+            }
+        }
         const float4 pos = A.rec_pos[r];
         float p[3] = {pos.x, pos.y, pos.z};
         node_space<true>(A, p[0], p[1], p[2]);
@@ -2615,9 +2637,10 @@ hipError_t gauss_secondary(const RenderArgs& A, hipStream_t stream, bool stats) 
     return stats ? secondary_launch<true, false>(A, stream) : secondary_launch<false, false>(A, stream);
 }
 
-hipError_t gauss_parents(const HNode4* nodes, uint32_t n, int32_t* parent, uint4* sib, hipStream_t stream) {
+hipError_t gauss_parents(const HNode4* nodes, uint32_t n, int32_t* parent, uint4* sib, int32_t* prim_node, hipStream_t stream) {
     hipLaunchKernelGGL(dev::parents_kernel, dim3((n + 255) / 256), dim3(256), 0, stream, nodes, n, parent);
     hipLaunchKernelGGL(dev::siblings_kernel, dim3((n + 255) / 256), dim3(256), 0, stream, nodes, n, sib);
+    if (prim_node != nullptr) hipLaunchKernelGGL(dev::prim_node_kernel, dim3((n + 255) / 256), dim3(256), 0, stream, nodes, n, prim_node);
     return hipGetLastError();
 }
 
