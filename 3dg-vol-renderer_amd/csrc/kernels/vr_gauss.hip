@@ -2503,7 +2503,13 @@ __global__ __launch_bounds__(256) void accumulate_kernel(RenderArgs A) {
 #ifndef VR_MARCH_BLOCK
 #define VR_MARCH_BLOCK 64  // lanes per march workgroup: 256 (a tile) or 64 (a quarter tile; -6 % march time)
 #endif
-constexpr int kActFast = 16, kBlockFast = VR_MARCH_BLOCK;
+#ifndef VR_MARCH_ACT
+#define VR_MARCH_ACT 16  // active-list LDS slots per lane of the primary march (A/B)
+#endif
+#ifndef VR_MARCH_STACK4
+#define VR_MARCH_STACK4 24  // LDS stack entries per lane of the primary march's 4-wide walks (A/B; overflow: fallback)
+#endif
+constexpr int kActFast = VR_MARCH_ACT, kBlockFast = VR_MARCH_BLOCK;
 constexpr int kActFallback = 64, kBlockFallback = 64;
 constexpr int kBlockSecondary = 256;
 
@@ -2527,7 +2533,7 @@ static hipError_t march_pass(const RenderArgs& A, hipStream_t stream) {
     if (A.bin_ent != nullptr)  // binned march (its overflowing pixels re-run in the BVH fallback below)
         hipLaunchKernelGGL((dev::march_binned_kernel<S>), dim3(A.num_tiles * 4), dim3(64), 0, stream, A);
     else if (H && A.hnodes4 != nullptr)  // 4-wide tree; a query that could overflow the stack goes to the fallback
-        hipLaunchKernelGGL((dev::march_kernel<kActFast, kBlockFast, S, kShallowStack, true, true>), dim3(A.num_tiles * (256 / kBlockFast)),
+        hipLaunchKernelGGL((dev::march_kernel<kActFast, kBlockFast, S, VR_MARCH_STACK4, true, true>), dim3(A.num_tiles * (256 / kBlockFast)),
                            dim3(kBlockFast), 0, stream, A);
     else if (shallow)
         hipLaunchKernelGGL((dev::march_kernel<kActFast, kBlockFast, S, kShallowStack, H>), dim3(A.num_tiles * (256 / kBlockFast)),

@@ -105,7 +105,10 @@ constexpr int kActDeep = 2048, kDeepThreads = 256, kDeepBlock = 64;
 constexpr uint32_t kDeepQueue = 65536;
 // march_wide_kernel: the fallback queue one pixel per lane, kActWide active-list slots per lane in global
 // memory ([slot][thread] rows), kWideThreads lanes; used when the queue holds at least A.wide_min pixels.
-constexpr int kActWide = 64, kWideThreads = 65536, kWideBlock = 64;
+#ifndef VR_WIDE_THREADS
+#define VR_WIDE_THREADS 262144  // lanes of march_wide_kernel (4 waves per SIMD; 64 MB of active-list slots)
+#endif
+constexpr int kActWide = 64, kWideThreads = VR_WIDE_THREADS, kWideBlock = 64;
 
 constexpr int kMaxSpheres = 64;
 // Deferred NEE (free-flight): a path's queued shadow rays are a linked list in the queue (kFFNone ends
