@@ -86,6 +86,8 @@ struct vr_ctx {
     // one launch tried to queue
     uint32_t* h_report = nullptr;
     bool report_gauss = false;  // the last frame ran the RayMarchingGaussians pipeline (fields [2..4])
+    uint64_t report_pixels = 0; // pixels of that frame (its march)
+    bool march_big = false;     // this scene's frames overflow the primary march's 16 slots often: kActBig (reset at upload)
     float* d_frame = nullptr;
     size_t frame_cap = 0;
     hipEvent_t ev_start = nullptr, ev_stop = nullptr;
@@ -650,6 +652,7 @@ vr_status gauss_pipeline(vr_ctx* c, RenderArgs& A, hipStream_t s, bool stats) {
     A.deep_act = (int32_t*)(A.deepq + kDeepQueue + 1);
     A.wide_act = A.deep_act + (size_t)kActDeep * kDeepThreads;
     A.wide_min = (uint32_t)c->opt_march_wide_min;
+    A.march_big = c->march_big ? 1 : 0;
 
     // Tile bins of the binned march: count, scan, then (with one host sync for the entry count) emit.
     A.bin_off = A.bin_ent = nullptr;
@@ -795,6 +798,7 @@ vr_status gauss_pipeline(vr_ctx* c, RenderArgs& A, hipStream_t s, bool stats) {
     HIP_TRY(gauss_accumulate(A, s), "accumulate");
     c->staged = true;
     c->report_gauss = true;
+    c->report_pixels = (uint64_t)A.num_tiles * 256u;
     c->last_secondary_per_record = S;
     return VR_OK;
 }
@@ -921,6 +925,9 @@ vr_status collect(vr_ctx* c) {
         const uint64_t nrec = c->h_report[2], nact = c->h_report[3];
         c->rec_hint = std::max<uint64_t>(c->rec_hint, nrec + nrec / 8);
         c->ovf_hint = std::max<uint64_t>(c->ovf_hint, nact + nact / 8);
+        // >= 5 % of the pixels re-marched: the scene's active sets outgrow 16 slots; later frames march with
+        // kActBig (same operations, so the frames are identical; kept until the next upload)
+        if ((uint64_t)c->h_report[0] * 20ull >= c->report_pixels && c->report_pixels > 0) c->march_big = true;
     }
     if (c->report_ff && c->last_nee_bound > 0) {
         // a launch that found the queue full counted its paths' first refused claim only (they then
@@ -1172,7 +1179,9 @@ vr_status vr_upload_scene(vr_ctx* c, const vr_scene* sc) {
     if (s.lights.size() > (size_t)kMaxLights) return fail(VR_ERR_UNSUPPORTED, "more than 16 lights");
     HIP_TRY(hipSetDevice(c->device), "hipSetDevice");
     HIP_TRY(hipDeviceSynchronize(), "hipDeviceSynchronize");
+    if (vr_status cs = collect(c); cs != VR_OK) return cs;  // the previous scene's last report, before the reset
     free_scene(c);
+    c->march_big = false;
     c->type = s.type;
     c->lights.clear();
     for (const vr_light& l : s.lights)

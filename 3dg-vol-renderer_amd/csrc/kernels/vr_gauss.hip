@@ -588,6 +588,18 @@ __device__ __forceinline__ void mark_error(const RenderArgs& A, uint32_t p) {
     A.px_T[p] = __builtin_nanf("");
 }
 
+// A pixel that overflowed a pass is marched again from its start by the next pass, which relinks it;
+// the records this pass already wrote for it are unreachable. Their weight T sigma_s (rec_pos.w, > 0 for
+// every live record) is zeroed so the secondary stage starts none of their rays (sec_init).
+#ifndef VR_ORPHAN_SKIP
+#define VR_ORPHAN_SKIP 1
+#endif
+__device__ __forceinline__ void orphan_records(const RenderArgs& A, uint32_t p) {
+    if (!VR_ORPHAN_SKIP) return;
+    for (uint32_t r = A.px_first[p]; r != kNoRecord && r < A.rec_cap; r = A.rec_next[r])
+        reinterpret_cast<float*>(A.rec_pos + r)[3] = 0.0f;
+}
+
 template <int ACT, int BLOCK, bool S, int STACK, bool H, bool W = false>
 __global__ __launch_bounds__(BLOCK) void march_kernel(RenderArgs A) {
     __shared__ int s_act[ACT * BLOCK];
@@ -611,6 +623,7 @@ __global__ __launch_bounds__(BLOCK) void march_kernel(RenderArgs A) {
     }
     if constexpr (S) flush_counters(A.work, c);
     if (st == kOverflow) {
+        orphan_records(A, p);
         uint32_t slot = atomicAdd(A.queue, 1u);
         if (slot < A.queue_cap) A.queue[1 + slot] = p;
         else mark_error(A, p);
@@ -640,6 +653,7 @@ __global__ __launch_bounds__(BLOCK) void march_fallback_kernel(RenderArgs A) {
         if constexpr (S)
             for (int i = 0; i < kNumCtr; ++i) atomicAdd(A.work + i, (unsigned long long)c.v[i]);
         if (st == kOverflow) {  // more than ACT Gaussians active at one step: the deep pass
+            orphan_records(A, p);
             const uint32_t slot = atomicAdd(A.deepq, 1u);
             if (slot < A.deepq_cap) A.deepq[1 + slot] = p;
             else mark_error(A, p);
@@ -670,6 +684,7 @@ __global__ __launch_bounds__(kWideBlock) void march_wide_kernel(RenderArgs A) {
         tile_pixel(A, p >> 8, (int)(p & 255u), lx, ly, x, y);
         const int st = march<kActWide, S, H, W, kStackSize>(A, p, x, y, A.wide_act + gt, s_stack + tid, kWideBlock, c, (int)nthreads);
         if (st == kOverflow) {
+            orphan_records(A, p);
             const uint32_t slot = atomicAdd(A.deepq, 1u);
             if (slot < A.deepq_cap) A.deepq[1 + slot] = p;
             else mark_error(A, p);
@@ -982,6 +997,7 @@ __global__ __launch_bounds__(64) void march_binned_kernel(RenderArgs A) {
         A.px_first[p] = kNoRecord;
         A.px_T[p] = 0.0f;
     } else if (st == kOverflow) {
+        orphan_records(A, p);
         uint32_t slot = atomicAdd(A.queue, 1u);
         if (slot < A.queue_cap) A.queue[1 + slot] = p;
         else mark_error(A, p);
@@ -1226,6 +1242,9 @@ __device__ __forceinline__ bool sec_init(const RenderArgs& A, uint32_t nrec, uin
     if (!ray_slot(A, chunk, rem, nrec, s, r)) return false;  // padding id
     R.slot = chunk * rays_per_chunk(A) + rem;
     const float4 pos = A.rec_pos[r];
+#if VR_ORPHAN_SKIP
+    if (!(pos.w > 0.0f)) return false;  // an orphaned record (orphan_records): no pixel reads its rays
+#endif
     const uint4 meta = A.rec_meta[r];
     R.rec = r;
     R.cut = A.tau_cut;  // (a select of the two addresses would make this one flat load)
@@ -2509,7 +2528,10 @@ __global__ __launch_bounds__(256) void accumulate_kernel(RenderArgs A) {
 #ifndef VR_MARCH_STACK4
 #define VR_MARCH_STACK4 24  // LDS stack entries per lane of the primary march's 4-wide walks (A/B; overflow: fallback)
 #endif
-constexpr int kActFast = VR_MARCH_ACT, kBlockFast = VR_MARCH_BLOCK;
+#ifndef VR_MARCH_ACT_BIG
+#define VR_MARCH_ACT_BIG 32  // the primary march's slots once a scene's frames overflow 16 on >= 5 % of their pixels
+#endif
+constexpr int kActFast = VR_MARCH_ACT, kActBig = VR_MARCH_ACT_BIG, kBlockFast = VR_MARCH_BLOCK;
 constexpr int kActFallback = 64, kBlockFallback = 64;
 constexpr int kBlockSecondary = 256;
 
@@ -2532,6 +2554,10 @@ static hipError_t march_pass(const RenderArgs& A, hipStream_t stream) {
     const bool shallow = A.bvh_depth <= kShallowStack + 1;
     if (A.bin_ent != nullptr)  // binned march (its overflowing pixels re-run in the BVH fallback below)
         hipLaunchKernelGGL((dev::march_binned_kernel<S>), dim3(A.num_tiles * 4), dim3(64), 0, stream, A);
+    else if (H && A.hnodes4 != nullptr && A.march_big)  // translucent, densely overlapping scenes (C2): fewer
+        // pixels overflow, and their records come from coherent quarter tiles instead of the fallback queue
+        hipLaunchKernelGGL((dev::march_kernel<kActBig, kBlockFast, S, VR_MARCH_STACK4, true, true>), dim3(A.num_tiles * (256 / kBlockFast)),
+                           dim3(kBlockFast), 0, stream, A);
     else if (H && A.hnodes4 != nullptr)  // 4-wide tree; a query that could overflow the stack goes to the fallback
         hipLaunchKernelGGL((dev::march_kernel<kActFast, kBlockFast, S, VR_MARCH_STACK4, true, true>), dim3(A.num_tiles * (256 / kBlockFast)),
                            dim3(kBlockFast), 0, stream, A);

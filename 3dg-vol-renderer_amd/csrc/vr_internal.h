@@ -179,6 +179,7 @@ struct RenderArgs {
     int32_t* deep_act;     // march_deep_kernel's active lists, [slot][thread]
     int32_t* wide_act;     // march_wide_kernel's active lists, [slot][thread]
     uint32_t wide_min;     // fallback pixels from which the per-lane wide pass takes the queue (VR_OPT_MARCH_WIDE_MIN)
+    int32_t march_big;     // 1: the primary march with kActBig LDS slots (a scene whose earlier frame overflowed 16 often)
     uint32_t* counters;    // [0] = error pixels / paths, [2] = free-flight paths re-run in ff_fallback_kernel,
                            // [3] = the most shadow rays a free-flight launch of the frame tried to queue
     unsigned long long* work;  // instrumented build only: [0..7] march-kernel counters, [8..15] secondary-kernel counters

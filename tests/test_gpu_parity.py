@@ -290,14 +290,35 @@ def test_wide_fallback_pass_equals_the_wave_pass(case, device_options):
         out[wide_min] = (img.pixels.copy(), dict(integ.last_stats))
     a, b = out[0], out[1 << 31]
     assert a[1]["fallback_pixels"] > 0 and a[1]["error_pixels"] == 0
-    for k in ("fallback_pixels", "deep_pixels", "scatter_records", "secondary_rays"):
-        assert a[1][k] == b[1][k], k
+    # (fallback_pixels and the allocated records — re-marched pixels leave their first records orphaned —
+    # depend on the context's history: a frame re-rendered with grown record buffers marches with the big
+    # slots once the first attempt re-marched >= 5 % of its pixels)
+    assert a[1]["deep_pixels"] == b[1]["deep_pixels"]
     assert np.array_equal(a[0].view(np.uint32), b[0].view(np.uint32))
     if case == "c2_1000_random":
         pix = _tile_stratified(W, H, 1, seed=3)[:48]
         ref = _oracle_gmm(scene_path("1000_random.txt"), W, H, env_samples=3, pixels=pix)
         err, nm = _linf(a[0][pix[:, 1], pix[:, 0]], ref)
         assert nm == 0 and err < TOL, err
+
+
+def test_often_overflowing_scene_switches_to_the_big_march_identically():
+    """A frame that re-marched >= 5 % of its pixels (active sets past the primary march's 16 LDS slots)
+    makes the context's later frames march with 32 slots (march_big, until the next upload): fewer
+    pixels re-marched, the same frame bit for bit."""
+    scene = vr.Scene.load_GMM(scene_path("1000_random.txt"))
+    cam = vr.Pinhole_Camera(CAM_POS, main_view_dir(), FOV)
+    integ = vr.RayMarchingGaussians(cam, env_samples=2)
+    integ.render(scene, vr.Image(96, 96))  # sizes the record buffers (no re-render below)
+    vr.Device.get(0).upload(scene, force=True)  # a fresh upload: 16 slots again
+    frames, fb = [], []
+    for _ in range(2):
+        img = vr.Image(96, 96)
+        integ.render(scene, img)
+        frames.append(img.pixels.copy())
+        fb.append(integ.last_stats["fallback_pixels"])
+    assert fb[0] * 20 >= 96 * 96 and fb[1] < fb[0], fb
+    assert np.array_equal(frames[0].view(np.uint32), frames[1].view(np.uint32))
 
 
 def test_overflow_beyond_every_capacity_fails_loudly():
@@ -440,6 +461,7 @@ def _check_full_size(W, H, n, t_eps, stride, fallback_cap):
     assert np.isfinite(px).all() and (px >= 0).all()
     strat = _tile_stratified(W, H, stride, seed=11)
     assert len(strat) >= 2048
+    fb = fb[np.lexsort((fb[:, 0], fb[:, 1]))]  # (the queue's order varies run to run: a reproducible sample)
     fbs = fb if len(fb) <= fallback_cap else fb[np.random.default_rng(5).choice(len(fb), fallback_cap, replace=False)]
     pix = np.concatenate([strat, fbs]).astype(np.int32)
     got = px[pix[:, 1], pix[:, 0]]
@@ -454,7 +476,8 @@ def _check_full_size(W, H, n, t_eps, stride, fallback_cap):
     print(f"{W}x{H}/{n} t_eps={t_eps}: {len(strat)} stratified + {len(fbs)} of {len(fb)} fallback pixels, "
           f"L-inf {err:.3e} (fallback pixels vs the reference order {err_fb:.3e}); {ties} tangent-tie pixels held to "
           f"the stable order")
-    assert nm == 0 and untied == 0 and err < TOL, f"{W}x{H}/{n}: L-inf {err:.3e}, {untied} pixels over the bar"
+    worst = pix[int(np.argmax(d))].tolist()
+    assert nm == 0 and untied == 0 and err < TOL, f"{W}x{H}/{n}: L-inf {err:.3e}, {untied} pixels over the bar (worst {worst})"
     # a pixel whose centre ray misses everything is env colour exactly (test_integrators.h:172-176)
     env = np.array([0.53, 0.81, 0.92], np.float32)
     is_env = np.all(ref == env, axis=-1)
