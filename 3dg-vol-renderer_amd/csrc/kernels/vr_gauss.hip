@@ -635,7 +635,7 @@ __global__ __launch_bounds__(BLOCK) void march_kernel(RenderArgs A) {
 // The fallback passes march one pixel per wave (march<COOP>): a pixel lands here because its active
 // set is large, and its serial march was the tail of the whole march stage (~1 ms at C4, also for a
 // 1/8 multi-GPU share). BLOCK = one wave.
-template <int ACT, int BLOCK, bool S, bool H>
+template <int ACT, int BLOCK, bool S, bool H, bool W = false>
 __global__ __launch_bounds__(BLOCK) void march_fallback_kernel(RenderArgs A) {
     static_assert(BLOCK == 64, "one pixel per wave");
     __shared__ int s_act[ACT * BLOCK];
@@ -648,7 +648,9 @@ __global__ __launch_bounds__(BLOCK) void march_fallback_kernel(RenderArgs A) {
         int lx, ly, x, y;
         tile_pixel(A, p >> 8, (int)(p & 255u), lx, ly, x, y);
         Ctr c{};
-        int st = march<ACT, S, H, false, kStackSize, true>(A, p, x, y, s_act + tid, s_stack + tid, BLOCK, c);  // re-links px_first
+        // (W: the 4-wide walks — half the dependent node fetches of the pair tree on a single pixel's
+        // serial queries; a walk past the kStackSize stack goes to the deep pass)
+        int st = march<ACT, S, H, W, kStackSize, true>(A, p, x, y, s_act + tid, s_stack + tid, BLOCK, c);  // re-links px_first
         if (tid != 0) continue;
         if constexpr (S)
             for (int i = 0; i < kNumCtr; ++i) atomicAdd(A.work + i, (unsigned long long)c.v[i]);
@@ -2533,6 +2535,9 @@ __global__ __launch_bounds__(256) void accumulate_kernel(RenderArgs A) {
 #endif
 constexpr int kActFast = VR_MARCH_ACT, kActBig = VR_MARCH_ACT_BIG, kBlockFast = VR_MARCH_BLOCK;
 constexpr int kActFallback = 64, kBlockFallback = 64;
+#ifndef VR_FALLBACK_WIDE
+#define VR_FALLBACK_WIDE 1  // 1: the one-pixel-per-wave fallback march walks the 4-wide tree (A/B)
+#endif
 constexpr int kBlockSecondary = 256;
 
 hipError_t gauss_bin(const RenderArgs& A, bool emit, hipStream_t stream) {
@@ -2569,8 +2574,12 @@ static hipError_t march_pass(const RenderArgs& A, hipStream_t stream) {
                            dim3(kBlockFast), 0, stream, A);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL((dev::march_fallback_kernel<kActFallback, kBlockFallback, S, H>), dim3(1024), dim3(kBlockFallback), 0,
-                       stream, A);
+    if (H && A.hnodes4 != nullptr && VR_FALLBACK_WIDE)
+        hipLaunchKernelGGL((dev::march_fallback_kernel<kActFallback, kBlockFallback, S, H, true>), dim3(1024), dim3(kBlockFallback), 0,
+                           stream, A);
+    else
+        hipLaunchKernelGGL((dev::march_fallback_kernel<kActFallback, kBlockFallback, S, H>), dim3(1024), dim3(kBlockFallback), 0,
+                           stream, A);
     if ((e = hipGetLastError()) != hipSuccess) return e;
     if (H && A.hnodes4 != nullptr)  // (exactly one of the two passes takes the queue, by its length)
         hipLaunchKernelGGL((dev::march_wide_kernel<S, H, true>), dim3(kWideThreads / kWideBlock), dim3(kWideBlock), 0, stream, A);
