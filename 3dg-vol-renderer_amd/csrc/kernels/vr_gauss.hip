@@ -2439,6 +2439,9 @@ __global__ __launch_bounds__(256) void record_cut_kernel(RenderArgs A, float bud
 // record's lights and environment samples in the reference's order. Without env_order a chunk's
 // rays are sample-major ([sample][record-in-chunk]) and are read in place (coalesced).
 constexpr int kRadBlock = 64;
+#ifndef VR_RAD_UNROLL
+#define VR_RAD_UNROLL 1  // the chunk gather's loads in flight per lane (A/B at C4: 1: 1.59 ms, 4: 1.85, 12: 2.48)
+#endif
 template <bool ORDERED>
 __global__ __launch_bounds__(kRadBlock) void record_radiance_kernel(RenderArgs A) {
     extern __shared__ float s_tr[];  // ORDERED: [record-in-chunk][sample]
@@ -2447,6 +2450,7 @@ __global__ __launch_bounds__(kRadBlock) void record_radiance_kernel(RenderArgs A
     for (uint32_t chunk = blockIdx.x; chunk < nch; chunk += gridDim.x) {
         const float* tr = A.tr + (size_t)chunk * per;
         if constexpr (ORDERED) {
+#pragma unroll VR_RAD_UNROLL
             for (uint32_t i = threadIdx.x; i < per; i += kRadBlock) {
                 uint32_t s, rl;
                 if (i < nl * cr) {
