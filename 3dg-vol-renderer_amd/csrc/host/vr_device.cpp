@@ -108,7 +108,7 @@ struct vr_ctx {
         size_t bytes = 0;
     };
     Buf px_first, px_T, rec_pos, rec_meta, rec_next, rec_act, tr, rec_rad, rec_alloc, rec_bloom, slowq;
-    Buf pcg_jump, ray_next, stack_ovf, env_order, rec_cut, rec_start;
+    Buf pcg_jump, ray_next, stack_ovf, env_order, env_base, rec_cut, rec_start;
     Buf deep;  // march_deep_kernel: pixel queue + global active lists (vr_gauss.hip)
     Buf bin_cnt, bin_off, bin_ent;  // tile bins of the binned march (VR_OPT_MARCH_BINNED)
     Buf ff_scratch, ff_tail, ff_sum, ff_nee;  // free-flight integrators (vr_freeflight.hip)
@@ -578,6 +578,7 @@ vr_status fill_args(vr_ctx* c, const vr_camera* cam, const vr_render_params* p, 
     A.t_eps = p->t_eps;
     A.pure = p->integrator == VR_PURE_RAYMARCH ? 1 : 0;
     A.env_order = nullptr;  // set per frame by gauss_pipeline
+    A.env_base = nullptr;
     A.rec_cut = nullptr;
     A.chunk_rec = 64u;
     A.chunk_shift = 6u;
@@ -783,6 +784,7 @@ vr_status gauss_pipeline(vr_ctx* c, RenderArgs& A, hipStream_t s, bool stats) {
 #define VR_CHUNK_SHIFT 5  // 32-record chunks (A/B at C4: 8/16/32/64/128 -> 156.1/150.4/149.1/152.9/161.9 ms)
 #endif
         constexpr uint32_t shift = VR_CHUNK_SHIFT, cr = 1u << shift;  // entries hold record-in-chunk in 8 bits
+        static_assert(VR_CHUNK_SHIFT <= 8, "environment-order entries and env_order_kernel hold record-in-chunk in 8 bits");
         A.env_order = nullptr;
         A.chunk_rec = cr;
         A.chunk_shift = shift;
@@ -791,6 +793,8 @@ vr_status gauss_pipeline(vr_ctx* c, RenderArgs& A, hipStream_t s, bool stats) {
             if ((st = grow(c->env_order, nch * cr * (uint64_t)A.env_samples * 2ull, "hipMalloc(environment-ray order)")) != VR_OK)
                 return st;
             A.env_order = (uint16_t*)c->env_order.p;
+            if ((st = grow(c->env_base, nch * cr * 8ull, "hipMalloc(environment generator states)")) != VR_OK) return st;
+            A.env_base = (uint64_t*)c->env_base.p;
         }
     }
     HIP_TRY(gauss_secondary(A, s, stats), "secondary rays");
@@ -1095,7 +1099,7 @@ void vr_destroy(vr_ctx* c) {
         if (e) (void)hipEventDestroy(e);
     for (vr_ctx::Buf* b : {&c->px_first, &c->px_T, &c->rec_pos, &c->rec_meta, &c->rec_next, &c->rec_act, &c->tr, &c->rec_rad,
                            &c->rec_alloc, &c->rec_bloom, &c->slowq, &c->pcg_jump, &c->ray_next,
-                           &c->stack_ovf, &c->env_order, &c->rec_cut, &c->rec_start, &c->deep, &c->bin_cnt, &c->bin_off, &c->bin_ent,
+                           &c->stack_ovf, &c->env_order, &c->env_base, &c->rec_cut, &c->rec_start, &c->deep, &c->bin_cnt, &c->bin_off, &c->bin_ent,
                            &c->ff_scratch, &c->ff_tail, &c->ff_sum, &c->ff_nee, &c->ff_fb, &c->ff_slots, &c->rec_bits[0], &c->rec_bits[1],
                            &c->sfd_tmp, &c->sfd_ref, &c->sfd_loss[0], &c->sfd_loss[1], &c->sfd_out})
         if (b->p) (void)hipFree(b->p);

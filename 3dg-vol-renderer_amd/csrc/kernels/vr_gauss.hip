@@ -1088,12 +1088,18 @@ __device__ __forceinline__ int act_find(const RenderArgs& A, const SecRay& R, in
 
 // Direction of environment sample e of a record: PCG32 keyed by (pixel, step) as the oracle does;
 // the 2e draws of the earlier samples are skipped by LCG jump-ahead s -> M s + C (host table).
-__device__ __forceinline__ void env_sample_xi(const RenderArgs& A, const uint4& meta, uint32_t e, float& xi1, float& xi2) {
+// A record's environment samples all jump from one state: its path's seeded stream-1 generator.
+__device__ __forceinline__ uint64_t env_base_state(const uint4& meta) {
     const int px = (int)(meta.x & 0xffffu), py = (int)(meta.x >> 16);
-    PCG32 rng(derive_path_seed(px, py, (int)meta.y), 1);
-    rng.state = A.pcg_jump[4 * e] * rng.state + A.pcg_jump[4 * e + 1];
+    return PCG32(derive_path_seed(px, py, (int)meta.y), 1).state;
+}
+__device__ __forceinline__ void env_xi_at(const RenderArgs& A, uint64_t base, uint32_t e, float& xi1, float& xi2) {
+    PCG32 rng(PCG32::FromState{}, A.pcg_jump[4 * e] * base + A.pcg_jump[4 * e + 1], 1);
     xi1 = rng.uniform_env();
     xi2 = rng.uniform_env();
+}
+__device__ __forceinline__ void env_sample_xi(const RenderArgs& A, const uint4& meta, uint32_t e, float& xi1, float& xi2) {
+    env_xi_at(A, env_base_state(meta), e, xi1, xi2);
 }
 __device__ __forceinline__ void env_sample_dir(const RenderArgs& A, const uint4& meta, uint32_t e, float& wx, float& wy,
                                                float& wz) {
@@ -1128,23 +1134,48 @@ __device__ __forceinline__ uint32_t dir_key(float x, float y, float z) {
     return k;
 }
 
-// One workgroup per record chunk: counting sort of the chunk's environment rays by direction key
-// (order inside a key is arbitrary: every ray's result is independent of when it is traced).
+// One sorting group per record chunk: counting sort of the chunk's environment rays by direction key
+// (order inside a key is arbitrary: every ray's result is independent of when it is traced). A group
+// is one wave (VR_ENV_ORDER_WAVE: BLOCK/64 chunks in flight per workgroup, wave-local LDS and no
+// workgroup barriers; the chunk's chain of dependent loads is the cost, not its arithmetic) or the
+// whole workgroup.
+#ifndef VR_ENV_ORDER_WAVE
+#define VR_ENV_ORDER_WAVE 1  // A/B at C4: 1.56 ms; workgroup per chunk 1.91 (2.12 seeding every sample)
+#endif
 template <int BLOCK>
 __global__ __launch_bounds__(BLOCK) void env_order_kernel(RenderArgs A) {
-    constexpr uint32_t kKeyCap = 16384;  // keys kept in LDS; larger chunks recompute them
+    constexpr int G = VR_ENV_ORDER_WAVE ? 64 : BLOCK, kGroups = BLOCK / G;
+    constexpr uint32_t kKeyCap = 8192 / kGroups;  // keys kept in LDS per group; larger chunks recompute them
     using KeyT = typename std::conditional<(kEnvCells <= 256), uint8_t, uint16_t>::type;
     constexpr int kPer = kEnvCells / 64;  // counts per lane of the scan
-    __shared__ uint32_t hist[kEnvCells];
-    __shared__ KeyT keys[kKeyCap];
+    __shared__ uint32_t hist_s[kGroups][kEnvCells];
+    __shared__ KeyT keys_s[kGroups][kKeyCap];
+    __shared__ uint64_t base_s[kGroups][256];  // the chunk's generator states (record-in-chunk fits 8 bits)
+    const uint32_t grp = threadIdx.x / G, tid = threadIdx.x % G;
+    uint32_t* hist = hist_s[grp];
+    KeyT* keys = keys_s[grp];
+    uint64_t* base = base_s[grp];
+    auto group_sync = [] {
+        if constexpr (G == 64) {  // the wave's own LDS traffic: wait for it, keep the compiler from moving it
+            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+            __builtin_amdgcn_wave_barrier();
+        } else {
+            __syncthreads();
+        }
+    };
     const uint32_t nrec = dev_nrec(A);
     const uint32_t cr = A.chunk_rec, ne = (uint32_t)A.env_samples;
     const uint32_t n = cr * ne, nch = (nrec + cr - 1) / cr;
     const bool cached = n <= kKeyCap;
-    for (uint32_t chunk = blockIdx.x; chunk < nch; chunk += gridDim.x) {  // block-uniform loop
+    for (uint32_t chunk = blockIdx.x * kGroups + grp; chunk < nch; chunk += gridDim.x * kGroups) {  // group-uniform loop
         const uint32_t r0 = chunk * cr;
-        for (uint32_t i = threadIdx.x; i < kEnvCells; i += BLOCK) hist[i] = 0;
-        __syncthreads();
+        for (uint32_t i = tid; i < kEnvCells; i += G) hist[i] = 0;
+        for (uint32_t rl = tid; rl < cr; rl += G)  // seeded once per record, not per sample
+            if (r0 + rl < nrec) {
+                base[rl] = env_base_state(A.rec_meta[r0 + rl]);
+                A.env_base[r0 + rl] = base[rl];  // for sec_init: one 8-B load instead of the seeding per ray
+            }
+        group_sync();
         auto key = [&](uint32_t i) -> uint32_t {
             const uint32_t rl = i / ne, r = r0 + rl;
             if (r >= nrec) return kEnvCells - 1;  // padding records
@@ -1152,7 +1183,7 @@ __global__ __launch_bounds__(BLOCK) void env_order_kernel(RenderArgs A) {
             // the cell of the sample's (xi1, xi2) = (azimuth, cos polar) grid: equal-area direction
             // cells without evaluating the direction
             float xi1, xi2;
-            env_sample_xi(A, A.rec_meta[r], i - rl * ne, xi1, xi2);
+            env_xi_at(A, base[rl], i - rl * ne, xi1, xi2);
             const uint32_t cu = min((uint32_t)(xi1 * kEnvSide), (uint32_t)kEnvSide - 1u);
             const uint32_t cv = min((uint32_t)(xi2 * kEnvSide), (uint32_t)kEnvSide - 1u);
             uint32_t k = 0;
@@ -1160,19 +1191,20 @@ __global__ __launch_bounds__(BLOCK) void env_order_kernel(RenderArgs A) {
             for (int b = 0; b < kEnvBits; ++b) k |= (((cu >> b) & 1u) << (2 * b)) | (((cv >> b) & 1u) << (2 * b + 1));
             return k;
 #else
-            float wx, wy, wz;
-            env_sample_dir(A, A.rec_meta[r], i - rl * ne, wx, wy, wz);
+            float xi1, xi2, wx, wy, wz;
+            env_xi_at(A, base[rl], i - rl * ne, xi1, xi2);
+            env_dir(xi1, xi2, wx, wy, wz);
             return dir_key(wx, wy, wz);
 #endif
         };
-        for (uint32_t i = threadIdx.x; i < n; i += BLOCK) {
+        for (uint32_t i = tid; i < n; i += G) {
             const uint32_t k = key(i);
             if (cached) keys[i] = (KeyT)k;
             atomicAdd(&hist[k], 1u);
         }
-        __syncthreads();
-        if (threadIdx.x < 64) {  // exclusive scan of the counts by one wave (kPer consecutive per lane)
-            const uint32_t l = threadIdx.x;
+        group_sync();
+        if (tid < 64) {  // exclusive scan of the counts by one wave (kPer consecutive per lane)
+            const uint32_t l = tid;
             uint32_t v[kPer], sum = 0;
 #pragma unroll
             for (int j = 0; j < kPer; ++j) {
@@ -1192,13 +1224,14 @@ __global__ __launch_bounds__(BLOCK) void env_order_kernel(RenderArgs A) {
                 ex += v[j];
             }
         }
-        __syncthreads();
+        group_sync();
         uint16_t* out = A.env_order + (size_t)chunk * n;
-        for (uint32_t i = threadIdx.x; i < n; i += BLOCK) {
+        for (uint32_t i = tid; i < n; i += G) {
             const uint32_t rl = i / ne;
             out[atomicAdd(&hist[cached ? (uint32_t)keys[i] : key(i)], 1u)] = (uint16_t)((rl << 8) | (i - rl * ne));
         }
-        __syncthreads();  // hist / keys are reused by the next chunk
+        group_sync();  // hist / keys / base are reused by the group's next chunk (staging the order in LDS
+                       // for coalesced stores measured slower: 1.64 vs 1.56 ms at C4)
     }
 }
 
@@ -1287,7 +1320,9 @@ __device__ __forceinline__ bool sec_init(const RenderArgs& A, uint32_t nrec, uin
         }
     } else {
         float wx, wy, wz;
-        env_sample_dir(A, meta, s - (uint32_t)A.num_lights, wx, wy, wz);
+        float xi1, xi2;  // (env_order_kernel left the record's generator state when it ran)
+        env_xi_at(A, A.env_order != nullptr ? A.env_base[r] : env_base_state(meta), s - (uint32_t)A.num_lights, xi1, xi2);
+        env_dir(xi1, xi2, wx, wy, wz);
 #if VR_SEC_FAST_INIT
         R.ray = Ray{pos.x, pos.y, pos.z, wx, wy, wz};  // env_dir's direction is unit up to rounding
 #else
@@ -2672,7 +2707,8 @@ hipError_t gauss_secondary(const RenderArgs& A, hipStream_t stream, bool stats) 
         if (e != hipSuccess) return e;
     }
     if (A.env_order != nullptr) {
-        hipLaunchKernelGGL(dev::env_order_kernel<256>, dim3(record_grid(A, A.chunk_rec, 4096)), dim3(256), 0, stream, A);
+        hipLaunchKernelGGL(dev::env_order_kernel<256>, dim3(record_grid(A, A.chunk_rec * (VR_ENV_ORDER_WAVE ? 4 : 1), 4096)), dim3(256), 0,
+                           stream, A);
         hipError_t e = hipGetLastError();
         if (e != hipSuccess) return e;
     }

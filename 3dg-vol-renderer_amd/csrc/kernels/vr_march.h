@@ -355,6 +355,9 @@ struct PCG32 {
         state += seed_state;
         next_u32();
     }
+    struct FromState {};
+    // a generator already seeded: `s` is the state a seeding constructor left (stream seed_seq)
+    __device__ __forceinline__ PCG32(FromState, uint64_t s, uint64_t seed_seq) : state(s), inc((seed_seq << 1) | 1) {}
     __device__ __forceinline__ uint32_t next_u32() {
         uint64_t old = state;
         state = old * 6364136223846793005ULL + inc;

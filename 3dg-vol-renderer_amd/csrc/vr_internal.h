@@ -203,6 +203,7 @@ struct RenderArgs {
     int32_t* stack_ovf;             // persistent secondary kernel: traversal-stack entries past its LDS stack
     uint32_t stack_ovf_lanes;       // lanes (grid x block) the overflow buffer holds
     uint16_t* env_order;            // per record chunk: its environment rays (record-in-chunk << 8 | sample), direction order
+    uint64_t* env_base;             // with env_order: per record, the generator state its environment samples jump from
     uint32_t chunk_rec;             // records per secondary-ray chunk (power of 2; 64 without env_order)
     uint32_t chunk_shift;           // log2(chunk_rec)
     float* rec_cut;                 // per record: optical-depth cut-off of its secondary rays (nullptr: tau_cut)
