@@ -2477,6 +2477,9 @@ constexpr int kRadBlock = 64;
 #ifndef VR_RAD_UNROLL
 #define VR_RAD_UNROLL 1  // the chunk gather's loads in flight per lane (A/B at C4: 1: 1.59 ms, 4: 1.85, 12: 2.48)
 #endif
+#ifndef VR_RAD_VEC
+#define VR_RAD_VEC 1  // the chunk gather in 16-B Tr / 8-B order loads (A/B at C4: 0.96 vs 1.59 ms)
+#endif
 template <bool ORDERED>
 __global__ __launch_bounds__(kRadBlock) void record_radiance_kernel(RenderArgs A) {
     extern __shared__ float s_tr[];  // ORDERED: [record-in-chunk][sample]
@@ -2485,6 +2488,27 @@ __global__ __launch_bounds__(kRadBlock) void record_radiance_kernel(RenderArgs A
     for (uint32_t chunk = blockIdx.x; chunk < nch; chunk += gridDim.x) {
         const float* tr = A.tr + (size_t)chunk * per;
         if constexpr (ORDERED) {
+#if VR_RAD_VEC
+          if ((cr & 3u) == 0u) {  // four rays per load: the light rows and the env entries stay 4-aligned
+            const uint32_t nlc = nl * cr;
+            const uint16_t* ord = A.env_order + (size_t)chunk * (cr * ne);
+            for (uint32_t q = threadIdx.x; q < per / 4u; q += kRadBlock) {
+                const uint32_t i = 4u * q;
+                const float4 v = *reinterpret_cast<const float4*>(tr + i);
+                const float vv[4] = {v.x, v.y, v.z, v.w};
+                if (i < nlc) {
+                    const uint32_t s = i >> A.chunk_shift, rl = i & (cr - 1u);
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) s_tr[(rl + j) * S + s] = vv[j];
+                } else {
+                    const uint2 o = *reinterpret_cast<const uint2*>(ord + (i - nlc));
+                    const uint32_t e4[4] = {o.x & 0xffffu, o.x >> 16, o.y & 0xffffu, o.y >> 16};
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) s_tr[(e4[j] >> 8) * S + nl + (e4[j] & 0xffu)] = vv[j];
+                }
+            }
+          } else
+#endif
 #pragma unroll VR_RAD_UNROLL
             for (uint32_t i = threadIdx.x; i < per; i += kRadBlock) {
                 uint32_t s, rl;
