@@ -99,6 +99,8 @@ struct vr_ctx {
     std::vector<hipEvent_t> ff_ev;
     uint32_t ff_launches = 0;
     bool stats_pending = false;  // h_report of the last frame has not been collected yet
+    bool sync_pending = false;   // the last frame's outcome (retry / overflow) is collected but not yet reported by
+                                 // vr_synchronize: sticky, whoever collected it (vr_get_stats, an upload, ...)
     int64_t last_pixels = 0;
     uint32_t last_first_tile = 0, last_tile_stride = 1, last_tiles_x = 1, last_w = 0, last_h = 0;  // tile map of the last frame
     uint32_t last_secondary_per_record = 0;
@@ -126,6 +128,10 @@ struct vr_ctx {
     uint64_t rec_hint = 0, ovf_hint = 0;  // record / overflow-pool capacities (0: not known yet)
     uint64_t nee_hint = 0;                // deferred-NEE queue capacity from earlier free-flight frames (0: not known)
     uint32_t last_nee_cap = 0, last_nee_bound = 0;  // the last free-flight frame's queue capacity and its bound
+    // A launch found the shadow-ray queue full at its VR_OPT_FF_NEE_QUEUE bound: the frame is reported
+    // (VR_ERR_RETRY) and this context's later frames trace every shadow ray inline — the queue's own walk and
+    // sums, so the same frame bit for bit as a queue with room — until the next upload or option change.
+    bool nee_inline = false;
     bool report_ff = false;               // the last frame ran the free-flight pipeline (h_report[7])
     // vr_set_option values (explicit per-context tuning; no environment variables are read)
     int64_t opt_half_nodes = 1;        // VR_OPT_HALF_NODES
@@ -843,7 +849,7 @@ vr_status free_flight_pipeline(vr_ctx* c, RenderArgs& A, hipStream_t s) {
        // grown queue (as the ray-march's record buffers), so frames never depend on the capacity.
         const uint64_t bound = std::min<uint64_t>(paths * (uint64_t)c->opt_ff_nee_queue, kFFNone);
         const uint64_t first = paths * (A.ff_multi ? (uint64_t)A.ff_min_bounces + 1ull : 1ull) + 4096ull;
-        const uint64_t cap = std::min<uint64_t>(bound, c->nee_hint ? std::max<uint64_t>(c->nee_hint, 4096ull) : first);
+        const uint64_t cap = c->nee_inline ? 0ull : std::min<uint64_t>(bound, c->nee_hint ? std::max<uint64_t>(c->nee_hint, 4096ull) : first);
         const size_t bytes = (size_t)cap * 3 * sizeof(float4);
         A.ff_nee_cap = (uint32_t)cap;
         c->last_nee_cap = (uint32_t)cap;
@@ -925,6 +931,7 @@ vr_status collect(vr_ctx* c) {
     if (!c->stats_pending) return VR_OK;
     HIP_TRY(hipEventSynchronize(c->ev_report), "hipEventSynchronize");
     c->stats_pending = false;
+    c->sync_pending = true;
     if (c->report_gauss) {
         const uint64_t nrec = c->h_report[2], nact = c->h_report[3];
         c->rec_hint = std::max<uint64_t>(c->rec_hint, nrec + nrec / 8);
@@ -939,6 +946,9 @@ vr_status collect(vr_ctx* c) {
         const uint64_t need = c->h_report[7];
         const bool over = need > c->last_nee_cap;
         c->nee_hint = std::max<uint64_t>({c->nee_hint, need + need / 8, over ? 2ull * c->last_nee_cap : 0ull});
+        // full at the bound: a path that met it traced the rest inline and added them as one partial sum (float
+        // association); the frame is rendered again with every shadow ray inline, which is the queued frame
+        if (over && c->last_nee_cap >= c->last_nee_bound) c->nee_inline = true;
     }
     return VR_OK;
 }
@@ -946,7 +956,8 @@ vr_status collect(vr_ctx* c) {
 bool frame_exceeded(const vr_ctx* c) {
     if (c->report_gauss && c->h_report[4] != 0) return true;
     // the shadow-ray queue overflowed below its VR_OPT_FF_NEE_QUEUE bound: render again with a larger one
-    return c->report_ff && c->h_report[7] > c->last_nee_cap && c->last_nee_cap < c->last_nee_bound;
+    // (or at it: the next frame traces inline, see nee_inline). A frame traced inline queues nothing.
+    return c->report_ff && c->h_report[7] > c->last_nee_cap;
 }
 
 vr_status launch(vr_ctx* c, RenderArgs& A, const vr_render_params* p, hipStream_t s, bool stats = false) {
@@ -955,6 +966,7 @@ vr_status launch(vr_ctx* c, RenderArgs& A, const vr_render_params* p, hipStream_
     A.queue = c->d_queue;
     A.queue_cap = c->queue_cap;
     if ((st = collect(c)) != VR_OK) return st;  // the previous report must land before the pinned buffer is reused
+    c->sync_pending = false;  // vr_synchronize reports the last frame's outcome: this one's from here on
     HIP_TRY(hipMemsetAsync(c->d_queue, 0, sizeof(uint32_t), s), "hipMemsetAsync(queue)");
     HIP_TRY(hipMemsetAsync(c->d_counters, 0, 4 * sizeof(uint32_t), s), "hipMemsetAsync(counters)");
     HIP_TRY(hipEventRecord(c->ev_start, s), "hipEventRecord");
@@ -1002,8 +1014,10 @@ vr_status render_sync(vr_ctx* c, RenderArgs& A, const vr_render_params* p, bool 
         if (st != VR_OK) return st;
         if ((st = collect(c)) != VR_OK) return st;
         if (!frame_exceeded(c)) break;
-        if (attempt >= 3) return fail(VR_ERR_OVERFLOW, "scatter-record / shadow-ray queue capacity could not be sized");
+        // (the queue at most doubles per attempt up to its bound, then goes inline: a handful of attempts)
+        if (attempt >= 6) return fail(VR_ERR_OVERFLOW, "scatter-record / shadow-ray queue capacity could not be sized");
     }
+    c->sync_pending = false;  // reported here
     if (c->h_report[1] != 0)
         return fail(VR_ERR_OVERFLOW, std::to_string(c->h_report[1]) + std::string(" ") + what);
     return VR_OK;
@@ -1186,6 +1200,7 @@ vr_status vr_upload_scene(vr_ctx* c, const vr_scene* sc) {
     if (vr_status cs = collect(c); cs != VR_OK) return cs;  // the previous scene's last report, before the reset
     free_scene(c);
     c->march_big = false;
+    c->nee_inline = false;  // (nee_hint is kept: the inverse loop re-uploads every iteration and renders alike)
     c->type = s.type;
     c->lights.clear();
     for (const vr_light& l : s.lights)
@@ -1542,6 +1557,7 @@ vr_status vr_set_option(vr_ctx* c, int32_t option, int64_t value) {
         case VR_OPT_FF_NEE_QUEUE:
             if (value < 0 || value > (int64_t)kFFNeeMaxPerPath) return fail(VR_ERR_INVALID, "VR_OPT_FF_NEE_QUEUE must be in [0, 16]");
             c->opt_ff_nee_queue = value;
+            c->nee_inline = false;
             return VR_OK;
         case VR_OPT_DEVICE_BVH:
             if (value != 0 && value != 1) return fail(VR_ERR_INVALID, "VR_OPT_DEVICE_BVH must be 0 or 1");
@@ -1606,9 +1622,9 @@ vr_status vr_synchronize(vr_ctx* c) {
     if (c->group) return vr::group_synchronize(c->group);
     HIP_TRY(hipSetDevice(c->device), "hipSetDevice");
     HIP_TRY(hipDeviceSynchronize(), "hipDeviceSynchronize");
-    const bool pending = c->stats_pending;
     vr_status st = collect(c);
-    if (st != VR_OK || !pending) return st;
+    if (st != VR_OK || !c->sync_pending) return st;
+    c->sync_pending = false;  // (a frame that vr_get_stats or an upload collected first is still reported here)
     if (frame_exceeded(c))
         return fail(VR_ERR_RETRY, "the last frame outgrew the scatter-record buffers / shadow-ray queue sized from earlier frames; "
                                   "they have been grown: render it again");

@@ -304,11 +304,16 @@ vr_status group_set_option(vr_group* g, int32_t option, int64_t value) {
 }
 
 vr_status group_synchronize(vr_group* g) {
+    vr_status first = VR_OK;  // every rank is synchronised (and its sticky frame outcome cleared); the first failure is returned
+    std::string msg;
     for (vr_ctx* c : g->ranks) {
         vr_status st = vr_synchronize(c);
-        if (st != VR_OK) return st;
+        if (first == VR_OK && st != VR_OK) {
+            first = st;
+            msg = vr_last_error();
+        }
     }
-    return VR_OK;
+    return first == VR_OK ? VR_OK : fail(first, msg);
 }
 
 // Whole-group statistics of the last frame: counts summed over ranks, times the slowest rank's.

@@ -1807,7 +1807,9 @@ static unsigned resident_grid(const void* fn, unsigned block) {
 // The staged pipeline of one launch: the pool's first paths, then iterations of collect -> sweep -> shade
 // until every path of the launch is done. The host learns that from the collect queue's length, copied
 // to pinned memory every kPoll iterations and read one block of iterations later (the GPU keeps the
-// block in between queued; iterations past the end find empty queues and return at once).
+// block in between queued; iterations past the end find empty queues and return at once). The host
+// therefore waits on the device inside the launch: with VR_OPT_FF_STAGED the asynchronous entry points
+// (vr_render_tiles_device) return only once the frame's iterations are issued and mostly done.
 template <bool MULTI, bool CNT>
 static hipError_t ffs_run(RenderArgs A, hipStream_t stream, const FFPoll& poll) {
     constexpr int kPoll = 4, kMaxIters = 1 << 18;
@@ -1817,8 +1819,9 @@ static hipError_t ffs_run(RenderArgs A, hipStream_t stream, const FFPoll& poll) 
     hipLaunchKernelGGL((dev::ffs_start_kernel<CNT>), dim3((A.ff_pool + dev::kFFBlock - 1) / dev::kFFBlock), dim3(dev::kFFBlock), 0,
                        stream, A);
     if ((e = hipGetLastError()) != hipSuccess) return e;
-    static const unsigned g_collect = resident_grid((const void*)dev::ffs_collect_kernel<CNT>, dev::kFFBlock);
-    static const unsigned g_sweep = resident_grid((const void*)dev::ffs_sweep_kernel<MULTI, CNT>, dev::kFFBlock);
+    // (per call: the current device's CU count; two occupancy queries per launch)
+    const unsigned g_collect = resident_grid((const void*)dev::ffs_collect_kernel<CNT>, dev::kFFBlock);
+    const unsigned g_sweep = resident_grid((const void*)dev::ffs_sweep_kernel<MULTI, CNT>, dev::kFFBlock);
     const unsigned g_shade = std::max(1u, std::min(A.ff_pool / dev::kFFBlock, 4096u));
     int pending = -1;
     for (int it = 0; it < kMaxIters; ++it) {

@@ -589,15 +589,16 @@ __device__ __forceinline__ void mark_error(const RenderArgs& A, uint32_t p) {
 }
 
 // A pixel that overflowed a pass is marched again from its start by the next pass, which relinks it;
-// the records this pass already wrote for it are unreachable. Their weight T sigma_s (rec_pos.w, > 0 for
-// every live record) is zeroed so the secondary stage starts none of their rays (sec_init).
+// the records this pass already wrote for it are unreachable. Their weight T sigma_s (rec_pos.w, >= 0 for
+// every live record) is set to the sentinel -1 so the secondary stage starts none of their rays (sec_init).
 #ifndef VR_ORPHAN_SKIP
 #define VR_ORPHAN_SKIP 1
 #endif
+constexpr float kOrphanWeight = -1.0f;  // rec_pos.w of an orphaned record (a live record's T sigma_s is >= 0)
 __device__ __forceinline__ void orphan_records(const RenderArgs& A, uint32_t p) {
     if (!VR_ORPHAN_SKIP) return;
     for (uint32_t r = A.px_first[p]; r != kNoRecord && r < A.rec_cap; r = A.rec_next[r])
-        reinterpret_cast<float*>(A.rec_pos + r)[3] = 0.0f;
+        reinterpret_cast<float*>(A.rec_pos + r)[3] = kOrphanWeight;
 }
 
 template <int ACT, int BLOCK, bool S, int STACK, bool H, bool W = false>
@@ -1277,9 +1278,13 @@ __device__ __forceinline__ bool sec_init(const RenderArgs& A, uint32_t nrec, uin
     if (!ray_slot(A, chunk, rem, nrec, s, r)) return false;  // padding id
     R.slot = chunk * rays_per_chunk(A) + rem;
     const float4 pos = A.rec_pos[r];
-#if VR_ORPHAN_SKIP
-    if (!(pos.w > 0.0f)) return false;  // an orphaned record (orphan_records): no pixel reads its rays
-#endif
+    if (!(pos.w > 0.0f)) {  // no ray to trace
+        // a live record whose weight T sigma_s is 0 (an f32 underflow, or an over-capacity frame's empty
+        // record): its radiance is weighed by 0, but record_radiance reads every slot, so a finite Tr;
+        // an orphaned record (orphan_records, weight -1): no pixel reads its rays
+        if (!(pos.w < 0.0f)) A.tr[R.slot] = 0.0f;
+        return false;
+    }
     const uint4 meta = A.rec_meta[r];
     R.rec = r;
     R.cut = A.tau_cut;  // (a select of the two addresses would make this one flat load)
@@ -2055,25 +2060,31 @@ __global__ __launch_bounds__(BLOCK, WAVES) void secondary_ww_kernel(RenderArgs A
             // one primitive test; ls >= 0: list member ls (pre-activated: optical depth from 0).
             // RayMarchingGaussians: the whitened record (WRecord); PureRayMarching: the record itself
             // (its marched depth evaluates mu_t)
+            // The whitened primitive test (RayMarchingGaussians). The list phase sums the members' depths into
+            // `credit` (the cut-off sees them at once); the tree walk then sums every Gaussian it meets into
+            // tau, members included, so no membership lookup is needed. A member's p.M.p is <= cmax (the same
+            // bits the list phase took), so it is a candidate when the walk meets it again; a candidate's
+            // depth comes off the credit, which stays a lower bound of what the walk has still to meet. The
+            // walk sums every Gaussian from its entry max(t0, 0): for a member that holds the origin (and for
+            // any Gaussian that does) that is 0, the reference's pre-activation. A member whose chord starts
+            // ahead of the origin (t0 > 0: the march's camera-ray test can activate a Gaussian a few percent
+            // outside its ellipsoid) is pre-activated all the same: the list phase adds its stretch [0, t0]
+            // to tau at once and only [t0, t1] to the credit. (Until round 5 every candidate was summed from
+            // 0, so a non-member the origin lies just outside of, heading in, had [0, t0] too — with cmax > 9
+            // such Gaussians pass the c test, and for a dense one that stretch is worth ~0.1 of optical depth:
+            // C4 at t_eps 0, pixel (2224, 3653) 2.3e-3 dark.) Selects rather than fmaxf where an operand is
+            // not known canonical: fmaxf would canonicalise it first, one more VALU op each.
             auto wtest = [&](const WRec& g, uint32_t j, int ls) {
                 if constexpr (S) c.v[ls >= 0 ? kCtrMu : kCtrPrims]++;  // list members counted apart
                 const WQuad q = wquad(g, R.ray);
-                // The list phase sums the members' depths into `credit` (the cut-off sees them at
-                // once); the tree walk then sums every Gaussian it meets into tau, members included,
-                // so no membership lookup is needed. A member holds the origin: its p.M.p is <= cmax
-                // (the same bits the list phase took). Such a candidate is summed from t = 0, as the
-                // reference sums a pre-activated member (for a member, or any Gaussian holding the
-                // origin, that is its entry max(t0, 0) anyway), and its depth comes off the credit: the
-                // credit stays a lower bound of what the walk has still to meet.
-                // (selects rather than fmaxf where an operand is not known canonical: fmaxf would
-                // canonicalise it first, one more VALU op each; equal for every non-NaN operand)
                 R.cmax = (ls >= 0 && q.c > R.cmax) ? q.c : R.cmax;
                 const bool cand = ls < 0 && q.c <= R.cmax;
                 float t0, t1, sd;
                 if (!wintersect(q, t0, t1, sd)) return;
-                const bool pre = ls >= 0 || cand;  // active from t = 0
-                const float lo = pre ? 0.0f : fmaxf(t0, 0.0f);
-                const float u0 = (pre || q.hr > -sd) ? q.hr : -sd;  // erf argument x sqrt 2 at lo
+                const bool inside = q.hr > -sd;  // t0 < 0: the origin lies in the 3-sigma sphere
+                const bool pre = ls >= 0 || inside;
+                const float lo = pre ? 0.0f : t0;
+                const float u0 = pre ? q.hr : -sd;  // erf argument x sqrt 2 at lo
                 if (ls >= 0) R.hitmask |= slot_bit(ls);
                 if constexpr (S) {
                     c.v[kCtrOD]++;
@@ -2085,10 +2096,15 @@ __global__ __launch_bounds__(BLOCK, WAVES) void secondary_ww_kernel(RenderArgs A
                 const bool add = !R.light || t1 < R.lim;
                 R.needs_stop = R.needs_stop | (!add & (lo < R.lim));
                 R.lim = (!R.light && t1 > R.lim) ? t1 : R.lim;
-                if (add) {
-                    const float od = wod_chord(g, q, u0, sd);  // [lo, t1] lies on the 3-sigma chord
-                    if (ls >= 0) {
-                        R.credit += od;
+                if (add) {  // wod_chord over [lo, t1] (the 3-sigma chord, but for a member's stretch [0, t0])
+                    constexpr float kRs2 = 0.70710678118654752f;
+                    const float F1 = erf_chord(sd * kRs2), F0 = erf_chord(u0 * kRs2);
+                    const float pf = (g.dn * q.r) * __expf(-0.5f * q.e2);
+                    const float od = pf * fmaxf(F1 - F0, 0.0f);  // (f32 noise can invert a tiny interval)
+                    if (ls >= 0) {  // the credit takes the chord [max(t0, 0), t1] (erf_chord is odd), tau the rest
+                        const float chord = inside ? od : pf * (F1 + F1);
+                        R.credit += chord;
+                        R.tau += od - chord;  // + 0 when the origin lies inside
                     } else {
                         R.tau += od;
                         if (cand) R.credit -= od;

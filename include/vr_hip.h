@@ -354,9 +354,11 @@ typedef enum vr_option {
     VR_OPT_FF_NEE_QUEUE = 6,     /* free-flight integrators: shadow-ray queue capacity, in rays per path of a
                                     launch, 0..16 (default 6). The path kernel queues each bounce's next-event
                                     shadow ray for a separate tracing kernel; 0 traces them inline. Results
-                                    are identical (the same walk and sums) except for a path that meets a full
-                                    queue: its later contributions are traced inline and added after the
-                                    queued ones as one partial sum (float association only).
+                                    are identical (the same walk and sums). A frame whose launch found the
+                                    queue full is reported (VR_ERR_RETRY from the asynchronous entry points;
+                                    vr_render re-renders by itself) and rendered again with a grown queue, or,
+                                    once the queue is at this bound, with every shadow ray inline (so for the
+                                    context's later frames, until the next upload or a change of this option).
                                     Memory: the queue holds value x (paths of a launch, at most 2^23) rays
                                     of 48 B, 2.4 GB at the default 6 per path; it is grown, never shrunk,
                                     per context (lower it for many contexts on one device). */
@@ -379,7 +381,9 @@ typedef enum vr_option {
                                     bounce per lane and wave iteration); 1: the staged pipeline (a pool of path
                                     slots stepping through hit-collection, event-sweep and shading kernels,
                                     queued between them, each with per-lane refill; slower).
-                                    Frames are identical. */
+                                    Frames are identical. The staged pipeline is host-synchronous: the host
+                                    polls the path queue between iterations, so vr_render_tiles_device blocks
+                                    until the frame's iterations are issued. */
     VR_OPT_SEC_TIGHT = 11,       /* RayMarchingGaussians secondary rays, applied at the next upload: 1 (default):
                                     their own copy of the 4-wide tree with the exact boxes of the ellipsoids the
                                     whitened test accepts (the shared tree's boxes are padded by 5 % for the
@@ -394,7 +398,8 @@ typedef enum vr_option {
 vr_status vr_set_option(vr_ctx* ctx, int32_t option, int64_t value);
 vr_status vr_get_option(vr_ctx* ctx, int32_t option, int64_t* value);
 /* Waits for the context's device work; returns VR_ERR_RETRY / VR_ERR_OVERFLOW if the last frame is
- * invalid (see vr_render_tiles_device). */
+ * invalid (see vr_render_tiles_device). The outcome is reported once per frame, also when vr_get_stats
+ * (or any other call) collected the frame's report first; a later frame's call replaces it. */
 vr_status vr_synchronize(vr_ctx* ctx);
 vr_status vr_get_stats(vr_ctx* ctx, vr_render_stats* out);
 /* Diagnostics: the pixels of the last RayMarchingGaussians / PureRayMarching frame that were re-run

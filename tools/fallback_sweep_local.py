@@ -1,0 +1,59 @@
+"""Oracle sweep of EVERY fallback pixel of the C4 frame at exact settings, on a CPU, against the device
+values tools/c4_exact_dump.py saved (gpurun_out/<tag>_fallback.npz). Pixels over 1e-4 are re-rendered with
+the stable tie order: a pixel is tie-dependent iff the two oracle orders differ there.
+    python3 tools/fallback_sweep_local.py [tag] [threads]"""
+import os, sys, time
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "3dg-vol-renderer_amd"), os.path.join(ROOT, "tests"), os.path.join(ROOT, "oracle")]
+import numpy as np
+import pyoracle as O
+import vr_amd as vr
+from helpers import CAM_POS, FOV, main_view_dir
+
+TOL = 1e-4
+
+
+def c4_oracle_scene():
+    from test_gpu_parity import LIGHTS_1000 as L
+    scene = vr.Scene(vr.Scene.GAUSSIANS)
+    scene.add_random_gaussians(1_000_000, seed=2025, variant=0)
+    g = scene.gaussians()
+    return O.OracleScene.from_gaussians(g[:, 0:3], g[:, 3:9], g[:, 9], g[:, 10], np.array([l[0] for l in L], np.float32),
+                                        np.array([l[1] for l in L], np.float32))
+
+
+def main():
+    tag = sys.argv[1] if len(sys.argv) > 1 else "c4x"
+    nthreads = int(sys.argv[2]) if len(sys.argv) > 2 else (os.cpu_count() or 8)
+    d = np.load(os.path.join(ROOT, "gpurun_out", f"{tag}_fallback.npz"))
+    xy, got = d["xy"].astype(np.int32), d["rgb"].astype(np.float64)
+    print(tag, "fallback pixels", len(xy), "device NaN pixels", int(d["nan"]), flush=True)
+    osc = c4_oracle_scene()
+    ref = np.zeros_like(got)
+    t0 = time.time()
+    B = 4096
+    render = lambda p: O.render(osc, O.PINHOLE, CAM_POS, main_view_dir(), FOV, 4096, 4096, O.RAYMARCH_GAUSSIANS_LISTS, 0.01, 20,
+                                pixels=p, nthreads=nthreads)
+    for i in range(0, len(xy), B):
+        ref[i:i + B] = render(xy[i:i + B])
+        done = min(i + B, len(xy))
+        print(f"{done}/{len(xy)} {time.time() - t0:.0f} s", flush=True)
+    np.save(os.path.join(ROOT, "gpurun_out", f"{tag}_fallback_oracle.npy"), ref)
+    dd = np.abs(got - ref).max(axis=1)
+    bad = np.nonzero(dd >= TOL)[0]
+    print("over 1e-4 (reference order):", len(bad), "L-inf", float(dd.max()), flush=True)
+    if len(bad):
+        with O.stable_ties():
+            ref_s = render(xy[bad])
+        tie = np.any(ref_s != ref[bad], axis=1)
+        ds = np.abs(got[bad] - ref_s).max(axis=1)
+        for k, i in enumerate(bad):
+            print(xy[i].tolist(), "dev", got[i].tolist(), "orc", ref[i].tolist(), "d", float(dd[i]), "tie" if tie[k] else "NOT-TIE",
+                  "d_stable", float(ds[k]), flush=True)
+        nontie = int(np.sum(~tie | (ds >= TOL)))
+        print("non-tie pixels >= 1e-4:", nontie, "tie pixels:", int(np.sum(tie)), "max d vs stable order over tie pixels:",
+              float(ds[tie].max()) if tie.any() else 0.0, flush=True)
+
+
+if __name__ == "__main__":
+    main()

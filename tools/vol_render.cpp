@@ -197,7 +197,9 @@ int main(int argc, char** argv) try {
     std::printf("Render time: %.6f seconds (device %.3f ms, %lld pixels, %lld fallback, %d device(s)%s)\n",
                 std::chrono::duration<double>(t1 - t0).count(), st.kernel_ms, (long long)st.pixels,
                 (long long)st.fallback_pixels, vr_ctx_num_devices(integrator->context()),
-                vr_ctx_uses_rccl(integrator->context()) ? ", RCCL gather" : "");
+                !vr_ctx_uses_rccl(integrator->context()) ? ""
+                : vr_ctx_num_devices(integrator->context()) > 1 ? ", RCCL gather"
+                                                                : ", RCCL communicator (one rank: nothing to gather)");
     image.make_PPM(out);
     return 0;
 } catch (const std::exception& e) {
