@@ -753,7 +753,9 @@ vr_status gauss_pipeline(vr_ctx* c, RenderArgs& A, hipStream_t s, bool stats) {
     A.tr = (float*)c->tr.p;
     if ((st = grow(c->rec_rad, std::max<uint64_t>(cap, 1) * 16ull, "hipMalloc(record radiance)")) != VR_OK) return st;
     A.rec_rad = (float4*)c->rec_rad.p;
-    const uint64_t nslow = cap * (uint64_t)A.num_lights;
+    // exact slow path: light rays (stopping event / missed member) and the rare rays with a member at its
+    // 3-sigma boundary (light or environment): up to every light ray plus one ray per record
+    const uint64_t nslow = cap * (uint64_t)A.num_lights + cap;
     if ((st = grow(c->slowq, (nslow + 1) * 4ull, "hipMalloc(slow queue)")) != VR_OK) return st;
     A.slowq = (uint32_t*)c->slowq.p;
     A.slowq_cap = (uint32_t)nslow;
@@ -1651,6 +1653,61 @@ vr_status vr_get_fallback_pixels(vr_ctx* c, uint32_t* xy, size_t cap, size_t* n)
         xy[2 * i] = (tile % c->last_tiles_x) * kTile + (wv & 1u) * 8u + (ln & 7u);
         xy[2 * i + 1] = (tile / c->last_tiles_x) * kTile + (wv >> 1) * 8u + (ln >> 3);
     }
+    return VR_OK;
+}
+
+vr_status vr_debug_pixel_records(vr_ctx* c, uint32_t x, uint32_t y, float* out, size_t cap, size_t* n) {
+    c = first_device(c);
+    if (!c || !n || (cap > 0 && !out)) return fail(VR_ERR_INVALID, "vr_debug_pixel_records: bad argument");
+    if (!c->report_gauss) return fail(VR_ERR_INVALID, "vr_debug_pixel_records: the last frame was not a ray-march frame");
+    HIP_TRY(hipSetDevice(c->device), "hipSetDevice");
+    HIP_TRY(hipDeviceSynchronize(), "hipDeviceSynchronize");
+    vr_status st = collect(c);
+    if (st != VR_OK) return st;
+    // the pixel's tile-local index (vr_dev_common.h tile_pixel: wave = 8x8 quadrant, lane row-major)
+    const uint32_t tx = x / kTile, ty = y / kTile, g = ty * c->last_tiles_x + tx;
+    if (x >= c->last_w || y >= c->last_h || g < c->last_first_tile || (g - c->last_first_tile) % c->last_tile_stride)
+        return fail(VR_ERR_INVALID, "vr_debug_pixel_records: pixel not rendered by the last frame");
+    const uint32_t lx = x % kTile, ly = y % kTile;
+    const uint32_t lane = ((lx >> 3) + 2u * (ly >> 3)) * 64u + (ly & 7u) * 8u + (lx & 7u);
+    const uint32_t p = ((g - c->last_first_tile) / c->last_tile_stride) * 256u + lane;
+    const uint32_t nl = (uint32_t)c->lights.size(), S = c->last_secondary_per_record, ne = S - nl, cr = 1u << VR_CHUNK_SHIFT;
+    const size_t row = 9 + S;
+    uint32_t r = 0;
+    HIP_TRY(hipMemcpy(&r, (uint32_t*)c->px_first.p + p, 4, hipMemcpyDeviceToHost), "hipMemcpy");
+    size_t k = 0;
+    std::vector<uint16_t> ord(cr * ne);
+    for (; r != kNoRecord; ++k) {
+        float4 pos, rad;
+        uint4 meta;
+        uint32_t next = kNoRecord;
+        HIP_TRY(hipMemcpy(&pos, (float4*)c->rec_pos.p + r, 16, hipMemcpyDeviceToHost), "hipMemcpy");
+        HIP_TRY(hipMemcpy(&meta, (uint4*)c->rec_meta.p + r, 16, hipMemcpyDeviceToHost), "hipMemcpy");
+        HIP_TRY(hipMemcpy(&rad, (float4*)c->rec_rad.p + r, 16, hipMemcpyDeviceToHost), "hipMemcpy");
+        HIP_TRY(hipMemcpy(&next, (uint32_t*)c->rec_next.p + r, 4, hipMemcpyDeviceToHost), "hipMemcpy");
+        if (k < cap) {
+            float* o = out + k * row;
+            const float v[9] = {(float)meta.y, pos.x, pos.y, pos.z, pos.w, rad.x, rad.y, rad.z, (float)meta.w};
+            std::copy(v, v + 9, o);
+            // Tr slots: hand-out order within the record's chunk (vr_gauss.hip ray_slot / tr_slot)
+            const uint32_t chunk = r / cr, rl = r % cr;
+            const size_t base = (size_t)chunk * cr * S;
+            if (ne > 0 && c->env_order.p)
+                HIP_TRY(hipMemcpy(ord.data(), (uint16_t*)c->env_order.p + (size_t)chunk * cr * ne, ord.size() * 2,
+                                  hipMemcpyDeviceToHost), "hipMemcpy");
+            for (uint32_t s = 0; s < S; ++s) {
+                size_t rem = 0;
+                if (s < nl) rem = (size_t)s * cr + rl;
+                else if (c->env_order.p) {
+                    const uint16_t want = (uint16_t)((rl << 8) | (s - nl));
+                    rem = (size_t)nl * cr + (size_t)(std::find(ord.begin(), ord.end(), want) - ord.begin());
+                } else rem = (size_t)s * cr + rl;
+                HIP_TRY(hipMemcpy(o + 9 + s, (float*)c->tr.p + base + rem, 4, hipMemcpyDeviceToHost), "hipMemcpy");
+            }
+        }
+        r = next;
+    }
+    *n = k;
     return VR_OK;
 }
 

@@ -382,6 +382,16 @@ class Device:
                                            ctypes.byref(n)))
         return xy[:n.value].astype(np.int32)
 
+    def debug_pixel_records(self, x, y, rays_per_record):
+        """vr_debug_pixel_records: the scatter records of pixel (x, y) of the last ray-march frame, (n, 9 + S)
+        rows (S = rays_per_record = lights + env_samples): step k, position xyz, T * sigma_s, Li + Le rgb,
+        active-list length, then each secondary ray's Tr (lights, then environment samples)."""
+        n = ctypes.c_size_t()
+        check(lib().vr_debug_pixel_records(self._h, int(x), int(y), None, 0, ctypes.byref(n)))
+        out = np.zeros((max(n.value, 1), 9 + int(rays_per_record)), np.float32)
+        check(lib().vr_debug_pixel_records(self._h, int(x), int(y), fptr(out), n.value, ctypes.byref(n)))
+        return out[:n.value]
+
     OPTIONS = {"half_nodes": L.VR_OPT_HALF_NODES, "secondary_budget": L.VR_OPT_SECONDARY_BUDGET,
                "ff_window0": L.VR_OPT_FF_WINDOW0, "record_capacity": L.VR_OPT_RECORD_CAPACITY,
                "device_bvh": L.VR_OPT_DEVICE_BVH, "ff_nee_queue": L.VR_OPT_FF_NEE_QUEUE,

@@ -406,6 +406,12 @@ vr_status vr_get_stats(vr_ctx* ctx, vr_render_stats* out);
  * on the large-capacity fallback path (vr_render_stats.fallback_pixels of them). Writes up to `cap`
  * (x, y) pairs into xy[2*cap] (global frame coordinates, queue order) and the total count into *n. */
 vr_status vr_get_fallback_pixels(vr_ctx* ctx, uint32_t* xy, size_t cap, size_t* n);
+/* Diagnostics (slow: one copy per value): the scatter records of pixel (x, y) of the last
+ * RayMarchingGaussians frame in step order, one row of 9 + S floats each (S = lights + env_samples):
+ * step index k, record position xyz, T * sigma_s, Li + Le (rgb), active-list length, then the
+ * transmittance of each secondary ray (lights first, then environment samples, in sample order).
+ * Writes up to `cap` rows into out and the record count into *n. */
+vr_status vr_debug_pixel_records(vr_ctx* ctx, uint32_t x, uint32_t y, float* out, size_t cap, size_t* n);
 
 #ifdef __cplusplus
 } /* extern "C" */

@@ -78,6 +78,23 @@ def lib():
     return L
 
 
+def debug_pixel_records(scene, pos, view_dir, fov, x, y, W, H, step_size=0.01, env_samples=20):
+    """orc_debug_pixel_records (pinhole, RAYMARCH_GAUSSIANS_LISTS): the scattering steps of pixel (x, y), one
+    row of 9 + lights + env_samples floats each (the layout of vr_debug_pixel_records). Test tooling only."""
+    pos, pp = _f(pos)
+    vd, pv = _f(view_dir)
+    L = lib()
+    L.orc_debug_pixel_records.restype = ctypes.c_int64
+    L.orc_debug_pixel_records.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_float), ctypes.POINTER(ctypes.c_float),
+                                          ctypes.c_float, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                          ctypes.c_float, ctypes.c_int, ctypes.POINTER(ctypes.c_float), ctypes.c_int64]
+    row = 9 + scene.num_lights + int(env_samples)
+    out = np.zeros((4096, row), np.float32)
+    n = L.orc_debug_pixel_records(scene.h, pp, pv, float(fov), int(x), int(y), int(W), int(H), float(step_size),
+                                  int(env_samples), out.ctypes.data_as(ctypes.POINTER(ctypes.c_float)), out.shape[0])
+    return out[:min(n, out.shape[0])]
+
+
 def primary_depths(scene, cam_type, pos, view_dir, fov, W, H, step_size=0.01, t_eps=1e-6, nthreads=0):
     """(H, W) termination distance of every primary ray (-1: no events); see orc_primary_depths."""
     pos, pp = _f(pos)
@@ -111,6 +128,22 @@ class stable_ties:
 
     def __exit__(self, *exc):
         lib().orc_set_stable_ties(self._old)
+        return False
+
+
+class accurate_chords:
+    """Context manager: the sparse-list restatement computes secondary-ray chords (intersect and optical
+    depth) in double instead of the reference's f32 forms (see g_accurate_chords in vr_oracle.cpp)."""
+
+    def __enter__(self):
+        L = lib()
+        L.orc_set_accurate_chords.argtypes = [ctypes.c_int]
+        L.orc_set_accurate_chords.restype = ctypes.c_int
+        self._old = L.orc_set_accurate_chords(1)
+        return self
+
+    def __exit__(self, *exc):
+        lib().orc_set_accurate_chords(self._old)
         return False
 
 

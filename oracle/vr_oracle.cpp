@@ -36,6 +36,7 @@
 #include <stdexcept>
 #include <string>
 #include <vector>
+#include <map>
 #include <omp.h>
 
 namespace orc {
@@ -131,6 +132,14 @@ static bool g_pcg_textbook = false;
 // (test switch, orc_set_stable_ties) resolves ties in emission order (entry before exit: the Gaussian
 // is never active), which is the device path's rule; the default is the reference's std::sort.
 static bool g_stable_ties = false;
+// Secondary-ray chords in double (test switch, orc_set_accurate_chords; sparse-list restatement only). The
+// reference's f32 quadratic loses a chord that grazes a Gaussian seen from far away: from an origin at
+// whitened distance sqrt(c) the discriminant carries an absolute error ~c * 1e-7, so with c ~ 2700 a chord
+// of 9 - e2 = 3e-4 collapses to a point (C4 pixel (598, 3212): [0.32260, 0.32282] becomes
+// [0.3227114, 0.3227114], 0.078 of optical depth lost). The device computes the chord in whitened
+// coordinates (error linear in sqrt(c)); with this switch the restatement does so too, in double, so a
+// pixel that differs from the reference only through such a chord can be told apart (tests/helpers.py).
+static bool g_accurate_chords = false;
 struct PCG32 {
     uint64_t state, inc;
     PCG32(uint64_t seed_state, uint64_t seed_seq) {
@@ -303,6 +312,36 @@ struct Gaussian {
         t_exit = t1;
         return true;
     }
+    // intersect_direct / optical_depth in double (g_accurate_chords: secondary rays of the sparse-list restatement)
+    void quad_acc(const Ray& ray, double& A, double& B, double& C) const {
+        const double p[3] = {(double)ray.origin.x - mean.x, (double)ray.origin.y - mean.y, (double)ray.origin.z - mean.z};
+        const double d[3] = {ray.direction.x, ray.direction.y, ray.direction.z};
+        A = B = C = 0.0;
+        for (int i = 0; i < 3; ++i)
+            for (int j = 0; j < 3; ++j) {
+                A += d[i] * inv_cov(i, j) * d[j];
+                B += 2.0 * p[i] * inv_cov(i, j) * d[j];
+                C += p[i] * inv_cov(i, j) * p[j];
+            }
+    }
+    bool intersect_direct_acc(const Ray& ray, float& t_enter, float& t_exit) const {
+        double A, B, C;
+        quad_acc(ray, A, B, C);
+        const double disc = B * B - 4.0 * A * (C - 9.0);
+        if (disc < 0.0) return false;
+        const double t0 = (-B - std::sqrt(disc)) / (2.0 * A), t1 = (-B + std::sqrt(disc)) / (2.0 * A);
+        if (t1 < 0.0) return false;
+        t_enter = (float)std::max(t0, 0.0);
+        t_exit = (float)t1;
+        return true;
+    }
+    float optical_depth_acc(const Ray& ray, float t0, float t1) const {
+        double A, B, C;
+        quad_acc(ray, A, B, C);
+        const double pref = (double)density * (double)norm * std::sqrt(std::numbers::pi / (2.0 * A));
+        auto F = [&](double t) { return std::erf((B + 2.0 * A * t) / (2.0 * std::sqrt(2.0 * A))); };
+        return (float)(pref * std::exp(-0.5 * (C - B * B / (4.0 * A))) * (F(t1) - F(t0)));
+    }
     // gaussian.h:208-231
     float optical_depth(const Ray& ray, float t0, float t1) const {
         V3 p = ray.origin - mean;
@@ -415,7 +454,7 @@ struct GMM {
         }
     }
     // gmm.h:457-515
-    void intersect_events(const Ray& ray, std::vector<PrimitiveHitEvent>& out) const {
+    void intersect_events(const Ray& ray, std::vector<PrimitiveHitEvent>& out, bool acc = false) const {
         out.clear();
         if (gaussians.empty() || nodes.empty()) return;
         std::vector<int> stack;
@@ -432,7 +471,7 @@ struct GMM {
                 for (int ii = 0; ii < (int)node.count; ++ii) {
                     uint32_t gidx = indices[node.leftFirst + ii];
                     float t0, t1;
-                    if (gaussians[gidx].intersect_direct(ray, t0, t1)) {
+                    if (acc ? gaussians[gidx].intersect_direct_acc(ray, t0, t1) : gaussians[gidx].intersect_direct(ray, t0, t1)) {
                         if (t0 >= 0.0f) out.push_back({t0, true, gidx});
                         if (t1 >= 0.0f) out.push_back({t1, false, gidx});
                     }
@@ -471,9 +510,9 @@ struct GMM {
         sigma_a = (1.0f - a_mix) * sum_mu_t;
     }
     // gmm.h:146-157
-    float transmittance_over_segment(const Ray& ray, float t0, float t1, const std::vector<size_t>& act) const {
+    float transmittance_over_segment(const Ray& ray, float t0, float t1, const std::vector<size_t>& act, bool acc = false) const {
         float s = 0.0f;
-        for (size_t i : act) s += gaussians[i].optical_depth(ray, t0, t1);
+        for (size_t i : act) s += acc ? gaussians[i].optical_depth_acc(ray, t0, t1) : gaussians[i].optical_depth(ray, t0, t1);
         return std::exp(-s);
     }
 };
@@ -816,6 +855,10 @@ struct SparseSet {
     }
 };
 
+// DEBUG trace of one rm_gaussians_pixel_lists call (orc_debug_pixel_records): per scattering step a row
+// (k, pos xyz, T sigma_s, Li + Le rgb, #active, then every secondary ray's Tr: lights, then env samples)
+static thread_local std::vector<float>* g_rec_trace = nullptr;
+static thread_local std::vector<float>* g_rec_active = nullptr;  // with it: per row, #active then the active ids
 static V3 rm_gaussians_pixel_lists(const Scene& scene, const Camera& cam, int x, int y, int W, int H,
                                    float step_size, int env_samples) {
     const GMM& gmm = scene.gmm;
@@ -843,7 +886,7 @@ static V3 rm_gaussians_pixel_lists(const Scene& scene, const Camera& cam, int x,
         if (to_light) {
             while (t_prev < dist) {
                 float t_next = (ei < ev.size() ? ev[ei].t : dist);
-                Tr *= gmm.transmittance_over_segment(r, t_prev, t_next, mask.list);
+                Tr *= gmm.transmittance_over_segment(r, t_prev, t_next, mask.list, g_accurate_chords);
                 if (ei < ev.size()) {
                     mask.set(ev[ei].index, ev[ei].entering);
                     ++ei;
@@ -853,7 +896,7 @@ static V3 rm_gaussians_pixel_lists(const Scene& scene, const Camera& cam, int x,
         } else {
             while (ei < ev.size()) {
                 float t_next = ev[ei].t;
-                Tr *= gmm.transmittance_over_segment(r, t_prev, t_next, mask.list);
+                Tr *= gmm.transmittance_over_segment(r, t_prev, t_next, mask.list, g_accurate_chords);
                 mask.set(ev[ei].index, ev[ei].entering);
                 t_prev = t_next;
                 ++ei;
@@ -880,13 +923,15 @@ static V3 rm_gaussians_pixel_lists(const Scene& scene, const Camera& cam, int x,
         }
         if (sigma_s > 0.0f) {
             V3 Li{0, 0, 0};
+            std::vector<float> trs;
             for (const auto& light : scene.lights) {
                 V3 wi = normalized(light.position - pos);
                 float dist = norm(light.position - pos);
                 Ray shadow_ray(pos, wi);
                 std::vector<PrimitiveHitEvent> shadow_ev;
-                gmm.intersect_events(shadow_ray, shadow_ev);
+                gmm.intersect_events(shadow_ray, shadow_ev, g_accurate_chords);
                 float Tr = secondary(shadow_ray, shadow_ev, true, dist);
+                if (g_rec_trace) trs.push_back(Tr);
                 float d2 = dist * dist;
                 Li = Li + V3{(Tr * light.intensity.x) / d2, (Tr * light.intensity.y) / d2, (Tr * light.intensity.z) / d2};
             }
@@ -897,14 +942,23 @@ static V3 rm_gaussians_pixel_lists(const Scene& scene, const Camera& cam, int x,
                 float xi2 = rng.uniform_env();
                 Ray env_ray(pos, env_dir(xi1, xi2));
                 std::vector<PrimitiveHitEvent> env_ev;
-                gmm.intersect_events(env_ray, env_ev);
+                gmm.intersect_events(env_ray, env_ev, g_accurate_chords);
                 float Tr_env = secondary(env_ray, env_ev, false, 0.0f);
+                if (g_rec_trace) trs.push_back(Tr_env);
                 Le = Le + Tr_env * scene.env_color;
             }
             float fs = float(env_samples);
             Le = V3{(Le.x / fs) * k4Pi, (Le.y / fs) * k4Pi, (Le.z / fs) * k4Pi};
             float Ts = T * sigma_s;
             V3 S = Li + Le;
+            if (g_rec_trace) {
+                g_rec_trace->insert(g_rec_trace->end(), {(float)k, pos.x, pos.y, pos.z, Ts, S.x, S.y, S.z, (float)active.list.size()});
+                g_rec_trace->insert(g_rec_trace->end(), trs.begin(), trs.end());
+                if (g_rec_active) {
+                    g_rec_active->push_back((float)active.list.size());
+                    for (size_t i : active.list) g_rec_active->push_back((float)i);
+                }
+            }
             L = L + V3{((Ts * S.x) * step_size) * kInv4Pi, ((Ts * S.y) * step_size) * kInv4Pi, ((Ts * S.z) * step_size) * kInv4Pi};
         }
         T *= gmm.transmittance_over_segment(ray, t, t + step_size, active.list);
@@ -1691,6 +1745,113 @@ int64_t orc_tile_bins(void* sp, const float* pos, const float* vd, float fov, in
 
 // DEBUG: the faithful RayMarchingGaussians march of one pixel; out gets, per step with a non-empty
 // active set, (t, n_active, sigma_s, T after the step, active ids...). Returns the floats written.
+// DEBUG: the scattering steps of pixel (x, y) of RayMarchingGaussians (sparse-list restatement, pinhole), one
+// row of 9 + nlights + env_samples floats each (see g_rec_trace); the device side is vr_debug_pixel_records.
+// Returns the number of rows (writes at most cap).
+int64_t orc_debug_pixel_records(void* sp, const float* pos, const float* vd, float fov, int x, int y, int W, int H,
+                                float step_size, int env_samples, float* out, int64_t cap) {
+    Scene& s = *(Scene*)sp;
+    Camera c = Camera::make_pinhole({pos[0], pos[1], pos[2]}, {vd[0], vd[1], vd[2]}, fov);
+    std::vector<float> tr;
+    g_rec_trace = &tr;
+    rm_gaussians_pixel_lists(s, c, x, y, W, H, step_size, env_samples);
+    g_rec_trace = nullptr;
+    const size_t row = 9 + s.lights.size() + (size_t)env_samples;
+    const int64_t n = (int64_t)(tr.size() / row);
+    std::copy(tr.begin(), tr.begin() + (size_t)std::min(n, cap) * row, out);
+    return n;
+}
+
+// DEBUG: the active list (scene indices) of the scattering step k of pixel (x, y) (see orc_debug_pixel_records);
+// returns its length (-1: no such step).
+int64_t orc_debug_record_active(void* sp, const float* pos, const float* vd, float fov, int x, int y, int W, int H,
+                                float step_size, int env_samples, int k, int64_t* out, int64_t cap) {
+    Scene& s = *(Scene*)sp;
+    Camera c = Camera::make_pinhole({pos[0], pos[1], pos[2]}, {vd[0], vd[1], vd[2]}, fov);
+    std::vector<float> tr, act;
+    g_rec_trace = &tr;
+    g_rec_active = &act;
+    rm_gaussians_pixel_lists(s, c, x, y, W, H, step_size, env_samples);
+    g_rec_trace = nullptr;
+    g_rec_active = nullptr;
+    const size_t row = 9 + s.lights.size() + (size_t)env_samples;
+    size_t a = 0;
+    for (size_t r = 0; r * row < tr.size(); ++r) {
+        const int64_t n = (int64_t)act[a];
+        if ((int)tr[r * row] == k) {
+            for (int64_t i = 0; i < n && i < cap; ++i) out[i] = (int64_t)act[a + 1 + i];
+            return n;
+        }
+        a += 1 + (size_t)n;
+    }
+    return -1;
+}
+
+// DEBUG: one secondary ray of RayMarchingGaussians (test_integrators.h:202-271, the restatement's segment loop)
+// from origin o along d (normalised by the Ray constructor) with the primary active set `pre` pre-activated;
+// is_light: a light at distance dist. Per Gaussian ever active on the ray, a row (index, pre-activated,
+// M-form hit, t0, t1, optical depth it contributed over the ray's segments (double)); out_tr[0] = the ray's Tr.
+// Returns the row count (writes at most cap).
+int64_t orc_debug_secondary_ray(void* sp, const float* o, const float* d, int is_light, float dist, const int64_t* pre,
+                                int64_t npre, float* out, int64_t cap, float* out_tr) {
+    Scene& s = *(Scene*)sp;
+    const GMM& gmm = s.gmm;
+    Ray r({o[0], o[1], o[2]}, {d[0], d[1], d[2]});
+    std::vector<PrimitiveHitEvent> ev;
+    gmm.intersect_events(r, ev);
+    std::map<size_t, double> contrib;
+    std::vector<size_t> act;  // ascending
+    for (int64_t i = 0; i < npre; ++i) act.push_back((size_t)pre[i]);
+    std::sort(act.begin(), act.end());
+    for (size_t i : act) ev.insert(ev.begin(), {0.0f, true, i});
+    auto set = [&](size_t i, bool on) {
+        auto it = std::lower_bound(act.begin(), act.end(), i);
+        const bool has = it != act.end() && *it == i;
+        if (on && !has) act.insert(it, i);
+        if (!on && has) act.erase(it);
+    };
+    float t_prev = 0.0f, Tr = 1.0f;
+    size_t ei = 0;
+    auto segment = [&](float t_next) {
+        float sum = 0.0f;
+        for (size_t i : act) {
+            const float od = gmm.gaussians[i].optical_depth(r, t_prev, t_next);
+            contrib[i] += (double)od;
+            sum += od;
+        }
+        Tr *= std::exp(-sum);
+    };
+    if (is_light) {
+        while (t_prev < dist) {
+            const float t_next = ei < ev.size() ? ev[ei].t : dist;
+            segment(t_next);
+            if (ei < ev.size()) { set(ev[ei].index, ev[ei].entering); ++ei; }
+            t_prev = t_next;
+        }
+    } else {
+        while (ei < ev.size()) {
+            const float t_next = ev[ei].t;
+            segment(t_next);
+            set(ev[ei].index, ev[ei].entering);
+            t_prev = t_next;
+            ++ei;
+        }
+    }
+    out_tr[0] = Tr;
+    int64_t n = 0;
+    for (auto& [i, od] : contrib) {
+        if (n < cap) {
+            float a = NAN, b = NAN;
+            const bool hit = gmm.gaussians[i].intersect_direct(r, a, b);
+            const bool is_pre = std::binary_search(pre, pre + npre, (int64_t)i) || std::find(pre, pre + npre, (int64_t)i) != pre + npre;
+            float* row = out + 6 * n;
+            row[0] = (float)i; row[1] = is_pre ? 1.0f : 0.0f; row[2] = hit ? 1.0f : 0.0f; row[3] = a; row[4] = b; row[5] = (float)od;
+        }
+        ++n;
+    }
+    return n;
+}
+
 int64_t orc_debug_march(void* sp, const float* pos, const float* vd, float fov, int x, int y, int W, int H,
                         float step_size, int env_samples, float* L_out, float* out, int64_t cap) {
     Scene& s = *(Scene*)sp;
@@ -1707,6 +1868,8 @@ int64_t orc_debug_march(void* sp, const float* pos, const float* vd, float fov, 
 int orc_set_solver(int mode) { int o = g_solver; g_solver = mode; return o; }
 // event-sort tie order: 0 = the reference's std::sort (default), 1 = stable (see g_stable_ties)
 int orc_set_stable_ties(int on) { int o = g_stable_ties; g_stable_ties = on != 0; return o; }
+// secondary-ray chords: 0 = the reference's f32 forms (default), 1 = double (see g_accurate_chords)
+int orc_set_accurate_chords(int on) { int o = g_accurate_chords; g_accurate_chords = on != 0; return o; }
 // PCG32 output rotation: 0 = the reference's rng.h:43 (default), 1 = textbook PCG32 (see PCG32)
 int orc_set_pcg_textbook(int on) { int o = g_pcg_textbook; g_pcg_textbook = on != 0; return o; }
 

@@ -191,3 +191,32 @@ def test_tangent_hit_tie_order_depends_on_the_reference_sort():
                       pixels=pix)
     assert np.abs(ref[0] - st[0]).max() > 0.05
     assert np.array_equal(ref[1:], st[1:])
+
+
+def test_reference_f32_quadratic_collapses_a_grazing_chord_seen_from_far():
+    """The reference's f32 quadratic (gaussian.h:126-164) loses a chord that grazes a Gaussian seen from far
+    away: from an origin at whitened distance sqrt(c) the discriminant carries an absolute error ~c * 1e-7.
+    At C4 (4096^2, the seeded 1M make_random scene), environment ray 14 of step 529 of pixel (598, 3212)
+    starts at whitened distance sqrt(2735) from Gaussian 542385 and grazes it (9 - e2 = 3.3e-4): the f32
+    roots collapse to one point ([0.3227114, 0.3227114] for [0.32260, 0.32282] in double) and the reference
+    drops the chord's 0.078 of optical depth. The device's whitened chord keeps it, so that pixel is held
+    to the restatement with the secondary rays' chords in double (pyoracle.accurate_chords, tests/helpers.py
+    tie_aware_linf): it moves by 3.3e-4 there and by < 1e-6 on ordinary pixels."""
+    import vr_amd as vr
+    scene = vr.Scene(vr.Scene.GAUSSIANS)
+    scene.add_random_gaussians(1_000_000, seed=2025, variant=0)
+    lights = [((0.0, 5.0, 0.1), (50.0, 0.0, 0.0)), ((-3.0, 3.0, 0.3), (0.0, 30.0, 0.0)),
+              ((3.0, 3.0, -0.2), (0.0, 0.0, 30.0))]
+    g = scene.gaussians()
+    osc = O.OracleScene.from_gaussians(g[:, 0:3], g[:, 3:9], g[:, 9], g[:, 10],
+                                       np.array([l[0] for l in lights], np.float32),
+                                       np.array([l[1] for l in lights], np.float32))
+    pix = np.array([[598, 3212], [2224, 3653], [2048, 2048], [1000, 3000]], np.int32)
+    render = lambda: O.render(osc, O.PINHOLE, CAM_POS, main_view_dir(), FOV, 4096, 4096, O.RAYMARCH_GAUSSIANS_LISTS, 0.01,
+                              20, pixels=pix).astype(np.float64)
+    ref = render()
+    with O.accurate_chords():
+        acc = render()
+    d = np.abs(ref - acc).max(axis=1)
+    assert 2e-4 < d[0] < 5e-4  # the lost chord: 0.0893521 -> 0.0891608 (red)
+    assert np.all(d[1:] < 1e-6)

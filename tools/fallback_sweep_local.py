@@ -1,7 +1,7 @@
 """Oracle sweep of EVERY fallback pixel of the C4 frame at exact settings, on a CPU, against the device
 values tools/c4_exact_dump.py saved (gpurun_out/<tag>_fallback.npz). Pixels over 1e-4 are re-rendered with
 the stable tie order: a pixel is tie-dependent iff the two oracle orders differ there.
-    python3 tools/fallback_sweep_local.py [tag] [threads]"""
+    python3 tools/fallback_sweep_local.py [tag] [threads] [reuse-tag: an earlier sweep of the same pixels]"""
 import os, sys, time
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path[:0] = [ROOT, os.path.join(ROOT, "3dg-vol-renderer_amd"), os.path.join(ROOT, "tests"), os.path.join(ROOT, "oracle")]
@@ -29,16 +29,22 @@ def main():
     xy, got = d["xy"].astype(np.int32), d["rgb"].astype(np.float64)
     print(tag, "fallback pixels", len(xy), "device NaN pixels", int(d["nan"]), flush=True)
     osc = c4_oracle_scene()
-    ref = np.zeros_like(got)
-    t0 = time.time()
-    B = 4096
     render = lambda p: O.render(osc, O.PINHOLE, CAM_POS, main_view_dir(), FOV, 4096, 4096, O.RAYMARCH_GAUSSIANS_LISTS, 0.01, 20,
                                 pixels=p, nthreads=nthreads)
-    for i in range(0, len(xy), B):
-        ref[i:i + B] = render(xy[i:i + B])
-        done = min(i + B, len(xy))
-        print(f"{done}/{len(xy)} {time.time() - t0:.0f} s", flush=True)
-    np.save(os.path.join(ROOT, "gpurun_out", f"{tag}_fallback_oracle.npy"), ref)
+    reuse = sys.argv[3] if len(sys.argv) > 3 else None  # an earlier sweep's oracle values of the same pixel list
+    if reuse:
+        r = np.load(os.path.join(ROOT, "gpurun_out", f"{reuse}_fallback.npz"))
+        assert np.array_equal(r["xy"].astype(np.int32), xy), "the reused sweep has another pixel list"
+        ref = np.load(os.path.join(ROOT, "gpurun_out", f"{reuse}_fallback_oracle.npy")).astype(np.float64)
+    else:
+        ref = np.zeros_like(got)
+        t0 = time.time()
+        B = 4096
+        for i in range(0, len(xy), B):
+            ref[i:i + B] = render(xy[i:i + B])
+            done = min(i + B, len(xy))
+            print(f"{done}/{len(xy)} {time.time() - t0:.0f} s", flush=True)
+        np.save(os.path.join(ROOT, "gpurun_out", f"{tag}_fallback_oracle.npy"), ref)
     dd = np.abs(got - ref).max(axis=1)
     bad = np.nonzero(dd >= TOL)[0]
     print("over 1e-4 (reference order):", len(bad), "L-inf", float(dd.max()), flush=True)
@@ -50,9 +56,18 @@ def main():
         for k, i in enumerate(bad):
             print(xy[i].tolist(), "dev", got[i].tolist(), "orc", ref[i].tolist(), "d", float(dd[i]), "tie" if tie[k] else "NOT-TIE",
                   "d_stable", float(ds[k]), flush=True)
-        nontie = int(np.sum(~tie | (ds >= TOL)))
-        print("non-tie pixels >= 1e-4:", nontie, "tie pixels:", int(np.sum(tie)), "max d vs stable order over tie pixels:",
+        nontie = ~tie | (ds >= TOL)
+        print("non-tie pixels >= 1e-4:", int(nontie.sum()), "tie pixels:", int(np.sum(tie)), "max d vs stable order over tie pixels:",
               float(ds[tie].max()) if tie.any() else 0.0, flush=True)
+        if nontie.any():  # grazing chords the reference's f32 quadratic loses (g_accurate_chords)
+            rest = bad[nontie]
+            with O.accurate_chords():
+                ref_c = render(xy[rest])
+            chord = np.any(ref_c != ref[rest], axis=1)
+            dc = np.abs(got[rest] - ref_c).max(axis=1)
+            for k, i in enumerate(rest):
+                print(xy[i].tolist(), "chord-dependent" if chord[k] else "chord-independent", "d_accurate", float(dc[k]), flush=True)
+            print("unexplained pixels >= 1e-4:", int(np.sum(~chord | (dc >= TOL))), flush=True)
 
 
 if __name__ == "__main__":
