@@ -1687,7 +1687,7 @@ vr_status vr_debug_pixel_records(vr_ctx* c, uint32_t x, uint32_t y, float* out, 
         HIP_TRY(hipMemcpy(&next, (uint32_t*)c->rec_next.p + r, 4, hipMemcpyDeviceToHost), "hipMemcpy");
         if (k < cap) {
             float* o = out + k * row;
-            const float v[9] = {(float)meta.y, pos.x, pos.y, pos.z, pos.w, rad.x, rad.y, rad.z, (float)meta.w};
+            const float v[9] = {(float)meta.y, pos.x, pos.y, pos.z, pos.w, rad.x, rad.y, rad.z, (float)(meta.w & 0x7fffffffu)};
             std::copy(v, v + 9, o);
             // Tr slots: hand-out order within the record's chunk (vr_gauss.hip ray_slot / tr_slot)
             const uint32_t chunk = r / cr, rl = r % cr;

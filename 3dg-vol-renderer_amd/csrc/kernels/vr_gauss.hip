@@ -49,6 +49,17 @@ namespace dev {
 // exponentials reaches 0 or a denormal <= 1.4e-45 at the same point.)
 constexpr float kTauCut = 104.0f;
 
+// Band around a list member's 3-sigma surface (in p.M.p and in the chord's 9 - e2) inside which a secondary
+// ray's decision for that member is left to the exact slow path: ~10x the f32 difference between the
+// whitened and the reference's M forms for an origin near the Gaussian (~1e-7 relative, times the
+// covariance's condition number). The march marks a record whose members include one with p.M.p above
+// 9 - 2 kMemberAmb (kRecBoundary in the active count), so only the rays of such records (~1 %) test it.
+#ifndef VR_MEMBER_AMB
+#define VR_MEMBER_AMB 5e-5f  // (A/B: 0 removes the test)
+#endif
+constexpr float kMemberAmb = VR_MEMBER_AMB;
+constexpr uint32_t kRecBoundary = 0x80000000u;  // rec_meta.w: active count | this flag
+
 // Bit of active-list slot `slot` in a ray's 64-bit hit mask. Records with more than 64 active
 // Gaussians (march_deep_kernel) find their missed members by re-intersecting the whole list instead.
 __device__ __forceinline__ uint64_t slot_bit(int slot) { return slot < 64 ? 1ull << slot : 0ull; }
@@ -279,6 +290,7 @@ __device__ __forceinline__ bool march_step(const RenderArgs& A, const Ray& ray, 
     const float t_k1 = t_k + step;  // `t + step_size` (test_integrators.h:286)
     float smu = 0.0f, smua = 0.0f, tau_seg = 0.0f;
     int w = 0;
+    bool bnd = false;  // a member's 3-sigma surface passes within the band of the position (kRecBoundary)
     if constexpr (COOP) {
         const int lane = (int)__lane_id();
         for (int i0 = 0; i0 < act.n; i0 += 64) {  // (compaction writes stay below i0 + 64)
@@ -293,11 +305,14 @@ __device__ __forceinline__ bool march_step(const RenderArgs& A, const Ray& ray, 
                 float a, b;
                 if (intersect(q, a, b) && b > t_k) {
                     surv = true;
-                    m = mu_t(g, px_, py_, pz_);
+                    float ex;
+                    m = mu_t(g, px_, py_, pz_, &ex);
+                    bnd = bnd || -2.0f * ex > 9.0f - 2.0f * kMemberAmb;
                     ma = m * g.albedo;
                     if (!A.pure) od = optical_depth(g, q, t_k, t_k1);
                 }
             }
+            bnd = __ballot(bnd) != 0ull;
             for (uint64_t sm = __ballot(surv); sm; sm &= sm - 1) {  // survivors in list order
                 const int sl = __ffsll((unsigned long long)sm) - 1;
                 act.set(w++, __shfl(j, sl, 64));
@@ -319,7 +334,9 @@ __device__ __forceinline__ bool march_step(const RenderArgs& A, const Ray& ray, 
             float a, b;
             if (!intersect(q, a, b) || b <= t_k) continue;
             act.set(w++, j);
-            float m = mu_t(g, px_, py_, pz_);
+            float ex;
+            float m = mu_t(g, px_, py_, pz_, &ex);
+            bnd = bnd || -2.0f * ex > 9.0f - 2.0f * kMemberAmb;
             smu += m;
             smua += m * g.albedo;
             if (!A.pure) tau_seg += optical_depth(g, q, t_k, t_k1);
@@ -373,7 +390,8 @@ __device__ __forceinline__ bool march_step(const RenderArgs& A, const Ray& ray, 
             }
             if (writer) {
                 A.rec_pos[r] = make_float4(px_, py_, pz_, T * sigma_s);
-                A.rec_meta[r] = make_uint4((uint32_t)px | ((uint32_t)py << 16), (uint32_t)k, aoff, (uint32_t)w);
+                A.rec_meta[r] = make_uint4((uint32_t)px | ((uint32_t)py << 16), (uint32_t)k, aoff,
+                                           (uint32_t)w | (bnd && kMemberAmb > 0.0f ? kRecBoundary : 0u));
                 A.rec_bloom[r] = bl;
                 A.rec_next[r] = kNoRecord;
                 if (prev == kNoRecord) A.px_first[p] = r;
@@ -498,7 +516,7 @@ __device__ int march(const RenderArgs& A, uint32_t p, int px, int py, int* act_b
     }
     if (A.num_prims > 0) {
         for (;;) {
-            const float t_lo = (kq == 0) ? -1.0f : ts[kq - 1];
+            float t_lo = (kq == 0) ? -1.0f : ts[kq - 1];
             int k;
             float pmin = INFINITY;  // the earliest pending entry (pending: every entry of (t_lo, ts[pend_k]])
             if constexpr (kLook) {
@@ -529,6 +547,10 @@ __device__ int march(const RenderArgs& A, uint32_t p, int px, int py, int* act_b
                 if (!ok) return kOverflow;
                 if (best == INFINITY) break;
                 k = kfirst(ts, nts, step, best);
+                // No entry lies in (t_lo, best) and ts[k - 1] < best: the step's entrant window (t_lo, t_k] holds
+                // exactly the entries of (ts[k - 1], t_k]. The short window keeps the query local to the step
+                // (from t_lo = -1 the first query of every pixel walked every box along [0, t_k]). Same set.
+                if (k > kq) t_lo = ts[k - 1];
             } else {
                 k = kq;
             }
@@ -1098,6 +1120,7 @@ struct SecRay {
     float credit;      // RayMarchingGaussians: list members' optical depth not yet met again by the tree walk
     uint32_t act_off, act_n;  // the record's active list
     bool light, needs_stop;
+    bool bnd;          // the record has a member at its 3-sigma surface (kRecBoundary): the list phase tests the band
     uint32_t nsteps;  // instrumented build only: node steps taken by this ray
     int32_t from;     // 4-wide walk: root of the subtree the ray walks / has finished (climbs from the record's start subtree)
 #ifdef VR_DIAG_LEVELS  // diagnostic builds only: this ray's node steps per tree depth (2 levels per bucket)
@@ -1339,7 +1362,8 @@ __device__ __forceinline__ bool sec_init(const RenderArgs& A, uint32_t nrec, uin
     R.cut = A.tau_cut;  // (a select of the two addresses would make this one flat load)
     if (A.rec_cut != nullptr) R.cut = __builtin_nontemporal_load(A.rec_cut + r);
     R.act_off = meta.z;
-    R.act_n = meta.w;
+    R.act_n = meta.w & ~kRecBoundary;
+    R.bnd = (meta.w & kRecBoundary) != 0u;
     R.bloom = A.rec_bloom[r];
     R.cmax = -INFINITY;
     R.credit = 0.0f;
@@ -1949,13 +1973,7 @@ __device__ __forceinline__ void sec_node(const RenderArgs& A, SecRay& R, LdsInt*
 // point query per record; the active list is a subset the march already holds: no list stage
 // (-6.1 ms at C4) and a 2.4 % faster secondary stage)
 constexpr int kNodeList = -2;
-// Band around a list member's 3-sigma surface (in p.M.p and in the chord's 9 - e2) inside which the secondary
-// ray is decided by the exact slow path: ~10x the f32 difference between the whitened and the reference's
-// M forms for an origin near the Gaussian (a few 1e-7 relative, times the covariance's condition number).
-#ifndef VR_MEMBER_AMB
-#define VR_MEMBER_AMB 5e-4f  // (A/B: 0 removes the test)
-#endif
-constexpr float kMemberAmb = VR_MEMBER_AMB;
+
 
 // Start ray R's list phase (or go straight to the tree).
 __device__ __forceinline__ void list_begin(SecRay& R, LeafQueue& Q, int& node) {
@@ -2170,8 +2188,8 @@ __global__ __launch_bounds__(BLOCK, WAVES) void secondary_ww_kernel(RenderArgs A
                 // (active to the ray's last event — for a dense Gaussian ~1 of optical depth) is a rounding
                 // decision the whitened form cannot reproduce: the exact slow path decides the ray (C4 at
                 // t_eps 0, pixel (470, 3144): c = 9.00000, t1 = -0.00000 in the reference, 2.6e-2 bright).
-                if (kMemberAmb > 0.0f && ls >= 0 && (fabsf(q.c - 9.0f) < kMemberAmb || fabsf(9.0f - q.e2) < kMemberAmb))
-                    R.needs_stop = true;
+                if (__builtin_expect(R.bnd, false))  // (~1 % of the records: rarely taken by a wave)
+                    if (ls >= 0 && (fabsf(q.c - 9.0f) < kMemberAmb || fabsf(9.0f - q.e2) < kMemberAmb)) R.needs_stop = true;
                 float t0, t1, sd;
                 if (!wintersect(q, t0, t1, sd)) return;
                 const bool inside = q.hr > -sd;  // t0 < 0: the origin lies in the 3-sigma sphere
@@ -2297,7 +2315,7 @@ __global__ __launch_bounds__(BLOCK) void secondary_slow_kernel(RenderArgs A) {
         ray_slot(A, chunk, rem, dev_nrec(A), s, r);
         const float4 pos = A.rec_pos[r];
         const uint4 meta = A.rec_meta[r];
-        ActList act{A.rec_act + meta.z, 1, (int)meta.w, A.rec_bloom[r]};
+        ActList act{A.rec_act + meta.z, 1, (int)(meta.w & ~kRecBoundary), A.rec_bloom[r]};
         if (s < (uint32_t)A.num_lights) {  // test_integrators.h:202-237
             const LightRecord& lr = A.lights[s];
             float dx = lr.px - pos.x, dy = lr.py - pos.y, dz = lr.pz - pos.z;
@@ -2501,7 +2519,7 @@ __global__ __launch_bounds__(256) void record_start_kernel(RenderArgs A) {
     for (uint32_t r = blockIdx.x * 256u + threadIdx.x; r < nrec; r += gridDim.x * 256u) {
         if (VR_START_FROM_MEMBER && A.prim_node4 != nullptr) {
             const uint4 meta = A.rec_meta[r];
-            if (meta.w > 0u) {
+            if ((meta.w & ~kRecBoundary) > 0u) {
                 A.rec_start[r] = A.prim_node4[A.rec_act[meta.z]];
                 continue;
             }

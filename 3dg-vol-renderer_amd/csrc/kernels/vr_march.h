@@ -329,13 +329,15 @@ __device__ __forceinline__ float wod_range(const WRec& g, const WQuad& q, float 
 
 // Gaussian::mu_t = density * evaluate(x) (gaussian.h:111-117), exponent -0.5 d^T M d with
 // Eigen's lazy-product order.
-__device__ __forceinline__ float mu_t(const GRec& g, float x, float y, float z) {
+// ex_out: the exponent -0.5 d^T M d (the march's record flag reads p.M.p = -2 ex off it).
+__device__ __forceinline__ float mu_t(const GRec& g, float x, float y, float z, float* ex_out = nullptr) {
     float d0 = x - g.mx, d1 = y - g.my, d2 = z - g.mz;
     float l0 = -0.5f * d0, l1 = -0.5f * d1, l2 = -0.5f * d2;
     float w0 = l0 * g.m00 + (l1 * g.m01 + l2 * g.m02);
     float w1 = l0 * g.m01 + (l1 * g.m11 + l2 * g.m12);
     float w2 = l0 * g.m02 + (l1 * g.m12 + l2 * g.m22);
     float ex = w0 * d0 + (w1 * d1 + w2 * d2);
+    if (ex_out) *ex_out = ex;
     return g.density * (g.norm * expf(ex));
 }
 

@@ -12,6 +12,8 @@ from helpers import CAM_POS, FOV, main_view_dir
 # the round-4 sweep's flagged non-tie / tie pixels and their reference-order oracle values
 FLAGGED = {
     (2224, 3653): (0.12168200314044952, 0.18596678972244263, 0.21122156083583832),
+    (470, 3144): (0.036182958632707596, 0.05529847741127014, 0.06280815601348877),
+    (598, 3212): (0.08916076, 0.13626456, 0.15476963),  # the accurate-chord oracle (the reference's f32: 0.0893521)
     (1551, 3645): (0.010016418062150478, 0.015308110974729061, 0.017386989668011665),
     (3322, 641): (0.020930394530296326, 0.03198796510696411, 0.03633200749754906),
     (2198, 1218): (0.0056490227580070496, 0.008633414283394814, 0.009805853478610516),
