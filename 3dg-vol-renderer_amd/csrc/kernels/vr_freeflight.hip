@@ -25,6 +25,9 @@
 #include <type_traits>
 
 #include "vr_dev_common.h"
+#ifndef VR_SOLVE_ATTR
+#define VR_SOLVE_ATTR  // (A/B) __noinline__: the double-precision analytic solver's registers stay out of the path kernels
+#endif
 
 namespace vr {
 namespace dev {
@@ -64,6 +67,9 @@ struct FFCount<true> {
     __device__ __forceinline__ void add(int k, uint32_t n = 1) {
 #ifdef VR_DIAG_FF_CYCLES  // these slots hold phase cycles in the diagnostic build (FFScratch::lap)
         if (k == kFFErf || k == kFFNode2 || k == kFFNeeInline || k == kFFNeeQueued) return;
+#endif
+#ifdef VR_DIAG_FFSM  // every slot holds ff_path_sm_kernel's per-phase wave statistics in this diagnostic build
+        return;
 #endif
         v[k] += n;
     }
@@ -203,7 +209,7 @@ __device__ __forceinline__ double erfinv_approx(double x) {
 }
 
 // gaussian.h:235-297 (double)
-__device__ bool solve_for_t_given_tau(const GRec& g, const Ray& r, float t0, float tb, float target_tau, float& t_out) {
+__device__ VR_SOLVE_ATTR bool solve_for_t_given_tau(const GRec& g, const Ray& r, float t0, float tb, float target_tau, float& t_out) {
     Quad q = quad(g, r);
     double Ad = (double)q.A;
     if (!(Ad > 0.0) || !isfinite(Ad)) return false;
@@ -503,15 +509,10 @@ __device__ float free_flight_distance(const RenderArgs& A, SC& S, const Ray& r, 
         int n = 0;
         float t_cut = INFINITY;
         float kfull = INFINITY;  // largest kept key while the buffer is full
-        bool pruned_full = false;
         auto prune = [&](float tmin, float tmax) {
             if (tmax < W0 - kTPad * (1.0f + W0)) return false;
             const float lim = fminf(t_cut, kfull);
-            if (tmin > lim + kTPad * (1.0f + fminf(lim, 1e30f))) {
-                pruned_full |= n == cap;
-                return false;
-            }
-            return true;
+            return !(tmin > lim + kTPad * (1.0f + fminf(lim, 1e30f)));
         };
         auto prim = [&](uint32_t j) {
             S.C.add(kFFPrims);
@@ -548,7 +549,6 @@ __device__ float free_flight_distance(const RenderArgs& A, SC& S, const Ray& r, 
         auto reset = [&]() {
             n = 0;
             t_cut = kfull = INFINITY;
-            pruned_full = false;
         };
         S.lap(kFFErf);  // (diagnostic builds: bounce setup / window bookkeeping, with the rest of the bounce)
         if (A.hnodes4 == nullptr || !collect_walk(A, r, stack, stack + kStackSize * kFFBlock, prune, prim, &S.C)) {
@@ -557,9 +557,10 @@ __device__ float free_flight_distance(const RenderArgs& A, SC& S, const Ray& r, 
             if (A.hnodes) traverse<true>(A, r, stack, stride, prune, leaf, on2);
             else traverse<false>(A, r, stack, stride, prune, leaf, on2);
         }
-        // skipped subtrees only hold keys beyond the (final) largest kept key
+        // a buffer that filled ends the window at its largest kept key (subtrees skipped while full hold
+        // only larger keys; whether one was skipped depends on the wave's NODE/PRIM schedule, so the cut must not)
         S.lap(kFFNode2);  // (diagnostic builds: hit collection)
-        if (pruned_full && n > 0) t_cut = fminf(t_cut, S.K(n - 1));
+        if (n == cap) t_cut = fminf(t_cut, S.K(n - 1));
         while (n > 0 && S.K(n - 1) >= t_cut) --n;  // entries past the window (t_cut fell after they were kept)
         if (t_cut <= W0) {  // more than cap Gaussians overlap at W0: no progress possible at this cap
             if (cap >= A.ff_hit_cap) return -2.0f;
@@ -894,6 +895,434 @@ __global__ void __launch_bounds__(kFFBlock, VR_FF_WAVES) ff_path_kernel(RenderAr
     }
 }
 
+// Phase-scheduled persistent path kernel. ff_path_kernel runs a whole bounce per wave iteration, so a
+// wave waits at every phase for its slowest lane (the hit collection of one lane's second window, the
+// event sweep of the lane with the most events, the shading of the lanes that scattered). Here every
+// lane carries its path's bounce as a state (COLLECT: the resumable while-while walk of the window's hit
+// collection; SWEEP: the window's events, one (or a budget of) per iteration; SHADE: the distance solver,
+// the albedo and the rest of the bounce), and each wave iteration runs the ONE phase most of the wave's
+// lanes are in, with those lanes only. Every path runs ff_bounce's operations in ff_bounce's order (the
+// same RNG draws, sums and decisions), so frames are the persistent kernel's, bit for bit.
+#ifndef VR_FF_SM
+#define VR_FF_SM 0  // 1: the path kernel is ff_path_sm_kernel (A/B)
+#endif
+#ifndef VR_FFSM_EVENT_BUDGET
+#define VR_FFSM_EVENT_BUDGET 0  // active-entry evaluations a lane may spend on events per SWEEP iteration (0: one event)
+#endif
+#ifndef VR_FFSM_SHADE_MIN
+#define VR_FFSM_SHADE_MIN 1  // SHADE runs when it has the most lanes and at least this many (or nothing else is left)
+#endif
+#ifndef VR_FFSM_WAVES
+#define VR_FFSM_WAVES 4  // waves per SIMD of the phase-scheduled path kernel (launch bounds)
+#endif
+enum : int { kSmIdle = 0, kSmCollect = 1, kSmSweep = 2, kSmShade = 3 };
+template <bool MULTI, bool CNT = false>
+__global__ void __launch_bounds__(kFFBlock, VR_FFSM_WAVES) ff_path_sm_kernel(RenderArgs A) {
+    using Acc = typename std::conditional<MULTI, double, float>::type;
+    __shared__ int s_stack[(kStackSize + kCollectQueue) * kFFBlock];  // walk stack + the walks' leaf FIFO
+    int* stack = s_stack + threadIdx.x;
+    int* ring = stack + kStackSize * kFFBlock;
+    const uint32_t gt = blockIdx.x * kFFBlock + threadIdx.x;
+    FFScratch<CNT> S{A.ff_hit + gt, A.ff_act0 + gt, A.ff_act1 + gt, A.ff_threads, 0, {}};
+    const uint32_t lane = threadIdx.x & 63u;
+    FFPath P{PCG32(0, 1)};
+    int phase = kSmIdle;
+    bool exhausted = false;
+    // the bounce (free_flight_distance's state across windows)
+    float target = 0.0f, t_prev = 0.0f, W0 = 0.0f;
+    Acc acc = 0;
+    int cap = 0;
+    // the window's hit collection (ffs_collect_kernel's walk state); in SHADE, t_cut holds ts (m < 0) or
+    // the scatter segment's end t_evt, and kfull the target left on that segment
+    int n = 0, sp = 0, node = -1, qh = 0, qn = 0;
+    float t_cut = INFINITY, kfull = INFINITY;
+    bool redo = false;
+    uint32_t j = 0, end = 0;
+    // the window's event sweep
+    int i = 0, m = 0, exit_pos = -1;
+    float next_exit = INFINITY;
+    auto begin_window = [&]() {
+        n = 0;
+        t_cut = kfull = INFINITY;
+        sp = 0;
+        node = 0;
+        qh = qn = 0;
+        j = end = 0;
+        redo = A.hnodes4 == nullptr;  // no 4-wide tree: the pair-tree walk at once
+        phase = kSmCollect;
+    };
+    auto begin_bounce = [&]() {  // ff_bounce's start: the target draw, window 0 from t = 0
+        target = -logf(1.0f - P.rng.uniform());
+        S.C.add(kFFBounces);
+        acc = 0;
+        t_prev = W0 = 0.0f;
+        cap = A.ff_hit_cap0;
+        begin_window();
+    };
+    auto to_shade = [&](float ts) {
+        m = -1;
+        t_cut = ts;
+        phase = kSmShade;
+    };
+    auto prune = [&](float tmin, float tmax) {
+        if (tmax < W0 - kTPad * (1.0f + W0)) return false;
+        const float lim = fminf(t_cut, kfull);
+        return !(tmin > lim + kTPad * (1.0f + fminf(lim, 1e30f)));
+    };
+    auto prim = [&](uint32_t jj) {  // free_flight_distance's insertion, term for term
+        S.C.add(kFFPrims);
+        GRec g = load_rec(A.gauss, (int)jj);
+        float t0, t1;
+        if (!intersect(quad(g, P.ray), t0, t1)) return;
+        if (!(t0 <= t1)) return;
+        if (W0 > 0.0f && !(t1 > W0)) return;
+        const float key = fmaxf(t0, W0);
+        if (key >= t_cut) return;
+        if (n == cap) {
+            if (key >= kfull) {
+                t_cut = fminf(t_cut, key);
+                return;
+            }
+            t_cut = fminf(t_cut, kfull);
+            --n;
+        }
+        int p = n;
+        while (p > 0) {
+            const float4 prev = S.H(p - 1);
+            if (!(prev.x > key)) break;
+            S.H(p) = prev;
+            --p;
+        }
+        S.H(p) = make_float4(key, t1, __int_as_float((int)jj), 0.0f);
+        ++n;
+        if (n == cap) kfull = S.K(n - 1);
+    };
+    for (;;) {
+        const uint64_t idle = __ballot(phase == kSmIdle);
+        if (!exhausted && (idle == ~0ull || __popcll(idle) >= VR_FF_REFILL)) {
+            unsigned long long base = 0;
+            if (lane == 0) base = atomicAdd(A.ff_next, (unsigned long long)__popcll(idle));
+            base = __shfl(base, 0, 64);
+            exhausted = base + (unsigned long long)__popcll(idle) >= A.ff_total;
+            if (phase == kSmIdle) {
+                const unsigned long long pid =
+                    base + __builtin_amdgcn_mbcnt_hi((uint32_t)(idle >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)idle, 0u));
+                if (pid < A.ff_total) {
+                    S.C.add(kFFPaths);
+                    if (ff_start(A, (uint32_t)pid, P)) begin_bounce();
+                }
+            }
+        }
+        const int nc = __popcll(__ballot(phase == kSmCollect)), ns = __popcll(__ballot(phase == kSmSweep)),
+                  nh = __popcll(__ballot(phase == kSmShade));
+        if (nc + ns + nh == 0) {
+            if (exhausted) break;
+            continue;
+        }
+        const bool shade_now = nh >= VR_FFSM_SHADE_MIN ? (nh >= ns && nh >= nc) : (ns + nc == 0);
+#ifdef VR_DIAG_FFSM  // (CNT builds) lane 0 of each wave: cycles/16 of each phase [0..2], its iterations [3..5], and the
+        // lanes it ran with, COLLECT [6] and SWEEP [7] (SHADE's are the bounces)
+        const int dphase = shade_now ? 2 : (ns >= nc ? 1 : 0);
+        const uint64_t dt0 = __builtin_amdgcn_s_memtime();
+#endif
+        if (shade_now) {
+            // ---- SHADE: ff_bounce after free_flight_distance, term for term ----
+            if (phase == kSmShade) {
+                float ts = t_cut;
+                const int ma = m;
+                if (ma >= 0) {  // the scatter lies in [t_prev, t_cut] with kfull of the target left
+                    const uint64_t useed = A.ff_solver == kSolverUniform ? ff_path_seed(A, P.out) : 0ull;
+                    ts = solve_distance(A, S, ma, P.ray, t_prev, t_cut, kfull, useed, P.bounce);
+                }
+                bool done = false, requeued = false;
+                if (MULTI && A.rec_bits && ts != -2.0f)
+                    record_hits(A, P.ray, ts >= 0.0f ? ts + 1e-6f : INFINITY, P.px, stack, kFFBlock);
+                if (ts == -2.0f && A.ff_fbq != nullptr) {  // over the hit-buffer capacity: the whole path re-runs
+                    const uint32_t q = atomicAdd(A.ff_fbq, 1u);  // in ff_fallback_kernel with larger rows
+                    atomicAdd(A.counters + 2, 1u);
+                    if (q < A.ff_fbq_cap) {
+                        A.ff_fbq[1 + q] = P.out;
+                        A.ff_tail[P.out] = make_float4(0.0f, 0.0f, 0.0f, __uint_as_float(kFFNone));
+                        requeued = true;
+                    }
+                }
+                if (requeued) {
+                    done = true;
+                } else if (ts == -2.0f || P.bounce >= A.ff_max_bounces) {
+                    P.L0 = P.L1 = P.L2 = __builtin_nanf("");
+                    P.after = true;
+                    atomicAdd(A.counters, 1u);
+                    done = true;
+                } else if (ts < 0.0f) {  // no event, or no scatter before the last event: environment
+                    P.L0 += P.tp0 * A.env[0];
+                    P.L1 += P.tp1 * A.env[1];
+                    P.L2 += P.tp2 * A.env[2];
+                    P.after |= P.first != kFFNone;
+                    done = true;
+                } else {
+                    const float px = P.ray.ox + ts * P.ray.dx, py = P.ray.oy + ts * P.ray.dy, pz = P.ray.oz + ts * P.ray.dz;
+                    const float albedo = evaluate_albedo(A, S, ma, px, py, pz);
+                    const int nl = A.num_lights;
+                    const bool is_env = P.rng.uniform() < __fdiv_rn(1.0f, (float)(nl + 1));
+                    int li = -1;
+                    float dist = INFINITY;
+                    Ray sr;
+                    if (!is_env) {
+                        li = (int)(P.rng.uniform() * (float)nl);
+                        const LightRecord& Lt = A.lights[li];
+                        float wx = Lt.px - px, wy = Lt.py - py, wz = Lt.pz - pz;
+                        dist = sqrtf(dot3(wx, wy, wz, wx, wy, wz));
+                        normalize3(wx, wy, wz);
+                        sr = make_ray(px, py, pz, wx, wy, wz);
+                    } else {
+                        float wx, wy, wz;
+                        sample_uniform_direction(P.rng, wx, wy, wz);
+                        sr = make_ray(px, py, pz, wx, wy, wz);
+                    }
+                    const float w = (albedo * kInv4Pi) * (float)(nl + 1);
+                    const float m0 = MULTI ? P.tp0 * w : w, m1 = MULTI ? P.tp1 * w : w, m2 = MULTI ? P.tp2 * w : w;
+                    const bool queued = nee_queue(A, sr, dist, li, m0, m1, m2, P.first, P.last, P.defer);
+                    S.C.add(queued ? kFFNeeQueued : kFFNeeInline);
+                    if (!queued) {
+                        float Li0, Li1, Li2;
+                        nee_radiance(A, transmittance_up_to(A, sr, dist, stack, kFFBlock), li, dist, Li0, Li1, Li2);
+                        P.after |= P.first != kFFNone;
+                        if constexpr (!MULTI) {
+                            P.L0 = m0 * Li0;
+                            P.L1 = m1 * Li1;
+                            P.L2 = m2 * Li2;
+                        } else {
+                            P.L0 += m0 * Li0;
+                            P.L1 += m1 * Li1;
+                            P.L2 += m2 * Li2;
+                        }
+                    }
+                    if constexpr (!MULTI) {
+                        done = true;
+                    } else {
+                        P.tp0 *= albedo;
+                        P.tp1 *= albedo;
+                        P.tp2 *= albedo;
+                        if (P.bounce >= A.ff_min_bounces) {  // integrator.h:691-695
+                            const float rr = fminf(fmaxf(P.tp0, fmaxf(P.tp1, P.tp2)), 0.9f);
+                            if (P.rng.uniform() > rr) {
+                                done = true;
+                            } else {
+                                P.tp0 = __fdiv_rn(P.tp0, rr);
+                                P.tp1 = __fdiv_rn(P.tp1, rr);
+                                P.tp2 = __fdiv_rn(P.tp2, rr);
+                            }
+                        }
+                        if (!done) {
+                            float nx, ny, nz;
+                            sample_uniform_direction(P.rng, nx, ny, nz);
+                            P.ray = make_ray(px, py, pz, nx, ny, nz);
+                            ++P.bounce;
+                        }
+                    }
+                }
+                if (done) {
+                    if (!requeued)
+                        A.ff_tail[P.out] = make_float4(P.L0, P.L1, P.L2, __uint_as_float(P.first | (P.after ? kFFTailAfter : 0u)));
+                    phase = kSmIdle;
+                } else {
+                    begin_bounce();
+                }
+            }
+        } else if (ns >= nc) {
+            // ---- SWEEP: free_flight_distance's event sweep, term for term ----
+            int budget = VR_FFSM_EVENT_BUDGET;
+            bool go = phase == kSmSweep;
+            while (go) {
+                budget -= max(m, 1);
+                const float next_entry = i < n ? S.K(i) : INFINITY;
+                float t_evt = fminf(next_entry, next_exit);
+                const bool window_end = t_cut <= t_evt;
+                if (window_end) t_evt = t_cut;
+                if (t_evt == INFINITY) {  // past the last event: no scatter (integrator.h:362-366)
+                    to_shade(-1.0f);
+                    break;
+                }
+                const bool is_entry = next_entry <= next_exit;
+                float nx = INFINITY;
+                int npos = -1;
+                Acc seg = 0;
+#pragma unroll VR_FF_SWEEP_UNROLL
+                for (int a = 0; a < m; ++a) {
+                    const float4 c = S.A0(a);
+                    float4& e1r = S.A1(a);
+                    const float4 e1 = e1r;
+                    S.C.add(kFFErf);
+                    const float f1 = erff(__fdiv_rn(c.y + c.z * t_evt, c.w));
+                    if (S.ph) e1r.x = f1;
+                    else e1r.y = f1;
+                    seg += (Acc)(c.x * (f1 - (S.ph ? e1.y : e1.x)));
+                    int pp = a;
+                    if (!is_entry && a == m - 1) pp = exit_pos;
+                    const bool gone = !is_entry && a == exit_pos;
+                    if (!gone && (e1.z < nx || (e1.z == nx && pp < npos))) {
+                        nx = e1.z;
+                        npos = pp;
+                    }
+                }
+                if (acc + seg > (Acc)target) {  // the scatter lies in [t_prev, t_evt]: SHADE solves for it
+                    kfull = (float)((Acc)target - acc);
+                    t_cut = t_evt;
+                    phase = kSmShade;
+                    break;
+                }
+                acc += seg;
+                t_prev = t_evt;
+                S.ph ^= 1;
+                if (window_end) {  // the next window starts at t_cut
+                    W0 = t_cut;
+                    cap = min(2 * cap, A.ff_hit_cap);
+                    begin_window();
+                    break;
+                }
+                if (is_entry) {
+                    if (m >= A.ff_act_cap) {
+                        to_shade(-2.0f);
+                        break;
+                    }
+                    const float t1n = S.enter(A, m, i++, P.ray, t_evt);
+                    if (t1n < nx) {
+                        nx = t1n;
+                        npos = m;
+                    }
+                    ++m;
+                } else {
+                    S.move(exit_pos, m - 1);
+                    --m;
+                }
+                next_exit = nx;
+                exit_pos = npos;
+                go = budget > 0;
+            }
+        } else {
+            // ---- COLLECT: one NODE or PRIM iteration of the window's while-while walk ----
+            const bool col = phase == kSmCollect;
+            const bool walking = col && !redo;
+            const bool has_prim = walking && (j < end || qn > 0);
+            const bool can_node = walking && node >= 0 && qn <= kCollectQueue - 4;
+            const int np = __popcll(__ballot(has_prim)), nn = __popcll(__ballot(can_node));
+            if (nn == 0 || (np > 0 && np >= nn)) {  // PRIM iteration
+                bool go = has_prim;
+                for (int k = 0; k < kCollectSteps; ++k) {
+                    if (go) {
+                        if (j == end) {
+                            const int32_t ref = ring[qh * kFFBlock];
+                            qh = (qh + 1) & (kCollectQueue - 1);
+                            --qn;
+                            j = leaf_first(ref);
+                            end = j + leaf_count(ref);
+                        }
+                        prim(j);
+                        ++j;
+                    }
+                    go = go && (j < end || qn > 0);
+                }
+            } else {  // NODE iteration (the ray's node-space slab constants, recomputed per iteration)
+                float ox = P.ray.ox, oy = P.ray.oy, oz = P.ray.oz;
+                node_space<true>(A, ox, oy, oz);
+                auto inv = [&](float d) {
+                    d *= A.hn_scale;
+                    return __frcp_rn(fabsf(d) > 1e-30f ? d : copysignf(1e-30f, d));
+                };
+                const float ix = inv(P.ray.dx), iy = inv(P.ray.dy), iz = inv(P.ray.dz);
+                const float oxi = ox * ix, oyi = oy * iy, ozi = oz * iz;
+                bool go = can_node;
+                for (int k = 0; k < kCollectSteps; ++k) {
+                    if (go) {
+                        S.C.add(kFFNode4);
+                        float key[4];
+                        int32_t kr[4];
+                        wide_children(A, node, ix, iy, iz, oxi, oyi, ozi, prune, key, kr);
+#pragma unroll
+                        for (int c = 0; c < 4; ++c)
+                            if (kr[c] < 0) {
+                                ring[((qh + qn) & (kCollectQueue - 1)) * kFFBlock] = kr[c];
+                                ++qn;
+                            }
+                        int first = -1;
+                        int32_t next = 0;
+#pragma unroll
+                        for (int c = 3; c >= 0; --c) {
+                            first = kr[c] > 0 ? c : first;
+                            next = kr[c] > 0 ? kr[c] : next;
+                        }
+                        if (sp + 3 > kStackSize) {
+                            redo = true;
+                            node = -1;
+                        } else {
+#pragma unroll
+                            for (int c = 3; c >= 0; --c)
+                                if (kr[c] > 0 && c != first) stack[(sp++) * kFFBlock] = kr[c];
+                            if (first >= 0) node = next;
+                            else if (sp > 0) node = stack[(--sp) * kFFBlock];
+                            else node = -1;
+                        }
+                    }
+                    go = go && node >= 0 && qn <= kCollectQueue - 4 && !redo;
+                }
+            }
+            if (col && (redo || (node < 0 && j == end && qn == 0))) {  // the window's collection is complete
+                if (redo) {  // the pair tree (at most one push per level) redoes the whole collection
+                    n = 0;
+                    t_cut = kfull = INFINITY;
+                    auto leaf = [&](uint32_t first, uint32_t count) {
+                        for (uint32_t jj = first; jj < first + count; ++jj) prim(jj);
+                        return true;
+                    };
+                    auto on2 = [&]() { S.C.add(kFFNode2); };
+                    if (A.hnodes) traverse<true>(A, P.ray, stack, kFFBlock, prune, leaf, on2);
+                    else traverse<false>(A, P.ray, stack, kFFBlock, prune, leaf, on2);
+                }
+                // a buffer that filled ends the window at its largest kept key (subtrees skipped while full hold
+                // only larger keys; whether one was skipped depends on the wave's NODE/PRIM schedule, so the cut must not)
+                if (n == cap) t_cut = fminf(t_cut, S.K(n - 1));
+                while (n > 0 && S.K(n - 1) >= t_cut) --n;
+                if (t_cut <= W0) {  // more than cap Gaussians overlap at W0: no progress at this cap
+                    if (cap >= A.ff_hit_cap) {
+                        to_shade(-2.0f);
+                    } else {
+                        cap = min(2 * cap, A.ff_hit_cap);
+                        begin_window();
+                    }
+                } else if (n == 0 && t_cut == INFINITY) {
+                    to_shade(-1.0f);
+                } else {
+                    i = m = 0;
+                    next_exit = INFINITY;
+                    exit_pos = -1;
+                    S.ph = 0;  // (entries write both F slots: the phase at a window's start is free)
+                    phase = kSmSweep;
+                }
+            }
+        }
+#ifdef VR_DIAG_FFSM
+        if constexpr (CNT) {
+            if (lane == 0u) {
+                S.C.v[dphase] += (uint32_t)((__builtin_amdgcn_s_memtime() - dt0) >> 4);
+                S.C.v[3 + dphase] += 1u;
+                if (dphase == 0) S.C.v[6] += (uint32_t)nc;
+                if (dphase == 1) S.C.v[7] += (uint32_t)ns;
+            }
+        }
+#endif
+    }
+    if constexpr (CNT) {
+        Ctr c{};
+        for (int k = 0; k < kFFNumCtr; ++k) c.v[k] = S.C.v[k];
+        flush_counters(A.work, c);
+    }
+}
+#if VR_FF_SM
+#define VR_FF_PATH_KERNEL ff_path_sm_kernel
+#else
+#define VR_FF_PATH_KERNEL ff_path_kernel
+#endif
+
 // Paths the path kernel queued because more Gaussians overlapped one point than its rows hold: each
 // re-runs from its first bounce (same seed, so the same path) with kFFBigCap-entry rows and inline
 // shadow rays, and writes its radiance as one inline sum (its earlier queued shadow rays are dropped).
@@ -1166,17 +1595,13 @@ __global__ void __launch_bounds__(kFFBlock) ffs_collect_kernel(RenderArgs A) {
     float ix = 0.0f, iy = 0.0f, iz = 0.0f, oxi = 0.0f, oyi = 0.0f, ozi = 0.0f;
     float W0 = 0.0f, t_cut = INFINITY, kfull = INFINITY;
     int cap = 0, n = 0, sp = 0, node = -1, qh = 0, qn = 0;
-    bool pruned_full = false, redo = false;
+    bool redo = false;
     uint32_t j = 0, end = 0;
     auto H = [&](int i) -> float4& { return A.ff_hit[(size_t)i * A.ff_pool + s]; };
     auto prune = [&](float tmin, float tmax) {
         if (tmax < W0 - kTPad * (1.0f + W0)) return false;
         const float lim = fminf(t_cut, kfull);
-        if (tmin > lim + kTPad * (1.0f + fminf(lim, 1e30f))) {
-            pruned_full |= n == cap;
-            return false;
-        }
-        return true;
+        return !(tmin > lim + kTPad * (1.0f + fminf(lim, 1e30f)));
     };
     auto prim = [&](uint32_t jj) {  // free_flight_distance's insertion, term for term
         C.add(kFFPrims);
@@ -1223,7 +1648,6 @@ __global__ void __launch_bounds__(kFFBlock) ffs_collect_kernel(RenderArgs A) {
                     cap = (int)A.fs_meta2[s].y;
                     n = 0;
                     t_cut = kfull = INFINITY;
-                    pruned_full = false;
                     float ox = r.ox, oy = r.oy, oz = r.oz;
                     node_space<true>(A, ox, oy, oz);
                     auto inv = [&](float d) {
@@ -1306,7 +1730,6 @@ __global__ void __launch_bounds__(kFFBlock) ffs_collect_kernel(RenderArgs A) {
             if (redo) {  // the pair tree (at most one push per level) redoes the whole collection
                 n = 0;
                 t_cut = kfull = INFINITY;
-                pruned_full = false;
                 auto leaf = [&](uint32_t first, uint32_t count) {
                     for (uint32_t jj = first; jj < first + count; ++jj) prim(jj);
                     return true;
@@ -1315,8 +1738,9 @@ __global__ void __launch_bounds__(kFFBlock) ffs_collect_kernel(RenderArgs A) {
                 if (A.hnodes) traverse<true>(A, r, stack, kFFBlock, prune, leaf, on2);
                 else traverse<false>(A, r, stack, kFFBlock, prune, leaf, on2);
             }
-            // skipped subtrees only hold keys beyond the (final) largest kept key
-            if (pruned_full && n > 0) t_cut = fminf(t_cut, H(n - 1).x);
+            // a buffer that filled ends the window at its largest kept key (subtrees skipped while full hold
+            // only larger keys; whether one was skipped depends on the wave's NODE/PRIM schedule, so the cut must not)
+            if (n == cap) t_cut = fminf(t_cut, H(n - 1).x);
             while (n > 0 && H(n - 1).x >= t_cut) --n;
             reinterpret_cast<float*>(A.fs_L + s)[3] = t_cut;
             reinterpret_cast<uint32_t*>(A.fs_meta2 + s)[2] = (uint32_t)n;
@@ -1789,7 +2213,7 @@ hipError_t launch_sfd_loss_diff(const uint32_t* bits0, const uint32_t* bits1, co
 // Threads of the resident path-kernel grid on a device with `cus` CUs (the scratch row stride).
 uint32_t free_flight_threads(int cus) {
     int per_cu = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)dev::ff_path_kernel<true, false>, dev::kFFBlock, 0) !=
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)dev::VR_FF_PATH_KERNEL<true, false>, dev::kFFBlock, 0) !=
             hipSuccess ||
         per_cu < 1)
         per_cu = 1;
@@ -1861,11 +2285,11 @@ hipError_t launch_free_flight(const RenderArgs& A, uint32_t chunk_tiles, hipStre
         else e0 = cnt ? ffs_run<false, true>(A, stream, poll) : ffs_run<false, false>(A, stream, poll);
         if (e0 != hipSuccess) return e0;
     } else if (A.ff_multi) {
-        if (cnt) hipLaunchKernelGGL((dev::ff_path_kernel<true, true>), grid, dim3(dev::kFFBlock), 0, stream, A);
-        else hipLaunchKernelGGL((dev::ff_path_kernel<true>), grid, dim3(dev::kFFBlock), 0, stream, A);
+        if (cnt) hipLaunchKernelGGL((dev::VR_FF_PATH_KERNEL<true, true>), grid, dim3(dev::kFFBlock), 0, stream, A);
+        else hipLaunchKernelGGL((dev::VR_FF_PATH_KERNEL<true>), grid, dim3(dev::kFFBlock), 0, stream, A);
     } else {
-        if (cnt) hipLaunchKernelGGL((dev::ff_path_kernel<false, true>), grid, dim3(dev::kFFBlock), 0, stream, A);
-        else hipLaunchKernelGGL((dev::ff_path_kernel<false>), grid, dim3(dev::kFFBlock), 0, stream, A);
+        if (cnt) hipLaunchKernelGGL((dev::VR_FF_PATH_KERNEL<false, true>), grid, dim3(dev::kFFBlock), 0, stream, A);
+        else hipLaunchKernelGGL((dev::VR_FF_PATH_KERNEL<false>), grid, dim3(dev::kFFBlock), 0, stream, A);
     }
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;

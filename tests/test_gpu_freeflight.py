@@ -265,6 +265,23 @@ def test_first_frame_queue_sizing_equals_queue_at_its_bound():
     assert np.array_equal(a, b)
 
 
+@pytest.mark.parametrize("window0", [0, 2])
+def test_multiscatter_frame_is_deterministic(window0):
+    """The same frame from three fresh contexts, bit for bit, and from the staged pipeline too, on the C2
+    scene with many hit windows. A window's cut once depended on whether the walk had skipped a subtree
+    while the hit buffer was full, which depends on the wave's NODE/PRIM schedule (so on which paths
+    shared the wave): about 100 of the C2 bench frame's 262k pixels then differed by an ulp from run to
+    run (round 5). A full buffer now always ends its window at its largest kept key."""
+    scene = vr.Scene.load_GMM(scene_path("1000_random.txt"))
+    integ = vr.MultiScatterGaussians(vr.Pinhole_Camera(CAM_POS, main_view_dir(), FOV), 4, 5)
+    opts = {"ff_window0": window0} if window0 else {}
+    frames = [_fresh_render(scene, integ, 160, 160, **opts)[0] for _ in range(3)]
+    frames.append(_fresh_render(scene, integ, 160, 160, ff_staged=1, **opts)[0])
+    for k, f in enumerate(frames[1:], 1):
+        d = np.abs(f - frames[0])
+        assert np.array_equal(f, frames[0], equal_nan=True), f"frame {k}: {int((d.max(-1) > 0).sum())} pixels differ, max {np.nanmax(d):.2e}"
+
+
 @pytest.mark.parametrize("queue", [1, 2])
 def test_small_nee_queue_through_tiles_is_reported_then_equal(queue):
     """The asynchronous tile path (vr_render_tiles_device, the multi-GPU building block) with a shadow-ray
