@@ -104,7 +104,9 @@ struct FFScratch {
     // entry i (hit slot `slot`) becomes active at t: cache its factors (optical_depth's own ops);
     // returns its exit t1
     __device__ __forceinline__ float enter(const RenderArgs& A, int i, int slot, const Ray& r, float t) const {
-        const float4 h = H(slot);
+        return enter_row(A, i, H(slot), r, t);
+    }
+    __device__ __forceinline__ float enter_row(const RenderArgs& A, int i, const float4 h, const Ray& r, float t) const {
         GRec g = load_rec(A.gauss, __float_as_int(h.z));
         Quad q = quad(g, r);
         float twoA = 2.0f * q.A;
@@ -129,6 +131,23 @@ struct FFScratch {
         return c.x * (erff(__fdiv_rn(c.y + c.z * t, c.w)) - (ph ? e.y : e.x));
     }
 };
+
+// The persistent path kernels' rows of thread gt. VR_FF_ROWS_WAVE: each wave's rows are one block
+// ([wave][slot][lane]: a slot of the wave is 1 KB, the wave's hit rows 128 KB), so a wave touches a few
+// pages instead of one per slot (the [slot][thread] layout puts consecutive slots ff_threads * 16 B apart).
+#ifndef VR_FF_ROWS_WAVE
+#define VR_FF_ROWS_WAVE 0
+#endif
+template <bool CNT>
+__device__ __forceinline__ FFScratch<CNT> ff_thread_scratch(const RenderArgs& A, uint32_t gt) {
+#if VR_FF_ROWS_WAVE
+    const size_t w = gt >> 6, l = gt & 63u;
+    return FFScratch<CNT>{A.ff_hit + w * (size_t)A.ff_hit_cap * 64u + l, A.ff_act0 + w * (size_t)A.ff_act_cap * 64u + l,
+                          A.ff_act1 + w * (size_t)A.ff_act_cap * 64u + l, 64u, 0, {}};
+#else
+    return FFScratch<CNT>{A.ff_hit + gt, A.ff_act0 + gt, A.ff_act1 + gt, A.ff_threads, 0, {}};
+#endif
+}
 
 // camera.h:45-53 / :64-73 for a float (u, v) (the stratified sample of integrator.h:564-568).
 __device__ __forceinline__ Ray camera_ray(const RenderArgs& A, float uvx, float uvy) {
@@ -862,7 +881,7 @@ __global__ void __launch_bounds__(kFFBlock, VR_FF_WAVES) ff_path_kernel(RenderAr
     __shared__ int s_stack[(kStackSize + kCollectQueue) * kFFBlock];  // walk stack + the walks' leaf FIFO
     int* stack = s_stack + threadIdx.x;
     const uint32_t gt = blockIdx.x * kFFBlock + threadIdx.x;
-    FFScratch<CNT> S{A.ff_hit + gt, A.ff_act0 + gt, A.ff_act1 + gt, A.ff_threads, 0, {}};
+    FFScratch<CNT> S = ff_thread_scratch<CNT>(A, gt);
     const uint32_t lane = threadIdx.x & 63u;
     FFPath P{PCG32(0, 1)};
     bool live = false, exhausted = false;
@@ -909,6 +928,12 @@ __global__ void __launch_bounds__(kFFBlock, VR_FF_WAVES) ff_path_kernel(RenderAr
 #ifndef VR_FFSM_EVENT_BUDGET
 #define VR_FFSM_EVENT_BUDGET 0  // active-entry evaluations a lane may spend on events per SWEEP iteration (0: one event)
 #endif
+#ifndef VR_FFSM_PF
+#define VR_FFSM_PF 1  // the sweep reads an entry's row once and the next active entry's rows one ahead
+#endif
+#ifndef VR_FFSM_EXP
+#define VR_FFSM_EXP 0  // (diagnostic experiments only)
+#endif
 #ifndef VR_FFSM_SHADE_MIN
 #define VR_FFSM_SHADE_MIN 1  // SHADE runs when it has the most lanes and at least this many (or nothing else is left)
 #endif
@@ -923,7 +948,7 @@ __global__ void __launch_bounds__(kFFBlock, VR_FFSM_WAVES) ff_path_sm_kernel(Ren
     int* stack = s_stack + threadIdx.x;
     int* ring = stack + kStackSize * kFFBlock;
     const uint32_t gt = blockIdx.x * kFFBlock + threadIdx.x;
-    FFScratch<CNT> S{A.ff_hit + gt, A.ff_act0 + gt, A.ff_act1 + gt, A.ff_threads, 0, {}};
+    FFScratch<CNT> S = ff_thread_scratch<CNT>(A, gt);
     const uint32_t lane = threadIdx.x & 63u;
     FFPath P{PCG32(0, 1)};
     int phase = kSmIdle;
@@ -935,7 +960,7 @@ __global__ void __launch_bounds__(kFFBlock, VR_FFSM_WAVES) ff_path_sm_kernel(Ren
     // the window's hit collection (ffs_collect_kernel's walk state); in SHADE, t_cut holds ts (m < 0) or
     // the scatter segment's end t_evt, and kfull the target left on that segment
     int n = 0, sp = 0, node = -1, qh = 0, qn = 0;
-    float t_cut = INFINITY, kfull = INFINITY;
+    float t_cut = INFINITY, kfull = INFINITY, klast = 0.0f;
     bool redo = false;
     uint32_t j = 0, end = 0;
     // the window's event sweep
@@ -985,17 +1010,24 @@ __global__ void __launch_bounds__(kFFBlock, VR_FFSM_WAVES) ff_path_sm_kernel(Ren
             }
             t_cut = fminf(t_cut, kfull);
             --n;
+            if (n > 0) klast = S.K(n - 1);  // (the evicted entry was the largest)
         }
+        // klast = the largest kept key (the last row): an entry in walk order past it is appended without
+        // reading the rows back (the rows live in global memory: a read there is a dependent round trip)
         int p = n;
-        while (p > 0) {
-            const float4 prev = S.H(p - 1);
-            if (!(prev.x > key)) break;
-            S.H(p) = prev;
-            --p;
+        if (n > 0 && klast > key) {
+            while (VR_FFSM_EXP != 4 && p > 0) {
+                const float4 prev = S.H(p - 1);
+                if (!(prev.x > key)) break;
+                S.H(p) = prev;
+                --p;
+            }
+        } else {
+            klast = key;
         }
         S.H(p) = make_float4(key, t1, __int_as_float((int)jj), 0.0f);
         ++n;
-        if (n == cap) kfull = S.K(n - 1);
+        if (n == cap) kfull = klast;
     };
     for (;;) {
         const uint64_t idle = __ballot(phase == kSmIdle);
@@ -1022,8 +1054,10 @@ __global__ void __launch_bounds__(kFFBlock, VR_FFSM_WAVES) ff_path_sm_kernel(Ren
         const bool shade_now = nh >= VR_FFSM_SHADE_MIN ? (nh >= ns && nh >= nc) : (ns + nc == 0);
 #ifdef VR_DIAG_FFSM  // (CNT builds) lane 0 of each wave: cycles/16 of each phase [0..2], its iterations [3..5], and the
         // lanes it ran with, COLLECT [6] and SWEEP [7] (SHADE's are the bounces)
+        // (VR_DIAG_FFSM=2: cycles/16 of NODE, PRIM, SWEEP, SHADE iterations [0..3] and their counts [4..7])
         const int dphase = shade_now ? 2 : (ns >= nc ? 1 : 0);
         const uint64_t dt0 = __builtin_amdgcn_s_memtime();
+        bool dnode = false;
 #endif
         if (shade_now) {
             // ---- SHADE: ff_bounce after free_flight_distance, term for term ----
@@ -1135,7 +1169,12 @@ __global__ void __launch_bounds__(kFFBlock, VR_FFSM_WAVES) ff_path_sm_kernel(Ren
             bool go = phase == kSmSweep;
             while (go) {
                 budget -= max(m, 1);
+#if VR_FFSM_PF
+                const float4 hn = i < n ? S.H(i) : make_float4(INFINITY, 0.0f, 0.0f, 0.0f);  // (the entry's row, once)
+                const float next_entry = hn.x;
+#else
                 const float next_entry = i < n ? S.K(i) : INFINITY;
+#endif
                 float t_evt = fminf(next_entry, next_exit);
                 const bool window_end = t_cut <= t_evt;
                 if (window_end) t_evt = t_cut;
@@ -1147,11 +1186,25 @@ __global__ void __launch_bounds__(kFFBlock, VR_FFSM_WAVES) ff_path_sm_kernel(Ren
                 float nx = INFINITY;
                 int npos = -1;
                 Acc seg = 0;
+#if VR_FFSM_PF
+                // the next entry's rows are read before this entry's F is written (one entry ahead in flight)
+                float4 cn = m > 0 ? S.A0(0) : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+                float4 en = m > 0 ? S.A1(0) : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+#endif
 #pragma unroll VR_FF_SWEEP_UNROLL
                 for (int a = 0; a < m; ++a) {
+#if VR_FFSM_PF
+                    const float4 c = cn, e1 = en;
+                    if (a + 1 < m) {
+                        cn = S.A0(a + 1);
+                        en = S.A1(a + 1);
+                    }
+                    float4& e1r = S.A1(a);
+#else
                     const float4 c = S.A0(a);
                     float4& e1r = S.A1(a);
                     const float4 e1 = e1r;
+#endif
                     S.C.add(kFFErf);
                     const float f1 = erff(__fdiv_rn(c.y + c.z * t_evt, c.w));
                     if (S.ph) e1r.x = f1;
@@ -1185,7 +1238,12 @@ __global__ void __launch_bounds__(kFFBlock, VR_FFSM_WAVES) ff_path_sm_kernel(Ren
                         to_shade(-2.0f);
                         break;
                     }
+#if VR_FFSM_PF
+                    const float t1n = S.enter_row(A, m, hn, P.ray, t_evt);
+                    ++i;
+#else
                     const float t1n = S.enter(A, m, i++, P.ray, t_evt);
+#endif
                     if (t1n < nx) {
                         nx = t1n;
                         npos = m;
@@ -1223,6 +1281,9 @@ __global__ void __launch_bounds__(kFFBlock, VR_FFSM_WAVES) ff_path_sm_kernel(Ren
                     go = go && (j < end || qn > 0);
                 }
             } else {  // NODE iteration (the ray's node-space slab constants, recomputed per iteration)
+#ifdef VR_DIAG_FFSM
+                dnode = true;
+#endif
                 float ox = P.ray.ox, oy = P.ray.oy, oz = P.ray.oz;
                 node_space<true>(A, ox, oy, oz);
                 auto inv = [&](float d) {
@@ -1303,10 +1364,17 @@ __global__ void __launch_bounds__(kFFBlock, VR_FFSM_WAVES) ff_path_sm_kernel(Ren
 #ifdef VR_DIAG_FFSM
         if constexpr (CNT) {
             if (lane == 0u) {
-                S.C.v[dphase] += (uint32_t)((__builtin_amdgcn_s_memtime() - dt0) >> 4);
+                const uint32_t dc = (uint32_t)((__builtin_amdgcn_s_memtime() - dt0) >> 4);
+#if VR_DIAG_FFSM == 2
+                const int k = dphase == 0 ? (dnode ? 0 : 1) : dphase + 1;
+                S.C.v[k] += dc;
+                S.C.v[4 + k] += 1u;
+#else
+                S.C.v[dphase] += dc;
                 S.C.v[3 + dphase] += 1u;
                 if (dphase == 0) S.C.v[6] += (uint32_t)nc;
                 if (dphase == 1) S.C.v[7] += (uint32_t)ns;
+#endif
             }
         }
 #endif

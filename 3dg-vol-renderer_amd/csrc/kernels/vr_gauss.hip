@@ -460,6 +460,19 @@ constexpr bool kMarchPretest = VR_MARCH_PRETEST;
 #define VR_MARCH_PENDING 4  // register slots for the later steps' entrants
 #endif
 constexpr int kMarchLook = VR_MARCH_LOOKAHEAD, kMarchPend = VR_MARCH_PENDING;
+// Merged first query: a closest-entry query (empty active list) is always followed by the entrant query of
+// the step holding that entry, over nearly the same part of the tree. With VR_MARCH_MERGE the closest
+// query's walk also keeps, in the (empty) active list's LDS slots, every hit (j, entry a, exit b) with
+// a <= best + 2 steps (best: the closest entry so far; prune widened to match), dropping the ones a
+// later, closer entry puts out of range. Once best is final, step k = kfirst(best) has t_k < best + 2 steps,
+// so the kept hits hold all of the step's entrants (best <= a <= t_k < b) and the entrant query is
+// skipped; more than kMarchCand kept hits at once run it as before. Same entrant set: bit-identical.
+#ifndef VR_MARCH_MERGE
+#define VR_MARCH_MERGE 0
+#endif
+#ifndef VR_MARCH_CAND
+#define VR_MARCH_CAND 5  // (j, a, b) hits the merged query keeps (3 LDS slots each, after slot 0)
+#endif
 
 template <int ACT, bool S, bool H, bool W = false, int CAP = kStackSize, bool COOP = false>
 __device__ int march(const RenderArgs& A, uint32_t p, int px, int py, int* act_base, int* stack, int stride, Ctr& c,
@@ -503,6 +516,9 @@ __device__ int march(const RenderArgs& A, uint32_t p, int px, int py, int* act_b
         }
     };
     int kq = 0;
+    constexpr bool kMerge = VR_MARCH_MERGE && !COOP;
+    constexpr int kCand = (ACT - 1) / 3 < VR_MARCH_CAND ? (ACT - 1) / 3 : VR_MARCH_CAND;
+    bool have = false;  // (kMerge) the active list already holds step k's entrants
     // look-ahead (W, not COOP): pend_k = the last step the pending slots are complete for (-1: none);
     // a consumed or empty slot has pa = +inf
     constexpr bool kLook = W && !COOP && kMarchLook > 1;
@@ -528,17 +544,46 @@ __device__ int march(const RenderArgs& A, uint32_t p, int px, int py, int* act_b
             } else if (act.n == 0) {  // closest entry strictly after t_lo
                 if constexpr (S) c.v[kCtrPrimQueries]++;
                 float best = INFINITY;
+                const float lookw = kMerge ? 2.0f * step : 0.0f;
+                int nc = 0;         // (kMerge) kept hits, triple c in act slots 1 + 3c .. 3 + 3c
+                bool covf = false;  // (kMerge) a hit in range did not fit
                 auto prune_c = [&](float tmin, float tmax) {
-                    return tmax >= t_lo - kTPad * (1.0f + fabsf(t_lo)) && tmin <= best + kTPad * (1.0f + best);
+                    const float lim = best + lookw;
+                    return tmax >= t_lo - kTPad * (1.0f + fabsf(t_lo)) && tmin <= lim + kTPad * (1.0f + lim);
                 };
                 auto leaf_c = [&](uint32_t first, uint32_t count) {
                     for (uint32_t j = first; j < first + count; ++j) {
                         if constexpr (S) c.v[kCtrPrims]++;
                         GRec g = load_rec(G, j);
-                        if (kMarchPretest && fast_reject_closest(g, ray, t_lo, best)) continue;
+                        if (kMarchPretest && !kMerge && fast_reject_closest(g, ray, t_lo, best)) continue;
                         Quad q = quad(g, ray);
                         float a, b;
-                        if (intersect(q, a, b) && a > t_lo && a < best) best = a;
+                        if (!intersect(q, a, b) || !(a > t_lo)) continue;
+                        if (a < best) best = a;
+                        if constexpr (kMerge) {
+                            if (!(a <= best + lookw) || !(b > a)) continue;
+                            if (nc == kCand) {  // full: drop the hits a closer entry put out of range
+                                int w = 0;
+                                for (int cc = 0; cc < kCand; ++cc) {
+                                    if (!(__int_as_float(act.get(2 + 3 * cc)) <= best + lookw)) continue;
+                                    if (w != cc) {
+                                        act.set(1 + 3 * w, act.get(1 + 3 * cc));
+                                        act.set(2 + 3 * w, act.get(2 + 3 * cc));
+                                        act.set(3 + 3 * w, act.get(3 + 3 * cc));
+                                    }
+                                    ++w;
+                                }
+                                nc = w;
+                            }
+                            if (nc < kCand) {
+                                act.set(1 + 3 * nc, (int)j);
+                                act.set(2 + 3 * nc, __float_as_int(a));
+                                act.set(3 + 3 * nc, __float_as_int(b));
+                                ++nc;
+                            } else {
+                                covf = true;
+                            }
+                        }
                     }
                     return true;
                 };
@@ -551,6 +596,24 @@ __device__ int march(const RenderArgs& A, uint32_t p, int px, int py, int* act_b
                 // exactly the entries of (ts[k - 1], t_k]. The short window keeps the query local to the step
                 // (from t_lo = -1 the first query of every pixel walked every box along [0, t_k]). Same set.
                 if (k > kq) t_lo = ts[k - 1];
+                if constexpr (kMerge) {
+                    if (!covf && k < nts - 1) {  // the step's entrants from the kept hits, sorted by index
+                        const float tk = ts[k];
+                        for (int cc = 0; cc < nc; ++cc) {  // (the list, <= cc entries, stays below triple cc)
+                            const int j = act.get(1 + 3 * cc);
+                            if (!(__int_as_float(act.get(2 + 3 * cc)) <= tk) || !(__int_as_float(act.get(3 + 3 * cc)) > tk))
+                                continue;
+                            int i = act.n;
+                            while (i > 0 && act.get(i - 1) > j) {
+                                act.set(i, act.get(i - 1));
+                                --i;
+                            }
+                            act.set(i, j);
+                            act.n++;
+                        }
+                        have = true;
+                    }
+                }
             } else {
                 k = kq;
             }
@@ -578,6 +641,12 @@ __device__ int march(const RenderArgs& A, uint32_t p, int px, int py, int* act_b
                     act.n++;
                 }
                 if (ovf) return kOverflow;
+                kq = k + 1;
+                if (!march_step<S, COOP>(A, ray, p, px, py, k, t_k, act, T, prev, c, writer)) break;
+                continue;
+            }
+            if (kMerge && have) {  // the merged closest query found this step's entrants
+                have = false;
                 kq = k + 1;
                 if (!march_step<S, COOP>(A, ray, p, px, py, k, t_k, act, T, prev, c, writer)) break;
                 continue;

@@ -32,4 +32,10 @@ if os.environ.get("DIAG_KIND") == "ffsm":
         "lanes_per_iteration": {"collect": round(raw[6] / max(1, it[0]), 2), "sweep": round(raw[7] / max(1, it[1]), 2)},
         "cycles_per_iteration": {k: round(16 * c / max(1, n), 1) for k, c, n in zip(("collect", "sweep", "shade"), cyc, it)},
     }
+if os.environ.get("DIAG_KIND") == "ffsm2":
+    names = ("node", "prim", "sweep", "shade")
+    cyc, it = raw[0:4], raw[4:8]
+    out["ffsm2"] = {"phase_share": {k: round(c / max(1, sum(cyc)), 4) for k, c in zip(names, cyc)},
+                    "iterations": dict(zip(names, it)),
+                    "cycles_per_iteration": {k: round(16 * c / max(1, n), 1) for k, c, n in zip(names, cyc, it)}}
 print(json.dumps(out))
