@@ -40,7 +40,7 @@ constexpr int kFFBlock = 256;
 #define VR_FF_SWEEP_UNROLL 1  // unroll of the loops over the active list (A/B: independent row loads in flight)
 #endif
 #ifndef VR_FF_SWEEP_NOWRITE
-#define VR_FF_SWEEP_NOWRITE 0  // 1: the event sweep recomputes F at the segment start instead of writing it (A/B)
+#define VR_FF_SWEEP_NOWRITE 1  // the event sweep recomputes F at each segment start instead of keeping it in the rows (C2 147.3 -> 141.1 ms)
 #endif
 
 // Per-thread scratch rows (global memory, [slot][thread] so a wave's lanes touch consecutive 16-B
@@ -106,6 +106,8 @@ struct FFScratch {
     __device__ __forceinline__ float enter(const RenderArgs& A, int i, int slot, const Ray& r, float t) const {
         return enter_row(A, i, H(slot), r, t);
     }
+    __device__ __forceinline__ float T1(int i) const { return reinterpret_cast<const float*>(a1 + (size_t)i * stride)[2]; }
+    template <bool F = true>
     __device__ __forceinline__ float enter_row(const RenderArgs& A, int i, const float4 h, const Ray& r, float t) const {
         GRec g = load_rec(A.gauss, __float_as_int(h.z));
         Quad q = quad(g, r);
@@ -114,9 +116,13 @@ struct FFScratch {
         float den = 2.0f * sqrtf(twoA);
         float e = expf(-0.5f * (q.Cq - __fdiv_rn(q.B * q.B, 4.0f * q.A)));
         A0(i) = make_float4(pref * e, q.B, twoA, den);
-        C.add(kFFErf);
-        const float F = erff(__fdiv_rn(q.B + twoA * t, den));
-        A1(i) = make_float4(F, F, h.y, h.z);
+        if constexpr (F) {
+            C.add(kFFErf);
+            const float Fv = erff(__fdiv_rn(q.B + twoA * t, den));
+            A1(i) = make_float4(Fv, Fv, h.y, h.z);
+        } else {  // (the sweep recomputes F at each segment start)
+            A1(i) = make_float4(0.0f, 0.0f, h.y, h.z);
+        }
         return h.y;
     }
     __device__ __forceinline__ void move(int dst, int src) const {
@@ -597,7 +603,12 @@ __device__ float free_flight_distance(const RenderArgs& A, SC& S, const Ray& r, 
         float next_exit = INFINITY;
         int exit_pos = -1;
         for (;;) {
+#if VR_FF_SWEEP_NOWRITE
+            const float4 hn = i < n ? S.H(i) : make_float4(INFINITY, 0.0f, 0.0f, 0.0f);  // (the entry's row, once)
+            const float next_entry = hn.x;
+#else
             const float next_entry = i < n ? S.K(i) : INFINITY;
+#endif
             float t_evt = fminf(next_entry, next_exit);
             const bool window_end = t_cut <= t_evt;
             if (window_end) t_evt = t_cut;
@@ -609,6 +620,33 @@ __device__ float free_flight_distance(const RenderArgs& A, SC& S, const Ray& r, 
             float nx = INFINITY;  // smallest t1 after the event, and its position in the list then
             int npos = -1;
             Acc seg = 0;
+#if VR_FF_SWEEP_NOWRITE
+            // F at the segment start recomputed (the same float operations as the cached value), so the
+            // sweep reads 20 B per active entry (factors and exit) and writes nothing; the next entry's
+            // read is in flight while this one is evaluated
+            float4 cn = m > 0 ? S.A0(0) : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+            float tn = m > 0 ? S.T1(0) : 0.0f;
+#pragma unroll VR_FF_SWEEP_UNROLL
+            for (int a = 0; a < m; ++a) {
+                const float4 c = cn;
+                const float t1a = tn;
+                if (a + 1 < m) {
+                    cn = S.A0(a + 1);
+                    tn = S.T1(a + 1);
+                }
+                S.C.add(kFFErf);
+                const float f1 = erff(__fdiv_rn(c.y + c.z * t_evt, c.w));
+                const float f0 = erff(__fdiv_rn(c.y + c.z * t_prev, c.w));
+                seg += (Acc)(c.x * (f1 - f0));
+                int pp = a;  // position after a swap-remove of exit_pos
+                if (!is_entry && a == m - 1) pp = exit_pos;
+                const bool gone = !is_entry && a == exit_pos;
+                if (!gone && (t1a < nx || (t1a == nx && pp < npos))) {
+                    nx = t1a;
+                    npos = pp;
+                }
+            }
+#else
 #pragma unroll VR_FF_SWEEP_UNROLL
             for (int a = 0; a < m; ++a) {
                 const float4 c = S.A0(a);
@@ -616,16 +654,9 @@ __device__ float free_flight_distance(const RenderArgs& A, SC& S, const Ray& r, 
                 const float4 e1 = e1r;
                 S.C.add(kFFErf);
                 const float f1 = erff(__fdiv_rn(c.y + c.z * t_evt, c.w));
-#if VR_FF_SWEEP_NOWRITE
-                // F at the segment start recomputed (the same float operations as the cached value):
-                // the sweep writes nothing, its rows are read-only between entries
-                const float f0 = erff(__fdiv_rn(c.y + c.z * t_prev, c.w));
-                seg += (Acc)(c.x * (f1 - f0));
-#else
                 if (S.ph) e1r.x = f1;
                 else e1r.y = f1;
                 seg += (Acc)(c.x * (f1 - (S.ph ? e1.y : e1.x)));
-#endif
                 int pp = a;  // position after a swap-remove of exit_pos
                 if (!is_entry && a == m - 1) pp = exit_pos;
                 const bool gone = !is_entry && a == exit_pos;
@@ -634,6 +665,7 @@ __device__ float free_flight_distance(const RenderArgs& A, SC& S, const Ray& r, 
                     npos = pp;
                 }
             }
+#endif
             if (acc + seg > (Acc)target) {
 #if VR_FF_SWEEP_NOWRITE
                 S.ph = 0;  // the solver reads F at the segment start from .x
@@ -657,7 +689,12 @@ __device__ float free_flight_distance(const RenderArgs& A, SC& S, const Ray& r, 
             if (window_end) break;
             if (is_entry) {
                 if (m >= A.ff_act_cap) return -2.0f;
+#if VR_FF_SWEEP_NOWRITE
+                const float t1n = S.template enter_row<false>(A, m, hn, r, t_evt);
+                ++i;
+#else
                 const float t1n = S.enter(A, m, i++, r, t_evt);
+#endif
                 if (t1n < nx) {  // ties: the earlier position stays first
                     nx = t1n;
                     npos = m;
@@ -931,6 +968,12 @@ __global__ void __launch_bounds__(kFFBlock, VR_FF_WAVES) ff_path_kernel(RenderAr
 #ifndef VR_FFSM_PF
 #define VR_FFSM_PF 1  // the sweep reads an entry's row once and the next active entry's rows one ahead
 #endif
+#ifndef VR_FFSM_PPF
+#define VR_FFSM_PPF 0  // the PRIM iterations read the next Gaussian one step ahead (A/B)
+#endif
+#ifndef VR_FFSM_NOWRITE
+#define VR_FFSM_NOWRITE 0  // the sweep recomputes F at each segment start instead of keeping it in the rows (A/B)
+#endif
 #ifndef VR_FFSM_EXP
 #define VR_FFSM_EXP 0  // (diagnostic experiments only)
 #endif
@@ -994,9 +1037,8 @@ __global__ void __launch_bounds__(kFFBlock, VR_FFSM_WAVES) ff_path_sm_kernel(Ren
         const float lim = fminf(t_cut, kfull);
         return !(tmin > lim + kTPad * (1.0f + fminf(lim, 1e30f)));
     };
-    auto prim = [&](uint32_t jj) {  // free_flight_distance's insertion, term for term
+    auto prim_g = [&](uint32_t jj, const GRec& g) {  // free_flight_distance's insertion, term for term
         S.C.add(kFFPrims);
-        GRec g = load_rec(A.gauss, (int)jj);
         float t0, t1;
         if (!intersect(quad(g, P.ray), t0, t1)) return;
         if (!(t0 <= t1)) return;
@@ -1029,6 +1071,7 @@ __global__ void __launch_bounds__(kFFBlock, VR_FFSM_WAVES) ff_path_sm_kernel(Ren
         ++n;
         if (n == cap) kfull = klast;
     };
+    auto prim = [&](uint32_t jj) { prim_g(jj, load_rec(A.gauss, (int)jj)); };
     for (;;) {
         const uint64_t idle = __ballot(phase == kSmIdle);
         if (!exhausted && (idle == ~0ull || __popcll(idle) >= VR_FF_REFILL)) {
@@ -1065,6 +1108,13 @@ __global__ void __launch_bounds__(kFFBlock, VR_FFSM_WAVES) ff_path_sm_kernel(Ren
                 float ts = t_cut;
                 const int ma = m;
                 if (ma >= 0) {  // the scatter lies in [t_prev, t_cut] with kfull of the target left
+#if VR_FFSM_NOWRITE
+                    S.ph = 0;  // the solver reads F at the segment start from .x
+                    for (int a = 0; a < ma; ++a) {
+                        const float4 c = S.A0(a);
+                        reinterpret_cast<float*>(&S.A1(a))[0] = erff(__fdiv_rn(c.y + c.z * t_prev, c.w));
+                    }
+#endif
                     const uint64_t useed = A.ff_solver == kSolverUniform ? ff_path_seed(A, P.out) : 0ull;
                     ts = solve_distance(A, S, ma, P.ray, t_prev, t_cut, kfull, useed, P.bounce);
                 }
@@ -1186,6 +1236,32 @@ __global__ void __launch_bounds__(kFFBlock, VR_FFSM_WAVES) ff_path_sm_kernel(Ren
                 float nx = INFINITY;
                 int npos = -1;
                 Acc seg = 0;
+#if VR_FFSM_NOWRITE
+                // F at the segment start recomputed (the cached value's own float operations: bit-identical),
+                // so the sweep reads 20 B per active entry and writes nothing; the next entry's read in flight
+                float4 cn = m > 0 ? S.A0(0) : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+                float tn = m > 0 ? S.T1(0) : 0.0f;
+#pragma unroll VR_FF_SWEEP_UNROLL
+                for (int a = 0; a < m; ++a) {
+                    const float4 c = cn;
+                    const float t1a = tn;
+                    if (a + 1 < m) {
+                        cn = S.A0(a + 1);
+                        tn = S.T1(a + 1);
+                    }
+                    S.C.add(kFFErf);
+                    const float f1 = erff(__fdiv_rn(c.y + c.z * t_evt, c.w));
+                    const float f0 = erff(__fdiv_rn(c.y + c.z * t_prev, c.w));
+                    seg += (Acc)(c.x * (f1 - f0));
+                    int pp = a;
+                    if (!is_entry && a == m - 1) pp = exit_pos;
+                    const bool gone = !is_entry && a == exit_pos;
+                    if (!gone && (t1a < nx || (t1a == nx && pp < npos))) {
+                        nx = t1a;
+                        npos = pp;
+                    }
+                }
+#else
 #if VR_FFSM_PF
                 // the next entry's rows are read before this entry's F is written (one entry ahead in flight)
                 float4 cn = m > 0 ? S.A0(0) : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
@@ -1218,6 +1294,7 @@ __global__ void __launch_bounds__(kFFBlock, VR_FFSM_WAVES) ff_path_sm_kernel(Ren
                         npos = pp;
                     }
                 }
+#endif
                 if (acc + seg > (Acc)target) {  // the scatter lies in [t_prev, t_evt]: SHADE solves for it
                     kfull = (float)((Acc)target - acc);
                     t_cut = t_evt;
@@ -1239,7 +1316,7 @@ __global__ void __launch_bounds__(kFFBlock, VR_FFSM_WAVES) ff_path_sm_kernel(Ren
                         break;
                     }
 #if VR_FFSM_PF
-                    const float t1n = S.enter_row(A, m, hn, P.ray, t_evt);
+                    const float t1n = S.template enter_row<!VR_FFSM_NOWRITE>(A, m, hn, P.ray, t_evt);
                     ++i;
 #else
                     const float t1n = S.enter(A, m, i++, P.ray, t_evt);
@@ -1266,6 +1343,40 @@ __global__ void __launch_bounds__(kFFBlock, VR_FFSM_WAVES) ff_path_sm_kernel(Ren
             const int np = __popcll(__ballot(has_prim)), nn = __popcll(__ballot(can_node));
             if (nn == 0 || (np > 0 && np >= nn)) {  // PRIM iteration
                 bool go = has_prim;
+#if VR_FFSM_PPF
+                // software-pipelined: the next Gaussian's record is read before this one's hit is stored
+                // (a load waits for every older store of the wave)
+                GRec gn{};
+                if (go) {
+                    if (j == end) {
+                        const int32_t ref = ring[qh * kFFBlock];
+                        qh = (qh + 1) & (kCollectQueue - 1);
+                        --qn;
+                        j = leaf_first(ref);
+                        end = j + leaf_count(ref);
+                    }
+                    gn = load_rec(A.gauss, (int)j);
+                }
+                for (int k = 0; k < kCollectSteps; ++k) {
+                    if (go) {
+                        const GRec g = gn;
+                        const uint32_t jc = j++;
+                        const bool more = k + 1 < kCollectSteps && (j < end || qn > 0);
+                        if (more) {
+                            if (j == end) {
+                                const int32_t ref = ring[qh * kFFBlock];
+                                qh = (qh + 1) & (kCollectQueue - 1);
+                                --qn;
+                                j = leaf_first(ref);
+                                end = j + leaf_count(ref);
+                            }
+                            gn = load_rec(A.gauss, (int)j);
+                        }
+                        prim_g(jc, g);
+                        go = more;
+                    }
+                }
+#else
                 for (int k = 0; k < kCollectSteps; ++k) {
                     if (go) {
                         if (j == end) {
@@ -1280,6 +1391,7 @@ __global__ void __launch_bounds__(kFFBlock, VR_FFSM_WAVES) ff_path_sm_kernel(Ren
                     }
                     go = go && (j < end || qn > 0);
                 }
+#endif
             } else {  // NODE iteration (the ray's node-space slab constants, recomputed per iteration)
 #ifdef VR_DIAG_FFSM
                 dnode = true;

@@ -6,6 +6,7 @@ import sys
 import numpy as np
 import torch  # noqa: F401
 
+sys.path.insert(0, __import__("os").path.dirname(__import__("os").path.dirname(__import__("os").path.abspath(__file__))))
 import bench
 import vr_amd as vr
 

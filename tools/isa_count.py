@@ -39,7 +39,9 @@ def iclass(op):
         return "salu"
     if op.startswith("ds_"):
         return "lds"
-    if op.startswith(("global_", "buffer_", "flat_", "scratch_")):
+    if op.startswith("scratch_") or (op.startswith("buffer_") and "scratch" in op):
+        return "scratch"
+    if op.startswith(("global_", "buffer_", "flat_")):
         return "vmem"
     return "other"
 
@@ -74,10 +76,10 @@ for (addr, c), blk in zip(insts, blocks):
     by_body[os.path.basename(body)][c] += 1
     total[c] += 1
 print(json.dumps({"kernel": args.kernel, "instructions": len(insts), "total": dict(total)}))
-hdr = f"{'':44s} {'valu':>6s} {'salu':>6s} {'vmem':>5s} {'lds':>5s} {'smem':>5s} {'br':>5s}"
+hdr = f"{'':44s} {'valu':>6s} {'salu':>6s} {'vmem':>5s} {'lds':>5s} {'smem':>5s} {'br':>5s} {'scr':>5s}"
 print("\nby function (innermost own frame)\n" + hdr)
 for r, c in sorted(by_func.items(), key=lambda kv: -kv[1]["valu"]):
-    print(f"{r[:44]:44s} {c['valu']:6d} {c['salu']:6d} {c['vmem']:5d} {c['lds']:5d} {c['smem']:5d} {c['branch']:5d}")
+    print(f"{r[:44]:44s} {c['valu']:6d} {c['salu']:6d} {c['vmem']:5d} {c['lds']:5d} {c['smem']:5d} {c['branch']:5d} {c['scratch']:5d}")
 print("\nby kernel-body line\n" + hdr)
 for r, c in sorted(by_body.items(), key=lambda kv: -kv[1]["valu"])[:args.top]:
-    print(f"{r[:44]:44s} {c['valu']:6d} {c['salu']:6d} {c['vmem']:5d} {c['lds']:5d} {c['smem']:5d} {c['branch']:5d}")
+    print(f"{r[:44]:44s} {c['valu']:6d} {c['salu']:6d} {c['vmem']:5d} {c['lds']:5d} {c['smem']:5d} {c['branch']:5d} {c['scratch']:5d}")
