@@ -139,6 +139,8 @@ struct vr_ctx {
     int64_t opt_ff_window0 = 0;        // VR_OPT_FF_WINDOW0 (0: auto_window0)
     int32_t auto_window0 = 8;          // first hit-window capacity derived from the uploaded scene
     int32_t auto_nee_refill = 40;      // shadow-ray kernel refill threshold derived from the uploaded scene
+    int64_t opt_ff_kernel = 0;         // VR_OPT_FF_KERNEL (0: auto_ff_sm)
+    bool auto_ff_sm = false;           // the uploaded scene's free-flight paths take the phase-scheduled kernel
     int64_t opt_ff_nee_queue = 6;      // VR_OPT_FF_NEE_QUEUE
     int64_t opt_device_bvh = 0;        // VR_OPT_DEVICE_BVH
     int64_t opt_march_binned = 0;      // VR_OPT_MARCH_BINNED
@@ -600,6 +602,7 @@ vr_status fill_args(vr_ctx* c, const vr_camera* cam, const vr_render_params* p, 
         A.ff_min_bounces = p->min_bounces;
         A.ff_max_bounces = 1 << 16;
         A.ff_solver = (int32_t)c->opt_ff_solver;
+        A.ff_sm = c->opt_ff_kernel == 2 || (c->opt_ff_kernel == 0 && c->auto_ff_sm) ? 1 : 0;
     } else if (p->integrator != VR_TEST_HITMASK) {
         const float* d;
         int n;
@@ -1218,6 +1221,9 @@ vr_status vr_upload_scene(vr_ctx* c, const vr_scene* sc) {
         const double med = scene_median_chord_depth(s);
         c->auto_window0 = scene_window0(med, scene_overlap(s));
         c->auto_nee_refill = scene_nee_refill(med);
+        // long per-bounce collections and sweeps (many translucent Gaussians per bounce: C2's 1000_random, median
+        // 4.5) favour the phase-scheduled kernel; short ones its per-iteration scheduling cost (C3/C4/C5, main)
+        c->auto_ff_sm = N >= 256 && med > 0.0 && med < 16.0;
         std::vector<float> boxes(6 * N);
         for (int k = 0; k < 3; ++k) c->sig_max[k] = 0.0f;
         for (size_t i = 0; i < N; ++i) {
@@ -1581,6 +1587,10 @@ vr_status vr_set_option(vr_ctx* c, int32_t option, int64_t value) {
             if (value != 0 && value != 1) return fail(VR_ERR_INVALID, "VR_OPT_FF_STAGED must be 0 or 1");
             c->opt_ff_staged = value;
             return VR_OK;
+        case VR_OPT_FF_KERNEL:
+            if (value < 0 || value > 2) return fail(VR_ERR_INVALID, "VR_OPT_FF_KERNEL must be in [0, 2]");
+            c->opt_ff_kernel = value;
+            return VR_OK;
         case VR_OPT_SEC_TIGHT:
             if (value != 0 && value != 1) return fail(VR_ERR_INVALID, "VR_OPT_SEC_TIGHT must be 0 or 1");
             c->opt_sec_tight = value;
@@ -1615,6 +1625,7 @@ vr_status vr_get_option(vr_ctx* c, int32_t option, int64_t* value) {
         case VR_OPT_FF_STAGED: *value = c->opt_ff_staged; return VR_OK;
         case VR_OPT_SEC_TIGHT: *value = c->opt_sec_tight; return VR_OK;
         case VR_OPT_MARCH_WIDE_MIN: *value = c->opt_march_wide_min; return VR_OK;
+        case VR_OPT_FF_KERNEL: *value = c->opt_ff_kernel; return VR_OK;
         default: return fail(VR_ERR_INVALID, "vr_get_option: unknown option " + std::to_string(option));
     }
 }

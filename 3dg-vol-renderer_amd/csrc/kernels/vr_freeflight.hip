@@ -959,9 +959,6 @@ __global__ void __launch_bounds__(kFFBlock, VR_FF_WAVES) ff_path_kernel(RenderAr
 // the albedo and the rest of the bounce), and each wave iteration runs the ONE phase most of the wave's
 // lanes are in, with those lanes only. Every path runs ff_bounce's operations in ff_bounce's order (the
 // same RNG draws, sums and decisions), so frames are the persistent kernel's, bit for bit.
-#ifndef VR_FF_SM
-#define VR_FF_SM 0  // 1: the path kernel is ff_path_sm_kernel (A/B)
-#endif
 #ifndef VR_FFSM_EVENT_BUDGET
 #define VR_FFSM_EVENT_BUDGET 0  // active-entry evaluations a lane may spend on events per SWEEP iteration (0: one event)
 #endif
@@ -972,7 +969,7 @@ __global__ void __launch_bounds__(kFFBlock, VR_FF_WAVES) ff_path_kernel(RenderAr
 #define VR_FFSM_PPF 0  // the PRIM iterations read the next Gaussian one step ahead (A/B)
 #endif
 #ifndef VR_FFSM_NOWRITE
-#define VR_FFSM_NOWRITE 0  // the sweep recomputes F at each segment start instead of keeping it in the rows (A/B)
+#define VR_FFSM_NOWRITE 1  // the sweep recomputes F at each segment start instead of keeping it in the rows
 #endif
 #ifndef VR_FFSM_EXP
 #define VR_FFSM_EXP 0  // (diagnostic experiments only)
@@ -1497,11 +1494,6 @@ __global__ void __launch_bounds__(kFFBlock, VR_FFSM_WAVES) ff_path_sm_kernel(Ren
         flush_counters(A.work, c);
     }
 }
-#if VR_FF_SM
-#define VR_FF_PATH_KERNEL ff_path_sm_kernel
-#else
-#define VR_FF_PATH_KERNEL ff_path_kernel
-#endif
 
 // Paths the path kernel queued because more Gaussians overlapped one point than its rows hold: each
 // re-runs from its first bounce (same seed, so the same path) with kFFBigCap-entry rows and inline
@@ -2393,10 +2385,13 @@ hipError_t launch_sfd_loss_diff(const uint32_t* bits0, const uint32_t* bits1, co
 // Threads of the resident path-kernel grid on a device with `cus` CUs (the scratch row stride).
 uint32_t free_flight_threads(int cus) {
     int per_cu = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)dev::VR_FF_PATH_KERNEL<true, false>, dev::kFFBlock, 0) !=
+    int per_sm = 0;  // (both path kernels run a resident grid over the same rows: the smaller occupancy)
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)dev::ff_path_kernel<true, false>, dev::kFFBlock, 0) !=
             hipSuccess ||
-        per_cu < 1)
-        per_cu = 1;
+        hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_sm, (const void*)dev::ff_path_sm_kernel<true, false>, dev::kFFBlock, 0) !=
+            hipSuccess)
+        per_cu = per_sm = 1;
+    per_cu = std::max(1, std::min(per_cu, per_sm));
     return (uint32_t)std::max(1, cus) * (uint32_t)per_cu * (uint32_t)dev::kFFBlock;
 }
 
@@ -2464,12 +2459,20 @@ hipError_t launch_free_flight(const RenderArgs& A, uint32_t chunk_tiles, hipStre
         if (A.ff_multi) e0 = cnt ? ffs_run<true, true>(A, stream, poll) : ffs_run<true, false>(A, stream, poll);
         else e0 = cnt ? ffs_run<false, true>(A, stream, poll) : ffs_run<false, false>(A, stream, poll);
         if (e0 != hipSuccess) return e0;
+    } else if (A.ff_sm) {  // the phase-scheduled path kernel (VR_OPT_FF_KERNEL)
+        if (A.ff_multi) {
+            if (cnt) hipLaunchKernelGGL((dev::ff_path_sm_kernel<true, true>), grid, dim3(dev::kFFBlock), 0, stream, A);
+            else hipLaunchKernelGGL((dev::ff_path_sm_kernel<true>), grid, dim3(dev::kFFBlock), 0, stream, A);
+        } else {
+            if (cnt) hipLaunchKernelGGL((dev::ff_path_sm_kernel<false, true>), grid, dim3(dev::kFFBlock), 0, stream, A);
+            else hipLaunchKernelGGL((dev::ff_path_sm_kernel<false>), grid, dim3(dev::kFFBlock), 0, stream, A);
+        }
     } else if (A.ff_multi) {
-        if (cnt) hipLaunchKernelGGL((dev::VR_FF_PATH_KERNEL<true, true>), grid, dim3(dev::kFFBlock), 0, stream, A);
-        else hipLaunchKernelGGL((dev::VR_FF_PATH_KERNEL<true>), grid, dim3(dev::kFFBlock), 0, stream, A);
+        if (cnt) hipLaunchKernelGGL((dev::ff_path_kernel<true, true>), grid, dim3(dev::kFFBlock), 0, stream, A);
+        else hipLaunchKernelGGL((dev::ff_path_kernel<true>), grid, dim3(dev::kFFBlock), 0, stream, A);
     } else {
-        if (cnt) hipLaunchKernelGGL((dev::VR_FF_PATH_KERNEL<false, true>), grid, dim3(dev::kFFBlock), 0, stream, A);
-        else hipLaunchKernelGGL((dev::VR_FF_PATH_KERNEL<false>), grid, dim3(dev::kFFBlock), 0, stream, A);
+        if (cnt) hipLaunchKernelGGL((dev::ff_path_kernel<false, true>), grid, dim3(dev::kFFBlock), 0, stream, A);
+        else hipLaunchKernelGGL((dev::ff_path_kernel<false>), grid, dim3(dev::kFFBlock), 0, stream, A);
     }
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;

@@ -2917,7 +2917,10 @@ static hipError_t secondary_launch(const RenderArgs& A, hipStream_t stream) {
         e = ww_launch<S, PURE, false, false>(A, stream);
     if (e != hipSuccess) return e;
     if (!PURE) {  // PureRayMarching has no first-event-past-the-light quirk, hence no slow path
-        hipLaunchKernelGGL((dev::secondary_slow_kernel<64, S>), dim3(512), dim3(64), 0, stream, A);
+#ifndef VR_SLOW_GRID
+#define VR_SLOW_GRID 512  // workgroups of the exact slow path (grid-stride over its queue)
+#endif
+        hipLaunchKernelGGL((dev::secondary_slow_kernel<64, S>), dim3(VR_SLOW_GRID), dim3(64), 0, stream, A);
         e = hipGetLastError();
     }
     return e;

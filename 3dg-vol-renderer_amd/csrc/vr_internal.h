@@ -245,6 +245,7 @@ struct RenderArgs {
     // hit-collection, an event-sweep and a shading kernel per iteration, queued between them; the scratch
     // rows above are indexed by slot (ff_threads = ff_pool). ff_pool == 0: the persistent path kernel.
     uint32_t ff_pool;
+    int32_t ff_sm;           // persistent path kernel: 1 the phase-scheduled ff_path_sm_kernel, 0 ff_path_kernel
     float4* fs_ray0;         // per slot: {origin, target optical depth of the bounce}
     float4* fs_ray1;         // {direction, W0: start of the hit window}
     float4* fs_tp;           // {throughput, t_prev: the sweep's segment start}

@@ -27,6 +27,7 @@ VR_OPT_START_SUBTREE = 9
 VR_OPT_FF_STAGED = 10
 VR_OPT_SEC_TIGHT = 11
 VR_OPT_MARCH_WIDE_MIN = 12
+VR_OPT_FF_KERNEL = 13
 
 f3 = ctypes.c_float * 3
 

@@ -389,11 +389,18 @@ typedef enum vr_option {
                                     whitened test accepts (the shared tree's boxes are padded by 5 % for the
                                     camera rays' M-form test); 0: the shared tree. Same Gaussians, same
                                     decisions; only the order of the optical-depth sum differs. */
-    VR_OPT_MARCH_WIDE_MIN = 12   /* RayMarchingGaussians / PureRayMarching: pixels whose active set outgrew the
+    VR_OPT_MARCH_WIDE_MIN = 12,  /* RayMarchingGaussians / PureRayMarching: pixels whose active set outgrew the
                                     primary march's 16 LDS slots are marched again; a queue of at least this
                                     many pixels (default 2048) goes one pixel per lane with 64 slots in
                                     global memory, a shorter one one pixel per wave (64 LDS slots). Same
                                     operations either way: frames are identical. */
+    VR_OPT_FF_KERNEL = 13        /* free-flight integrators, persistent path kernel: 0 (default) chosen from the
+                                    uploaded scene: the phase-scheduled kernel for translucent scenes of many
+                                    Gaussians (at least 256, median central-chord optical depth below 16: long
+                                    hit collections and event sweeps per bounce), else the bounce kernel;
+                                    1: the bounce kernel (a whole bounce per lane and wave iteration);
+                                    2: the phase-scheduled kernel (each wave iteration runs the collection, sweep
+                                    or shading phase most of its lanes are in). Frames are identical. */
 } vr_option;
 vr_status vr_set_option(vr_ctx* ctx, int32_t option, int64_t value);
 vr_status vr_get_option(vr_ctx* ctx, int32_t option, int64_t* value);
