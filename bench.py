@@ -52,7 +52,7 @@ CAM_VIEW = np.array([0.0, 0.0, -1.0], np.float32)
 FOV = np.float32(0.25 * np.pi)
 HBM_PEAK_GBPS = 8000.0   # MI355X_MICROARCH.md: 8.0 TB/s spec
 FP32_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md: FP32 vector peak
-PMC_SUMMARY = "r04_c4_pmc_summary.json"  # rocprofv3 --pmc passes of this command (profiles/)
+PMC_SUMMARY = "r05_c4_pmc_summary.json"  # rocprofv3 --pmc passes of this command (profiles/)
 
 # Flops per executed operation of the secondary stage (an FMA counts 2, min / max / compare 1, and
 # sqrt / rcp / div / exp / erf 4, the quarter-rate transcendental model of SURVEY §8(d)):
@@ -84,7 +84,7 @@ def secondary_flops(sec):
 # a ray-Gaussian quadratic + intersect 72, an erf evaluation of the event sweep / cached entry factors /
 # distance solver 12 (fma 2 + div 4 + erf 4 + sub/mul 2), a shadow-ray optical depth 98.
 FF_FLOP_WEIGHTS = {"node4": 105, "node2": 44, "prim": 72, "erf": 12, "od": 98}
-FF_PMC_SUMMARY = "r04_ff_{cfg}_pmc_summary.json"  # rocprofv3 --pmc passes of the free-flight lines (profiles/)
+FF_PMC_SUMMARY = "r05_ff_{cfg}_pmc_summary.json"  # rocprofv3 --pmc passes of the free-flight lines (profiles/)
 
 
 def ff_roofline(work, stage_ms, cfg):
@@ -112,7 +112,9 @@ def ff_roofline(work, stage_ms, cfg):
     pmc_path = os.path.join(ROOT, "profiles", FF_PMC_SUMMARY.format(cfg=cfg))
     if os.path.exists(pmc_path):
         for k, d in json.load(open(pmc_path)).items():
-            if k.startswith("vr::dev::ff_path_kernel") and "hbm_read_bytes_gfx950_corrected" in d:
+            # the persistent path kernel of this scene (VR_OPT_FF_KERNEL: the bounce or the phase-scheduled one)
+            if k.startswith(("vr::dev::ff_path_kernel", "vr::dev::ff_path_sm_kernel")) and "hbm_read_bytes_gfx950_corrected" in d:
+                roof["kernel"] = "ff_path_sm_kernel" if "ff_path_sm_kernel" in k else "ff_path_kernel"
                 roof["traffic"] = d["hbm_read_bytes_gfx950_corrected"] + d.get("hbm_write_bytes", 0.0)
                 roof["traffic_unit"] = "bytes per launch"
                 roof["traffic_source"] = f"profiles/{os.path.basename(pmc_path)} (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE)"

@@ -4,8 +4,8 @@
 cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
 O=gpurun_out/pmc_ff; mkdir -p $O
 SETS=("FETCH_SIZE" "WRITE_SIZE" "SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_INSTS_SALU SQ_BUSY_CYCLES" "TCC_HIT_sum TCC_MISS_sum SQ_INSTS_VMEM_RD SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_WAVES")
-for c in ${PMC_FF_CONFIGS:-"c2 multiscatter 16" "c4 multiscatter 1" "c5 multiscatter 16" "main multiscatter 256"}; do
-  set -- $c
+for c in ${PMC_FF_CONFIGS:-c2:multiscatter:16 c4:multiscatter:1 c5:multiscatter:16 main:multiscatter:256}; do
+  set -- ${c//:/ }
   i=0
   for set in "${SETS[@]}"; do
     i=$((i+1)); mkdir -p $O/$1
