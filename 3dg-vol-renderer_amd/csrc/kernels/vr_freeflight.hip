@@ -960,7 +960,7 @@ __global__ void __launch_bounds__(kFFBlock, VR_FF_WAVES) ff_path_kernel(RenderAr
 // lanes are in, with those lanes only. Every path runs ff_bounce's operations in ff_bounce's order (the
 // same RNG draws, sums and decisions), so frames are the persistent kernel's, bit for bit.
 #ifndef VR_FFSM_EVENT_BUDGET
-#define VR_FFSM_EVENT_BUDGET 0  // active-entry evaluations a lane may spend on events per SWEEP iteration (0: one event)
+#define VR_FFSM_EVENT_BUDGET 24  // active-entry evaluations a lane may spend on events per SWEEP iteration (0: one event)
 #endif
 #ifndef VR_FFSM_PF
 #define VR_FFSM_PF 1  // the sweep reads an entry's row once and the next active entry's rows one ahead
@@ -975,7 +975,7 @@ __global__ void __launch_bounds__(kFFBlock, VR_FF_WAVES) ff_path_kernel(RenderAr
 #define VR_FFSM_EXP 0  // (diagnostic experiments only)
 #endif
 #ifndef VR_FFSM_SHADE_MIN
-#define VR_FFSM_SHADE_MIN 1  // SHADE runs when it has the most lanes and at least this many (or nothing else is left)
+#define VR_FFSM_SHADE_MIN 20  // SHADE runs when it has the most lanes and at least this many (or nothing else is left)
 #endif
 #ifndef VR_FFSM_WAVES
 #define VR_FFSM_WAVES 4  // waves per SIMD of the phase-scheduled path kernel (launch bounds)
