@@ -971,9 +971,6 @@ __global__ void __launch_bounds__(kFFBlock, VR_FF_WAVES) ff_path_kernel(RenderAr
 #ifndef VR_FFSM_NOWRITE
 #define VR_FFSM_NOWRITE 1  // the sweep recomputes F at each segment start instead of keeping it in the rows
 #endif
-#ifndef VR_FFSM_EXP
-#define VR_FFSM_EXP 0  // (diagnostic experiments only)
-#endif
 #ifndef VR_FFSM_SHADE_MIN
 #define VR_FFSM_SHADE_MIN 20  // SHADE runs when it has the most lanes and at least this many (or nothing else is left)
 #endif
@@ -1055,7 +1052,7 @@ __global__ void __launch_bounds__(kFFBlock, VR_FFSM_WAVES) ff_path_sm_kernel(Ren
         // reading the rows back (the rows live in global memory: a read there is a dependent round trip)
         int p = n;
         if (n > 0 && klast > key) {
-            while (VR_FFSM_EXP != 4 && p > 0) {
+            while (p > 0) {
                 const float4 prev = S.H(p - 1);
                 if (!(prev.x > key)) break;
                 S.H(p) = prev;
