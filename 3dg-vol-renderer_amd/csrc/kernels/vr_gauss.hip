@@ -231,7 +231,9 @@ __device__ float env_transmittance(const RenderArgs& A, const Ray& er, const Act
                  if constexpr (S) c.v[kCtrOD]++;
                  tau += optical_depth(g, q, slot >= 0 ? 0.0f : a, b);
              }
-             return true;  // (the whole walk: a missed member needs the last event)
+             // the whole walk (a missed member needs the last event) unless Tr is already 0: expf(-tau) == 0
+             // in f32 from tau >= 104, and later terms (the missed members' too) only add to tau
+             return tau < 104.0f;
          },
          [&]() {
              tau = t_last = 0.0f;
