@@ -1586,10 +1586,12 @@ __global__ void __launch_bounds__(kFFBlock) ff_nee_kernel(RenderArgs A) {
                         lim = shadow_prune_lim(tmax);
                         sum = 0.0;
                         sp = 0;
-                        node = 0;
                         qh = qn = 0;
                         j = end = 0;
-                        redo = false;
+                        // no 4-wide tree (VR_OPT_HALF_NODES = 0 or f32 boxes): the ray goes straight to the
+                        // pair-tree walk of transmittance_up_to at its completion
+                        redo = A.hnodes4 == nullptr;
+                        node = redo ? -1 : 0;
                         live = true;
                         C.add(kNeeRays);
                     }
