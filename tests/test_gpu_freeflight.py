@@ -282,21 +282,21 @@ def test_multiscatter_frame_is_deterministic(window0):
         assert np.array_equal(f, frames[0], equal_nan=True), f"frame {k}: {int((d.max(-1) > 0).sum())} pixels differ, max {np.nanmax(d):.2e}"
 
 
-@pytest.mark.parametrize("name,multi,half", [("1000_random.txt", True, 1), ("1000_random.txt", False, 1),
-                                             ("50_random.txt", True, 1), ("many_gaussians.txt", True, 1),
-                                             ("2g_altered.txt", True, 1), ("1000_random.txt", True, 0)])
-def test_phase_scheduled_kernel_equals_bounce_kernel(name, multi, half):
+@pytest.mark.parametrize("name,multi,tree", [("1000_random.txt", True, {}), ("1000_random.txt", False, {}),
+                                             ("50_random.txt", True, {}), ("many_gaussians.txt", True, {}),
+                                             ("2g_altered.txt", True, {}), ("1000_random.txt", True, {"half_nodes": 0}),
+                                             ("1000_random.txt", True, {"device_bvh": 1})])
+def test_phase_scheduled_kernel_equals_bounce_kernel(name, multi, tree):
     """VR_OPT_FF_KERNEL: the phase-scheduled path kernel (each wave iteration runs the collection, sweep or
     shading phase most of its lanes are in) and the bounce kernel run every path's operations in the same
-    order, so their frames are equal bit for bit, with a small first window (many windows) too, and without
-    the half-precision trees (VR_OPT_HALF_NODES = 0: every collection walks the f32 pair tree)."""
+    order, so their frames are equal bit for bit, with a small first window (many windows) too, without
+    the half-precision trees (VR_OPT_HALF_NODES = 0: every walk on the f32 pair tree) and on the device
+    linear BVH."""
     scene = vr.Scene.load_GMM(scene_path(name))
     cam = vr.Pinhole_Camera(CAM_POS, main_view_dir(), FOV)
     integ = vr.MultiScatterGaussians(cam, 4, 5) if multi else vr.FreeFlightGaussians(cam, 4)
     for w0 in (0, 2):
-        opts = {"ff_window0": w0} if w0 else {}
-        if not half:
-            opts["half_nodes"] = 0
+        opts = dict(tree, **({"ff_window0": w0} if w0 else {}))
         a, _ = _fresh_render(scene, integ, 96, 80, ff_kernel=1, **opts)
         b, _ = _fresh_render(scene, integ, 96, 80, ff_kernel=2, **opts)
         assert np.array_equal(a, b, equal_nan=True), f"window0 {w0}: max|d| {np.nanmax(np.abs(a - b)):.2e}"
