@@ -291,14 +291,14 @@ def test_phase_scheduled_kernel_equals_bounce_kernel(name, multi, tree):
     shading phase most of its lanes are in) and the bounce kernel run every path's operations in the same
     order, so their frames are equal bit for bit, with a small first window (many windows) too, without
     the half-precision trees (VR_OPT_HALF_NODES = 0: every walk on the f32 pair tree) and on the device
-    linear BVH."""
+    linear BVH; a ragged frame (90 x 70: tiles with pixels outside it)."""
     scene = vr.Scene.load_GMM(scene_path(name))
     cam = vr.Pinhole_Camera(CAM_POS, main_view_dir(), FOV)
     integ = vr.MultiScatterGaussians(cam, 4, 5) if multi else vr.FreeFlightGaussians(cam, 4)
     for w0 in (0, 2):
         opts = dict(tree, **({"ff_window0": w0} if w0 else {}))
-        a, _ = _fresh_render(scene, integ, 96, 80, ff_kernel=1, **opts)
-        b, _ = _fresh_render(scene, integ, 96, 80, ff_kernel=2, **opts)
+        a, _ = _fresh_render(scene, integ, 90, 70, ff_kernel=1, **opts)
+        b, _ = _fresh_render(scene, integ, 90, 70, ff_kernel=2, **opts)
         assert np.array_equal(a, b, equal_nan=True), f"window0 {w0}: max|d| {np.nanmax(np.abs(a - b)):.2e}"
 
 
