@@ -2372,6 +2372,13 @@ __global__ __launch_bounds__(BLOCK, WAVES) void secondary_ww_kernel(RenderArgs A
 #endif
 }
 
+#ifndef VR_SLOW_RPW
+#define VR_SLOW_RPW 4  // rays per wave of the exact slow path: each ray is a long dependent chain (~250 us), so a wave
+                        // of 64 lasts as long as its slowest; 64 / 16 / 4 / 1 -> 377 / 309 / 276 / 342 us per C4 frame
+#endif
+#ifdef VR_DIAG_SLOW
+__device__ uint32_t g_slow_hist[2][16], g_slow_max[2], g_slow_done;
+#endif
 // Exact three-pass light transmittance for the queued rays (see light_transmittance).
 template <int BLOCK, bool S>
 __global__ __launch_bounds__(BLOCK) void secondary_slow_kernel(RenderArgs A) {
@@ -2379,7 +2386,16 @@ __global__ __launch_bounds__(BLOCK) void secondary_slow_kernel(RenderArgs A) {
     int* stack = s_stack + threadIdx.x;
     const uint32_t n = min(A.slowq[0], A.slowq_cap);
     Ctr c{};
-    for (uint32_t q = blockIdx.x * BLOCK + threadIdx.x; q < n; q += gridDim.x * BLOCK) {
+#ifdef VR_DIAG_SLOW  // diagnostic builds only: a histogram of the rays' latencies, printed by the last block
+    uint32_t my_max = 0;
+#endif
+    // VR_SLOW_RPW rays per wave (the rest of its lanes idle): a wave lasts as long as its slowest ray
+    const uint32_t lane = threadIdx.x % 64u, wave = (blockIdx.x * BLOCK + threadIdx.x) / 64u;
+    const uint32_t q0 = lane < VR_SLOW_RPW ? wave * VR_SLOW_RPW + lane : n;
+    for (uint32_t q = q0; q < n; q += gridDim.x * (BLOCK / 64u) * VR_SLOW_RPW) {
+#ifdef VR_DIAG_SLOW
+        const uint64_t t_beg = wall_clock64();
+#endif
         const uint64_t t = A.slowq[1 + q];  // result slot (hand-out order, see tr_slot)
         const uint32_t per = rays_per_chunk(A), chunk = (uint32_t)(t / per), rem = (uint32_t)(t - (uint64_t)chunk * per);
         uint32_t s, r;
@@ -2400,7 +2416,31 @@ __global__ __launch_bounds__(BLOCK) void secondary_slow_kernel(RenderArgs A) {
             env_dir(xi1, xi2, wx, wy, wz);
             A.tr[t] = env_transmittance<S>(A, make_ray(pos.x, pos.y, pos.z, wx, wy, wz), act, stack, BLOCK, c);
         }
+#ifdef VR_DIAG_SLOW
+        const uint32_t us = (uint32_t)((wall_clock64() - t_beg) / 100);  // 100 MHz constant clock
+        const int kind = s < (uint32_t)A.num_lights;
+        atomicAdd(&g_slow_hist[kind][min(31 - __clz(us | 1), 15)], 1u);
+        atomicMax(&g_slow_max[kind], us);
+        my_max = max(my_max, us);
+#endif
     }
+#ifdef VR_DIAG_SLOW
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        __threadfence();
+        if (atomicAdd(&g_slow_done, 1u) == gridDim.x - 1) {
+            printf("slowq n=%u grid=%u max_us env %u light %u\n", n, gridDim.x, atomicAdd(&g_slow_max[0], 0u), atomicAdd(&g_slow_max[1], 0u));
+            for (int k = 0; k < 2; ++k)
+                for (int b = 0; b < 16; ++b) {
+                    const uint32_t v = atomicExch(&g_slow_hist[k][b], 0u);
+                    if (v) printf("  %s us<%u: %u\n", k ? "light" : "env", 2u << b, v);
+                }
+            atomicExch(&g_slow_max[0], 0u);
+            atomicExch(&g_slow_max[1], 0u);
+            atomicExch(&g_slow_done, 0u);
+        }
+    }
+#endif
     if constexpr (S)
         for (int i = 0; i < kNumCtr; ++i)
             if (c.v[i]) atomicAdd(A.work + kNumCtr + i, (unsigned long long)c.v[i]);
@@ -2920,7 +2960,7 @@ static hipError_t secondary_launch(const RenderArgs& A, hipStream_t stream) {
     if (e != hipSuccess) return e;
     if (!PURE) {  // PureRayMarching has no first-event-past-the-light quirk, hence no slow path
 #ifndef VR_SLOW_GRID
-#define VR_SLOW_GRID 512  // workgroups of the exact slow path (grid-stride over its queue)
+#define VR_SLOW_GRID 8192  // workgroups of the exact slow path (grid-stride over its queue; 32 k rays a pass at 4 per wave)
 #endif
         hipLaunchKernelGGL((dev::secondary_slow_kernel<64, S>), dim3(VR_SLOW_GRID), dim3(64), 0, stream, A);
         e = hipGetLastError();

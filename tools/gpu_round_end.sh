@@ -9,4 +9,6 @@ tail -1 $OUT/smoke.log | cut -c1-120
 timeout -k 10 400 python3 bench.py > $OUT/c4.json 2> $OUT/c4.log || { tail -5 $OUT/c4.log; exit 1; }
 python3 -c "import json;d=json.load(open('$OUT/c4.json'));print(round(d['value'],2), d['unit'], round(d['ms_per_step'],2), d['roofline']['frac'])"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/stats_c4 -o run --output-format csv -- python3 bench.py --steps 3 --warmup 1 --cpu-budget 0 --flops 0 > $OUT/stats_c4.log 2>&1 || { echo "stats failed"; exit 1; }
+timeout -k 10 600 python3 tools/share_balance.py --ranks 2,4,8 > $OUT/share_balance_c4.json 2> $OUT/share_balance.log || { tail -5 $OUT/share_balance.log; exit 1; }
+grep share_balance $OUT/share_balance.log
 echo done
