@@ -2373,8 +2373,9 @@ __global__ __launch_bounds__(BLOCK, WAVES) void secondary_ww_kernel(RenderArgs A
 }
 
 #ifndef VR_SLOW_RPW
-#define VR_SLOW_RPW 4  // rays per wave of the exact slow path: each ray is a long dependent chain (~250 us), so a wave
-                        // of 64 lasts as long as its slowest; 64 / 16 / 4 / 1 -> 377 / 309 / 276 / 342 us per C4 frame
+#define VR_SLOW_RPW 8  // rays per wave of the exact slow path: each ray is a long dependent chain (~250 us), so a wave
+                        // of 64 lasts as long as its slowest; 64 / 16 / 12 / 8 / 6 / 4 / 2 / 1 -> 377 / 309 / 273 / 254-270 /
+                        // 262 / 276-290 / 306 / 342 us per C4 frame
 #endif
 #ifdef VR_DIAG_SLOW
 __device__ uint32_t g_slow_hist[2][16], g_slow_max[2], g_slow_done;
@@ -2960,7 +2961,7 @@ static hipError_t secondary_launch(const RenderArgs& A, hipStream_t stream) {
     if (e != hipSuccess) return e;
     if (!PURE) {  // PureRayMarching has no first-event-past-the-light quirk, hence no slow path
 #ifndef VR_SLOW_GRID
-#define VR_SLOW_GRID 8192  // workgroups of the exact slow path (grid-stride over its queue; 32 k rays a pass at 4 per wave)
+#define VR_SLOW_GRID 4096  // workgroups of the exact slow path (grid-stride over its queue; 32 k rays a pass at 8 per wave)
 #endif
         hipLaunchKernelGGL((dev::secondary_slow_kernel<64, S>), dim3(VR_SLOW_GRID), dim3(64), 0, stream, A);
         e = hipGetLastError();
