@@ -1014,15 +1014,18 @@ vr_status launch(vr_ctx* c, RenderArgs& A, const vr_render_params* p, hipStream_
 // vr_count_work): a frame that outgrew the record buffers sized from earlier frames is rendered
 // again with grown ones; pixels / paths over every per-ray capacity fail the call.
 vr_status render_sync(vr_ctx* c, RenderArgs& A, const vr_render_params* p, bool stats, const char* what) {
-    for (int attempt = 0;; ++attempt) {
+    struct Reported {  // every exit reports this frame's outcome itself: vr_synchronize must not report it again
+        vr_ctx* c;
+        ~Reported() { c->sync_pending = false; }
+    } reported{c};
+    for (int attempt = 1;; ++attempt) {
         vr_status st = launch(c, A, p, c->stream, stats);
         if (st != VR_OK) return st;
         if ((st = collect(c)) != VR_OK) return st;
         if (!frame_exceeded(c)) break;
-        // (the queue at most doubles per attempt up to its bound, then goes inline: a handful of attempts)
-        if (attempt >= 6) return fail(VR_ERR_OVERFLOW, "scatter-record / shadow-ray queue capacity could not be sized");
+        if (attempt >= kFrameAttempts)
+            return fail(VR_ERR_OVERFLOW, "scatter-record / shadow-ray queue capacity could not be sized");
     }
-    c->sync_pending = false;  // reported here
     if (c->h_report[1] != 0)
         return fail(VR_ERR_OVERFLOW, std::to_string(c->h_report[1]) + std::string(" ") + what);
     return VR_OK;
@@ -1374,7 +1377,7 @@ vr_status vr_count_work(vr_ctx* c, const vr_camera* cam, const vr_render_params*
         if (hipMemsetAsync(d_work, 0, 16 * sizeof(unsigned long long), c->stream) != hipSuccess) break;
         st = launch(c, A, p, c->stream, true);
         if (st == VR_OK) st = collect(c);
-        if (st != VR_OK || !frame_exceeded(c) || attempt >= 3) break;
+        if (st != VR_OK || !frame_exceeded(c) || attempt + 1 >= kFrameAttempts) break;
     }
     if (st == VR_OK) {
         hipError_t e = hipMemcpy(h, d_work, sizeof(h), hipMemcpyDeviceToHost);
@@ -1667,7 +1670,8 @@ vr_status vr_get_fallback_pixels(vr_ctx* c, uint32_t* xy, size_t cap, size_t* n)
     return VR_OK;
 }
 
-vr_status vr_debug_pixel_records(vr_ctx* c, uint32_t x, uint32_t y, float* out, size_t cap, size_t* n) {
+vr_status vr_debug_pixel_records(vr_ctx* c, uint32_t x, uint32_t y, float* out, size_t cap, size_t row_in, size_t* n,
+                                 size_t* row_out) {
     c = first_device(c);
     if (!c || !n || (cap > 0 && !out)) return fail(VR_ERR_INVALID, "vr_debug_pixel_records: bad argument");
     if (!c->report_gauss) return fail(VR_ERR_INVALID, "vr_debug_pixel_records: the last frame was not a ray-march frame");
@@ -1684,6 +1688,10 @@ vr_status vr_debug_pixel_records(vr_ctx* c, uint32_t x, uint32_t y, float* out, 
     const uint32_t p = ((g - c->last_first_tile) / c->last_tile_stride) * 256u + lane;
     const uint32_t nl = (uint32_t)c->lights.size(), S = c->last_secondary_per_record, ne = S - nl, cr = 1u << VR_CHUNK_SHIFT;
     const size_t row = 9 + S;
+    if (row_out) *row_out = row;
+    if (cap > 0 && row_in != row)
+        return fail(VR_ERR_INVALID, "vr_debug_pixel_records: rows of " + std::to_string(row_in) + " floats, the frame's are " +
+                                        std::to_string(row) + " (9 + lights + env_samples)");
     uint32_t r = 0;
     HIP_TRY(hipMemcpy(&r, (uint32_t*)c->px_first.p + p, 4, hipMemcpyDeviceToHost), "hipMemcpy");
     size_t k = 0;

@@ -286,12 +286,13 @@ vr_status group_upload(vr_group* g, const vr_scene* s) {
 vr_status group_render(vr_group* g, const vr_camera* cam, const vr_render_params* p, uint32_t W, uint32_t H, float* rgb) {
     if (!cam || !p || !rgb) return fail(VR_ERR_INVALID, "vr_render: NULL argument");
     if (W == 0 || H == 0 || W > 65535 || H > 65535) return fail(VR_ERR_INVALID, "width/height must be in [1, 65535]");
-    for (int attempt = 0;; ++attempt) {
+    for (int attempt = 1;; ++attempt) {  // the same schedule as one context's render_sync (kFrameAttempts)
         bool again = false;
         vr_status st = group_frame(g, cam, p, W, H, rgb, &again);
         if (st != VR_OK) return st;
         if (!again) return VR_OK;
-        if (attempt >= 3) return fail(VR_ERR_OVERFLOW, "scatter-record capacity could not be sized");
+        if (attempt >= kFrameAttempts)
+            return fail(VR_ERR_OVERFLOW, "scatter-record / shadow-ray queue capacity could not be sized");
     }
 }
 

@@ -116,6 +116,12 @@ constexpr int kMaxSpheres = 64;
 constexpr uint32_t kFFNone = 0x7fffffffu;
 constexpr uint32_t kFFTailAfter = 0x80000000u;
 constexpr uint32_t kFFNeeMaxPerPath = 16;  // VR_OPT_FF_NEE_QUEUE bound (queue rays per path of a launch)
+// Renders of one frame before a capacity report becomes VR_ERR_OVERFLOW, shared by a context
+// (render_sync) and a group (group_render). A frame over its record buffers fits the next time (they are
+// grown to the counted need + 1/8). The shadow-ray queue starts at >= 1 ray per path and at most doubles
+// per render up to its bound (<= kFFNeeMaxPerPath rays per path: log2 16 = 4 doublings), then one
+// render traces every shadow ray inline: 1 + 4 + 1 renders, + 1 for a record-capacity retry.
+constexpr int kFrameAttempts = 7;
 constexpr int32_t kFFBigCap = 1024;          // ff_fallback_kernel: Gaussians overlapping one point it can sweep
 constexpr uint32_t kFFBigThreads = 1024;     // ff_fallback_kernel: threads (scratch row stride)
 

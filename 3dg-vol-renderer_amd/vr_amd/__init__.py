@@ -382,14 +382,15 @@ class Device:
                                            ctypes.byref(n)))
         return xy[:n.value].astype(np.int32)
 
-    def debug_pixel_records(self, x, y, rays_per_record):
+    def debug_pixel_records(self, x, y):
         """vr_debug_pixel_records: the scatter records of pixel (x, y) of the last ray-march frame, (n, 9 + S)
-        rows (S = rays_per_record = lights + env_samples): step k, position xyz, T * sigma_s, Li + Le rgb,
-        active-list length, then each secondary ray's Tr (lights, then environment samples)."""
-        n = ctypes.c_size_t()
-        check(lib().vr_debug_pixel_records(self._h, int(x), int(y), None, 0, ctypes.byref(n)))
-        out = np.zeros((max(n.value, 1), 9 + int(rays_per_record)), np.float32)
-        check(lib().vr_debug_pixel_records(self._h, int(x), int(y), fptr(out), n.value, ctypes.byref(n)))
+        rows (S = lights + env_samples, the row width the context reports): step k, position xyz,
+        T * sigma_s, Li + Le rgb, active-list length, then each secondary ray's Tr (lights, then
+        environment samples)."""
+        n, row = ctypes.c_size_t(), ctypes.c_size_t()
+        check(lib().vr_debug_pixel_records(self._h, int(x), int(y), None, 0, 0, ctypes.byref(n), ctypes.byref(row)))
+        out = np.zeros((max(n.value, 1), row.value), np.float32)
+        check(lib().vr_debug_pixel_records(self._h, int(x), int(y), fptr(out), n.value, row.value, ctypes.byref(n), None))
         return out[:n.value]
 
     OPTIONS = {"half_nodes": L.VR_OPT_HALF_NODES, "secondary_budget": L.VR_OPT_SECONDARY_BUDGET,

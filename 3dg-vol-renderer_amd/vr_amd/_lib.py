@@ -154,7 +154,7 @@ SIGNATURES = {
     "vr_get_stats": (ST, [P, ctypes.POINTER(vr_render_stats)]),
     "vr_get_fallback_pixels": (ST, [P, ctypes.POINTER(ctypes.c_uint32), ctypes.c_size_t, ctypes.POINTER(ctypes.c_size_t)]),
     "vr_debug_pixel_records": (ST, [P, ctypes.c_uint32, ctypes.c_uint32, ctypes.POINTER(ctypes.c_float), ctypes.c_size_t,
-                                    ctypes.POINTER(ctypes.c_size_t)]),
+                                    ctypes.c_size_t, ctypes.POINTER(ctypes.c_size_t), ctypes.POINTER(ctypes.c_size_t)]),
 }
 
 _lib = None

@@ -417,8 +417,11 @@ vr_status vr_get_fallback_pixels(vr_ctx* ctx, uint32_t* xy, size_t cap, size_t* 
  * RayMarchingGaussians frame in step order, one row of 9 + S floats each (S = lights + env_samples):
  * step index k, record position xyz, T * sigma_s, Li + Le (rgb), active-list length, then the
  * transmittance of each secondary ray (lights first, then environment samples, in sample order).
- * Writes up to `cap` rows into out and the record count into *n. */
-vr_status vr_debug_pixel_records(vr_ctx* ctx, uint32_t x, uint32_t y, float* out, size_t cap, size_t* n);
+ * Writes up to `cap` rows of `row` floats into out, the record count into *n and the frame's row
+ * width 9 + S into *row_out (if not NULL). With cap > 0, `row` must equal that width (VR_ERR_INVALID
+ * otherwise: a narrower buffer would be written past its end); call with cap = 0 to learn both. */
+vr_status vr_debug_pixel_records(vr_ctx* ctx, uint32_t x, uint32_t y, float* out, size_t cap, size_t row, size_t* n,
+                                 size_t* row_out);
 
 #ifdef __cplusplus
 } /* extern "C" */

@@ -147,6 +147,23 @@ class accurate_chords:
         return False
 
 
+class padded_boxes:
+    """Context manager: scenes built inside it get their BVH on the padded tight 3-sigma boxes instead of the
+    reference's eigen-derived get_aabb boxes (gaussian.h:304-319; see g_padded_boxes in vr_oracle.cpp).
+    Read when a scene is built, not when it renders."""
+
+    def __enter__(self):
+        L = lib()
+        L.orc_set_padded_boxes.argtypes = [ctypes.c_int]
+        L.orc_set_padded_boxes.restype = ctypes.c_int
+        self._old = L.orc_set_padded_boxes(1)
+        return self
+
+    def __exit__(self, *exc):
+        lib().orc_set_padded_boxes(self._old)
+        return False
+
+
 def _f(a):
     a = np.ascontiguousarray(a, dtype=np.float32)
     return a, a.ctypes.data_as(ctypes.POINTER(ctypes.c_float))
@@ -228,8 +245,10 @@ def primary_ray(cam_type, pos, view_dir, fov, x, y, W, H):
 
 
 def render(scene, cam_type, pos, view_dir, fov, W, H, integrator=RAYMARCH_GAUSSIANS, step_size=0.01,
-           env_samples=20, pixels=None, nthreads=0):
-    """Render the full W x H frame (returns H x W x 3) or only `pixels` ((n,2) int x,y; returns n x 3)."""
+           env_samples=20, pixels=None, nthreads=0, ties=None):
+    """Render the full W x H frame (returns H x W x 3) or only `pixels` ((n,2) int x,y; returns n x 3).
+    ties: an int32 array of one entry per rendered pixel that receives the pixel's count of tangent-hit ties
+    (rays on which a Gaussian's entry and exit keys are equal, so std::sort decides their order)."""
     pos, pp = _f(pos)
     vd, pv = _f(view_dir)
     if pixels is not None:
@@ -241,9 +260,18 @@ def render(scene, cam_type, pos, view_dir, fov, W, H, integrator=RAYMARCH_GAUSSI
         out = np.zeros((H, W, 3), np.float32)
         pix_p = None
         npix = 0
-    rc = lib().orc_render(scene.h, cam_type, pp, pv, float(fov), integrator, float(step_size), int(env_samples),
+    L = lib()
+    if ties is not None:
+        assert ties.dtype == np.int32 and ties.flags.c_contiguous and ties.size == (npix if pixels is not None else W * H)
+        L.orc_tie_flags.argtypes = [ctypes.POINTER(ctypes.c_int32)]
+        L.orc_tie_flags(ties.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)))
+    try:
+        rc = L.orc_render(scene.h, cam_type, pp, pv, float(fov), integrator, float(step_size), int(env_samples),
                           int(W), int(H), pix_p, npix, out.ctypes.data_as(ctypes.POINTER(ctypes.c_float)),
                           int(nthreads))
+    finally:
+        if ties is not None:
+            L.orc_tie_flags(None)
     if rc != 0:
         raise RuntimeError("oracle render failed: " + lib().orc_last_error().decode())
     return out

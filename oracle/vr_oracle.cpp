@@ -110,6 +110,163 @@ static inline float determinant3(const M3& m) {
 }
 
 // ---------------------------------------------------------------------------------------------
+// Eigen 3.4.0 SelfAdjointEigenSolver<Matrix3f>(cov) (gaussian.h:57-59), restated from Eigen's
+// published algorithm (third-party, absent here: extern/eigen-3.4.0 is an empty submodule) in f32,
+// statement for statement: SelfAdjointEigenSolver::compute (the lower triangle scaled by its largest
+// magnitude), tridiagonalization_inplace_selector<MatrixType, 3, false> (closed-form 3x3
+// Householder), computeFromTridiagonal_impl (deflation test scaled by 1/epsilon, at most 30 * n
+// implicit QR steps), tridiagonal_qr_step (Wilkinson shift through numext::hypot, Givens rotations
+// from JacobiRotation::makeGivens, Q = Q * G through applyOnTheRight), then the selection sort of the
+// eigenvalues (ascending, first minimum) with their vectors and the eigenvalues scaled back.
+// Only get_aabb (gaussian.h:304-319) reads the result here: the reference's BVH boxes.
+// ---------------------------------------------------------------------------------------------
+static inline float eig_hypot(float x, float y) {  // Eigen MathFunctions.h positive_real_hypot(|x|, |y|)
+    x = std::fabs(x);
+    y = std::fabs(y);
+    if (std::isinf(x) || std::isinf(y)) return INFINITY;
+    if (std::isnan(x) || std::isnan(y)) return NAN;
+    const float p = std::max(x, y);
+    if (p == 0.0f) return 0.0f;
+    const float qp = std::min(y, x) / p;
+    return p * std::sqrt(1.0f + qp * qp);
+}
+static inline void eig_givens(float p, float q, float& c, float& s) {  // Jacobi.h makeGivens (real)
+    if (q == 0.0f) {
+        c = p < 0.0f ? -1.0f : 1.0f;
+        s = 0.0f;
+    } else if (p == 0.0f) {
+        c = 0.0f;
+        s = q < 0.0f ? 1.0f : -1.0f;
+    } else if (std::fabs(p) > std::fabs(q)) {
+        const float t = q / p;
+        float u = std::sqrt(1.0f + t * t);
+        if (p < 0.0f) u = -u;
+        c = 1.0f / u;
+        s = -t * c;
+    } else {
+        const float t = p / q;
+        float u = std::sqrt(1.0f + t * t);
+        if (q < 0.0f) u = -u;
+        s = -1.0f / u;
+        c = -t * s;
+    }
+}
+// eigvals ascending; eigvecs column j (Q[.][j]) belongs to eigvals[j]
+static void eigen_selfadjoint3(const M3& A, float eigvals[3], float Q[3][3]) {
+    // compute(): mat = lower triangle of A, scaled
+    float L[3][3] = {{A(0, 0), 0.0f, 0.0f}, {A(1, 0), A(1, 1), 0.0f}, {A(2, 0), A(2, 1), A(2, 2)}};
+    float scale = 0.0f;
+    for (int i = 0; i < 3; ++i)
+        for (int j = 0; j < 3; ++j) scale = std::max(scale, std::fabs(L[i][j]));
+    if (scale == 0.0f) scale = 1.0f;
+    for (int i = 0; i < 3; ++i)
+        for (int j = 0; j <= i; ++j) L[i][j] /= scale;
+    // tridiagonalization_inplace_selector<MatrixType, 3, false>::run(..., extractQ = true)
+    float diag[3], sub[2];
+    const float tol = std::numeric_limits<float>::min();
+    diag[0] = L[0][0];
+    const float v1norm2 = L[2][0] * L[2][0];
+    if (v1norm2 <= tol) {
+        diag[1] = L[1][1];
+        diag[2] = L[2][2];
+        sub[0] = L[1][0];
+        sub[1] = L[2][1];
+        const float I[3][3] = {{1, 0, 0}, {0, 1, 0}, {0, 0, 1}};
+        std::memcpy(Q, I, sizeof(I));
+    } else {
+        const float beta = std::sqrt(L[1][0] * L[1][0] + v1norm2);
+        const float invBeta = 1.0f / beta;
+        const float m01 = L[1][0] * invBeta;
+        const float m02 = L[2][0] * invBeta;
+        const float q = 2.0f * m01 * L[2][1] + m02 * (L[2][2] - L[1][1]);
+        diag[1] = L[1][1] + m02 * q;
+        diag[2] = L[2][2] - m02 * q;
+        sub[0] = beta;
+        sub[1] = L[2][1] - m01 * q;
+        const float M[3][3] = {{1, 0, 0}, {0, m01, m02}, {0, m02, -m01}};
+        std::memcpy(Q, M, sizeof(M));
+    }
+    // computeFromTridiagonal_impl (maxIterations = 30)
+    const int n = 3;
+    int end = n - 1, start = 0, iter = 0;
+    const float considerAsZero = std::numeric_limits<float>::min();
+    const float precision_inv = 1.0f / std::numeric_limits<float>::epsilon();
+    bool ok = true;
+    while (end > 0) {
+        for (int i = start; i < end; ++i) {
+            if (std::fabs(sub[i]) < considerAsZero) {
+                sub[i] = 0.0f;
+            } else {
+                const float scaled = precision_inv * sub[i];
+                if (scaled * scaled <= (std::fabs(diag[i]) + std::fabs(diag[i + 1]))) sub[i] = 0.0f;
+            }
+        }
+        while (end > 0 && sub[end - 1] == 0.0f) end--;
+        if (end <= 0) break;
+        iter++;
+        if (iter > 30 * n) {
+            ok = false;
+            break;
+        }
+        start = end - 1;
+        while (start > 0 && sub[start - 1] != 0.0f) start--;
+        // tridiagonal_qr_step: Wilkinson shift
+        const float td = (diag[end - 1] - diag[end]) * 0.5f;
+        const float e = sub[end - 1];
+        float mu = diag[end];
+        if (td == 0.0f) {
+            mu -= std::fabs(e);
+        } else if (e != 0.0f) {
+            const float e2 = e * e;
+            const float h = eig_hypot(td, e);
+            if (e2 == 0.0f) mu -= e / ((td + (td > 0.0f ? h : -h)) / e);
+            else mu -= e2 / (td + (td > 0.0f ? h : -h));
+        }
+        float x = diag[start] - mu;
+        float z = sub[start];
+        for (int k = start; k < end && z != 0.0f; ++k) {
+            float c, s;
+            eig_givens(x, z, c, s);
+            const float sdk = s * diag[k] + c * sub[k];
+            const float dkp1 = s * sub[k] + c * diag[k + 1];
+            diag[k] = c * (c * diag[k] - s * sub[k]) - s * (c * sub[k] - s * diag[k + 1]);
+            diag[k + 1] = s * sdk + c * dkp1;
+            sub[k] = c * sdk - s * dkp1;
+            if (k > start) sub[k - 1] = c * sub[k - 1] - s * z;
+            x = sub[k];
+            if (k < end - 1) {
+                z = -s * sub[k + 1];
+                sub[k + 1] = c * sub[k + 1];
+            }
+            // Q.applyOnTheRight(k, k + 1, G): apply_rotation_in_the_plane(col k, col k+1, G^T), G^T = (c, -s)
+            if (!(c == 1.0f && s == 0.0f)) {
+                for (int i = 0; i < 3; ++i) {
+                    const float xi = Q[i][k], yi = Q[i][k + 1];
+                    Q[i][k] = c * xi + (-s) * yi;
+                    Q[i][k + 1] = -(-s) * xi + c * yi;
+                }
+            }
+        }
+    }
+    if (ok) {  // sort ascending (minCoeff keeps the first minimum), vectors with their values
+        for (int i = 0; i < n - 1; ++i) {
+            int k = 0;
+            float best = diag[i];
+            for (int j = 1; j < n - i; ++j)
+                if (diag[i + j] < best) {
+                    best = diag[i + j];
+                    k = j;
+                }
+            if (k > 0) {
+                std::swap(diag[i], diag[k + i]);
+                for (int r = 0; r < 3; ++r) std::swap(Q[r][i], Q[r][k + i]);
+            }
+        }
+    }
+    for (int i = 0; i < 3; ++i) eigvals[i] = diag[i] * scale;
+}
+
+// ---------------------------------------------------------------------------------------------
 // rng.h:13-57 — splitmix64, non-standard PCG32 (rotation (-rot+1u)&31 at rng.h:43), path seed.
 // ---------------------------------------------------------------------------------------------
 static inline uint64_t splitmix64(uint64_t x) {
@@ -140,6 +297,14 @@ static bool g_stable_ties = false;
 // coordinates (error linear in sqrt(c)); with this switch the restatement does so too, in double, so a
 // pixel that differs from the reference only through such a chord can be told apart (tests/helpers.py).
 static bool g_accurate_chords = false;
+// BVH boxes (test switch, orc_set_padded_boxes; read when a scene is built). The default is the reference's own
+// boxes, get_aabb (gaussian.h:304-319) from the eigen-decomposition, so the midpoint BVH (gmm.h:231-446), its
+// near-first traversal order (gmm.h:457-506) and with them std::sort's tie outcome (gmm.h:510-514) are the
+// reference's, up to the bits of Eigen's f32 eigensolver (restated below from Eigen 3.4.0's algorithm: parity
+// unpinned at that boundary). A box only culls: it also decides which fringe hits the f32 quadratic accepts
+// outside the ellipsoid the reference keeps. g_padded_boxes = true builds the tree on the padded tight 3-sigma
+// boxes instead (every such hit kept, the event set tree-independent), the oracle's rule before round 6.
+static bool g_padded_boxes = false;
 struct PCG32 {
     uint64_t state, inc;
     PCG32(uint64_t seed_state, uint64_t seed_seq) {
@@ -263,7 +428,8 @@ struct Gaussian {
     float density, albedo;
     M3 inv_cov;
     float norm;
-    V3 bmin, bmax;  // conservative AABB (see BuildBVH note)
+    V3 bmin, bmax;    // BVH box: the reference's get_aabb (gaussian.h:304-319), or the padded box (g_padded_boxes)
+    V3 tbmin, tbmax;  // padded tight 3-sigma box (B_frame binning, orc_tile_bins)
 
     Gaussian(V3 mean_, const M3& cov_, float density_, float albedo_)
         : mean(mean_), cov(cov_), density(density_), albedo(albedo_) {
@@ -271,15 +437,32 @@ struct Gaussian {
         inv_cov = inverse3(cov);
         float det_cov = determinant3(cov);
         norm = std::pow(2.0f * std::numbers::pi, -1.5f) * std::pow(det_cov, -0.5f);
-        // AABB: tight 3-sigma box of the ellipsoid, +-R*sqrt(Sigma_kk), padded. The reference
-        // derives a looser box from the eigen-decomposition (gaussian.h:304-319); both are
-        // conservative, so the BVH event SET (what the integrators consume) is identical.
+        // Tight 3-sigma box of the ellipsoid, +-R*sqrt(Sigma_kk), padded by 5 % (it holds every point the f32
+        // M-form quadratic accepts from a camera several units away).
         for (int k = 0; k < 3; ++k) {
             float h = R * std::sqrt(std::max(cov(k, k), 0.0f));
             h = h * 1.05f + 1e-6f;
-            bmin[k] = mean[k] - h;
-            bmax[k] = mean[k] + h;
+            tbmin[k] = mean[k] - h;
+            tbmax[k] = mean[k] + h;
         }
+        if (g_padded_boxes) {
+            bmin = tbmin;
+            bmax = tbmax;
+            return;
+        }
+        // gaussian.h:57-59 (SelfAdjointEigenSolver) + get_aabb gaussian.h:304-319: extents_j = R sqrt(max(l_j, 0)),
+        // h = sum_j |u_j| extents_j (u_j = column j of eigvecs, accumulated j = 0, 1, 2 from zero)
+        float ev[3], U[3][3];
+        eigen_selfadjoint3(cov, ev, U);
+        float ext[3];
+        for (int j = 0; j < 3; ++j) ext[j] = R * std::sqrt(std::max(ev[j], 0.0f));
+        V3 h{0.0f, 0.0f, 0.0f};
+        for (int j = 0; j < 3; ++j) {
+            const V3 u{std::fabs(U[0][j]), std::fabs(U[1][j]), std::fabs(U[2][j])};
+            h = h + ext[j] * u;
+        }
+        bmin = mean - h;
+        bmax = mean + h;
     }
     // gaussian.h:111-117
     float evaluate(V3 x) const {
@@ -359,6 +542,11 @@ struct Gaussian {
     }
 };
 
+// Tangent-hit ties met by the calling thread (intersect_events: a Gaussian whose entry and exit keys are equal);
+// orc_render reports them per pixel into g_tie_out when set (orc_tie_flags).
+static thread_local int64_t g_ties = 0;
+static int32_t* g_tie_out = nullptr;
+
 // smm.h:7-15
 struct PrimitiveHitEvent {
     float t;
@@ -373,6 +561,7 @@ struct PrimitiveHitEvent {
 struct GMM {
     struct Node {
         V3 bmin{INFINITY, INFINITY, INFINITY}, bmax{-INFINITY, -INFINITY, -INFINITY};
+        V3 tbmin{INFINITY, INFINITY, INFINITY}, tbmax{-INFINITY, -INFINITY, -INFINITY};  // union of the padded boxes
         uint32_t leftFirst = 0, count = 0;
         bool isLeaf() const { return count > 0; }
     };
@@ -398,13 +587,15 @@ struct GMM {
     }
     void UpdateNodeBounds(uint32_t ni) {
         Node& n = nodes[ni];
-        n.bmin = {INFINITY, INFINITY, INFINITY};
-        n.bmax = {-INFINITY, -INFINITY, -INFINITY};
+        n.bmin = n.tbmin = {INFINITY, INFINITY, INFINITY};
+        n.bmax = n.tbmax = {-INFINITY, -INFINITY, -INFINITY};
         for (uint32_t i = 0; i < n.count; ++i) {
             const Gaussian& g = gaussians[indices[n.leftFirst + i]];
             for (int k = 0; k < 3; ++k) {
                 n.bmin[k] = std::min(n.bmin[k], g.bmin[k]);
                 n.bmax[k] = std::max(n.bmax[k], g.bmax[k]);
+                n.tbmin[k] = std::min(n.tbmin[k], g.tbmin[k]);
+                n.tbmax[k] = std::max(n.tbmax[k], g.tbmax[k]);
             }
         }
     }
@@ -474,6 +665,7 @@ struct GMM {
                     if (acc ? gaussians[gidx].intersect_direct_acc(ray, t0, t1) : gaussians[gidx].intersect_direct(ray, t0, t1)) {
                         if (t0 >= 0.0f) out.push_back({t0, true, gidx});
                         if (t1 >= 0.0f) out.push_back({t1, false, gidx});
+                        if (t0 == t1) ++g_ties;  // entry and exit with equal keys: std::sort decides their order
                     }
                 }
             } else {
@@ -1613,11 +1805,13 @@ int orc_render(void* sp, int cam_type, const float* pos, const float* vd, float 
         for (int64_t q = 0; q < total; ++q) {
             int x = pix ? pix[2 * q] : (int)(q % W);
             int y = pix ? pix[2 * q + 1] : (int)(q / W);
+            g_ties = 0;
             V3 L = integrator == 0   ? rm_gaussians_pixel(*s, c, x, y, W, H, step_size, env_samples)
                    : integrator == 2 ? rm_gaussians_pixel_lists(*s, c, x, y, W, H, step_size, env_samples)
                    : integrator == 3 ? rm_pure_pixel(*s, c, x, y, W, H, step_size, env_samples)
                                      : rm_spheres_pixel(*s, c, x, y, W, H, step_size, env_samples);
             out[3 * q] = L.x; out[3 * q + 1] = L.y; out[3 * q + 2] = L.z;
+            if (g_tie_out) g_tie_out[q] = (int32_t)std::min<int64_t>(g_ties, INT32_MAX);
         }
         return 0;
     } catch (const std::exception& e) {
@@ -1726,11 +1920,11 @@ int64_t orc_tile_bins(void* sp, const float* pos, const float* vd, float fov, in
         while (!stack.empty()) {
             const GMM::Node& nd = gmm.nodes[stack.back()];
             stack.pop_back();
-            if (!overlaps(nd.bmin, nd.bmax)) continue;
+            if (!overlaps(nd.tbmin, nd.tbmax)) continue;
             if (nd.isLeaf()) {
                 for (uint32_t i = 0; i < nd.count; ++i) {
                     const Gaussian& g = gmm.gaussians[gmm.indices[nd.leftFirst + i]];
-                    if (overlaps(g.bmin, g.bmax)) ++cnt;
+                    if (overlaps(g.tbmin, g.tbmax)) ++cnt;
                 }
             } else {
                 stack.push_back(nd.leftFirst);
@@ -1869,6 +2063,9 @@ int orc_set_solver(int mode) { int o = g_solver; g_solver = mode; return o; }
 // event-sort tie order: 0 = the reference's std::sort (default), 1 = stable (see g_stable_ties)
 int orc_set_stable_ties(int on) { int o = g_stable_ties; g_stable_ties = on != 0; return o; }
 // secondary-ray chords: 0 = the reference's f32 forms (default), 1 = double (see g_accurate_chords)
+// DEBUG: orc_render writes each pixel's count of tangent-hit ties (over all its rays) into buf (NULL: off).
+void orc_tie_flags(int32_t* buf) { g_tie_out = buf; }
+int orc_set_padded_boxes(int on) { int o = g_padded_boxes; g_padded_boxes = on != 0; return o; }
 int orc_set_accurate_chords(int on) { int o = g_accurate_chords; g_accurate_chords = on != 0; return o; }
 // PCG32 output rotation: 0 = the reference's rng.h:43 (default), 1 = textbook PCG32 (see PCG32)
 int orc_set_pcg_textbook(int on) { int o = g_pcg_textbook; g_pcg_textbook = on != 0; return o; }

@@ -19,7 +19,7 @@ integ.render(scene, img)
 dev = vr.Device.get(0)
 out = {}
 for x, y in pix:
-    out[f"{x}_{y}"] = dev.debug_pixel_records(x, y, 23)
+    out[f"{x}_{y}"] = dev.debug_pixel_records(x, y)
     out[f"{x}_{y}_px"] = img.pixels[y, x]
     print((x, y), "records", len(out[f"{x}_{y}"]), "pixel", img.pixels[y, x].tolist(), flush=True)
 os.makedirs(os.path.join(ROOT, "gpurun_out"), exist_ok=True)
