@@ -42,6 +42,10 @@ hipError_t launch_unshuffle_part(const float* slabs, uint32_t first, uint32_t ns
 
 using namespace vr;
 
+// Pinned report of a frame's counts (launch): [0] fallback queue, [1] error pixels, [2..4] rec_alloc (records,
+// overflow-pool words, capacity exceeded), [5] deep queue, [6..7] counters 2..3 (free-flight fallback paths,
+// shadow-ray queue need), [8] exact slow-path queue.
+constexpr int kReportWords = 9;
 struct vr_ctx {
     int device = 0;
     hipStream_t stream = nullptr;  // used by the synchronous vr_render
@@ -84,7 +88,7 @@ struct vr_ctx {
     // [4] record capacity exceeded (the frame is invalid and must be rendered again), [5] deep-pass
     // pixels, [6] free-flight paths re-run in ff_fallback_kernel, [7] free-flight: the most shadow rays
     // one launch tried to queue
-    uint32_t* h_report = nullptr;
+    uint32_t* h_report = nullptr;  // kReportWords words: see launch()
     bool report_gauss = false;  // the last frame ran the RayMarchingGaussians pipeline (fields [2..4])
     uint64_t report_pixels = 0; // pixels of that frame (its march)
     bool march_big = false;     // this scene's frames overflow the primary march's 16 slots often: kActBig (reset at upload)
@@ -126,6 +130,7 @@ struct vr_ctx {
     int pcg_jump_n = -1;
     uint32_t* h_sizing = nullptr;  // pinned copy of rec_alloc for the sizing march of a context's first frame
     uint64_t rec_hint = 0, ovf_hint = 0;  // record / overflow-pool capacities (0: not known yet)
+    uint64_t slow_hint = 0;               // exact slow-path queue: the most rays an earlier frame queued (+ 1/8)
     uint64_t nee_hint = 0;                // deferred-NEE queue capacity from earlier free-flight frames (0: not known)
     uint32_t last_nee_cap = 0, last_nee_bound = 0;  // the last free-flight frame's queue capacity and its bound
     // A launch found the shadow-ray queue full at its VR_OPT_FF_NEE_QUEUE bound: the frame is reported
@@ -756,9 +761,11 @@ vr_status gauss_pipeline(vr_ctx* c, RenderArgs& A, hipStream_t s, bool stats) {
     A.tr = (float*)c->tr.p;
     if ((st = grow(c->rec_rad, std::max<uint64_t>(cap, 1) * 16ull, "hipMalloc(record radiance)")) != VR_OK) return st;
     A.rec_rad = (float4*)c->rec_rad.p;
-    // exact slow path: light rays (stopping event / missed member) and the rare rays with a member at its
-    // 3-sigma boundary (light or environment): up to every light ray plus one ray per record
-    const uint64_t nslow = cap * (uint64_t)A.num_lights + cap;
+    // exact slow path: light rays (stopping event / missed member), the rare rays with a member at its 3-sigma
+    // boundary and those with a chord in the f32 error band (light or environment). Sized for every light ray plus
+    // one more ray per record, or what earlier frames queued (+ 1/8); a frame that queues more (a boundary record's
+    // environment rays can all go there) raises rec_alloc[2] and is rendered again with the grown queue
+    const uint64_t nslow = std::min<uint64_t>(std::max<uint64_t>(cap * (uint64_t)A.num_lights + cap, c->slow_hint), 0xfffffffeull);
     if ((st = grow(c->slowq, (nslow + 1) * 4ull, "hipMalloc(slow queue)")) != VR_OK) return st;
     A.slowq = (uint32_t*)c->slowq.p;
     A.slowq_cap = (uint32_t)nslow;
@@ -938,9 +945,10 @@ vr_status collect(vr_ctx* c) {
     c->stats_pending = false;
     c->sync_pending = true;
     if (c->report_gauss) {
-        const uint64_t nrec = c->h_report[2], nact = c->h_report[3];
+        const uint64_t nrec = c->h_report[2], nact = c->h_report[3], nslow = c->h_report[8];
         c->rec_hint = std::max<uint64_t>(c->rec_hint, nrec + nrec / 8);
         c->ovf_hint = std::max<uint64_t>(c->ovf_hint, nact + nact / 8);
+        c->slow_hint = std::max<uint64_t>(c->slow_hint, nslow + nslow / 8);
         // >= 5 % of the pixels re-marched: the scene's active sets outgrow 16 slots; later frames march with
         // kActBig (same operations, so the frames are identical; kept until the next upload)
         if ((uint64_t)c->h_report[0] * 20ull >= c->report_pixels && c->report_pixels > 0) c->march_big = true;
@@ -996,6 +1004,7 @@ vr_status launch(vr_ctx* c, RenderArgs& A, const vr_render_params* p, hipStream_
         HIP_TRY(hipMemcpyAsync(&c->h_report[2], A.rec_alloc, 3 * sizeof(uint32_t), hipMemcpyDeviceToHost, s),
                 "hipMemcpyAsync(report)");
         HIP_TRY(hipMemcpyAsync(&c->h_report[5], A.deepq, sizeof(uint32_t), hipMemcpyDeviceToHost, s), "hipMemcpyAsync(report)");
+        HIP_TRY(hipMemcpyAsync(&c->h_report[8], A.slowq, sizeof(uint32_t), hipMemcpyDeviceToHost, s), "hipMemcpyAsync(report)");
     }
     HIP_TRY(hipMemcpyAsync(&c->h_report[6], c->d_counters + 2, 2 * sizeof(uint32_t), hipMemcpyDeviceToHost, s),
             "hipMemcpyAsync(report)");
@@ -1046,7 +1055,7 @@ vr_status vr_init(int device, vr_ctx** out) {
     c->device = device;
     if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
         hipMalloc(&c->d_counters, 4 * sizeof(uint32_t)) != hipSuccess ||
-        hipHostMalloc(&c->h_report, 8 * sizeof(uint32_t), hipHostMallocDefault) != hipSuccess ||
+        hipHostMalloc(&c->h_report, kReportWords * sizeof(uint32_t), hipHostMallocDefault) != hipSuccess ||
         hipHostMalloc(&c->h_sizing, 4 * sizeof(uint32_t), hipHostMallocDefault) != hipSuccess ||
         hipHostMalloc(&c->h_poll, 4 * sizeof(uint32_t), hipHostMallocDefault) != hipSuccess ||
         hipEventCreateWithFlags(&c->poll_ev[0], hipEventDisableTiming) != hipSuccess ||
@@ -1058,7 +1067,7 @@ vr_status vr_init(int device, vr_ctx** out) {
         vr_destroy(c);
         return fail(VR_ERR_HIP, "vr_init: failed to create stream/workspace");
     }
-    std::memset(c->h_report, 0, 8 * sizeof(uint32_t));
+    std::memset(c->h_report, 0, kReportWords * sizeof(uint32_t));
     *out = c;
     return VR_OK;
 }
@@ -1765,6 +1774,7 @@ vr_status vr_get_stats(vr_ctx* c, vr_render_stats* o) {
     o->secondary_rays = o->scatter_records * (int64_t)c->last_secondary_per_record;
     o->record_overflow = frame_exceeded(c) ? 1 : 0;
     o->deep_pixels = c->report_gauss ? (int64_t)std::min(c->h_report[5], kDeepQueue) : 0;
+    o->slow_rays = c->report_gauss ? (int64_t)c->h_report[8] : 0;
     return VR_OK;
 }
 

@@ -333,6 +333,7 @@ vr_status group_stats(vr_group* g, vr_render_stats* o) {
         o->secondary_rays += s.secondary_rays;
         o->record_overflow |= s.record_overflow;
         o->deep_pixels += s.deep_pixels;
+        o->slow_rays += s.slow_rays;
     }
     return VR_OK;
 }

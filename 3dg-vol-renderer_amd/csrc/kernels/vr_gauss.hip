@@ -58,6 +58,19 @@ constexpr float kTauCut = 104.0f;
 #define VR_MEMBER_AMB 5e-5f  // (A/B: 0 removes the test)
 #endif
 constexpr float kMemberAmb = VR_MEMBER_AMB;
+
+// Band around a secondary ray's grazing chords inside which the reference's f32 quadratic (gaussian.h:137-151:
+// B*B - 4*A*C with A = d.M.d, B = 2 p.M.d, C = p.M.p - 9) may decide otherwise than the whitened chord test: its
+// discriminant, in units of D = 9 - e2 (the chord's half length squared in whitened units), carries an absolute
+// error of up to ~5 eps c (eps = 2^-23, c = p.M.p; measured maximum 5.1 eps c over 2.3e5 grazing rays of the
+// make_random distribution, tools/chord_band.py). Inside it the reference can collapse a chord to a point or miss it
+// (C4 at t_eps 0, pixel (598, 3212): D = 3.3e-4 at c = 2735, [0.32260, 0.32282] became [0.3227114, 0.3227114] and its
+// 0.078 of optical depth was lost) or keep a tiny phantom chord the whitened test misses. A ray with a test inside
+// |D| < kChordBand c goes to the exact slow path, which runs the reference's M forms on the exactly normalised ray.
+#ifndef VR_CHORD_BAND
+#define VR_CHORD_BAND 8.0f  // in eps c (A/B: 0 removes the test)
+#endif
+constexpr float kChordBand = VR_CHORD_BAND * 1.1920928955078125e-7f;
 constexpr uint32_t kRecBoundary = 0x80000000u;  // rec_meta.w: active count | this flag
 
 // Bit of active-list slot `slot` in a ray's 64-bit hit mask. Records with more than 64 active
@@ -1560,6 +1573,19 @@ __device__ __forceinline__ void sec_add(const RenderArgs& A, SecRay& R, const GR
 #define VR_TR_STORE(A, slot, v) ((A).tr[slot] = (v))
 #endif
 
+// Hands a ray to the exact slow path (secondary_slow_kernel). A full queue raises the frame's capacity flag
+// (rec_alloc[2], as a full record buffer does): the frame is reported and rendered again with the queue grown to
+// what this one queued (the host's slow_hint), so no ray is ever lost to the queue's size.
+__device__ __forceinline__ void to_slow(const RenderArgs& A, uint32_t slot) {
+    const uint32_t q = atomicAdd(A.slowq, 1u);
+    if (q < A.slowq_cap) {
+        A.slowq[1 + q] = slot;
+    } else {
+        A.rec_alloc[2] = 1u;
+        A.tr[slot] = __builtin_nanf("");
+    }
+}
+
 // Ray complete: write its transmittance (or hand it to the exact slow path). WH: the scene's whitened
 // records (A.wrec); false: the M forms of the records (a scene with a non-positive-definite M).
 template <bool S, bool FAST, bool PURE, bool WH = !PURE>
@@ -1581,13 +1607,8 @@ __device__ __forceinline__ void sec_finish(const RenderArgs& A, SecRay& R, Ctr& 
         VR_TR_STORE(A, R.slot, 0.0f);
         return;
     }
-    if (!PURE && R.needs_stop) {  // the exact slow path: a light ray's stopping event, or a member at the boundary
-        uint32_t slot = atomicAdd(A.slowq, 1u);
-        if (slot < A.slowq_cap) A.slowq[1 + slot] = R.slot;
-        else {
-            atomicAdd(A.counters, 1u);
-            A.tr[R.slot] = __builtin_nanf("");
-        }
+    if (!PURE && R.needs_stop) {  // the exact slow path: a light ray's stopping event, a member at the boundary,
+        to_slow(A, R.slot);       // a chord in the f32 error band
         return;
     }
     if (R.act_n > 64) {  // (march_deep_kernel records) missed members: re-intersect the whole list
@@ -1614,12 +1635,7 @@ __device__ __forceinline__ void sec_finish(const RenderArgs& A, SecRay& R, Ctr& 
             else break;
         }
         if (!PURE && R.light && (R.needs_stop || any)) {
-            uint32_t slot = atomicAdd(A.slowq, 1u);
-            if (slot < A.slowq_cap) A.slowq[1 + slot] = R.slot;
-            else {
-                atomicAdd(A.counters, 1u);
-                A.tr[R.slot] = __builtin_nanf("");
-            }
+            to_slow(A, R.slot);
             return;
         }
         VR_TR_STORE(A, R.slot, expf(-R.tau));
@@ -1636,12 +1652,7 @@ __device__ __forceinline__ void sec_finish(const RenderArgs& A, SecRay& R, Ctr& 
         }
     } else if (R.light) {
         if (R.needs_stop || missed) {
-            uint32_t slot = atomicAdd(A.slowq, 1u);
-            if (slot < A.slowq_cap) A.slowq[1 + slot] = R.slot;
-            else {
-                atomicAdd(A.counters, 1u);
-                A.tr[R.slot] = __builtin_nanf("");
-            }
+            to_slow(A, R.slot);
             return;
         }
     } else {
@@ -2252,6 +2263,8 @@ __global__ __launch_bounds__(BLOCK, WAVES) void secondary_ww_kernel(RenderArgs A
             auto wtest = [&](const WRec& g, uint32_t j, int ls) {
                 if constexpr (S) c.v[ls >= 0 ? kCtrMu : kCtrPrims]++;  // list members counted apart
                 const WQuad q = wquad(g, R.ray);
+                // A chord within the reference's f32 error band (kChordBand): the exact slow path decides the ray
+                if (__builtin_expect(fabsf(9.0f - q.e2) < kChordBand * q.c, false)) R.needs_stop = true;
                 R.cmax = (ls >= 0 && q.c > R.cmax) ? q.c : R.cmax;
                 const bool cand = ls < 0 && q.c <= R.cmax;
                 // A member whose 3-sigma surface passes within rounding of the record position (or that the ray
@@ -2390,10 +2403,15 @@ __global__ __launch_bounds__(BLOCK) void secondary_slow_kernel(RenderArgs A) {
 #ifdef VR_DIAG_SLOW  // diagnostic builds only: a histogram of the rays' latencies, printed by the last block
     uint32_t my_max = 0;
 #endif
-    // VR_SLOW_RPW rays per wave (the rest of its lanes idle): a wave lasts as long as its slowest ray
+    // VR_SLOW_RPW rays per wave (the rest of its lanes idle): a wave lasts as long as its slowest ray. A queue
+    // longer than one pass at that rate (many chord-band rays) takes as many lanes per wave as one pass needs
+    // (a power of two up to 64): a second pass would cost a whole ray chain again.
     const uint32_t lane = threadIdx.x % 64u, wave = (blockIdx.x * BLOCK + threadIdx.x) / 64u;
-    const uint32_t q0 = lane < VR_SLOW_RPW ? wave * VR_SLOW_RPW + lane : n;
-    for (uint32_t q = q0; q < n; q += gridDim.x * (BLOCK / 64u) * VR_SLOW_RPW) {
+    const uint32_t waves = gridDim.x * (BLOCK / 64u);
+    uint32_t rpw = VR_SLOW_RPW;
+    while (rpw < 64u && (uint64_t)waves * rpw < n) rpw *= 2u;
+    const uint32_t q0 = lane < rpw ? wave * rpw + lane : n;
+    for (uint32_t q = q0; q < n; q += waves * rpw) {
 #ifdef VR_DIAG_SLOW
         const uint64_t t_beg = wall_clock64();
 #endif

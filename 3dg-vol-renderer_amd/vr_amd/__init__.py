@@ -201,7 +201,7 @@ class Scene:
 
     def __del__(self):
         h = getattr(self, "_h", None)
-        if h is not None and L._lib is not None:
+        if h is not None and L is not None and L._lib is not None:  # (L is None during interpreter teardown)
             L._lib.vr_scene_destroy(h)
             self._h = None
 
@@ -370,7 +370,8 @@ class Device:
         return {"kernel_ms": s.kernel_ms, "pixels": s.pixels, "fallback_pixels": s.fallback_pixels,
                 "error_pixels": s.error_pixels, "stage_ms": dict(zip(self.STAGES, list(s.stage_ms))),
                 "scatter_records": s.scatter_records, "secondary_rays": s.secondary_rays,
-                "record_overflow": bool(s.record_overflow), "deep_pixels": s.deep_pixels}
+                "record_overflow": bool(s.record_overflow), "deep_pixels": s.deep_pixels,
+                "slow_rays": s.slow_rays}
 
     def fallback_pixels(self):
         """(n, 2) int array of the (x, y) pixels of the last ray-march frame that were re-run on the
@@ -459,7 +460,7 @@ class Device:
 
     def __del__(self):
         h = getattr(self, "_h", None)
-        if h is not None and L._lib is not None:
+        if h is not None and L is not None and L._lib is not None:  # (L is None during interpreter teardown)
             L._lib.vr_destroy(h)
             self._h = None
 

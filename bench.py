@@ -286,6 +286,9 @@ def bench_sfd(args, scene, camera, W, H, t_setup):
             raise SystemExit("SFD iteration failed")
         return opt
 
+    def log(msg):
+        print(f"[bench] {msg}", file=sys.stderr, flush=True)
+
     for _ in range(args.warmup):
         one_iter()
     torch.cuda.synchronize()
@@ -295,6 +298,37 @@ def bench_sfd(args, scene, camera, W, H, t_setup):
     torch.cuda.synchronize()
     ms = (time.perf_counter() - t0) / args.steps * 1e3
     paths = 5 * W * H * args.spp
+    # Roofline of the iteration: its five forward renders (base + num_stoch_samples perturbed) are the
+    # multi-scatter path and shadow-ray kernels; the instrumented build of those kernels counts one render of the
+    # start scene (vr_count_work, untimed), x 5 over the timed iteration (the recording walks, the device BVH
+    # builds, the losses, the union statistic and Adam are counted as time, not work: a lower bound)
+    roof = None
+    if args.flops:
+        integ = vr.MultiScatterGaussians(camera, args.spp)
+        dev = vr.Device.get(integ.device)
+        dev.upload(start)
+        work = dev.count_work(camera, integ.params, W, H)
+        w, p_, n_ = FF_FLOP_WEIGHTS, work["path"], work["nee"]
+        path_fl = (w["node4"] * p_["node4_steps"] + w["node2"] * p_["node2_steps"] + w["prim"] * p_["gaussian_tests"]
+                   + w["erf"] * p_["erf_evals"])
+        nee_fl = w["node4"] * n_["node4_steps"] + w["prim"] * n_["gaussian_tests"] + w["od"] * n_["optical_depths"]
+        alg_fl = w["prim"] * (p_["gaussian_tests"] + n_["gaussian_tests"]) + w["erf"] * p_["erf_evals"] + w["od"] * n_["optical_depths"]
+        executed = 5 * (path_fl + nee_fl)
+        roof = {"bound": "valu", "unit": "TFLOP/s", "peak": FP32_PEAK_TFLOPS, "kernel": "the iteration's 5 forward renders "
+                "(ff_path_kernel / ff_path_sm_kernel + ff_nee_kernel), over the whole iteration's time",
+                "achieved": executed / (ms * 1e-3) / 1e12, "executed_flops": executed,
+                "alg_achieved": 5 * alg_fl / (ms * 1e-3) / 1e12, "alg_flops": 5 * alg_fl, "traffic": None,
+                "work_per_render": work, "flop_weights": w,
+                "flops_note": "achieved: the flops the five renders' path and shadow-ray kernels execute (node steps, "
+                              "ray-Gaussian tests, erf evaluations, optical depths of one render of the start scene, "
+                              "counted by the instrumented build of the same kernels, x flop_weights, x 5) over the "
+                              "timed iteration; alg_*: tests and integration alone (no tree steps)"}
+        roof["frac"] = roof["achieved"] / FP32_PEAK_TFLOPS
+        roof["alg_frac"] = roof["alg_achieved"] / FP32_PEAK_TFLOPS
+    cpu = None
+    if args.cpu_budget > 0:
+        cpu = cpu_baseline_sfd(start, p, W, H, args.spp, args.cpu_budget, args.cpu_threads, log)
+        cpu.update(host_cores()[1])
     print(json.dumps({
         "metric": "SFD inverse iterations/s (5 recorded multi-scatter renders each)", "value": 1e3 / ms,
         "unit": "iter/s", "n_gpus": 1, "steps": args.steps, "warmup": args.warmup, "ms_per_step": ms,
@@ -304,7 +338,52 @@ def bench_sfd(args, scene, camera, W, H, t_setup):
                    "gaussians": scene.get_num_primitives(), "integrator": "StochasticFiniteDiffInverseIntegrator",
                    "forward": "MultiScatterGaussians", "spp": args.spp, "num_stoch_samples": 4,
                    "paths_per_iter": paths, "mpaths_per_s": paths / (ms * 1e-3) / 1e6, "setup_s": t_setup,
-                   "mean_l1_loss": opt.history[-1]}}), flush=True)
+                   "mean_l1_loss": opt.history[-1]},
+        "roofline": roof,
+        "cpu_baseline": cpu}), flush=True)
+
+
+def cpu_baseline_sfd(start, params, W, H, spp, budget_s, threads, log):
+    """Config 5 on the host cores: one SFD iteration is five recorded MultiScatterGaussians renders
+    (inverse_integrator.h:115-189: the base render of the current parameters and num_stoch_samples = 4
+    renders of parameters perturbed by a sign vector x eps), each with RECORD_PIXEL_GAUSSIANS; the oracle's
+    restatement (orc_render_ms_record_px) renders the five scenes on the same uniformly random pixel sample,
+    timed and extrapolated to the whole frame. The host bookkeeping (losses, union statistic, Adam: O(N + W H))
+    is not timed. iter/s."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import pyoracle as O
+    from vr_amd import inverse as inv
+    eps = inv.make_default_eps_for_params(params)
+    scenes = [start] + [inv.apply_params(params + eps * inv.sign_vector(0, k, params.size), start.lights, start.env_color,
+                                         base=start) for k in range(4)]
+
+    def oracle_scene(sc):
+        g, ls = sc.gaussians(), sc.lights
+        return O.OracleScene.from_gaussians(g[:, 0:3], g[:, 3:9], g[:, 9], g[:, 10],
+                                            np.array([l.position for l in ls], np.float32),
+                                            np.array([l.intensity for l in ls], np.float32))
+
+    osc = [oracle_scene(sc) for sc in scenes]
+    rng = np.random.default_rng(1234)
+    done, t_total = 0, 0.0
+    batch = 2 * max(1, threads)
+    while t_total < budget_s and done < W * H:
+        idx = rng.choice(W * H, size=batch, replace=False)
+        pix = np.stack([idx % W, idx // W], 1).astype(np.int32)
+        t0 = time.perf_counter()
+        for s in osc:
+            O.render_ms_record(s, O.PINHOLE, CAM_POS, CAM_VIEW, FOV, W, H, num_samples=spp, min_bounces=5,
+                               nthreads=threads, pixels=pix)
+        t_total += time.perf_counter() - t0
+        done += batch
+        log(f"cpu baseline (SFD): {done} px x 5 renders in {t_total:.1f} s")
+    t_iter = t_total * (W * H) / done
+    return {"value": 1.0 / t_iter, "unit": "iter/s", "cores": threads, "kind": "port",
+            "seconds_per_iter": t_iter,
+            "sample": f"{done} uniformly random pixels of the {W}x{H} frame x {spp} paths x 5 recorded renders (base + 4 "
+                      f"perturbed parameter sets) in {t_total:.1f} s on {threads} OpenMP threads, extrapolated to the "
+                      f"frame (subsampled); host bookkeeping not timed; oracle restatement of the reference's "
+                      f"StochasticFiniteDiffInverseIntegrator renders"}
 
 
 def main():
@@ -326,6 +405,8 @@ def main():
                          "secondary lines (unit Mpaths/s = pixel samples per second)")
     ap.add_argument("--spp", type=int, default=None,
                     help="free-flight paths per pixel (default 16; 256 with --config main, as tests/main.cpp:27)")
+    ap.add_argument("--dump-frame", default=None,
+                    help="rank 0 saves the last timed frame (H x W x 3 f32 .npy; ray-march): multi-GPU equality tests")
     ap.add_argument("--opt", action="append", default=[],
                     help="name=value device option (vr_set_option, e.g. ff_staged=0) for A/B runs")
     args = ap.parse_args()
@@ -426,6 +507,8 @@ def main():
         raise SystemExit(f"rank {rank}: a timed frame outgrew the scatter-record buffers (sized by the warmup)")
     kernel_ms = float(np.mean([st["kernel_ms"] for st in per_step]))
     stage_ms = {k: float(np.mean([st["stage_ms"][k] for st in per_step])) for k in vr.Device.STAGES}
+    if args.dump_frame and rank == 0 and not ff:
+        np.save(args.dump_frame, frame.cpu().numpy())
     t = torch.tensor([elapsed, kernel_ms], dtype=torch.float64, device="cuda")
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)

@@ -133,6 +133,9 @@ typedef struct vr_render_stats {
                                  frames (its output is invalid; the buffers have been grown, render
                                  again). vr_render does that itself. */
     int64_t deep_pixels;      /* pixels re-run on the global-memory active-list pass (> 64 active) */
+    int64_t slow_rays;        /* RayMarchingGaussians: secondary rays traced again on the exact slow path (a light
+                                 ray's stopping event, a missed member, a member at its 3-sigma boundary, a chord
+                                 within the reference f32 quadratic's error band) */
 } vr_render_stats;
 
 typedef struct vr_scene vr_scene; /* host-side scene: primitives, lights, env colour */

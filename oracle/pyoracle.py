@@ -299,10 +299,28 @@ def render_ff(scene, cam_type, pos, view_dir, fov, W, H, multi=True, num_samples
     return out
 
 
-def render_ms_record(scene, cam_type, pos, view_dir, fov, W, H, num_samples=16, min_bounces=5, nthreads=0):
-    """MultiScatterGaussians with RECORD_PIXEL_GAUSSIANS: (image H x W x 3, bits (ceil(N/32), W*H))."""
+def render_ms_record(scene, cam_type, pos, view_dir, fov, W, H, num_samples=16, min_bounces=5, nthreads=0,
+                     pixels=None):
+    """MultiScatterGaussians with RECORD_PIXEL_GAUSSIANS: (image H x W x 3, bits (ceil(N/32), W*H)); with
+    `pixels` ((n, 2) x, y) only those: (n x 3, bits (ceil(N/32), n))."""
     pos, pp = _f(pos)
     vd, pv = _f(view_dir)
+    if pixels is not None:
+        pix = np.ascontiguousarray(np.asarray(pixels, dtype=np.int32).reshape(-1, 2))
+        out = np.zeros((pix.shape[0], 3), np.float32)
+        bits = np.zeros(((scene.num + 31) // 32, pix.shape[0]), np.uint32)
+        L = lib()
+        L.orc_render_ms_record_px.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.POINTER(ctypes.c_float),
+                                              ctypes.POINTER(ctypes.c_float), ctypes.c_float, ctypes.c_int, ctypes.c_int,
+                                              ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_int), ctypes.c_int64,
+                                              ctypes.POINTER(ctypes.c_float), ctypes.POINTER(ctypes.c_uint32), ctypes.c_int]
+        rc = L.orc_render_ms_record_px(scene.h, cam_type, pp, pv, float(fov), int(num_samples), int(min_bounces), int(W),
+                                       int(H), pix.ctypes.data_as(ctypes.POINTER(ctypes.c_int)), pix.shape[0],
+                                       out.ctypes.data_as(ctypes.POINTER(ctypes.c_float)),
+                                       bits.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32)), int(nthreads))
+        if rc != 0:
+            raise RuntimeError("oracle render failed: " + lib().orc_last_error().decode())
+        return out, bits
     out = np.zeros((H, W, 3), np.float32)
     bits = np.zeros(((scene.num + 31) // 32, W * H), np.uint32)
     rc = lib().orc_render_ms_record(scene.h, cam_type, pp, pv, float(fov), int(num_samples), int(min_bounces), int(W),

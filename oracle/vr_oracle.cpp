@@ -2096,6 +2096,31 @@ int orc_render_ms_record(void* sp, int cam_type, const float* pos, const float* 
     }
 }
 
+// orc_render_ms_record on the pixels pix[2 q], pix[2 q + 1] only (q < npix): out (npix x 3) and bits
+// ((N + 31) / 32 rows of npix words). bench.py's CPU baseline of an SFD iteration times these on a pixel sample.
+int orc_render_ms_record_px(void* sp, int cam_type, const float* pos, const float* vd, float fov, int num_samples,
+                            int min_bounces, int W, int H, const int* pix, int64_t npix, float* out, uint32_t* bits,
+                            int nthreads) {
+    try {
+        Scene* s = (Scene*)sp;
+        if (s->volume_type != 0) { g_err = "free-flight integrators need a Gaussian scene"; return 1; }
+        Camera c = cam_type == 0 ? Camera::make_pinhole({pos[0], pos[1], pos[2]}, {vd[0], vd[1], vd[2]}, fov)
+                                 : Camera::make_ortho({pos[0], pos[1], pos[2]}, {vd[0], vd[1], vd[2]});
+        if (nthreads > 0) omp_set_num_threads(nthreads);
+#pragma omp parallel for schedule(dynamic, 1)
+        for (int64_t q = 0; q < npix; ++q) {
+            std::vector<uint32_t> list;
+            V3 L = free_flight_pixel(*s, c, pix[2 * q], pix[2 * q + 1], W, H, num_samples, min_bounces, true, &list);
+            out[3 * q] = L.x; out[3 * q + 1] = L.y; out[3 * q + 2] = L.z;
+            for (uint32_t g : list) bits[(size_t)(g >> 5) * npix + q] |= 1u << (g & 31u);
+        }
+        return 0;
+    } catch (const std::exception& e) {
+        g_err = e.what();
+        return 2;
+    }
+}
+
 // FreeFlightGaussians (multi = 0, integrator.h:300-408) / MultiScatterGaussians (multi = 1,
 // integrator.h:532-717). Same pixel selection and output convention as orc_render.
 int orc_render_ff(void* sp, int cam_type, const float* pos, const float* vd, float fov, int multi, int num_samples,

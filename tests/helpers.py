@@ -36,18 +36,14 @@ def to8(img):
     return np.clip(np.asarray(img, np.float32) * np.float32(255.0), 0.0, 255.0).astype(np.uint8)
 
 
-def tie_aware_linf(got, pixels, render, tol, chords=False):
+def tie_aware_linf(got, pixels, render, tol):
     """Per-pixel L-inf of device pixels `got` ((n, 3)) against the oracle `render(pixels)` run with the
-    reference's std::sort event order and f32 arithmetic. A pixel over `tol` is re-rendered with stable tie
-    order (pyoracle.stable_ties): it is tie-dependent only if the two oracle orders disagree there, and is
-    then held to the same bar against the stable order (the device's rule). With chords=True (the
-    sparse-list restatement only), a pixel still over the bar is re-rendered with the secondary rays'
-    chords in double (pyoracle.accurate_chords): it is chord-dependent only if that changes the oracle's
-    value (the reference's f32 quadratic lost a grazing chord seen from far away, see g_accurate_chords in
-    oracle/vr_oracle.cpp) and is then held to the bar against the accurate chords (the device's whitened
-    form). Returns (max error, number of tie- or chord-dependent pixels, number of NaN mismatches, pixels
-    over the bar that are neither, the reference-order oracle pixels); the chord-dependent count is in
-    tie_aware_linf.last_chords."""
+    reference's std::sort event order (on the reference's own BVH) and f32 arithmetic. A pixel over `tol` is
+    re-rendered with stable tie order (pyoracle.stable_ties): it is tie-dependent only if the two oracle
+    orders disagree there (a tangent hit whose entry and exit keys are equal), and is then held to the same
+    bar against the stable order (the device's rule). Returns (max error, number of tie-dependent pixels,
+    number of NaN mismatches, pixels over the bar that are not tie-dependent, the reference-order oracle
+    pixels)."""
     import pyoracle as O
     got = np.asarray(got, np.float64)
     ref = np.asarray(render(pixels), np.float64)
@@ -57,7 +53,6 @@ def tie_aware_linf(got, pixels, render, tol, chords=False):
     d = np.nanmax(d, axis=-1) if d.size else np.zeros(0)
     bad = np.nonzero(d >= tol)[0]
     explained = 0
-    tie_aware_linf.last_chords = 0
     if bad.size:
         with O.stable_ties():
             ref_s = np.asarray(render(pixels[bad]), np.float64)
@@ -65,18 +60,5 @@ def tie_aware_linf(got, pixels, render, tol, chords=False):
         d_s = np.nanmax(np.abs(got[bad] - ref_s), axis=-1)
         ok = tie & (d_s < tol)
         d[bad] = np.where(tie, d_s, d[bad])
-        if chords and np.any(~ok):
-            rest = bad[~ok]
-            with O.accurate_chords():
-                ref_c = np.asarray(render(pixels[rest]), np.float64)
-            chord = np.any(ref_c != ref[rest], axis=-1)
-            d_c = np.nanmax(np.abs(got[rest] - ref_c), axis=-1)
-            ok_c = chord & (d_c < tol)
-            d[rest] = np.where(ok_c, d_c, d[rest])
-            tie_aware_linf.last_chords = int(ok_c.sum())
-            ok[~ok] = ok_c
         explained = int(ok.sum())
     return float(d.max()) if d.size else 0.0, explained, nan_mismatch, int(bad.size - explained), ref
-
-
-tie_aware_linf.last_chords = 0

@@ -113,7 +113,7 @@ def test_group_stats_sum_the_ranks():
     dev = vr.Device.get(devices)
     ranks = [dev.rank_stats(r) for r in range(len(devices))]
     assert len(st["stage_ms"]) == 4
-    for key in ("pixels", "scatter_records", "secondary_rays", "fallback_pixels", "error_pixels", "deep_pixels"):
+    for key in ("pixels", "scatter_records", "secondary_rays", "fallback_pixels", "error_pixels", "deep_pixels", "slow_rays"):
         assert st[key] == sum(r[key] for r in ranks), key
     assert st["scatter_records"] > 0
     for stage, ms in st["stage_ms"].items():
@@ -140,3 +140,103 @@ def test_c4_eight_way_split_equals_single_device():
     assert st8["scatter_records"] == st1["scatter_records"]
     assert np.array_equal(got, ref)
     vr.Device._cache.pop(devices, None)  # release the eight full-size rank contexts
+
+
+# ---- groups of distinct GPUs: RCCL between devices (runs itself on any multi-GPU box, skips on one GPU) ----
+
+def _distinct_devices():
+    n = vr.Device.count()
+    if n < 2:
+        pytest.skip(f"{n} GPU(s): the RCCL send/receive branch needs at least two distinct devices")
+    return tuple(range(min(8, n)))
+
+
+@pytest.mark.timeout(600)
+def test_c4_split_over_distinct_gpus_equals_single_device():
+    """BASELINE config 4 (4096^2, 1M make_random Gaussians, bench settings) through vr_init_multi over up to
+    eight distinct GPUs: every rank renders its interleaved tiles on its own device, ranks 1 .. N-1 ncclSend
+    their packed slabs to the root, which ncclRecvs them in one group and unshuffles them
+    (vr_multi.cpp group_frame). The reference's pixel loop is what the split shards (test_integrators.h:164):
+    the frame must equal the one-device frame bit for bit."""
+    devices = _distinct_devices()
+    scene = vr.Scene(vr.Scene.GAUSSIANS)
+    scene.add_random_gaussians(1_000_000, seed=2025, variant=0)
+    for p, i in [((0.0, 5.0, 0.1), (50.0, 0.0, 0.0)), ((-3.0, 3.0, 0.3), (0.0, 30.0, 0.0)),
+                 ((3.0, 3.0, -0.2), (0.0, 0.0, 30.0))]:
+        scene.add_light(vr.Light(p, i))
+    W = H = 4096
+    ref, st1 = _render(vr.RayMarchingGaussians, scene, W, H, 0, t_eps=1e-6)
+    got, stn = _render(vr.RayMarchingGaussians, scene, W, H, devices, t_eps=1e-6)
+    dev = vr.Device.get(devices)
+    assert dev.uses_rccl and dev.num_devices == len(devices)
+    assert st1["error_pixels"] == 0 and stn["error_pixels"] == 0
+    assert stn["scatter_records"] == st1["scatter_records"]
+    assert np.array_equal(got, ref)
+    vr.Device._cache.pop(devices, None)
+
+
+@pytest.mark.parametrize("integ,kw", [(vr.RayMarchingGaussians, {}), (vr.MultiScatterGaussians, {"samples": 4})])
+def test_group_over_distinct_gpus_equals_single_device(integ, kw):
+    """50_random.txt through a group of distinct GPUs (RCCL gather) for the ray-march and the free-flight
+    integrators, and the group statistics summed over the ranks."""
+    devices = _distinct_devices()
+    scene = vr.Scene.load_GMM(scene_path("50_random.txt"))
+    ref, _ = _render(integ, scene, 200, 150, 0, **kw)
+    got, st = _render(integ, scene, 200, 150, devices, **kw)
+    dev = vr.Device.get(devices)
+    assert dev.uses_rccl
+    assert np.array_equal(got, ref)
+    assert st["pixels"] == sum(dev.rank_stats(r)["pixels"] for r in range(len(devices)))
+
+
+@pytest.mark.timeout(600)
+def test_bench_torchrun_over_distinct_gpus_equals_one_gpu(tmp_path):
+    """bench.py --gpus N under torch.distributed.run (one process per GPU, nccl = RCCL): every rank renders
+    its interleaved tiles, the slabs reach rank 0 in one batch_isend_irecv and are unshuffled there
+    (vr_amd/tiles.py). Config 3 (1920x1080, 100k Gaussians): the gathered frame equals bench.py's one-GPU
+    frame bit for bit, and the JSON line reports N GPUs."""
+    import json
+    import socket
+    import sys
+    devices = _distinct_devices()
+    n = len(devices)
+    common = ["--config", "c3", "--steps", "1", "--warmup", "1", "--cpu-budget", "0", "--flops", "0"]
+    one = tmp_path / "one.npy"
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "1", *common, "--dump-frame", str(one)],
+                       capture_output=True, text=True, timeout=300, cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-2000:]
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    many = tmp_path / "many.npy"
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+                        "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.join(ROOT, "bench.py"),
+                        "--gpus", str(n), *common, "--dump-frame", str(many)],
+                       capture_output=True, text=True, timeout=420, cwd=ROOT, env=env)
+    assert r.returncode == 0, r.stderr[-3000:]
+    line = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
+    assert line["n_gpus"] == n and line["value"] > 0
+    assert np.array_equal(np.load(many), np.load(one))
+
+
+def test_group_first_frame_queue_grows_to_its_bound_then_inline():
+    """A fresh group sizes its first frame's shadow-ray queue as one context does (one ray per bounce up to
+    min_bounces + 1) and renders the frame again while it is outgrown: with VR_OPT_FF_NEE_QUEUE = 16 a
+    MultiScatter frame with min_bounces = 1 doubles its queue up to the bound and then traces inline, about
+    five renders. The group follows the same attempt schedule as vr_render on one context (kFrameAttempts;
+    it used to give up after four) and equals that context's frame bit for bit."""
+    import ctypes
+    scene = vr.Scene.load_GMM(scene_path("50_random.txt"))
+    integ = vr.MultiScatterGaussians(_cam(), 16, 1)
+    frames = []
+    for devices in (0, (0, 0)):
+        dev = vr.Device(devices)
+        dev.set_option("ff_nee_queue", 16)
+        dev.upload(scene)
+        out = np.empty((40, 48, 3), np.float32)
+        vr.check(vr.lib().vr_render(dev._h, ctypes.byref(integ.camera.struct), ctypes.byref(integ.params), 48, 40,
+                                    vr.fptr(out)))
+        frames.append(out)
+    assert np.array_equal(frames[0], frames[1])
