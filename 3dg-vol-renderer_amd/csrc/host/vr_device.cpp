@@ -20,14 +20,14 @@ hipError_t launch_render(const RenderArgs& A, hipStream_t stream, int volume_typ
 hipError_t gauss_march(const RenderArgs& A, hipStream_t stream, bool stats);
 hipError_t gauss_secondary(const RenderArgs& A, hipStream_t stream, bool stats);
 hipError_t gauss_accumulate(const RenderArgs& A, hipStream_t stream);
-hipError_t launch_free_flight(const RenderArgs& A, uint32_t chunk_tiles, hipStream_t stream, hipEvent_t* ev, const FFPoll& poll);
+hipError_t launch_free_flight(const RenderArgs& A, uint32_t chunk_tiles, hipStream_t stream, hipEvent_t* ev);
 uint32_t free_flight_threads(int cus);
 hipError_t launch_sfd_loss_diff(const uint32_t* bits0, const uint32_t* bits1, const float* lb, const float* lp, uint32_t npix,
                                 uint32_t n, double* out, hipStream_t stream);
 hipError_t gauss_record_cut(const RenderArgs& A, float budget, hipStream_t stream);
 hipError_t gauss_whiten(const GaussianRecord* rec, WRecord* out, uint32_t n, uint32_t* bad, hipStream_t stream);
 hipError_t gauss_bin(const RenderArgs& A, bool emit, hipStream_t stream);
-hipError_t gauss_parents(const HNode4* nodes, uint32_t n, int32_t* parent, uint4* sib, int32_t* prim_node, hipStream_t stream);
+hipError_t gauss_parents(const HNode4* nodes, uint32_t n, int32_t* parent, int32_t* prim_node, hipStream_t stream);
 hipError_t gauss_refit_secondary(const HNode4* src, HNode4* dst, uint32_t n, const GaussianRecord* rec, const int32_t* parent,
                                  uint8_t* depth, float* nbox, uint32_t* maxd, const float hc[3], float hs, float diag,
                                  hipStream_t stream);
@@ -61,7 +61,6 @@ struct vr_ctx {
     HNode4* d_hnodes4 = nullptr;
     HNode4* d_hnodes4s = nullptr;  // the secondary rays' copy with tight boxes (VR_OPT_SEC_TIGHT)
     int32_t* d_parent4 = nullptr;  // parent of every HNode4 (the secondary rays' climb out of their start subtree)
-    uint4* d_sib4 = nullptr;       // union box of every HNode4's siblings (the climb's skip test)
     int32_t* d_prim_node4 = nullptr;  // the HNode4 whose child is each record's leaf (record starts)
     size_t num_nodes4 = 0;
     float hn_center[3] = {0, 0, 0}, hn_scale = 1.0f;
@@ -119,9 +118,6 @@ struct vr_ctx {
     Buf bin_cnt, bin_off, bin_ent;  // tile bins of the binned march (VR_OPT_MARCH_BINNED)
     Buf ff_scratch, ff_tail, ff_sum, ff_nee;  // free-flight integrators (vr_freeflight.hip)
     Buf ff_fb;                                // ff_fallback_kernel: path queue + kFFBigCap rows
-    Buf ff_slots;                             // staged free-flight pipeline: per-slot path state + queues
-    uint32_t* h_poll = nullptr;               // pinned: the staged pipeline's queue-length polls
-    hipEvent_t poll_ev[2] = {nullptr, nullptr};
     uint32_t* d_order = nullptr;      // record (leaf order) -> scene index
     Buf rec_bits[2];                  // RECORD_PIXEL_GAUSSIANS bitsets (vr_render_record slots)
     uint32_t rec_npix[2] = {0, 0}, rec_n[2] = {0, 0};
@@ -151,7 +147,6 @@ struct vr_ctx {
     int64_t opt_march_binned = 0;      // VR_OPT_MARCH_BINNED
     int64_t opt_ff_solver = 0;         // VR_OPT_FF_SOLVER
     int64_t opt_start_subtree = 1;     // VR_OPT_START_SUBTREE
-    int64_t opt_ff_staged = 0;         // VR_OPT_FF_STAGED
     int64_t opt_sec_tight = 1;         // VR_OPT_SEC_TIGHT (next upload)
     int64_t opt_march_wide_min = 2048;  // VR_OPT_MARCH_WIDE_MIN
     bool last_upload_device_bvh = false;  // the current scene's tree came from the device builder
@@ -191,8 +186,6 @@ void free_scene(vr_ctx* c) {
     c->d_hnodes4s = nullptr;
     if (c->d_parent4) (void)hipFree(c->d_parent4);
     c->d_parent4 = nullptr;
-    if (c->d_sib4) (void)hipFree(c->d_sib4);
-    c->d_sib4 = nullptr;
     if (c->d_prim_node4) (void)hipFree(c->d_prim_node4);
     c->d_prim_node4 = nullptr;
     c->num_nodes4 = 0;
@@ -461,16 +454,13 @@ vr_status upload_secondary_tree(vr_ctx* c) {
 vr_status upload_parents(vr_ctx* c) {
     if (c->d_parent4) (void)hipFree(c->d_parent4);
     c->d_parent4 = nullptr;
-    if (c->d_sib4) (void)hipFree(c->d_sib4);
-    c->d_sib4 = nullptr;
     if (c->d_prim_node4) (void)hipFree(c->d_prim_node4);
     c->d_prim_node4 = nullptr;
     if (!c->d_hnodes4 || c->num_nodes4 == 0) return VR_OK;
     HIP_TRY(hipMalloc(&c->d_parent4, c->num_nodes4 * sizeof(int32_t)), "hipMalloc(wide-node parents)");
-    HIP_TRY(hipMalloc(&c->d_sib4, c->num_nodes4 * sizeof(uint4)), "hipMalloc(wide-node siblings)");
     if (c->num_prims > 0)
         HIP_TRY(hipMalloc(&c->d_prim_node4, (size_t)c->num_prims * sizeof(int32_t)), "hipMalloc(record leaf nodes)");
-    HIP_TRY(gauss_parents(c->d_hnodes4, (uint32_t)c->num_nodes4, c->d_parent4, c->d_sib4, c->d_prim_node4, c->stream),
+    HIP_TRY(gauss_parents(c->d_hnodes4, (uint32_t)c->num_nodes4, c->d_parent4, c->d_prim_node4, c->stream),
             "wide-node parents");
     HIP_TRY(hipStreamSynchronize(c->stream), "wide-node parents");
     return upload_secondary_tree(c);
@@ -577,7 +567,6 @@ vr_status fill_args(vr_ctx* c, const vr_camera* cam, const vr_render_params* p, 
     A.hn4_parent = c->d_parent4;
     A.prim_node4 = c->d_prim_node4;
     A.num_nodes4 = (uint32_t)c->num_nodes4;
-    A.hn4_sib = c->d_sib4;
     for (int k = 0; k < 3; ++k) A.hn_center[k] = c->hn_center[k];
     A.hn_scale = c->hn_scale;
     A.spheres = c->d_spheres;
@@ -830,10 +819,6 @@ vr_status gauss_pipeline(vr_ctx* c, RenderArgs& A, hipStream_t s, bool stats) {
 // launch's queued shadow rays (deferred NEE), then the paths' radiance is added to the pixels in
 // sample order (vr_freeflight.hip).
 constexpr uint64_t kFFMaxPaths = 1ull << 23;
-#ifndef VR_FF_POOL
-#define VR_FF_POOL (1u << 19)  // path slots of the staged pipeline (scratch rows: 6 KB per slot)
-#endif
-constexpr uint64_t kFFPool = VR_FF_POOL;
 // The active list indexes the hit buffer, so it never holds more than kFFHitCap entries: the only
 // capacity a path can exceed is kFFHitCap Gaussians overlapping one point; such a path re-runs in
 // ff_fallback_kernel with kFFBigCap-entry rows (only beyond that: error path, NaN).
@@ -845,10 +830,8 @@ vr_status free_flight_pipeline(vr_ctx* c, RenderArgs& A, hipStream_t s) {
     const uint32_t nsb = (uint32_t)std::min<uint64_t>(spp, kFFMaxPaths / 256u);  // samples per launch
     const uint32_t chunk = (uint32_t)std::min<uint64_t>(A.num_tiles, kFFMaxPaths / ((uint64_t)nsb * 256u));
     const uint64_t paths = (uint64_t)chunk * nsb * 256u;  // most paths of one launch
-    // staged pipeline: a pool of path slots (scratch rows per slot); else the persistent path kernel's
-    // resident grid (scratch rows per thread)
-    const uint32_t pool = c->opt_ff_staged ? (uint32_t)std::min<uint64_t>(kFFPool, paths) : 0u;
-    const uint32_t threads = pool ? pool : free_flight_threads(cus);
+    // the persistent path kernel's resident grid (scratch rows per thread)
+    const uint32_t threads = free_flight_threads(cus);
     vr_status st = grow(c->ff_scratch, (size_t)threads * (kFFHitCap + 2 * kFFActCap) * 16 + 64, "free-flight scratch");
     if (st != VR_OK) return st;
     if ((st = grow(c->ff_tail, paths * sizeof(float4), "free-flight paths")) != VR_OK) return st;
@@ -880,28 +863,6 @@ vr_status free_flight_pipeline(vr_ctx* c, RenderArgs& A, hipStream_t s) {
         A.ff_fbq = (uint32_t*)((char*)c->ff_fb.p + rows);
         A.ff_fbq_cap = (uint32_t)qcap;
     }
-    A.ff_pool = pool;
-    if (pool) {  // per-slot path state (10 x 16 B + 2 x 8 B) and four slot queues
-        const size_t P = pool;
-        if ((st = grow(c->ff_slots, P * (7 * 16 + 2 * 8 + 4 * 4) + 64, "free-flight path slots")) != VR_OK) return st;
-        char* q = (char*)c->ff_slots.p;
-        auto take = [&](size_t bytes) {
-            char* r = q;
-            q += bytes;
-            return r;
-        };
-        A.fs_ray0 = (float4*)take(P * 16);
-        A.fs_ray1 = (float4*)take(P * 16);
-        A.fs_tp = (float4*)take(P * 16);
-        A.fs_L = (float4*)take(P * 16);
-        A.fs_out = (float4*)take(P * 16);
-        A.fs_meta = (uint4*)take(P * 16);
-        A.fs_meta2 = (uint4*)take(P * 16);
-        A.fs_acc = (double*)take(P * 8);
-        A.fs_rng = (unsigned long long*)take(P * 8);
-        A.fs_q = (uint32_t*)take(P * 16);
-        A.fs_cnt = (uint32_t*)take(64);
-    }
     float4* base = (float4*)c->ff_scratch.p;
     A.ff_threads = threads;
     A.ff_hit_cap = kFFHitCap;
@@ -929,7 +890,7 @@ vr_status free_flight_pipeline(vr_ctx* c, RenderArgs& A, hipStream_t s) {
                 HIP_TRY(hipEventCreate(&e), "hipEventCreate");
                 c->ff_ev.push_back(e);
             }
-            HIP_TRY(launch_free_flight(A, nt, s, &c->ff_ev[e0], FFPoll{c->h_poll, {c->poll_ev[0], c->poll_ev[1]}}),
+            HIP_TRY(launch_free_flight(A, nt, s, &c->ff_ev[e0]),
                     "free-flight launch");
             ++c->ff_launches;
         }
@@ -1057,9 +1018,6 @@ vr_status vr_init(int device, vr_ctx** out) {
         hipMalloc(&c->d_counters, 4 * sizeof(uint32_t)) != hipSuccess ||
         hipHostMalloc(&c->h_report, kReportWords * sizeof(uint32_t), hipHostMallocDefault) != hipSuccess ||
         hipHostMalloc(&c->h_sizing, 4 * sizeof(uint32_t), hipHostMallocDefault) != hipSuccess ||
-        hipHostMalloc(&c->h_poll, 4 * sizeof(uint32_t), hipHostMallocDefault) != hipSuccess ||
-        hipEventCreateWithFlags(&c->poll_ev[0], hipEventDisableTiming) != hipSuccess ||
-        hipEventCreateWithFlags(&c->poll_ev[1], hipEventDisableTiming) != hipSuccess ||
         hipEventCreate(&c->ev_start) != hipSuccess || hipEventCreate(&c->ev_stop) != hipSuccess ||
         hipEventCreate(&c->ev_report) != hipSuccess ||
         hipEventCreate(&c->ev_stage[0]) != hipSuccess || hipEventCreate(&c->ev_stage[1]) != hipSuccess ||
@@ -1125,13 +1083,10 @@ void vr_destroy(vr_ctx* c) {
     if (c->d_counters) (void)hipFree(c->d_counters);
     if (c->h_report) (void)hipHostFree(c->h_report);
     if (c->h_sizing) (void)hipHostFree(c->h_sizing);
-    if (c->h_poll) (void)hipHostFree(c->h_poll);
-    for (hipEvent_t e : c->poll_ev)
-        if (e) (void)hipEventDestroy(e);
     for (vr_ctx::Buf* b : {&c->px_first, &c->px_T, &c->rec_pos, &c->rec_meta, &c->rec_next, &c->rec_act, &c->tr, &c->rec_rad,
                            &c->rec_alloc, &c->rec_bloom, &c->slowq, &c->pcg_jump, &c->ray_next,
                            &c->stack_ovf, &c->env_order, &c->env_base, &c->rec_cut, &c->rec_start, &c->deep, &c->bin_cnt, &c->bin_off, &c->bin_ent,
-                           &c->ff_scratch, &c->ff_tail, &c->ff_sum, &c->ff_nee, &c->ff_fb, &c->ff_slots, &c->rec_bits[0], &c->rec_bits[1],
+                           &c->ff_scratch, &c->ff_tail, &c->ff_sum, &c->ff_nee, &c->ff_fb, &c->rec_bits[0], &c->rec_bits[1],
                            &c->sfd_tmp, &c->sfd_ref, &c->sfd_loss[0], &c->sfd_loss[1], &c->sfd_out})
         if (b->p) (void)hipFree(b->p);
     if (c->d_frame) (void)hipFree(c->d_frame);
@@ -1595,10 +1550,6 @@ vr_status vr_set_option(vr_ctx* c, int32_t option, int64_t value) {
             if (value != 0 && value != 1) return fail(VR_ERR_INVALID, "VR_OPT_START_SUBTREE must be 0 or 1");
             c->opt_start_subtree = value;
             return VR_OK;
-        case VR_OPT_FF_STAGED:
-            if (value != 0 && value != 1) return fail(VR_ERR_INVALID, "VR_OPT_FF_STAGED must be 0 or 1");
-            c->opt_ff_staged = value;
-            return VR_OK;
         case VR_OPT_FF_KERNEL:
             if (value < 0 || value > 2) return fail(VR_ERR_INVALID, "VR_OPT_FF_KERNEL must be in [0, 2]");
             c->opt_ff_kernel = value;
@@ -1634,7 +1585,6 @@ vr_status vr_get_option(vr_ctx* c, int32_t option, int64_t* value) {
         case VR_OPT_MARCH_BINNED: *value = c->opt_march_binned; return VR_OK;
         case VR_OPT_FF_SOLVER: *value = c->opt_ff_solver; return VR_OK;
         case VR_OPT_START_SUBTREE: *value = c->opt_start_subtree; return VR_OK;
-        case VR_OPT_FF_STAGED: *value = c->opt_ff_staged; return VR_OK;
         case VR_OPT_SEC_TIGHT: *value = c->opt_sec_tight; return VR_OK;
         case VR_OPT_MARCH_WIDE_MIN: *value = c->opt_march_wide_min; return VR_OK;
         case VR_OPT_FF_KERNEL: *value = c->opt_ff_kernel; return VR_OK;

@@ -25,23 +25,13 @@
 #include <type_traits>
 
 #include "vr_dev_common.h"
-#ifndef VR_SOLVE_ATTR
-#define VR_SOLVE_ATTR  // (A/B) __noinline__: the double-precision analytic solver's registers stay out of the path kernels
-#endif
 
 namespace vr {
 namespace dev {
 
 constexpr int kFFBlock = 256;
-#ifndef VR_FF_ALBEDO_UNROLL
-#define VR_FF_ALBEDO_UNROLL 1  // unroll of evaluate_albedo's loop over the active list (A/B)
-#endif
-#ifndef VR_FF_SWEEP_UNROLL
-#define VR_FF_SWEEP_UNROLL 1  // unroll of the loops over the active list (A/B: independent row loads in flight)
-#endif
-#ifndef VR_FF_SWEEP_NOWRITE
-#define VR_FF_SWEEP_NOWRITE 1  // the event sweep recomputes F at each segment start instead of keeping it in the rows (C2 147.3 -> 141.1 ms)
-#endif
+// The loops over the active list stay rolled (unrolled by 4, independent row loads in flight: within +-2 %, round
+// 3); the event sweep recomputes F at each segment start instead of keeping it in the rows (C2 147.3 -> 141.1 ms).
 
 // Per-thread scratch rows (global memory, [slot][thread] so a wave's lanes touch consecutive 16-B
 // cells): every slot is one float4, so an insert shift, an entry or a cache read is ONE 16-B access
@@ -138,21 +128,11 @@ struct FFScratch {
     }
 };
 
-// The persistent path kernels' rows of thread gt. VR_FF_ROWS_WAVE: each wave's rows are one block
-// ([wave][slot][lane]: a slot of the wave is 1 KB, the wave's hit rows 128 KB), so a wave touches a few
-// pages instead of one per slot (the [slot][thread] layout puts consecutive slots ff_threads * 16 B apart).
-#ifndef VR_FF_ROWS_WAVE
-#define VR_FF_ROWS_WAVE 0
-#endif
+// The persistent path kernels' rows of thread gt ([slot][thread]; a wave-major [wave][slot][lane] layout measured
+// the same, round 5).
 template <bool CNT>
 __device__ __forceinline__ FFScratch<CNT> ff_thread_scratch(const RenderArgs& A, uint32_t gt) {
-#if VR_FF_ROWS_WAVE
-    const size_t w = gt >> 6, l = gt & 63u;
-    return FFScratch<CNT>{A.ff_hit + w * (size_t)A.ff_hit_cap * 64u + l, A.ff_act0 + w * (size_t)A.ff_act_cap * 64u + l,
-                          A.ff_act1 + w * (size_t)A.ff_act_cap * 64u + l, 64u, 0, {}};
-#else
     return FFScratch<CNT>{A.ff_hit + gt, A.ff_act0 + gt, A.ff_act1 + gt, A.ff_threads, 0, {}};
-#endif
 }
 
 // camera.h:45-53 / :64-73 for a float (u, v) (the stratified sample of integrator.h:564-568).
@@ -234,7 +214,7 @@ __device__ __forceinline__ double erfinv_approx(double x) {
 }
 
 // gaussian.h:235-297 (double)
-__device__ VR_SOLVE_ATTR bool solve_for_t_given_tau(const GRec& g, const Ray& r, float t0, float tb, float target_tau, float& t_out) {
+__device__ bool solve_for_t_given_tau(const GRec& g, const Ray& r, float t0, float tb, float target_tau, float& t_out) {
     Quad q = quad(g, r);
     double Ad = (double)q.A;
     if (!(Ad > 0.0) || !isfinite(Ad)) return false;
@@ -272,7 +252,7 @@ __device__ VR_SOLVE_ATTR bool solve_for_t_given_tau(const GRec& g, const Ray& r,
 template <class SC>
 __device__ __forceinline__ float act_tau(const RenderArgs& A, const SC& S, int m, const Ray& r, float ta, float t) {
     float s = 0.0f;  // ta is the segment start t_prev, where the cached F values were taken
-#pragma unroll VR_FF_SWEEP_UNROLL
+#pragma unroll 1
     for (int i = 0; i < m; ++i) s += S.od_to(i, t);
     return s;
 }
@@ -340,7 +320,7 @@ __device__ float solve_distance(const RenderArgs& A, const SC& S, int m, const R
 template <class SC>
 __device__ float evaluate_albedo(const RenderArgs& A, const SC& S, int m, float x, float y, float z) {
     float sum = 0.0f, sum_alb = 0.0f;
-#pragma unroll VR_FF_ALBEDO_UNROLL
+#pragma unroll 1
     for (int i = 0; i < m; ++i) {
         GRec g = load_rec(A.gauss, S.Rec(i));
         float mt = mu_t(g, x, y, z);
@@ -603,12 +583,8 @@ __device__ float free_flight_distance(const RenderArgs& A, SC& S, const Ray& r, 
         float next_exit = INFINITY;
         int exit_pos = -1;
         for (;;) {
-#if VR_FF_SWEEP_NOWRITE
             const float4 hn = i < n ? S.H(i) : make_float4(INFINITY, 0.0f, 0.0f, 0.0f);  // (the entry's row, once)
             const float next_entry = hn.x;
-#else
-            const float next_entry = i < n ? S.K(i) : INFINITY;
-#endif
             float t_evt = fminf(next_entry, next_exit);
             const bool window_end = t_cut <= t_evt;
             if (window_end) t_evt = t_cut;
@@ -620,13 +596,12 @@ __device__ float free_flight_distance(const RenderArgs& A, SC& S, const Ray& r, 
             float nx = INFINITY;  // smallest t1 after the event, and its position in the list then
             int npos = -1;
             Acc seg = 0;
-#if VR_FF_SWEEP_NOWRITE
             // F at the segment start recomputed (the same float operations as the cached value), so the
             // sweep reads 20 B per active entry (factors and exit) and writes nothing; the next entry's
             // read is in flight while this one is evaluated
             float4 cn = m > 0 ? S.A0(0) : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
             float tn = m > 0 ? S.T1(0) : 0.0f;
-#pragma unroll VR_FF_SWEEP_UNROLL
+#pragma unroll 1
             for (int a = 0; a < m; ++a) {
                 const float4 c = cn;
                 const float t1a = tn;
@@ -646,34 +621,12 @@ __device__ float free_flight_distance(const RenderArgs& A, SC& S, const Ray& r, 
                     npos = pp;
                 }
             }
-#else
-#pragma unroll VR_FF_SWEEP_UNROLL
-            for (int a = 0; a < m; ++a) {
-                const float4 c = S.A0(a);
-                float4& e1r = S.A1(a);
-                const float4 e1 = e1r;
-                S.C.add(kFFErf);
-                const float f1 = erff(__fdiv_rn(c.y + c.z * t_evt, c.w));
-                if (S.ph) e1r.x = f1;
-                else e1r.y = f1;
-                seg += (Acc)(c.x * (f1 - (S.ph ? e1.y : e1.x)));
-                int pp = a;  // position after a swap-remove of exit_pos
-                if (!is_entry && a == m - 1) pp = exit_pos;
-                const bool gone = !is_entry && a == exit_pos;
-                if (!gone && (e1.z < nx || (e1.z == nx && pp < npos))) {
-                    nx = e1.z;
-                    npos = pp;
-                }
-            }
-#endif
             if (acc + seg > (Acc)target) {
-#if VR_FF_SWEEP_NOWRITE
                 S.ph = 0;  // the solver reads F at the segment start from .x
                 for (int a = 0; a < m; ++a) {
                     const float4 c = S.A0(a);
                     S.A1(a).x = erff(__fdiv_rn(c.y + c.z * t_prev, c.w));
                 }
-#endif
                 float rem = (float)((Acc)target - acc);
                 S.lap(kFFNeeInline);  // (diagnostic builds: event sweep)
                 const uint64_t useed = A.ff_solver == kSolverUniform ? ff_path_seed(A, path) : 0ull;
@@ -683,18 +636,11 @@ __device__ float free_flight_distance(const RenderArgs& A, SC& S, const Ray& r, 
             }
             acc += seg;
             t_prev = t_evt;
-#if !VR_FF_SWEEP_NOWRITE
-            S.ph ^= 1;  // F at t_evt is now the segment start
-#endif
             if (window_end) break;
             if (is_entry) {
                 if (m >= A.ff_act_cap) return -2.0f;
-#if VR_FF_SWEEP_NOWRITE
                 const float t1n = S.template enter_row<false>(A, m, hn, r, t_evt);
                 ++i;
-#else
-                const float t1n = S.enter(A, m, i++, r, t_evt);
-#endif
                 if (t1n < nx) {  // ties: the earlier position stays first
                     nx = t1n;
                     npos = m;
@@ -962,15 +908,9 @@ __global__ void __launch_bounds__(kFFBlock, VR_FF_WAVES) ff_path_kernel(RenderAr
 #ifndef VR_FFSM_EVENT_BUDGET
 #define VR_FFSM_EVENT_BUDGET 24  // active-entry evaluations a lane may spend on events per SWEEP iteration (0: one event)
 #endif
-#ifndef VR_FFSM_PF
-#define VR_FFSM_PF 1  // the sweep reads an entry's row once and the next active entry's rows one ahead
-#endif
-#ifndef VR_FFSM_PPF
-#define VR_FFSM_PPF 0  // the PRIM iterations read the next Gaussian one step ahead (A/B)
-#endif
-#ifndef VR_FFSM_NOWRITE
-#define VR_FFSM_NOWRITE 1  // the sweep recomputes F at each segment start instead of keeping it in the rows
-#endif
+// The sweep reads an entry's row once and the next active entry's rows one ahead, and recomputes F at each segment
+// start instead of keeping it in the rows. (Measured and not kept: the PRIM iterations reading the next Gaussian one
+// step ahead, 134.8 vs 134.3 ms at C2.)
 #ifndef VR_FFSM_SHADE_MIN
 #define VR_FFSM_SHADE_MIN 20  // SHADE runs when it has the most lanes and at least this many (or nothing else is left)
 #endif
@@ -1102,13 +1042,11 @@ __global__ void __launch_bounds__(kFFBlock, VR_FFSM_WAVES) ff_path_sm_kernel(Ren
                 float ts = t_cut;
                 const int ma = m;
                 if (ma >= 0) {  // the scatter lies in [t_prev, t_cut] with kfull of the target left
-#if VR_FFSM_NOWRITE
                     S.ph = 0;  // the solver reads F at the segment start from .x
                     for (int a = 0; a < ma; ++a) {
                         const float4 c = S.A0(a);
                         reinterpret_cast<float*>(&S.A1(a))[0] = erff(__fdiv_rn(c.y + c.z * t_prev, c.w));
                     }
-#endif
                     const uint64_t useed = A.ff_solver == kSolverUniform ? ff_path_seed(A, P.out) : 0ull;
                     ts = solve_distance(A, S, ma, P.ray, t_prev, t_cut, kfull, useed, P.bounce);
                 }
@@ -1213,12 +1151,8 @@ __global__ void __launch_bounds__(kFFBlock, VR_FFSM_WAVES) ff_path_sm_kernel(Ren
             bool go = phase == kSmSweep;
             while (go) {
                 budget -= max(m, 1);
-#if VR_FFSM_PF
                 const float4 hn = i < n ? S.H(i) : make_float4(INFINITY, 0.0f, 0.0f, 0.0f);  // (the entry's row, once)
                 const float next_entry = hn.x;
-#else
-                const float next_entry = i < n ? S.K(i) : INFINITY;
-#endif
                 float t_evt = fminf(next_entry, next_exit);
                 const bool window_end = t_cut <= t_evt;
                 if (window_end) t_evt = t_cut;
@@ -1230,12 +1164,11 @@ __global__ void __launch_bounds__(kFFBlock, VR_FFSM_WAVES) ff_path_sm_kernel(Ren
                 float nx = INFINITY;
                 int npos = -1;
                 Acc seg = 0;
-#if VR_FFSM_NOWRITE
                 // F at the segment start recomputed (the cached value's own float operations: bit-identical),
                 // so the sweep reads 20 B per active entry and writes nothing; the next entry's read in flight
                 float4 cn = m > 0 ? S.A0(0) : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
                 float tn = m > 0 ? S.T1(0) : 0.0f;
-#pragma unroll VR_FF_SWEEP_UNROLL
+#pragma unroll 1
                 for (int a = 0; a < m; ++a) {
                     const float4 c = cn;
                     const float t1a = tn;
@@ -1255,40 +1188,6 @@ __global__ void __launch_bounds__(kFFBlock, VR_FFSM_WAVES) ff_path_sm_kernel(Ren
                         npos = pp;
                     }
                 }
-#else
-#if VR_FFSM_PF
-                // the next entry's rows are read before this entry's F is written (one entry ahead in flight)
-                float4 cn = m > 0 ? S.A0(0) : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-                float4 en = m > 0 ? S.A1(0) : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-#endif
-#pragma unroll VR_FF_SWEEP_UNROLL
-                for (int a = 0; a < m; ++a) {
-#if VR_FFSM_PF
-                    const float4 c = cn, e1 = en;
-                    if (a + 1 < m) {
-                        cn = S.A0(a + 1);
-                        en = S.A1(a + 1);
-                    }
-                    float4& e1r = S.A1(a);
-#else
-                    const float4 c = S.A0(a);
-                    float4& e1r = S.A1(a);
-                    const float4 e1 = e1r;
-#endif
-                    S.C.add(kFFErf);
-                    const float f1 = erff(__fdiv_rn(c.y + c.z * t_evt, c.w));
-                    if (S.ph) e1r.x = f1;
-                    else e1r.y = f1;
-                    seg += (Acc)(c.x * (f1 - (S.ph ? e1.y : e1.x)));
-                    int pp = a;
-                    if (!is_entry && a == m - 1) pp = exit_pos;
-                    const bool gone = !is_entry && a == exit_pos;
-                    if (!gone && (e1.z < nx || (e1.z == nx && pp < npos))) {
-                        nx = e1.z;
-                        npos = pp;
-                    }
-                }
-#endif
                 if (acc + seg > (Acc)target) {  // the scatter lies in [t_prev, t_evt]: SHADE solves for it
                     kfull = (float)((Acc)target - acc);
                     t_cut = t_evt;
@@ -1309,12 +1208,8 @@ __global__ void __launch_bounds__(kFFBlock, VR_FFSM_WAVES) ff_path_sm_kernel(Ren
                         to_shade(-2.0f);
                         break;
                     }
-#if VR_FFSM_PF
-                    const float t1n = S.template enter_row<!VR_FFSM_NOWRITE>(A, m, hn, P.ray, t_evt);
+                    const float t1n = S.template enter_row<false>(A, m, hn, P.ray, t_evt);
                     ++i;
-#else
-                    const float t1n = S.enter(A, m, i++, P.ray, t_evt);
-#endif
                     if (t1n < nx) {
                         nx = t1n;
                         npos = m;
@@ -1337,40 +1232,6 @@ __global__ void __launch_bounds__(kFFBlock, VR_FFSM_WAVES) ff_path_sm_kernel(Ren
             const int np = __popcll(__ballot(has_prim)), nn = __popcll(__ballot(can_node));
             if (nn == 0 || (np > 0 && np >= nn)) {  // PRIM iteration
                 bool go = has_prim;
-#if VR_FFSM_PPF
-                // software-pipelined: the next Gaussian's record is read before this one's hit is stored
-                // (a load waits for every older store of the wave)
-                GRec gn{};
-                if (go) {
-                    if (j == end) {
-                        const int32_t ref = ring[qh * kFFBlock];
-                        qh = (qh + 1) & (kCollectQueue - 1);
-                        --qn;
-                        j = leaf_first(ref);
-                        end = j + leaf_count(ref);
-                    }
-                    gn = load_rec(A.gauss, (int)j);
-                }
-                for (int k = 0; k < kCollectSteps; ++k) {
-                    if (go) {
-                        const GRec g = gn;
-                        const uint32_t jc = j++;
-                        const bool more = k + 1 < kCollectSteps && (j < end || qn > 0);
-                        if (more) {
-                            if (j == end) {
-                                const int32_t ref = ring[qh * kFFBlock];
-                                qh = (qh + 1) & (kCollectQueue - 1);
-                                --qn;
-                                j = leaf_first(ref);
-                                end = j + leaf_count(ref);
-                            }
-                            gn = load_rec(A.gauss, (int)j);
-                        }
-                        prim_g(jc, g);
-                        go = more;
-                    }
-                }
-#else
                 for (int k = 0; k < kCollectSteps; ++k) {
                     if (go) {
                         if (j == end) {
@@ -1385,7 +1246,6 @@ __global__ void __launch_bounds__(kFFBlock, VR_FFSM_WAVES) ff_path_sm_kernel(Ren
                     }
                     go = go && (j < end || qn > 0);
                 }
-#endif
             } else {  // NODE iteration (the ray's node-space slab constants, recomputed per iteration)
 #ifdef VR_DIAG_FFSM
                 dnode = true;
@@ -1670,590 +1530,6 @@ __global__ void __launch_bounds__(kFFBlock) ff_nee_kernel(RenderArgs A) {
     }
 }
 
-// =============================================================================================
-// Staged free-flight pipeline (A.ff_pool > 0). The persistent path kernel above runs a whole bounce per
-// lane — hit collection, event sweep, solver, shading — so a wave waits at every phase for its slowest
-// lane, and the kernel needs every phase's registers at once (128 VGPRs, spills). Here a pool of path
-// slots steps through one kernel per phase and iteration, the slots passed between them in queues:
-//   ffs_collect_kernel: the window's hits (the walk of free_flight_distance's collection, per-lane
-//                       refill: a lane whose walk is done takes the next queued slot);
-//   ffs_sweep_kernel:   the window's events (integrator.h:438-495), one event per lane and wave
-//                       iteration, per-lane refill, up to the segment holding the scatter;
-//   ffs_shade_kernel:   the distance solver on that segment and the albedo, then the rest of the bounce
-//                       (integrator.h:646-700: NEE, throughput, Russian roulette, the next direction)
-//                       and, for a finished path, the next path of the launch.
-// Every path runs the same operations in the same order as in ff_bounce (the same RNG draws, sums and
-// decisions), so frames are those of the persistent kernel.
-// =============================================================================================
-template <bool CNT>
-__device__ __forceinline__ FFScratch<CNT> ffs_scratch(const RenderArgs& A, uint32_t s) {
-    return FFScratch<CNT>{A.ff_hit + s, A.ff_act0 + s, A.ff_act1 + s, A.ff_pool, 0, {}};
-}
-// Append slot s to queue q (wave-aggregated: one atomic per wave of pushing lanes).
-__device__ __forceinline__ void ffs_push(const RenderArgs& A, int q, uint32_t s, bool pred) {
-    const uint64_t m = __ballot(pred);
-    if (!pred) return;
-    const uint32_t leader = (uint32_t)__ffsll((unsigned long long)m) - 1u;
-    uint32_t base = 0;
-    if (__lane_id() == leader) base = atomicAdd(A.fs_cnt + q, (uint32_t)__popcll(m));
-    base = (uint32_t)__builtin_amdgcn_readlane((int)base, (int)leader);
-    const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
-    A.fs_q[(size_t)q * A.ff_pool + base + rank] = s;
-}
-__device__ __forceinline__ PCG32 ffs_rng(unsigned long long state) {
-    PCG32 r(0ull, 1ull);  // stream 1 (inc 3); the state is the path's
-    r.state = state;
-    return r;
-}
-// A new bounce of slot s: its ray, target optical depth, window 0 from t = 0.
-__device__ __forceinline__ void ffs_begin_bounce(const RenderArgs& A, uint32_t s, const Ray& r, float target) {
-    A.fs_ray0[s] = make_float4(r.ox, r.oy, r.oz, target);
-    A.fs_ray1[s] = make_float4(r.dx, r.dy, r.dz, 0.0f);
-    A.fs_acc[s] = 0.0;
-}
-// Claims paths of the launch for slot s until one starts (a pixel outside the frame completes at once);
-// false once the launch has none left. The camera ray and the first bounce's target draw are ff_bounce's.
-template <bool CNT>
-__device__ __forceinline__ bool ffs_new_path(const RenderArgs& A, uint32_t s, FFCount<CNT>& C) {
-    for (;;) {
-        const unsigned long long pid = atomicAdd(A.ff_next, 1ull);
-        if (pid >= A.ff_total) return false;
-        C.add(kFFPaths);
-        FFPath P{PCG32(0, 1)};
-        if (!ff_start(A, (uint32_t)pid, P)) continue;
-        const float target = -logf(1.0f - P.rng.uniform());
-        C.add(kFFBounces);
-        ffs_begin_bounce(A, s, P.ray, target);
-        A.fs_tp[s] = make_float4(1.0f, 1.0f, 1.0f, 0.0f);
-        A.fs_L[s] = make_float4(0.0f, 0.0f, 0.0f, INFINITY);
-        A.fs_rng[s] = P.rng.state;
-        A.fs_meta[s] = make_uint4(P.out, kFFNone, kFFNone, 0u);
-        A.fs_meta2[s] = make_uint4(P.defer ? 1u : 0u, (uint32_t)A.ff_hit_cap0, 0u, 0u);
-        return true;
-    }
-}
-
-template <bool CNT>
-__global__ void __launch_bounds__(kFFBlock) ffs_start_kernel(RenderArgs A) {
-    FFCount<CNT> C;
-    const uint32_t s = blockIdx.x * kFFBlock + threadIdx.x;
-    const bool ok = s < A.ff_pool && ffs_new_path<CNT>(A, s, C);
-    ffs_push(A, 0, s, ok);
-    if constexpr (CNT) {
-        Ctr c{};
-        for (int i = 0; i < kFFNumCtr; ++i) c.v[i] = C.v[i];
-        flush_counters(A.work, c);
-    }
-}
-
-// The hit collection of free_flight_distance for every queued slot: the cap smallest entry keys
-// max(t0, W0) of the hits overlapping [W0, inf), sorted, in the slot's hit rows, and the window's end
-// t_cut. The walk is ff_nee_kernel's (while-while NODE / PRIM iterations, leaves through an 8-entry LDS
-// FIFO in walk order, per-lane refill); a walk whose 4-wide stack could overflow redoes the collection
-// on the pair tree (as collect_walk's caller does).
-template <bool CNT>
-__global__ void __launch_bounds__(kFFBlock) ffs_collect_kernel(RenderArgs A) {
-    FFCount<CNT> C;
-    __shared__ int s_stack[(kStackSize + kCollectQueue) * kFFBlock];
-    int* stack = s_stack + threadIdx.x;
-    int* ring = stack + kStackSize * kFFBlock;
-    const uint32_t cur = A.fs_cur, nq = A.fs_cnt[cur];
-    const uint32_t* queue = A.fs_q + (size_t)cur * A.ff_pool;
-    const uint32_t lane = threadIdx.x & 63u;
-    bool live = false, exhausted = false;
-    uint32_t s = 0;
-    Ray r{};
-    float ix = 0.0f, iy = 0.0f, iz = 0.0f, oxi = 0.0f, oyi = 0.0f, ozi = 0.0f;
-    float W0 = 0.0f, t_cut = INFINITY, kfull = INFINITY;
-    int cap = 0, n = 0, sp = 0, node = -1, qh = 0, qn = 0;
-    bool redo = false;
-    uint32_t j = 0, end = 0;
-    auto H = [&](int i) -> float4& { return A.ff_hit[(size_t)i * A.ff_pool + s]; };
-    auto prune = [&](float tmin, float tmax) {
-        if (tmax < W0 - kTPad * (1.0f + W0)) return false;
-        const float lim = fminf(t_cut, kfull);
-        return !(tmin > lim + kTPad * (1.0f + fminf(lim, 1e30f)));
-    };
-    auto prim = [&](uint32_t jj) {  // free_flight_distance's insertion, term for term
-        C.add(kFFPrims);
-        GRec g = load_rec(A.gauss, (int)jj);
-        float t0, t1;
-        if (!intersect(quad(g, r), t0, t1)) return;
-        if (!(t0 <= t1)) return;
-        if (W0 > 0.0f && !(t1 > W0)) return;
-        const float key = fmaxf(t0, W0);
-        if (key >= t_cut) return;
-        if (n == cap) {
-            if (key >= kfull) {
-                t_cut = fminf(t_cut, key);
-                return;
-            }
-            t_cut = fminf(t_cut, kfull);
-            --n;
-        }
-        int p = n;
-        while (p > 0) {
-            const float4 prev = H(p - 1);
-            if (!(prev.x > key)) break;
-            H(p) = prev;
-            --p;
-        }
-        H(p) = make_float4(key, t1, __int_as_float((int)jj), 0.0f);
-        ++n;
-        if (n == cap) kfull = H(n - 1).x;
-    };
-    for (;;) {
-        const uint64_t idle = __ballot(!live);
-        if (!exhausted && (idle == ~0ull || __popcll(idle) >= 24)) {
-            uint32_t base = 0;
-            if (lane == 0) base = atomicAdd(A.fs_cnt + 4, (uint32_t)__popcll(idle));
-            base = (uint32_t)__builtin_amdgcn_readfirstlane((int)base);
-            exhausted = base + (uint32_t)__popcll(idle) >= nq;
-            if (!live) {
-                const uint32_t k = base + __builtin_amdgcn_mbcnt_hi((uint32_t)(idle >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)idle, 0u));
-                if (k < nq) {
-                    s = queue[k];
-                    const float4 a = A.fs_ray0[s], b = A.fs_ray1[s];
-                    r = Ray{a.x, a.y, a.z, b.x, b.y, b.z};
-                    W0 = b.w;
-                    cap = (int)A.fs_meta2[s].y;
-                    n = 0;
-                    t_cut = kfull = INFINITY;
-                    float ox = r.ox, oy = r.oy, oz = r.oz;
-                    node_space<true>(A, ox, oy, oz);
-                    auto inv = [&](float d) {
-                        d *= A.hn_scale;
-                        return __frcp_rn(fabsf(d) > 1e-30f ? d : copysignf(1e-30f, d));
-                    };
-                    ix = inv(r.dx), iy = inv(r.dy), iz = inv(r.dz);
-                    oxi = ox * ix, oyi = oy * iy, ozi = oz * iz;
-                    sp = 0;
-                    node = 0;
-                    qh = qn = 0;
-                    j = end = 0;
-                    redo = A.hnodes4 == nullptr;  // no 4-wide tree: the pair-tree walk at once
-                    live = true;
-                }
-            }
-        }
-        if (!__any(live)) {
-            if (exhausted) break;
-            continue;
-        }
-        const bool walking = live && !redo;
-        const bool has_prim = walking && (j < end || qn > 0);
-        const bool can_node = walking && node >= 0 && qn <= kCollectQueue - 4;
-        const int np = __popcll(__ballot(has_prim)), nn = __popcll(__ballot(can_node));
-        if (nn == 0 || (np > 0 && np >= nn)) {  // PRIM iteration
-            bool go = has_prim;
-            for (int k = 0; k < kCollectSteps; ++k) {
-                if (go) {
-                    if (j == end) {
-                        const int32_t ref = ring[qh * kFFBlock];
-                        qh = (qh + 1) & (kCollectQueue - 1);
-                        --qn;
-                        j = leaf_first(ref);
-                        end = j + leaf_count(ref);
-                    }
-                    prim(j);
-                    ++j;
-                }
-                go = go && (j < end || qn > 0);
-            }
-        } else {  // NODE iteration
-            bool go = can_node;
-            for (int k = 0; k < kCollectSteps; ++k) {
-                if (go) {
-                    C.add(kFFNode4);
-                    float key[4];
-                    int32_t kr[4];
-                    wide_children(A, node, ix, iy, iz, oxi, oyi, ozi, prune, key, kr);
-#pragma unroll
-                    for (int i = 0; i < 4; ++i)
-                        if (kr[i] < 0) {
-                            ring[((qh + qn) & (kCollectQueue - 1)) * kFFBlock] = kr[i];
-                            ++qn;
-                        }
-                    int first = -1;
-                    int32_t next = 0;
-#pragma unroll
-                    for (int i = 3; i >= 0; --i) {
-                        first = kr[i] > 0 ? i : first;
-                        next = kr[i] > 0 ? kr[i] : next;
-                    }
-                    if (sp + 3 > kStackSize) {
-                        redo = true;
-                        node = -1;
-                    } else {
-#pragma unroll
-                        for (int i = 3; i >= 0; --i)
-                            if (kr[i] > 0 && i != first) stack[(sp++) * kFFBlock] = kr[i];
-                        if (first >= 0) node = next;
-                        else if (sp > 0) node = stack[(--sp) * kFFBlock];
-                        else node = -1;
-                    }
-                }
-                go = go && node >= 0 && qn <= kCollectQueue - 4 && !redo;
-            }
-        }
-        const bool done = live && (redo || (node < 0 && j == end && qn == 0));
-        if (done) {
-            if (redo) {  // the pair tree (at most one push per level) redoes the whole collection
-                n = 0;
-                t_cut = kfull = INFINITY;
-                auto leaf = [&](uint32_t first, uint32_t count) {
-                    for (uint32_t jj = first; jj < first + count; ++jj) prim(jj);
-                    return true;
-                };
-                auto on2 = [&]() { C.add(kFFNode2); };
-                if (A.hnodes) traverse<true>(A, r, stack, kFFBlock, prune, leaf, on2);
-                else traverse<false>(A, r, stack, kFFBlock, prune, leaf, on2);
-            }
-            // a buffer that filled ends the window at its largest kept key (subtrees skipped while full hold
-            // only larger keys; whether one was skipped depends on the wave's NODE/PRIM schedule, so the cut must not)
-            if (n == cap) t_cut = fminf(t_cut, H(n - 1).x);
-            while (n > 0 && H(n - 1).x >= t_cut) --n;
-            reinterpret_cast<float*>(A.fs_L + s)[3] = t_cut;
-            reinterpret_cast<uint32_t*>(A.fs_meta2 + s)[2] = (uint32_t)n;
-            live = false;
-        }
-        ffs_push(A, 2, s, done);
-    }
-    if constexpr (CNT) {
-        Ctr c{};
-        for (int i = 0; i < kFFNumCtr; ++i) c.v[i] = C.v[i];
-        flush_counters(A.work, c);
-    }
-}
-
-// The event sweep of free_flight_distance for every queued slot, one event per lane and wave iteration
-// (per-lane refill). Outcomes: the segment holding the scatter ({t_prev, t_evt, target left, m | ph <<
-// 16}, to the shading queue), the window's end (the next window's collection, next iteration), no
-// scatter (-1) or a capacity exceeded (-2), both to the shading queue ({ts, -, -, -1}).
-#ifndef VR_FFS_EVENT_BUDGET
-#define VR_FFS_EVENT_BUDGET 0  // active-entry evaluations a lane may spend on events per wave iteration (0: one event)
-#endif
-constexpr int kFFSEventBudget = VR_FFS_EVENT_BUDGET;
-#ifndef VR_FFS_SWEEP_WAVES
-#define VR_FFS_SWEEP_WAVES 6  // waves per SIMD of the sweep kernel (launch bounds)
-#endif
-template <bool MULTI, bool CNT>
-__global__ void __launch_bounds__(kFFBlock, VR_FFS_SWEEP_WAVES) ffs_sweep_kernel(RenderArgs A) {
-    using Acc = typename std::conditional<MULTI, double, float>::type;
-    const uint32_t nq = A.fs_cnt[2];
-    const uint32_t* queue = A.fs_q + (size_t)2 * A.ff_pool;
-    const int nxt = (int)(A.fs_cur ^ 1u);
-    const uint32_t lane = threadIdx.x & 63u;
-    FFScratch<CNT> S = ffs_scratch<CNT>(A, 0);
-    bool live = false, exhausted = false;
-    uint32_t s = 0;
-    Ray r{};
-    float target = 0.0f, t_prev = 0.0f, W0 = 0.0f, t_cut = INFINITY, next_exit = INFINITY;
-    Acc acc = 0;
-    int cap = 0, n = 0, i = 0, m = 0, exit_pos = -1;
-    for (;;) {
-        const uint64_t idle = __ballot(!live);
-        bool to_shade = false, to_collect = false;
-        if (!exhausted && (idle == ~0ull || __popcll(idle) >= 16)) {
-            uint32_t base = 0;
-            if (lane == 0) base = atomicAdd(A.fs_cnt + 5, (uint32_t)__popcll(idle));
-            base = (uint32_t)__builtin_amdgcn_readfirstlane((int)base);
-            exhausted = base + (uint32_t)__popcll(idle) >= nq;
-            if (!live) {
-                const uint32_t k = base + __builtin_amdgcn_mbcnt_hi((uint32_t)(idle >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)idle, 0u));
-                if (k < nq) {
-                    s = queue[k];
-                    S.hit = A.ff_hit + s;
-                    S.a0 = A.ff_act0 + s;
-                    S.a1 = A.ff_act1 + s;
-                    S.ph = 0;
-                    const float4 a = A.fs_ray0[s], b = A.fs_ray1[s];
-                    r = Ray{a.x, a.y, a.z, b.x, b.y, b.z};
-                    target = a.w;
-                    W0 = b.w;
-                    t_prev = A.fs_tp[s].w;
-                    t_cut = A.fs_L[s].w;
-                    acc = (Acc)A.fs_acc[s];
-                    const uint4 m2 = A.fs_meta2[s];
-                    cap = (int)m2.y;
-                    n = (int)m2.z;
-                    i = m = 0;
-                    next_exit = INFINITY;
-                    exit_pos = -1;
-                    if (t_cut <= W0) {  // more than cap Gaussians overlap at W0: no progress at this cap
-                        if (cap >= A.ff_hit_cap) {
-                            A.fs_out[s] = make_float4(-2.0f, 0.0f, 0.0f, __int_as_float(-1));
-                            to_shade = true;
-                        } else {
-                            reinterpret_cast<uint32_t*>(A.fs_meta2 + s)[1] = (uint32_t)min(2 * cap, A.ff_hit_cap);
-                            to_collect = true;
-                        }
-                    } else if (n == 0 && t_cut == INFINITY) {
-                        A.fs_out[s] = make_float4(-1.0f, 0.0f, 0.0f, __int_as_float(-1));
-                        to_shade = true;
-                    } else {
-                        live = true;
-                    }
-                }
-            }
-        }
-        if (!__any(live)) {
-            ffs_push(A, 3, s, to_shade);
-            ffs_push(A, nxt, s, to_collect);
-            if (exhausted) break;
-            continue;
-        }
-        // One event per lane (free_flight_distance's sweep, term for term); with an event budget, a lane
-        // whose events are cheap (few active entries) takes several in one wave iteration.
-        int budget = kFFSEventBudget;
-        while (live) {
-            budget -= max(m, 1);
-            const float next_entry = i < n ? S.K(i) : INFINITY;
-            float t_evt = fminf(next_entry, next_exit);
-            const bool window_end = t_cut <= t_evt;
-            if (window_end) t_evt = t_cut;
-            if (t_evt == INFINITY) {  // past the last event: no scatter
-                A.fs_out[s] = make_float4(-1.0f, 0.0f, 0.0f, __int_as_float(-1));
-                to_shade = true;
-                live = false;
-            } else {
-                const bool is_entry = next_entry <= next_exit;
-                float nx = INFINITY;
-                int npos = -1;
-                Acc seg = 0;
-#pragma unroll VR_FF_SWEEP_UNROLL
-                for (int a = 0; a < m; ++a) {
-                    const float4 c = S.A0(a);
-                    float4& e1r = S.A1(a);
-                    const float4 e1 = e1r;
-                    S.C.add(kFFErf);
-                    const float f1 = erff(__fdiv_rn(c.y + c.z * t_evt, c.w));
-                    if (S.ph) e1r.x = f1;
-                    else e1r.y = f1;
-                    seg += (Acc)(c.x * (f1 - (S.ph ? e1.y : e1.x)));
-                    int pp = a;
-                    if (!is_entry && a == m - 1) pp = exit_pos;
-                    const bool gone = !is_entry && a == exit_pos;
-                    if (!gone && (e1.z < nx || (e1.z == nx && pp < npos))) {
-                        nx = e1.z;
-                        npos = pp;
-                    }
-                }
-                if (acc + seg > (Acc)target) {  // the scatter lies in this segment: the shading kernel solves
-                    // for it over the segment [t_prev, t_evt] (the slot's active rows hold F at t_prev in ph)
-                    const float rem = (float)((Acc)target - acc);
-                    A.fs_out[s] = make_float4(t_prev, t_evt, rem, __int_as_float(m | (S.ph << 16)));
-                    to_shade = true;
-                    live = false;
-                } else {
-                    acc += seg;
-                    t_prev = t_evt;
-                    S.ph ^= 1;
-                    if (window_end) {  // the next window starts at t_cut
-                        A.fs_acc[s] = (double)acc;
-                        reinterpret_cast<float*>(A.fs_tp + s)[3] = t_prev;
-                        reinterpret_cast<float*>(A.fs_ray1 + s)[3] = t_cut;
-                        reinterpret_cast<uint32_t*>(A.fs_meta2 + s)[1] = (uint32_t)min(2 * cap, A.ff_hit_cap);
-                        to_collect = true;
-                        live = false;
-                    } else if (is_entry) {
-                        if (m >= A.ff_act_cap) {
-                            A.fs_out[s] = make_float4(-2.0f, 0.0f, 0.0f, __int_as_float(-1));
-                            to_shade = true;
-                            live = false;
-                        } else {
-                            const float t1n = S.enter(A, m, i++, r, t_evt);
-                            if (t1n < nx) {
-                                nx = t1n;
-                                npos = m;
-                            }
-                            ++m;
-                        }
-                    } else {
-                        S.move(exit_pos, m - 1);
-                        --m;
-                    }
-                    next_exit = nx;
-                    exit_pos = npos;
-                }
-            }
-            if (budget <= 0) break;
-        }
-        ffs_push(A, 3, s, to_shade);
-        ffs_push(A, nxt, s, to_collect);
-    }
-    if constexpr (CNT) {
-        Ctr c{};
-        for (int k = 0; k < kFFNumCtr; ++k) c.v[k] = S.C.v[k];
-        flush_counters(A.work, c);
-    }
-}
-
-// The rest of the bounce for every queued slot (ff_bounce after free_flight_distance, term for term):
-// recording, the capacity fallback, the environment, NEE (queued or inline), throughput, Russian
-// roulette, the next direction and target; a finished path writes its tail and the slot takes the next
-// path of the launch.
-template <bool MULTI, bool CNT>
-__global__ void __launch_bounds__(kFFBlock) ffs_shade_kernel(RenderArgs A) {
-    FFCount<CNT> C;
-    __shared__ int s_stack[(kStackSize + kCollectQueue) * kFFBlock];  // recording / inline shadow-ray walks
-    int* stack = s_stack + threadIdx.x;
-    const uint32_t nq = A.fs_cnt[3];
-    const uint32_t* queue = A.fs_q + (size_t)3 * A.ff_pool;
-    const int nxt = (int)(A.fs_cur ^ 1u);
-    for (uint32_t k0 = blockIdx.x * kFFBlock; k0 < nq; k0 += gridDim.x * kFFBlock) {  // block-uniform loop
-        const uint32_t k = k0 + threadIdx.x;
-        bool next = false;
-        uint32_t s = 0;
-        if (k < nq) {
-            s = queue[k];
-            const float4 a = A.fs_ray0[s], b = A.fs_ray1[s], tpv = A.fs_tp[s], Lv = A.fs_L[s], o = A.fs_out[s];
-            const uint4 meta = A.fs_meta[s], m2 = A.fs_meta2[s];
-            FFPath P{ffs_rng(A.fs_rng[s])};
-            P.ray = Ray{a.x, a.y, a.z, b.x, b.y, b.z};
-            P.tp0 = tpv.x, P.tp1 = tpv.y, P.tp2 = tpv.z;
-            P.L0 = Lv.x, P.L1 = Lv.y, P.L2 = Lv.z;
-            P.out = meta.x;
-            P.first = meta.y;
-            P.last = meta.z;
-            P.bounce = (int)meta.w;
-            P.defer = (m2.x & 1u) != 0u;
-            P.after = (m2.x & 2u) != 0u;
-            float ts = o.x, albedo = 0.0f;
-            const int mph = __float_as_int(o.w);
-            if (mph >= 0) {  // the scatter's segment [o.x, o.y] with o.z of the target left: solve, then the albedo
-                FFScratch<CNT> S{A.ff_hit + s, A.ff_act0 + s, A.ff_act1 + s, A.ff_pool, mph >> 16, {}};
-                const int m = mph & 0xffff;
-                const uint64_t useed = A.ff_solver == kSolverUniform ? ff_path_seed(A, P.out) : 0ull;
-                ts = solve_distance(A, S, m, P.ray, o.x, o.y, o.z, useed, P.bounce);
-                albedo = evaluate_albedo(A, S, m, P.ray.ox + ts * P.ray.dx, P.ray.oy + ts * P.ray.dy, P.ray.oz + ts * P.ray.dz);
-                if constexpr (CNT)
-                    for (int i = 0; i < kFFNumCtr; ++i) C.v[i] += S.C.v[i];
-            }
-            bool done = false, requeued = false;
-            if (MULTI && A.rec_bits && ts != -2.0f) {
-                int lx, ly, x, y;
-                const uint32_t bb = P.out / kFFBlock;
-                tile_pixel(A, A.ff_tile_base + bb / A.ff_nsb, (int)(P.out % kFFBlock), lx, ly, x, y);
-                record_hits(A, P.ray, ts >= 0.0f ? ts + 1e-6f : INFINITY, (uint32_t)y * A.width + (uint32_t)x, stack, kFFBlock);
-            }
-            if (ts == -2.0f && A.ff_fbq != nullptr) {  // over the hit-buffer capacity: the whole path re-runs
-                const uint32_t q = atomicAdd(A.ff_fbq, 1u);  // in ff_fallback_kernel with larger rows
-                atomicAdd(A.counters + 2, 1u);
-                if (q < A.ff_fbq_cap) {
-                    A.ff_fbq[1 + q] = P.out;
-                    A.ff_tail[P.out] = make_float4(0.0f, 0.0f, 0.0f, __uint_as_float(kFFNone));
-                    requeued = true;
-                }
-            }
-            if (requeued) {
-                done = true;
-            } else if (ts == -2.0f || P.bounce >= A.ff_max_bounces) {
-                P.L0 = P.L1 = P.L2 = __builtin_nanf("");
-                P.after = true;
-                atomicAdd(A.counters, 1u);
-                done = true;
-            } else if (ts < 0.0f) {  // no event, or no scatter before the last event: environment
-                P.L0 += P.tp0 * A.env[0];
-                P.L1 += P.tp1 * A.env[1];
-                P.L2 += P.tp2 * A.env[2];
-                P.after |= P.first != kFFNone;
-                done = true;
-            } else {
-                const float px = P.ray.ox + ts * P.ray.dx, py = P.ray.oy + ts * P.ray.dy, pz = P.ray.oz + ts * P.ray.dz;
-                const int nl = A.num_lights;
-                const bool is_env = P.rng.uniform() < __fdiv_rn(1.0f, (float)(nl + 1));
-                int li = -1;
-                float dist = INFINITY;
-                Ray sr;
-                if (!is_env) {
-                    li = (int)(P.rng.uniform() * (float)nl);
-                    const LightRecord& Lt = A.lights[li];
-                    float wx = Lt.px - px, wy = Lt.py - py, wz = Lt.pz - pz;
-                    dist = sqrtf(dot3(wx, wy, wz, wx, wy, wz));
-                    normalize3(wx, wy, wz);
-                    sr = make_ray(px, py, pz, wx, wy, wz);
-                } else {
-                    float wx, wy, wz;
-                    sample_uniform_direction(P.rng, wx, wy, wz);
-                    sr = make_ray(px, py, pz, wx, wy, wz);
-                }
-                const float w = (albedo * kInv4Pi) * (float)(nl + 1);
-                const float m0 = MULTI ? P.tp0 * w : w, m1 = MULTI ? P.tp1 * w : w, m2v = MULTI ? P.tp2 * w : w;
-                const bool queued = nee_queue(A, sr, dist, li, m0, m1, m2v, P.first, P.last, P.defer);
-                C.add(queued ? kFFNeeQueued : kFFNeeInline);
-                if (!queued) {
-                    float Li0, Li1, Li2;
-                    nee_radiance(A, transmittance_up_to(A, sr, dist, stack, kFFBlock), li, dist, Li0, Li1, Li2);
-                    P.after |= P.first != kFFNone;
-                    if constexpr (!MULTI) {
-                        P.L0 = m0 * Li0;
-                        P.L1 = m1 * Li1;
-                        P.L2 = m2v * Li2;
-                    } else {
-                        P.L0 += m0 * Li0;
-                        P.L1 += m1 * Li1;
-                        P.L2 += m2v * Li2;
-                    }
-                }
-                if constexpr (!MULTI) {
-                    done = true;
-                } else {
-                    P.tp0 *= albedo;
-                    P.tp1 *= albedo;
-                    P.tp2 *= albedo;
-                    if (P.bounce >= A.ff_min_bounces) {  // integrator.h:691-695
-                        const float rr = fminf(fmaxf(P.tp0, fmaxf(P.tp1, P.tp2)), 0.9f);
-                        if (P.rng.uniform() > rr) {
-                            done = true;
-                        } else {
-                            P.tp0 = __fdiv_rn(P.tp0, rr);
-                            P.tp1 = __fdiv_rn(P.tp1, rr);
-                            P.tp2 = __fdiv_rn(P.tp2, rr);
-                        }
-                    }
-                    if (!done) {
-                        float nx, ny, nz;
-                        sample_uniform_direction(P.rng, nx, ny, nz);
-                        P.ray = make_ray(px, py, pz, nx, ny, nz);
-                        ++P.bounce;
-                    }
-                }
-            }
-            if (done) {
-                if (!requeued)
-                    A.ff_tail[P.out] = make_float4(P.L0, P.L1, P.L2, __uint_as_float(P.first | (P.after ? kFFTailAfter : 0u)));
-                next = ffs_new_path<CNT>(A, s, C);  // the slot takes the launch's next path
-            } else {  // the next bounce (its target draw starts ff_bounce)
-                const float target = -logf(1.0f - P.rng.uniform());
-                C.add(kFFBounces);
-                ffs_begin_bounce(A, s, P.ray, target);
-                A.fs_tp[s] = make_float4(P.tp0, P.tp1, P.tp2, 0.0f);
-                A.fs_L[s] = make_float4(P.L0, P.L1, P.L2, INFINITY);
-                A.fs_rng[s] = P.rng.state;
-                A.fs_meta[s] = make_uint4(P.out, P.first, P.last, (uint32_t)P.bounce);
-                A.fs_meta2[s] = make_uint4((P.defer ? 1u : 0u) | (P.after ? 2u : 0u), (uint32_t)A.ff_hit_cap0, 0u, 0u);
-                next = true;
-            }
-        }
-        ffs_push(A, nxt, s, next);
-    }
-    if constexpr (CNT) {
-        Ctr c{};
-        for (int i = 0; i < kFFNumCtr; ++i) c.v[i] = C.v[i];
-        flush_counters(A.work, c);
-    }
-}
-
-// End of an iteration: the consumed queues and the claim counters restart empty.
-__global__ void ffs_advance_kernel(RenderArgs A) {
-    if (threadIdx.x == 0) {
-        A.fs_cnt[A.fs_cur] = 0u;
-        A.fs_cnt[2] = A.fs_cnt[3] = 0u;
-        A.fs_cnt[4] = A.fs_cnt[5] = 0u;
-    }
-}
-
 // Each path's radiance from its queued contributions (bounce order) and its inline part, one thread
 // per path of the launch (the chains are walked in parallel, not by the pixel's thread sample after
 // sample); written back into the path's ff_tail entry with no chain left.
@@ -2394,59 +1670,8 @@ uint32_t free_flight_threads(int cus) {
     return (uint32_t)std::max(1, cus) * (uint32_t)per_cu * (uint32_t)dev::kFFBlock;
 }
 
-// Grid of a persistent kernel: every CU filled to the kernel's occupancy.
-static unsigned resident_grid(const void* fn, unsigned block) {
-    int dv = 0, cus = 1, per = 1;
-    if (hipGetDevice(&dv) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dv);
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, fn, (int)block, 0) != hipSuccess || per < 1) per = 1;
-    return (unsigned)std::max(1, cus) * (unsigned)per;
-}
-
-// The staged pipeline of one launch: the pool's first paths, then iterations of collect -> sweep -> shade
-// until every path of the launch is done. The host learns that from the collect queue's length, copied
-// to pinned memory every kPoll iterations and read one block of iterations later (the GPU keeps the
-// block in between queued; iterations past the end find empty queues and return at once). The host
-// therefore waits on the device inside the launch: with VR_OPT_FF_STAGED the asynchronous entry points
-// (vr_render_tiles_device) return only once the frame's iterations are issued and mostly done.
-template <bool MULTI, bool CNT>
-static hipError_t ffs_run(RenderArgs A, hipStream_t stream, const FFPoll& poll) {
-    constexpr int kPoll = 4, kMaxIters = 1 << 18;
-    hipError_t e = hipMemsetAsync(A.fs_cnt, 0, 8 * sizeof(uint32_t), stream);
-    if (e != hipSuccess) return e;
-    A.fs_cur = 0;
-    hipLaunchKernelGGL((dev::ffs_start_kernel<CNT>), dim3((A.ff_pool + dev::kFFBlock - 1) / dev::kFFBlock), dim3(dev::kFFBlock), 0,
-                       stream, A);
-    if ((e = hipGetLastError()) != hipSuccess) return e;
-    // (per call: the current device's CU count; two occupancy queries per launch)
-    const unsigned g_collect = resident_grid((const void*)dev::ffs_collect_kernel<CNT>, dev::kFFBlock);
-    const unsigned g_sweep = resident_grid((const void*)dev::ffs_sweep_kernel<MULTI, CNT>, dev::kFFBlock);
-    const unsigned g_shade = std::max(1u, std::min(A.ff_pool / dev::kFFBlock, 4096u));
-    int pending = -1;
-    for (int it = 0; it < kMaxIters; ++it) {
-        hipLaunchKernelGGL((dev::ffs_collect_kernel<CNT>), dim3(g_collect), dim3(dev::kFFBlock), 0, stream, A);
-        hipLaunchKernelGGL((dev::ffs_sweep_kernel<MULTI, CNT>), dim3(g_sweep), dim3(dev::kFFBlock), 0, stream, A);
-        hipLaunchKernelGGL((dev::ffs_shade_kernel<MULTI, CNT>), dim3(g_shade), dim3(dev::kFFBlock), 0, stream, A);
-        hipLaunchKernelGGL(dev::ffs_advance_kernel, dim3(1), dim3(64), 0, stream, A);
-        if ((e = hipGetLastError()) != hipSuccess) return e;
-        A.fs_cur ^= 1u;
-        if ((it + 1) % kPoll == 0) {  // pipelined poll of the next iteration's queue length
-            const int slot = (it / kPoll) & 1;
-            if ((e = hipMemcpyAsync(poll.host + slot, A.fs_cnt + A.fs_cur, sizeof(uint32_t), hipMemcpyDeviceToHost, stream)) !=
-                hipSuccess)
-                return e;
-            if ((e = hipEventRecord(poll.ev[slot], stream)) != hipSuccess) return e;
-            if (pending >= 0) {
-                if ((e = hipEventSynchronize(poll.ev[pending])) != hipSuccess) return e;
-                if (poll.host[pending] == 0u) return hipSuccess;
-            }
-            pending = slot;
-        }
-    }
-    return hipErrorLaunchTimeOut;  // (a path longer than kMaxIters bounces and windows)
-}
-
 // Host launcher: one (tile chunk, sample batch) step. A.ff_* describe the step.
-hipError_t launch_free_flight(const RenderArgs& A, uint32_t chunk_tiles, hipStream_t stream, hipEvent_t* ev, const FFPoll& poll) {
+hipError_t launch_free_flight(const RenderArgs& A, uint32_t chunk_tiles, hipStream_t stream, hipEvent_t* ev) {
     hipError_t e0 = hipMemsetAsync(A.ff_next, 0, sizeof(unsigned long long), stream);
     if (e0 != hipSuccess) return e0;
     if (A.ff_nee_cap > 0 && (e0 = hipMemsetAsync(A.ff_nee_n, 0, 2 * sizeof(uint32_t), stream)) != hipSuccess) return e0;
@@ -2454,11 +1679,7 @@ hipError_t launch_free_flight(const RenderArgs& A, uint32_t chunk_tiles, hipStre
     dim3 grid(A.ff_threads / dev::kFFBlock);
     const bool cnt = A.work != nullptr;  // vr_count_work: the instrumented kernels
     if ((e0 = hipEventRecord(ev[0], stream)) != hipSuccess) return e0;
-    if (A.ff_pool > 0) {  // the staged pipeline
-        if (A.ff_multi) e0 = cnt ? ffs_run<true, true>(A, stream, poll) : ffs_run<true, false>(A, stream, poll);
-        else e0 = cnt ? ffs_run<false, true>(A, stream, poll) : ffs_run<false, false>(A, stream, poll);
-        if (e0 != hipSuccess) return e0;
-    } else if (A.ff_sm) {  // the phase-scheduled path kernel (VR_OPT_FF_KERNEL)
+    if (A.ff_sm) {  // the phase-scheduled path kernel (VR_OPT_FF_KERNEL)
         if (A.ff_multi) {
             if (cnt) hipLaunchKernelGGL((dev::ff_path_sm_kernel<true, true>), grid, dim3(dev::kFFBlock), 0, stream, A);
             else hipLaunchKernelGGL((dev::ff_path_sm_kernel<true>), grid, dim3(dev::kFFBlock), 0, stream, A);

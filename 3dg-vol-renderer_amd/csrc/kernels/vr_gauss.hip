@@ -452,43 +452,9 @@ __device__ __forceinline__ bool march_step(const RenderArgs& A, const Ray& ray, 
 // active list is split over the lanes (one Gaussian each), its sums and compaction then taken in
 // list order through lane broadcasts — the serial loop's operations in its order, so the result is
 // bit-identical — and lane 0 writes the records.
-#ifndef VR_MARCH_UNSORTED
-#define VR_MARCH_UNSORTED 1  // 1: the march's entrant queries walk the 4-wide nodes without sorting (A/B)
-#endif
-constexpr bool kMarchUnsorted = VR_MARCH_UNSORTED;
-#ifndef VR_MARCH_LOCAL
-#define VR_MARCH_LOCAL 0  // 1: the march's queries start in the subtree holding their window and climb (A/B: C4 march 14.0 -> 14.9 ms)
-#endif
-constexpr bool kMarchLocal = VR_MARCH_LOCAL;
-#ifndef VR_MARCH_PRETEST
-#define VR_MARCH_PRETEST 0  // 1: the march's BVH queries skip certain misses with the fast forms (fast_reject_*; A/B: C4 14.0 -> 16.4 ms)
-#endif
-constexpr bool kMarchPretest = VR_MARCH_PRETEST;
-// Look-ahead windows: one entrant query covers this many steps; the entrants of the later steps wait in
-// up to kMarchPending register slots (j, entry, exit) and join the active list at their step. The
-// entrant set of every step is the one its own query would return, so the march is unchanged bit for
-// bit; a window with more later entrants than slots keeps only its first step's (the next step queries).
-#ifndef VR_MARCH_LOOKAHEAD
-#define VR_MARCH_LOOKAHEAD 1  // steps per entrant query (1: one query per step; A/B at C4: 2 steps 14.4 ms, 3 17.8, 4 21.5 vs 14.0)
-#endif
-#ifndef VR_MARCH_PENDING
-#define VR_MARCH_PENDING 4  // register slots for the later steps' entrants
-#endif
-constexpr int kMarchLook = VR_MARCH_LOOKAHEAD, kMarchPend = VR_MARCH_PENDING;
-// Merged first query: a closest-entry query (empty active list) is always followed by the entrant query of
-// the step holding that entry, over nearly the same part of the tree. With VR_MARCH_MERGE the closest
-// query's walk also keeps, in the (empty) active list's LDS slots, every hit (j, entry a, exit b) with
-// a <= best + 2 steps (best: the closest entry so far; prune widened to match), dropping the ones a
-// later, closer entry puts out of range. Once best is final, step k = kfirst(best) has t_k < best + 2 steps,
-// so the kept hits hold all of the step's entrants (best <= a <= t_k < b) and the entrant query is
-// skipped; more than kMarchCand kept hits at once run it as before. Same entrant set: bit-identical.
-#ifndef VR_MARCH_MERGE
-#define VR_MARCH_MERGE 0
-#endif
-#ifndef VR_MARCH_CAND
-#define VR_MARCH_CAND 5  // (j, a, b) hits the merged query keeps (3 LDS slots each, after slot 0)
-#endif
-
+// (Measured and not kept, DESIGN.md §3: window queries starting in the subtree holding the window and climbing,
+// a fast-form pre-test of the candidates, look-ahead windows over 2-4 steps, a closest-entry query merged with
+// the following entrant query, a sorting network in the entrant walk; all bit-identical, all slower at C4.)
 template <int ACT, bool S, bool H, bool W = false, int CAP = kStackSize, bool COOP = false>
 __device__ int march(const RenderArgs& A, uint32_t p, int px, int py, int* act_base, int* stack, int stride, Ctr& c,
                      int act_stride = -1) {
@@ -510,20 +476,9 @@ __device__ int march(const RenderArgs& A, uint32_t p, int px, int py, int* act_b
             return true;
         }
     };
-    // Queries local to a point of the ray start in the deepest subtree holding it (and the window's other
-    // end) and climb (traverse_wide_climb): a window query of one step then walks a few local nodes and
-    // one sibling-box test per ancestor instead of the descent from the root.
-    auto walk_local = [&](float ta, float tb, auto prune, auto leaf) -> bool {
-        float p[3] = {ray.ox + ta * ray.dx, ray.oy + ta * ray.dy, ray.oz + ta * ray.dz};
-        float q[3] = {ray.ox + tb * ray.dx, ray.oy + tb * ray.dy, ray.oz + tb * ray.dz};
-        node_space<true>(A, p[0], p[1], p[2]);
-        node_space<true>(A, q[0], q[1], q[2]);
-        return traverse_wide_climb<CAP>(A, ray, wide_start_node(A, p, q), stack, stride, prune, leaf, NodeCount<S>{&c});
-    };
-    const bool local = W && kMarchLocal && A.hn4_parent != nullptr && A.hn4_sib != nullptr;
     // the entrants query collects every entry of (t_lo, t_k] whatever the visit order: no sorting network
     auto walk_any = [&](auto prune, auto leaf) -> bool {
-        if constexpr (W && kMarchUnsorted) {
+        if constexpr (W) {
             return traverse_wide<CAP, decltype(prune), decltype(leaf), NodeCount<S>, false>(A, ray, stack, stride, prune, leaf,
                                                                                              NodeCount<S>{&c});
         } else {
@@ -531,180 +486,54 @@ __device__ int march(const RenderArgs& A, uint32_t p, int px, int py, int* act_b
         }
     };
     int kq = 0;
-    constexpr bool kMerge = VR_MARCH_MERGE && !COOP;
-    constexpr int kCand = (ACT - 1) / 3 < VR_MARCH_CAND ? (ACT - 1) / 3 : VR_MARCH_CAND;
-    bool have = false;  // (kMerge) the active list already holds step k's entrants
-    // look-ahead (W, not COOP): pend_k = the last step the pending slots are complete for (-1: none);
-    // a consumed or empty slot has pa = +inf
-    constexpr bool kLook = W && !COOP && kMarchLook > 1;
-    int pend_k = -1;
-    int pj[kMarchPend];
-    float pa[kMarchPend], pb[kMarchPend];
-#pragma unroll
-    for (int i = 0; i < kMarchPend; ++i) {
-        pj[i] = 0;
-        pa[i] = pb[i] = INFINITY;
-    }
     if (A.num_prims > 0) {
         for (;;) {
             float t_lo = (kq == 0) ? -1.0f : ts[kq - 1];
             int k;
-            float pmin = INFINITY;  // the earliest pending entry (pending: every entry of (t_lo, ts[pend_k]])
-            if constexpr (kLook) {
-#pragma unroll
-                for (int i = 0; i < kMarchPend; ++i) pmin = fminf(pmin, pa[i]);
-            }
-            if (kLook && act.n == 0 && pmin < INFINITY) {  // the closest entry after t_lo is pending
-                k = kfirst(ts, nts, step, pmin);
-            } else if (act.n == 0) {  // closest entry strictly after t_lo
+            if (act.n == 0) {  // closest entry strictly after t_lo
                 if constexpr (S) c.v[kCtrPrimQueries]++;
                 float best = INFINITY;
-                const float lookw = kMerge ? 2.0f * step : 0.0f;
-                int nc = 0;         // (kMerge) kept hits, triple c in act slots 1 + 3c .. 3 + 3c
-                bool covf = false;  // (kMerge) a hit in range did not fit
                 auto prune_c = [&](float tmin, float tmax) {
-                    const float lim = best + lookw;
-                    return tmax >= t_lo - kTPad * (1.0f + fabsf(t_lo)) && tmin <= lim + kTPad * (1.0f + lim);
+                    return tmax >= t_lo - kTPad * (1.0f + fabsf(t_lo)) && tmin <= best + kTPad * (1.0f + best);
                 };
                 auto leaf_c = [&](uint32_t first, uint32_t count) {
                     for (uint32_t j = first; j < first + count; ++j) {
                         if constexpr (S) c.v[kCtrPrims]++;
                         GRec g = load_rec(G, j);
-                        if (kMarchPretest && !kMerge && fast_reject_closest(g, ray, t_lo, best)) continue;
                         Quad q = quad(g, ray);
                         float a, b;
                         if (!intersect(q, a, b) || !(a > t_lo)) continue;
                         if (a < best) best = a;
-                        if constexpr (kMerge) {
-                            if (!(a <= best + lookw) || !(b > a)) continue;
-                            if (nc == kCand) {  // full: drop the hits a closer entry put out of range
-                                int w = 0;
-                                for (int cc = 0; cc < kCand; ++cc) {
-                                    if (!(__int_as_float(act.get(2 + 3 * cc)) <= best + lookw)) continue;
-                                    if (w != cc) {
-                                        act.set(1 + 3 * w, act.get(1 + 3 * cc));
-                                        act.set(2 + 3 * w, act.get(2 + 3 * cc));
-                                        act.set(3 + 3 * w, act.get(3 + 3 * cc));
-                                    }
-                                    ++w;
-                                }
-                                nc = w;
-                            }
-                            if (nc < kCand) {
-                                act.set(1 + 3 * nc, (int)j);
-                                act.set(2 + 3 * nc, __float_as_int(a));
-                                act.set(3 + 3 * nc, __float_as_int(b));
-                                ++nc;
-                            } else {
-                                covf = true;
-                            }
-                        }
                     }
                     return true;
                 };
-                // (the closest entry after t_lo: local from the ray's point at t_lo once the march is past 0)
-                const bool ok = (local && t_lo >= 0.0f) ? walk_local(t_lo, t_lo, prune_c, leaf_c) : walk(prune_c, leaf_c);
-                if (!ok) return kOverflow;
+                if (!walk(prune_c, leaf_c)) return kOverflow;
                 if (best == INFINITY) break;
                 k = kfirst(ts, nts, step, best);
                 // No entry lies in (t_lo, best) and ts[k - 1] < best: the step's entrant window (t_lo, t_k] holds
                 // exactly the entries of (ts[k - 1], t_k]. The short window keeps the query local to the step
                 // (from t_lo = -1 the first query of every pixel walked every box along [0, t_k]). Same set.
                 if (k > kq) t_lo = ts[k - 1];
-                if constexpr (kMerge) {
-                    if (!covf && k < nts - 1) {  // the step's entrants from the kept hits, sorted by index
-                        const float tk = ts[k];
-                        for (int cc = 0; cc < nc; ++cc) {  // (the list, <= cc entries, stays below triple cc)
-                            const int j = act.get(1 + 3 * cc);
-                            if (!(__int_as_float(act.get(2 + 3 * cc)) <= tk) || !(__int_as_float(act.get(3 + 3 * cc)) > tk))
-                                continue;
-                            int i = act.n;
-                            while (i > 0 && act.get(i - 1) > j) {
-                                act.set(i, act.get(i - 1));
-                                --i;
-                            }
-                            act.set(i, j);
-                            act.n++;
-                        }
-                        have = true;
-                    }
-                }
             } else {
                 k = kq;
             }
             if (k >= nts - 1) return kError;  // step table too short (host sizes it from scene bounds)
             const float t_k = ts[k];
             bool ovf = false;
-            if (kLook && k <= pend_k) {  // this step's entrants wait in the pending slots
-#pragma unroll
-                for (int i = 0; i < kMarchPend; ++i) {
-                    if (!(pa[i] <= t_k)) continue;  // a later step's (or an empty slot)
-                    const int j = pj[i];
-                    const bool inside = pb[i] > t_k;
-                    pa[i] = INFINITY;
-                    if (!inside) continue;
-                    if (act.n >= ACT) {
-                        ovf = true;
-                        continue;
-                    }
-                    int q = act.n;  // sorted insert, as the query's
-                    while (q > 0 && act.get(q - 1) > j) {
-                        act.set(q, act.get(q - 1));
-                        --q;
-                    }
-                    act.set(q, j);
-                    act.n++;
-                }
-                if (ovf) return kOverflow;
-                kq = k + 1;
-                if (!march_step<S, COOP>(A, ray, p, px, py, k, t_k, act, T, prev, c, writer)) break;
-                continue;
-            }
-            if (kMerge && have) {  // the merged closest query found this step's entrants
-                have = false;
-                kq = k + 1;
-                if (!march_step<S, COOP>(A, ray, p, px, py, k, t_k, act, T, prev, c, writer)) break;
-                continue;
-            }
-            // entrants: t_lo < a <= t_k and still inside at t_k (b > t_k); with look-ahead the window
-            // runs on to t_end and the later steps' entrants go to the pending slots
-            const int k_end = kLook ? min(k + kMarchLook - 1, nts - 2) : k;
-            const float t_end = ts[k_end];
-            int pn = 0;
-            bool pend_ovf = false;
-            if constexpr (kLook) {
-#pragma unroll
-                for (int i = 0; i < kMarchPend; ++i) pa[i] = INFINITY;
-            }
+            // entrants: t_lo < a <= t_k and still inside at t_k (b > t_k)
             if constexpr (S) c.v[kCtrPrimQueries]++;
             auto prune_w = [&](float tmin, float tmax) {
-                return tmax >= t_lo - kTPad * (1.0f + fabsf(t_lo)) && tmin <= t_end + kTPad * (1.0f + t_end);
+                return tmax >= t_lo - kTPad * (1.0f + fabsf(t_lo)) && tmin <= t_k + kTPad * (1.0f + t_k);
             };
-            auto walk_w = [&](auto prune, auto leaf) -> bool {  // a window of one step: local; from 0: the root
-                return (local && t_lo >= 0.0f) ? walk_local(t_lo, t_end, prune, leaf) : walk_any(prune, leaf);
-            };
-            const bool ok = walk_w(
+            const bool ok = walk_any(
                 prune_w,
                 [&](uint32_t first, uint32_t count) {
                     for (uint32_t j = first; j < first + count; ++j) {
                         if constexpr (S) c.v[kCtrPrims]++;
                         GRec g = load_rec(G, j);
-                        if (kMarchPretest && fast_reject_window(g, ray, t_lo, t_k)) continue;
                         Quad q = quad(g, ray);
                         float a, b;
-                        if (!intersect(q, a, b) || !(a > t_lo) || !(a <= t_end)) continue;
-                        if (kLook && !(a <= t_k)) {  // a later step's entrant
-#pragma unroll
-                            for (int i = 0; i < kMarchPend; ++i)
-                                if (i == pn) {
-                                    pj[i] = (int)j;
-                                    pa[i] = a;
-                                    pb[i] = b;
-                                }
-                            pend_ovf = pend_ovf || pn == kMarchPend;
-                            pn = min(pn + 1, kMarchPend);
-                            continue;
-                        }
+                        if (!intersect(q, a, b) || !(a > t_lo) || !(a <= t_k)) continue;
                         if (!(b > t_k)) continue;
                         if (act.n >= ACT) {
                             ovf = true;
@@ -721,14 +550,6 @@ __device__ int march(const RenderArgs& A, uint32_t p, int px, int py, int* act_b
                     return true;
                 });
             if (ovf || !ok) return kOverflow;
-            if constexpr (kLook) {
-                pend_k = k_end;
-                if (pend_ovf) {  // more later entrants than slots: only this step's are complete
-                    pend_k = k;
-#pragma unroll
-                    for (int i = 0; i < kMarchPend; ++i) pa[i] = INFINITY;
-                }
-            }
             kq = k + 1;
             if (!march_step<S, COOP>(A, ray, p, px, py, k, t_k, act, T, prev, c, writer)) break;
         }
@@ -746,12 +567,8 @@ __device__ __forceinline__ void mark_error(const RenderArgs& A, uint32_t p) {
 // A pixel that overflowed a pass is marched again from its start by the next pass, which relinks it;
 // the records this pass already wrote for it are unreachable. Their weight T sigma_s (rec_pos.w, >= 0 for
 // every live record) is set to the sentinel -1 so the secondary stage starts none of their rays (sec_init).
-#ifndef VR_ORPHAN_SKIP
-#define VR_ORPHAN_SKIP 1
-#endif
 constexpr float kOrphanWeight = -1.0f;  // rec_pos.w of an orphaned record (a live record's T sigma_s is >= 0)
 __device__ __forceinline__ void orphan_records(const RenderArgs& A, uint32_t p) {
-    if (!VR_ORPHAN_SKIP) return;
     for (uint32_t r = A.px_first[p]; r != kNoRecord && r < A.rec_cap; r = A.rec_next[r])
         reinterpret_cast<float*>(A.rec_pos + r)[3] = kOrphanWeight;
 }
@@ -1179,10 +996,6 @@ __global__ __launch_bounds__(64) void march_binned_kernel(RenderArgs A) {
 // ---------------------------------------------------------------------------------------------
 // A 4-wide node index (< 2^27 nodes) in the walk's `node`; bits 28-30 may carry a child slot to skip.
 constexpr int32_t kNodeIndexMask = 0x0fffffff;
-#ifndef VR_CLIMB_SKIP
-#define VR_CLIMB_SKIP 0  // 1: a climbing ray tests its finished subtree's siblings' union box first (A/B)
-#endif
-constexpr bool kClimbSkip = VR_CLIMB_SKIP;
 #ifdef VR_DIAG_LEVELS
 // Diagnostic builds only: VR_DIAG_LEVELS = 1 counts the node steps of the rays that end uncut, 2 those of
 // the rays that reach their cut-off, by tree depth (secondary counters [8 + b]: depths 2b, 2b + 1; b = 7:
@@ -1265,43 +1078,18 @@ __device__ __forceinline__ void env_sample_dir(const RenderArgs& A, const uint4&
     env_dir(xi1, xi2, wx, wy, wz);
 }
 
-// Direction key of an environment ray: octahedral map of the unit sphere onto [-1, 1]^2, 16 x 16
-// cells numbered in Morton order (neighbouring keys = neighbouring directions).
-#ifndef VR_ENV_KEY_BITS
-#define VR_ENV_KEY_BITS 4  // cells per octahedral axis = 2^bits (A/B)
-#endif
-#ifndef VR_ENV_KEY_XI
-#define VR_ENV_KEY_XI 1  // 1: direction cells of the (xi1, xi2) sample grid instead of the octahedral map (A/B)
-#endif
-constexpr int kEnvBits = VR_ENV_KEY_BITS, kEnvSide = 1 << kEnvBits, kEnvCells = kEnvSide * kEnvSide;
-__device__ __forceinline__ uint32_t dir_key(float x, float y, float z) {
-    const float n = fabsf(x) + fabsf(y) + fabsf(z);
-    float u = x / n, v = y / n;
-    if (z < 0.0f) {
-        const float uu = (1.0f - fabsf(v)) * (u >= 0.0f ? 1.0f : -1.0f);
-        const float vv = (1.0f - fabsf(u)) * (v >= 0.0f ? 1.0f : -1.0f);
-        u = uu;
-        v = vv;
-    }
-    const uint32_t cu = (uint32_t)min(kEnvSide - 1, max(0, (int)((u + 1.0f) * (0.5f * kEnvSide))));
-    const uint32_t cv = (uint32_t)min(kEnvSide - 1, max(0, (int)((v + 1.0f) * (0.5f * kEnvSide))));
-    uint32_t k = 0;
-#pragma unroll
-    for (int b = 0; b < kEnvBits; ++b) k |= (((cu >> b) & 1u) << (2 * b)) | (((cv >> b) & 1u) << (2 * b + 1));
-    return k;
-}
+// Direction cells of the environment rays: the 16 x 16 cells of the sample's (xi1, xi2) = (azimuth, cos polar)
+// grid, Morton-numbered (equal-area direction cells without evaluating the direction; measured against the
+// octahedral map of the evaluated direction, round 3: 3.3 ms slower at C4).
+constexpr int kEnvBits = 4, kEnvSide = 1 << kEnvBits, kEnvCells = kEnvSide * kEnvSide;
 
 // One sorting group per record chunk: counting sort of the chunk's environment rays by direction key
 // (order inside a key is arbitrary: every ray's result is independent of when it is traced). A group
-// is one wave (VR_ENV_ORDER_WAVE: BLOCK/64 chunks in flight per workgroup, wave-local LDS and no
-// workgroup barriers; the chunk's chain of dependent loads is the cost, not its arithmetic) or the
-// whole workgroup.
-#ifndef VR_ENV_ORDER_WAVE
-#define VR_ENV_ORDER_WAVE 1  // A/B at C4: 1.56 ms; workgroup per chunk 1.91 (2.12 seeding every sample)
-#endif
+// is one wave: BLOCK/64 chunks in flight per workgroup, wave-local LDS and no workgroup barriers; the
+// chunk's chain of dependent loads is the cost, not its arithmetic (C4: 1.56 ms; a workgroup per chunk 1.91).
 template <int BLOCK>
 __global__ __launch_bounds__(BLOCK) void env_order_kernel(RenderArgs A) {
-    constexpr int G = VR_ENV_ORDER_WAVE ? 64 : BLOCK, kGroups = BLOCK / G;
+    constexpr int G = 64, kGroups = BLOCK / G;
     constexpr uint32_t kKeyCap = 8192 / kGroups;  // keys kept in LDS per group; larger chunks recompute them
     using KeyT = typename std::conditional<(kEnvCells <= 256), uint8_t, uint16_t>::type;
     constexpr int kPer = kEnvCells / 64;  // counts per lane of the scan
@@ -1336,7 +1124,6 @@ __global__ __launch_bounds__(BLOCK) void env_order_kernel(RenderArgs A) {
         auto key = [&](uint32_t i) -> uint32_t {
             const uint32_t rl = i / ne, r = r0 + rl;
             if (r >= nrec) return kEnvCells - 1;  // padding records
-#if VR_ENV_KEY_XI
             // the cell of the sample's (xi1, xi2) = (azimuth, cos polar) grid: equal-area direction
             // cells without evaluating the direction
             float xi1, xi2;
@@ -1347,12 +1134,6 @@ __global__ __launch_bounds__(BLOCK) void env_order_kernel(RenderArgs A) {
 #pragma unroll
             for (int b = 0; b < kEnvBits; ++b) k |= (((cu >> b) & 1u) << (2 * b)) | (((cv >> b) & 1u) << (2 * b + 1));
             return k;
-#else
-            float xi1, xi2, wx, wy, wz;
-            env_xi_at(A, base[rl], i - rl * ne, xi1, xi2);
-            env_dir(xi1, xi2, wx, wy, wz);
-            return dir_key(wx, wy, wz);
-#endif
         };
         for (uint32_t i = tid; i < n; i += G) {
             const uint32_t k = key(i);
@@ -1425,9 +1206,6 @@ __device__ __forceinline__ uint32_t rays_per_chunk(const RenderArgs& A) {
 // Start ray `rem` of record chunk `chunk`. Returns false if the ray is already complete (Tr
 // written) or a padding id. norm: slab-test terms in the half nodes' scene-normalised
 // coordinates (HNode).
-#ifndef VR_SEC_FAST_INIT
-#define VR_SEC_FAST_INIT 1  // A/B (round 3, C4): secondary stage -1.1 ms
-#endif
 __device__ __forceinline__ bool sec_init(const RenderArgs& A, uint32_t nrec, uint32_t chunk, uint32_t rem, SecRay& R,
                                          bool norm = false) {
     uint32_t s, r;
@@ -1462,18 +1240,12 @@ __device__ __forceinline__ bool sec_init(const RenderArgs& A, uint32_t nrec, uin
     if (s < (uint32_t)A.num_lights) {
         const LightRecord& lr = A.lights[s];
         float dx = lr.px - pos.x, dy = lr.py - pos.y, dz = lr.pz - pos.z;
-#if VR_SEC_FAST_INIT
         // a secondary ray feeds only its Tr (continuous): one hardware-rsqrt normalisation instead of
         // the reference's two correctly rounded ones (direction within ~1 ulp)
         const float d2 = dot3(dx, dy, dz, dx, dy, dz);
         const float dist = sqrtf(d2);
         const float inv = __builtin_amdgcn_rsqf(d2);
         R.ray = Ray{pos.x, pos.y, pos.z, dx * inv, dy * inv, dz * inv};
-#else
-        float dist = sqrtf(dot3(dx, dy, dz, dx, dy, dz));
-        normalize3(dx, dy, dz);
-        R.ray = make_ray(pos.x, pos.y, pos.z, dx, dy, dz);
-#endif
         R.light = true;
         R.lim = dist;
         if (!(dist > 0.0f)) {  // `while (t_prev < dist)` never runs
@@ -1485,11 +1257,7 @@ __device__ __forceinline__ bool sec_init(const RenderArgs& A, uint32_t nrec, uin
         float xi1, xi2;  // (env_order_kernel left the record's generator state when it ran)
         env_xi_at(A, A.env_order != nullptr ? A.env_base[r] : env_base_state(meta), s - (uint32_t)A.num_lights, xi1, xi2);
         env_dir(xi1, xi2, wx, wy, wz);
-#if VR_SEC_FAST_INIT
         R.ray = Ray{pos.x, pos.y, pos.z, wx, wy, wz};  // env_dir's direction is unit up to rounding
-#else
-        R.ray = make_ray(pos.x, pos.y, pos.z, wx, wy, wz);
-#endif
         R.light = false;
         R.lim = 0.0f;  // last event so far
     }
@@ -1497,15 +1265,9 @@ __device__ __forceinline__ bool sec_init(const RenderArgs& A, uint32_t nrec, uin
     // |d| clamped away from 0: the fma slab form b/d - o/d must never see inf - inf
     const float sc = norm ? A.hn_scale : 1.0f;
     const float dx = R.ray.dx * sc, dy = R.ray.dy * sc, dz = R.ray.dz * sc;
-#if VR_SEC_FAST_INIT  // slab tests only propose candidates (boxes bound 3.15 sigma, the test is at 3)
     R.ix = __builtin_amdgcn_rcpf(fabsf(dx) > 1e-30f ? dx : copysignf(1e-30f, dx));
     R.iy = __builtin_amdgcn_rcpf(fabsf(dy) > 1e-30f ? dy : copysignf(1e-30f, dy));
     R.iz = __builtin_amdgcn_rcpf(fabsf(dz) > 1e-30f ? dz : copysignf(1e-30f, dz));
-#else
-    R.ix = __frcp_rn(fabsf(dx) > 1e-30f ? dx : copysignf(1e-30f, dx));
-    R.iy = __frcp_rn(fabsf(dy) > 1e-30f ? dy : copysignf(1e-30f, dy));
-    R.iz = __frcp_rn(fabsf(dz) > 1e-30f ? dz : copysignf(1e-30f, dz));
-#endif
     if (norm) {
         R.oxi = (R.ray.ox - A.hn_center[0]) * sc * R.ix;
         R.oyi = (R.ray.oy - A.hn_center[1]) * sc * R.iy;
@@ -1595,9 +1357,13 @@ __device__ __forceinline__ void sec_finish(const RenderArgs& A, SecRay& R, Ctr& 
         if ((VR_DIAG_LEVELS == 2) == cut_reached<PURE>(R))
             for (int b = 0; b < 8; ++b)
                 if (R.lv[b]) atomicAdd(A.work + kNumCtr + b, (unsigned long long)R.lv[b]);
-#elif !defined(VR_DIAG_WAVE_UTIL) && !defined(VR_DIAG_CYCLES) && !defined(VR_DIAG_ORIGIN)
+#elif !defined(VR_DIAG_WAVE_UTIL) && !defined(VR_DIAG_CYCLES)
     if constexpr (S) {  // secondary-stage diagnostics in otherwise unused counter slots
+#ifdef VR_DIAG_LIGHT  // diagnostic builds only: the light rays and their node steps instead of the cut rays'
+        if (R.light) {
+#else
         if (cut_reached<PURE>(R)) {
+#endif
             c.v[kCtrSteps]++;                 // rays ended by the optical-depth cut-off
             c.v[kCtrPrimQueries] += R.nsteps;  // ... and their node steps
         }
@@ -1752,154 +1518,8 @@ __device__ __forceinline__ uint32_t ovf_slot(const RenderArgs& A, int sp) {
     return (uint32_t)(sp - STACK) * A.stack_ovf_lanes + blockIdx.x * BLOCK + threadIdx.x;
 }
 
-#ifndef VR_WW_NOSORT
-#define VR_WW_NOSORT 0  // 1: no near-to-far sort of a node's children (A/B)
-#endif
-// One step of the 4-wide traversal: the four children of HNode4 `node` are tested, sorted near to
-// far (misses last); leaf children go to the leaf queue in that order, the nearest inner child
-// is walked next and the other inner ones are pushed far-first (so the nearer pop first).
-template <int BLOCK, bool S, int QCAP, int STACK>
-__device__ __forceinline__ void sec_node4(const RenderArgs& A, SecRay& R, LdsInt* stack, int& sp, int& node, LeafQueue& Q,
-                                          Ctr& c) {
-    if constexpr (S) {
-        c.v[kCtrNodes]++;
-        ++R.nsteps;
-    }
-    const uint4* np = reinterpret_cast<const uint4*>(A.hnodes4s + node);
-    const uint4 q0 = np[0], q1 = np[1], q2 = np[2], rf = np[3];
-    const uint32_t w[12] = {q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, q1.z, q1.w, q2.x, q2.y, q2.z, q2.w};
-    const int32_t ref[4] = {(int32_t)rf.x, (int32_t)rf.y, (int32_t)rf.z, (int32_t)rf.w};
-    const float lim = R.plim;
-    float key[4];
-    int32_t kr[4];
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-        float f[6];
-#pragma unroll
-        for (int k = 0; k < 6; ++k) {
-            const uint32_t word = w[(6 * i + k) >> 1];
-            f[k] = (float)__builtin_bit_cast(_Float16, (uint16_t)(((6 * i + k) & 1) ? (word >> 16) : (word & 0xffffu)));
-        }
-        const float tx1 = fmaf(f[0], R.ix, -R.oxi), tx2 = fmaf(f[3], R.ix, -R.oxi);
-        const float ty1 = fmaf(f[1], R.iy, -R.oyi), ty2 = fmaf(f[4], R.iy, -R.oyi);
-        const float tz1 = fmaf(f[2], R.iz, -R.ozi), tz2 = fmaf(f[5], R.iz, -R.ozi);
-        const float tmin = fmaxf(fmaxf(fminf(tx1, tx2), fminf(ty1, ty2)), fminf(tz1, tz2));
-        const float tmax = fminf(fminf(fmaxf(tx1, tx2), fmaxf(ty1, ty2)), fmaxf(tz1, tz2));
-        const bool hit = (ref[i] != 0) & (tmax >= fmaxf(tmin, 0.0f)) & (tmin <= lim);
-        key[i] = hit ? tmin : INFINITY;
-        kr[i] = hit ? ref[i] : 0;
-#ifdef VR_DIAG_ORIGIN  // diagnostic builds only: child boxes hit that hold the ray origin (inner / leaf), inner hits
-        if constexpr (S) {
-            c.v[kCtrSteps] += (hit && ref[i] > 0 && tmin < 0.0f) ? 1u : 0u;
-            c.v[kCtrPixels] += (hit && ref[i] < 0 && tmin < 0.0f) ? 1u : 0u;
-            c.v[kCtrPrimQueries] += (hit && ref[i] > 0) ? 1u : 0u;
-        }
-#endif
-    }
-#if !VR_WW_NOSORT
-    // 4-input sorting network (5 compare-exchanges)
-    cswap(key[0], kr[0], key[1], kr[1]);
-    cswap(key[2], kr[2], key[3], kr[3]);
-    cswap(key[0], kr[0], key[2], kr[2]);
-    cswap(key[1], kr[1], key[3], kr[3]);
-    cswap(key[1], kr[1], key[2], kr[2]);
-#endif
-    // leaves -> queue, nearest first
-    if constexpr (kQueueRing<QCAP>) {
-        // Branch-free: every lane stores each child at the queue's end; a non-leaf store lands past
-        // the last entry (never read, overwritten by the next put). A NODE step starts with at most
-        // QCAP - 4 entries, so that slot is always a free ring word.
-        LdsInt* ext = stack + STACK * BLOCK;
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            const bool leaf = kr[i] < 0;
-            Q.q0 = (leaf && Q.n == 0) ? kr[i] : Q.q0;
-            ext[((Q.q1 + Q.n - 1) & (QCAP - 2)) * BLOCK] = kr[i];
-            Q.n += (int)leaf;
-        }
-    } else {
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            const bool leaf = kr[i] < 0;
-            Q.put<QCAP, BLOCK>(leaf ? Q.n : -1, kr[i], stack + STACK * BLOCK);
-            Q.n += (int)leaf;
-        }
-    }
-    // inner children: the nearest continues, the others are pushed far-first
-    int first = -1;
-    int32_t next = 0;  // the nearest inner child (selects only: no dynamic register indexing)
-#if VR_WW_NOSORT
-    float best = INFINITY;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-        const bool b = (kr[i] > 0) & (key[i] < best);
-        best = b ? key[i] : best;
-        first = b ? i : first;
-        next = b ? kr[i] : next;
-    }
-    constexpr int kLowPush = 0;
-#else
-#pragma unroll
-    for (int i = 3; i >= 0; --i) {
-        first = kr[i] > 0 ? i : first;
-        next = kr[i] > 0 ? kr[i] : next;
-    }
-    constexpr int kLowPush = 1;  // child 0 is never pushed: if it is inner it is the nearest inner child
-#endif
-    // Common case, wave-uniform: every stepping lane can take 3 pushes in LDS. Then the pushes
-    // are branch-free (a lane that does not push stores above its top: dead) and the pop is LDS.
-    if (__builtin_expect(__ballot(sp > STACK - 3) == 0ull, 1)) {
-#pragma unroll
-        for (int i = 3; i >= kLowPush; --i) {
-            stack[sp * BLOCK] = kr[i];
-            sp += (int)((kr[i] > 0) & (i != first));
-        }
-        if (first >= 0) {
-            node = next;
-        } else if (sp > 0) {
-            --sp;
-            node = stack[sp * BLOCK];
-        } else {
-            node = -1;
-        }
-        return;
-    }
-#pragma unroll
-    for (int i = 3; i >= 0; --i) {
-        if (kr[i] > 0 && i != first) {
-            if (sp < STACK) stack[sp * BLOCK] = kr[i];
-            else A.stack_ovf[ovf_slot<BLOCK, STACK>(A, sp)] = kr[i];
-            ++sp;
-        }
-    }
-    if (first >= 0) {
-        node = next;
-    } else if (sp > 0) {
-        --sp;
-        node = sp < STACK ? stack[sp * BLOCK] : A.stack_ovf[ovf_slot<BLOCK, STACK>(A, sp)];
-    } else {
-        node = -1;
-    }
-}
-
-// The ray's slab test against a sibling-union box (siblings_kernel's layout: 6 f16 in the first 12 B).
-__device__ __forceinline__ bool sibling_hit(const RenderArgs& A, const SecRay& R, const uint4& b) {
-    const uint32_t w[3] = {b.x, b.y, b.z};
-    float f[6];
-#pragma unroll
-    for (int k = 0; k < 6; ++k) f[k] = (float)__builtin_bit_cast(_Float16, (uint16_t)((k & 1) ? (w[k >> 1] >> 16) : (w[k >> 1] & 0xffffu)));
-    const float tx1 = fmaf(f[0], R.ix, -R.oxi), tx2 = fmaf(f[3], R.ix, -R.oxi);
-    const float ty1 = fmaf(f[1], R.iy, -R.oyi), ty2 = fmaf(f[4], R.iy, -R.oyi);
-    const float tz1 = fmaf(f[2], R.iz, -R.ozi), tz2 = fmaf(f[5], R.iz, -R.ozi);
-    const float tmin = fmaxf(fmaxf(fminf(tx1, tx2), fminf(ty1, ty2)), fminf(tz1, tz2));
-    const float tmax = fminf(fminf(fmaxf(tx1, tx2), fmaxf(ty1, ty2)), fmaxf(tz1, tz2));
-    return (tmin <= fminf(tmax, R.plim)) & (tmax >= 0.0f);
-}
-
-#ifndef VR_NODE4_V2
-#define VR_NODE4_V2 1  // 1: sec_node4v (no sorting network), 0: sec_node4 (A/B)
-#endif
-// One step of the 4-wide traversal without a sorting network: the nearest inner child is walked next
+// One step of the 4-wide traversal without a sorting network (measured against one with a near-to-far sorting
+// network of the children, round 3: 102.4 -> 99.2 ms at C4): the nearest inner child is walked next
 // (a min-reduction over the inner children's entry distances), the other inner children are pushed
 // and the leaf children queued in the node's child order. Empty slots carry NaN boxes, so the slab
 // test alone rejects them. Ring queues only (QCAP = 1 + 2^k).
@@ -1981,13 +1601,7 @@ __device__ __forceinline__ void sec_node4v(const RenderArgs& A, SecRay& R, LdsIn
         // the subtree rooted at R.from is done: its parent next, without that child (every node is still
         // visited at most once: the walk from the record's start subtree up to the root covers the tree).
         // The parent entry carries the child's slot in bits 28-30 (slot + 1), which the next step skips.
-        int32_t up = A.hn4_parent[R.from];
-        if constexpr (kClimbSkip) {  // parents whose other children the ray misses are passed over
-            while (up > 0 && !sibling_hit(A, R, A.hn4_sib[R.from])) {
-                R.from = up & kNodeIndexMask;
-                up = A.hn4_parent[R.from];
-            }
-        }
+        const int32_t up = A.hn4_parent[R.from];
         R.from = up & kNodeIndexMask;
         node = up;  // (-1: the root's subtree is done)
     } else {
@@ -2091,11 +1705,7 @@ __device__ __forceinline__ void list_advance(LeafQueue& Q, int& node, int start)
 #ifndef VR_WW_NODE_UNROLL
 #define VR_WW_NODE_UNROLL 1
 #endif
-#ifndef VR_WW_MIN_LANES
-#define VR_WW_MIN_LANES 0  // > 0: a NODE / PRIM iteration ends once fewer lanes than this can go on (A/B)
-#endif
 constexpr int kRefillMin = VR_WW_REFILL, kNodeSteps = VR_WW_NODE_STEPS, kPrimSteps = VR_WW_PRIM_STEPS;
-constexpr int kMinLanes = VR_WW_MIN_LANES;
 #ifndef VR_WW_PRIM_BIAS
 #define VR_WW_PRIM_BIAS 70  // a PRIM iteration needs this many % of the lanes a NODE iteration could use (A/B)
 #endif
@@ -2121,7 +1731,7 @@ __global__ __launch_bounds__(BLOCK, WAVES) void secondary_ww_kernel(RenderArgs A
     // wave-uniform: the record chunk being handed out and its rays [pool, pool_end) not yet handed out
     uint32_t chunk = 0, pool = 0, pool_end = 0;
     bool counter_done = false;  // wave-uniform: the global chunk counter has passed nchunks
-    bool fin = false;           // the lane's ray is complete and its Tr not yet written (VR_WW_BATCH_FINISH)
+    bool fin = false;           // the lane's ray is complete and its Tr not yet written (batched completions)
     const uint32_t per = A.chunk_rec * (uint32_t)(A.num_lights + A.env_samples);
     const uint32_t nrec = dev_nrec(A), nchunks = (nrec + A.chunk_rec - 1u) >> A.chunk_shift;
     // Claim units: a chunk's rays in hand-out order, cut into 2^split equal parts when the launch has
@@ -2129,9 +1739,6 @@ __global__ __launch_bounds__(BLOCK, WAVES) void secondary_ww_kernel(RenderArgs A
     // tail of the persistent launch (8-way C4 share: 22.7 -> 21.7 ms). Whole chunks otherwise (record
     // locality).
     const uint32_t waves = gridDim.x * (BLOCK / 64u), cpw = nchunks / max(waves, 1u);
-#ifndef VR_WW_BATCH_FINISH
-#define VR_WW_BATCH_FINISH 1  // 1: completed rays write their Tr at the next refill, all in one pass (A/B)
-#endif
 #ifndef VR_WW_SPLIT_CPW
 #define VR_WW_SPLIT_CPW 32  // chunks per resident wave below which claim units get shorter (A/B)
 #endif
@@ -2170,12 +1777,10 @@ __global__ __launch_bounds__(BLOCK, WAVES) void secondary_ww_kernel(RenderArgs A
 #ifdef VR_DIAG_REFILL
             rf_t = __builtin_amdgcn_s_memtime();
 #endif
-#if VR_WW_BATCH_FINISH
             if (fin) {  // the completions since the last refill, in one pass
                 sec_finish<S, true, PURE, WH>(A, R, c);
                 fin = false;
             }
-#endif
             rf_lap(0, true);
             if (pool == pool_end && !counter_done) {  // next unit of a record chunk
                 uint32_t cnext = 0;
@@ -2200,7 +1805,7 @@ __global__ __launch_bounds__(BLOCK, WAVES) void secondary_ww_kernel(RenderArgs A
                 Q.n = 0;
                 Q.j = Q.end = 0;
                 if (live) {
-                    if constexpr (W && VR_NODE4_V2)  // the tree walk starts in the record's start subtree
+                    if constexpr (W)  // the tree walk starts in the record's start subtree
                         if (A.rec_start != nullptr) R.from = A.rec_start[R.rec];
                     list_begin(R, Q, node);
                 }
@@ -2211,12 +1816,10 @@ __global__ __launch_bounds__(BLOCK, WAVES) void secondary_ww_kernel(RenderArgs A
             rf_lap(3, true);
         }
         if (!__any(live)) {
-#if VR_WW_BATCH_FINISH
             if (fin) {  // (only if the refill threshold exceeded the wave: every lane idle refills above)
                 sec_finish<S, true, PURE, WH>(A, R, c);
                 fin = false;
             }
-#endif
             if (counter_done && pool == pool_end) break;
             continue;
         }
@@ -2264,7 +1867,7 @@ __global__ __launch_bounds__(BLOCK, WAVES) void secondary_ww_kernel(RenderArgs A
                 if constexpr (S) c.v[ls >= 0 ? kCtrMu : kCtrPrims]++;  // list members counted apart
                 const WQuad q = wquad(g, R.ray);
                 // A chord within the reference's f32 error band (kChordBand): the exact slow path decides the ray
-                if (__builtin_expect(fabsf(9.0f - q.e2) < kChordBand * q.c, false)) R.needs_stop = true;
+                if constexpr (kChordBand > 0.0f) R.needs_stop = R.needs_stop | (fmaf(-kChordBand, q.c, fabsf(9.0f - q.e2)) < 0.0f);
                 R.cmax = (ls >= 0 && q.c > R.cmax) ? q.c : R.cmax;
                 const bool cand = ls < 0 && q.c <= R.cmax;
                 // A member whose 3-sigma surface passes within rounding of the record position (or that the ray
@@ -2283,7 +1886,7 @@ __global__ __launch_bounds__(BLOCK, WAVES) void secondary_ww_kernel(RenderArgs A
                 if (ls >= 0) R.hitmask |= slot_bit(ls);
                 if constexpr (S) {
                     c.v[kCtrOD]++;
-#if !defined(VR_DIAG_WAVE_UTIL) && !defined(VR_DIAG_CYCLES) && !defined(VR_DIAG_ORIGIN)
+#if !defined(VR_DIAG_WAVE_UTIL) && !defined(VR_DIAG_CYCLES)
                     c.v[kCtrPixels] += cand ? 1u : 0u;  // a list member's depth again (the credit scheme)
 #endif
                 }
@@ -2343,8 +1946,6 @@ __global__ __launch_bounds__(BLOCK, WAVES) void secondary_ww_kernel(RenderArgs A
                     else wtest(load_wrec(A.wrec, (int)j), j, ls);
                 }
                 go = go && Q.has_prim() && !cut_reached<PURE>(R);
-                if constexpr (kMinLanes > 0)  // too few lanes left to fill a wave: end the iteration
-                    if (k + 1 < kPrimSteps && __popcll(__ballot(go)) < kMinLanes) break;
             }
             diag_lap(kCtrPrimQueries);
         } else {  // NODE iteration: up to kNodeSteps node steps per lane
@@ -2355,22 +1956,15 @@ __global__ __launch_bounds__(BLOCK, WAVES) void secondary_ww_kernel(RenderArgs A
                 if constexpr (S) c.v[kCtrSteps] += (__ballot(go) != 0ull && lane == 0u) ? 1u : 0u;
 #endif
                 if (go) {
-                    if constexpr (W && VR_NODE4_V2) sec_node4v<BLOCK, S, QCAP, STACK>(A, R, stack, sp, node, Q, c);
-                    else if constexpr (W) sec_node4<BLOCK, S, QCAP, STACK>(A, R, stack, sp, node, Q, c);
+                    if constexpr (W) sec_node4v<BLOCK, S, QCAP, STACK>(A, R, stack, sp, node, Q, c);
                     else sec_node<BLOCK, S, QCAP, STACK, H>(A, R, stack, sp, node, Q, c);
                 }
                 go = go && node >= 0 && Q.n <= QCAP - kRoom;
-                if constexpr (kMinLanes > 0)
-                    if (k + 1 < kNodeSteps && __popcll(__ballot(go)) < kMinLanes) break;
             }
             diag_lap(kCtrSteps);
         }
         if (live && (cut_reached<PURE>(R) || (node == -1 && !Q.has_prim()))) {
-#if VR_WW_BATCH_FINISH
             fin = true;  // written at the next refill (the lane idles until then anyway)
-#else
-            sec_finish<S, true, PURE, WH>(A, R, c);
-#endif
             live = false;
         }
     }
@@ -2487,39 +2081,6 @@ __global__ __launch_bounds__(256) void parents_kernel(const HNode4* __restrict__
     if (c.w > 0) parent[c.w] = (int32_t)(i | (4u << 28));
 }
 
-// Box (f16, scene-normalised, as the node's) of the union of every node's siblings: the children of its
-// parent other than itself (leaves included, empty slots not). A ray climbing out of a finished subtree
-// that misses its siblings' box has nothing to do at the parent (VR_CLIMB_SKIP).
-__global__ __launch_bounds__(256) void siblings_kernel(const HNode4* __restrict__ nodes, uint32_t n, uint4* __restrict__ sib) {
-    const uint32_t p = blockIdx.x * 256u + threadIdx.x;
-    if (p >= n) return;
-    const HNode4 h = nodes[p];
-    float lo[4][3], hi[4][3];
-    for (int i = 0; i < 4; ++i)
-        for (int k = 0; k < 3; ++k) {
-            lo[i][k] = (float)__builtin_bit_cast(_Float16, h.h[i][k]);
-            hi[i][k] = (float)__builtin_bit_cast(_Float16, h.h[i][3 + k]);
-        }
-    for (int i = 0; i < 4; ++i) {
-        if (h.c[i] <= 0) continue;
-        float ul[3] = {INFINITY, INFINITY, INFINITY}, uh[3] = {-INFINITY, -INFINITY, -INFINITY};
-        for (int j = 0; j < 4; ++j) {
-            if (j == i || h.c[j] == 0) continue;
-            for (int k = 0; k < 3; ++k) {
-                ul[k] = fminf(ul[k], lo[j][k]);
-                uh[k] = fmaxf(uh[k], hi[j][k]);
-            }
-        }
-        uint16_t b[8];
-        for (int k = 0; k < 3; ++k) {  // (f16 values: the conversions are exact; no sibling: an inverted box)
-            b[k] = __builtin_bit_cast(uint16_t, (_Float16)ul[k]);
-            b[3 + k] = __builtin_bit_cast(uint16_t, (_Float16)uh[k]);
-        }
-        b[6] = b[7] = 0;
-        sib[h.c[i]] = make_uint4(b[0] | ((uint32_t)b[1] << 16), b[2] | ((uint32_t)b[3] << 16), b[4] | ((uint32_t)b[5] << 16), 0u);
-    }
-}
-
 // ---- the secondary rays' own 4-wide tree: the same nodes with tight boxes (round 4) -------------------
 // The shared tree's boxes are the primitives' 3-sigma boxes padded by 5 % (gaussian_bounds): the exact
 // M-form quadratic of the primary and free-flight rays, evaluated from a camera several units away,
@@ -2620,20 +2181,14 @@ __global__ __launch_bounds__(256) void refit_kernel(const HNode4* __restrict__ s
     }
 }
 
-// Start subtree of a record's secondary rays: the deepest 4-wide node whose box holds the record position
-// with `margin` (scene-normalised units) to spare, taking at every level the inner child with the most
-// room. The rays walk that subtree first and then climb to its parents (sec_node4v), so every node is
+// Start subtree of a record's secondary rays: the deepest 4-wide node whose box holds the record position,
+// taking at every level the inner child with the most room. The rays walk that subtree first and then climb to its parents (sec_node4v), so every node is
 // still visited at most once, and a ray whose optical-depth cut-off is reached near its origin — most of
 // them: the record sits inside an opaque blob's neighbours — skips the descent from the root.
-#ifndef VR_START_MARGIN
-#define VR_START_MARGIN 0.0f  // room (world units) the start subtree's box keeps around the record position (A/B)
-#endif
-#ifndef VR_START_FROM_MEMBER
-#define VR_START_FROM_MEMBER 1  // 1: a record with an active Gaussian starts at the node holding that Gaussian's leaf (A/B)
-#endif
 // Every record has an active Gaussian (a step scatters only with sigma_s > 0): the 4-wide node whose
 // child is that Gaussian's leaf is a leaf-level node near the record (the Gaussian holds the position),
-// found with two loads instead of a descent from the root.
+// found with two loads instead of a descent from the root (record_start_kernel 0.63 -> ~0.1 ms at C4); the
+// descent remains for a record without one.
 __global__ __launch_bounds__(256) void prim_node_kernel(const HNode4* __restrict__ nodes, uint32_t n, int32_t* __restrict__ map) {
     const uint32_t i = blockIdx.x * 256u + threadIdx.x;
     if (i >= n) return;
@@ -2645,9 +2200,8 @@ __global__ __launch_bounds__(256) void prim_node_kernel(const HNode4* __restrict
 }
 __global__ __launch_bounds__(256) void record_start_kernel(RenderArgs A) {
     const uint32_t nrec = dev_nrec(A);
-    const float margin = VR_START_MARGIN * A.hn_scale;
     for (uint32_t r = blockIdx.x * 256u + threadIdx.x; r < nrec; r += gridDim.x * 256u) {
-        if (VR_START_FROM_MEMBER && A.prim_node4 != nullptr) {
+        if (A.prim_node4 != nullptr) {
             const uint4 meta = A.rec_meta[r];
             if ((meta.w & ~kRecBoundary) > 0u) {
                 A.rec_start[r] = A.prim_node4[A.rec_act[meta.z]];
@@ -2663,7 +2217,7 @@ __global__ __launch_bounds__(256) void record_start_kernel(RenderArgs A) {
             const uint4 q0 = np[0], q1 = np[1], q2 = np[2], rf = np[3];
             const uint32_t w[12] = {q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, q1.z, q1.w, q2.x, q2.y, q2.z, q2.w};
             const int32_t ref[4] = {(int32_t)rf.x, (int32_t)rf.y, (int32_t)rf.z, (int32_t)rf.w};
-            float best = margin;
+            float best = 0.0f;
             int32_t next = -1;
 #pragma unroll
             for (int i = 0; i < 4; ++i) {
@@ -2745,12 +2299,6 @@ __global__ __launch_bounds__(256) void record_cut_kernel(RenderArgs A, float bud
 // record's lights and environment samples in the reference's order. Without env_order a chunk's
 // rays are sample-major ([sample][record-in-chunk]) and are read in place (coalesced).
 constexpr int kRadBlock = 64;
-#ifndef VR_RAD_UNROLL
-#define VR_RAD_UNROLL 1  // the chunk gather's loads in flight per lane (A/B at C4: 1: 1.59 ms, 4: 1.85, 12: 2.48)
-#endif
-#ifndef VR_RAD_VEC
-#define VR_RAD_VEC 1  // the chunk gather in 16-B Tr / 8-B order loads (A/B at C4: 0.96 vs 1.59 ms)
-#endif
 template <bool ORDERED>
 __global__ __launch_bounds__(kRadBlock) void record_radiance_kernel(RenderArgs A) {
     extern __shared__ float s_tr[];  // ORDERED: [record-in-chunk][sample]
@@ -2759,7 +2307,7 @@ __global__ __launch_bounds__(kRadBlock) void record_radiance_kernel(RenderArgs A
     for (uint32_t chunk = blockIdx.x; chunk < nch; chunk += gridDim.x) {
         const float* tr = A.tr + (size_t)chunk * per;
         if constexpr (ORDERED) {
-#if VR_RAD_VEC
+          // the chunk gather in 16-B Tr / 8-B order loads (C4: 0.96 ms; 4-B loads 1.59, unrolled 4-B loads 1.85-2.48)
           if ((cr & 3u) == 0u) {  // four rays per load: the light rows and the env entries stay 4-aligned
             const uint32_t nlc = nl * cr;
             const uint16_t* ord = A.env_order + (size_t)chunk * (cr * ne);
@@ -2779,8 +2327,6 @@ __global__ __launch_bounds__(kRadBlock) void record_radiance_kernel(RenderArgs A
                 }
             }
           } else
-#endif
-#pragma unroll VR_RAD_UNROLL
             for (uint32_t i = threadIdx.x; i < per; i += kRadBlock) {
                 uint32_t s, rl;
                 if (i < nl * cr) {
@@ -2869,9 +2415,6 @@ __global__ __launch_bounds__(256) void accumulate_kernel(RenderArgs A) {
 #endif
 constexpr int kActFast = VR_MARCH_ACT, kActBig = VR_MARCH_ACT_BIG, kBlockFast = VR_MARCH_BLOCK;
 constexpr int kActFallback = 64, kBlockFallback = 64;
-#ifndef VR_FALLBACK_WIDE
-#define VR_FALLBACK_WIDE 1  // 1: the one-pixel-per-wave fallback march walks the 4-wide tree (A/B)
-#endif
 constexpr int kBlockSecondary = 256;
 
 hipError_t gauss_bin(const RenderArgs& A, bool emit, hipStream_t stream) {
@@ -2908,7 +2451,7 @@ static hipError_t march_pass(const RenderArgs& A, hipStream_t stream) {
                            dim3(kBlockFast), 0, stream, A);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
-    if (H && A.hnodes4 != nullptr && VR_FALLBACK_WIDE)
+    if (H && A.hnodes4 != nullptr)  // the one-pixel-per-wave fallback march walks the 4-wide tree
         hipLaunchKernelGGL((dev::march_fallback_kernel<kActFallback, kBlockFallback, S, H, true>), dim3(1024), dim3(kBlockFallback), 0,
                            stream, A);
     else
@@ -3005,7 +2548,7 @@ hipError_t gauss_secondary(const RenderArgs& A, hipStream_t stream, bool stats) 
         if (e != hipSuccess) return e;
     }
     if (A.env_order != nullptr) {
-        hipLaunchKernelGGL(dev::env_order_kernel<256>, dim3(record_grid(A, A.chunk_rec * (VR_ENV_ORDER_WAVE ? 4 : 1), 4096)), dim3(256), 0,
+        hipLaunchKernelGGL(dev::env_order_kernel<256>, dim3(record_grid(A, A.chunk_rec * 4, 4096)), dim3(256), 0,
                            stream, A);
         hipError_t e = hipGetLastError();
         if (e != hipSuccess) return e;
@@ -3016,9 +2559,8 @@ hipError_t gauss_secondary(const RenderArgs& A, hipStream_t stream, bool stats) 
     return stats ? secondary_launch<true, false>(A, stream) : secondary_launch<false, false>(A, stream);
 }
 
-hipError_t gauss_parents(const HNode4* nodes, uint32_t n, int32_t* parent, uint4* sib, int32_t* prim_node, hipStream_t stream) {
+hipError_t gauss_parents(const HNode4* nodes, uint32_t n, int32_t* parent, int32_t* prim_node, hipStream_t stream) {
     hipLaunchKernelGGL(dev::parents_kernel, dim3((n + 255) / 256), dim3(256), 0, stream, nodes, n, parent);
-    hipLaunchKernelGGL(dev::siblings_kernel, dim3((n + 255) / 256), dim3(256), 0, stream, nodes, n, sib);
     if (prim_node != nullptr) hipLaunchKernelGGL(dev::prim_node_kernel, dim3((n + 255) / 256), dim3(256), 0, stream, nodes, n, prim_node);
     return hipGetLastError();
 }

@@ -172,46 +172,6 @@ __device__ __forceinline__ bool intersect_fast(const Quad& q, float& t_enter, fl
     return true;
 }
 
-// Conservative pre-test for the primary march's exact decisions (intersect() + an interval condition):
-// the same crossing in the FMA-contracted / hardware-rcp forms with a margin that bounds the difference
-// to the exact forms many times over (discriminant: 1e-3 of its terms' magnitude, distances: 1 % of the
-// chord + 1e-4 (1 + |t|)). Returns the crossing [t0, t1] of the fast forms and false when the exact test
-// could go either way — grazing rays, a degenerate or non-positive-definite M, NaN — so only Gaussians
-// the exact test would certainly reject are ever skipped: every accepted Gaussian, and every decision,
-// stays the exact test's (bit-identical march).
-__device__ __forceinline__ bool fast_crossing(const GRec& g, const Ray& r, float& t0, float& t1, float& tol) {
-    const Quad f = quad_fast(g, r);
-    if (!(f.A > 0.0f)) return false;
-    const float c4 = 4.0f * f.A * (f.Cq - 9.0f);
-    const float disc = fmaf(f.B, f.B, -c4), scale = fmaf(f.B, f.B, fabsf(c4));
-    if (disc < -1e-3f * scale) {  // certainly no crossing
-        t0 = t1 = INFINITY;
-        tol = 0.0f;
-        return true;
-    }
-    if (!(disc > 1e-3f * scale)) return false;  // grazing (or NaN): the exact test decides
-    const float sd = __builtin_amdgcn_sqrtf(disc), inv = __builtin_amdgcn_rcpf(2.0f * f.A);
-    t0 = (-f.B - sd) * inv;
-    t1 = (-f.B + sd) * inv;
-    tol = 1e-2f * (t1 - t0) + 1e-4f * (1.0f + fabsf(t0) + fabsf(t1));
-    return true;
-}
-// True if the exact test certainly rejects Gaussian g as an entrant of the window (t_lo, t_k]: the exact
-// condition is intersect(q, a, b) && a > t_lo && a <= t_k && b > t_k with a = max(t0, 0), b = t1.
-__device__ __forceinline__ bool fast_reject_window(const GRec& g, const Ray& r, float t_lo, float t_k) {
-    float t0, t1, tol;
-    if (!fast_crossing(g, r, t0, t1, tol)) return false;
-    if (t0 == INFINITY) return true;
-    return (t1 + tol <= t_k) || (fmaxf(t0 - tol, 0.0f) > t_k) || (fmaxf(t0 + tol, 0.0f) <= t_lo);
-}
-// ... as the closest entry after t_lo below `best`: intersect(q, a, b) && a > t_lo && a < best.
-__device__ __forceinline__ bool fast_reject_closest(const GRec& g, const Ray& r, float t_lo, float best) {
-    float t0, t1, tol;
-    if (!fast_crossing(g, r, t0, t1, tol)) return false;
-    if (t0 == INFINITY) return true;
-    return (t1 + tol < 0.0f) || (fmaxf(t0 + tol, 0.0f) <= t_lo) || (fmaxf(t0 - tol, 0.0f) >= best);
-}
-
 __device__ __forceinline__ float optical_depth_fast(const GRec& g, const Quad& q, float t0, float t1) {
     const float twoA = 2.0f * q.A;
     const float r2A = __builtin_amdgcn_rcpf(twoA);
@@ -612,113 +572,6 @@ __device__ __forceinline__ bool traverse_wide(const RenderArgs& A, const Ray& r0
             if (sp == 0) return true;
             --sp;
             node = stack[sp * stride];
-        }
-    }
-}
-
-// ---- walks that start in a local subtree and climb (the 4-wide tree with parents) -----------------
-// Deepest 4-wide node whose (f16) box holds the points p and q (scene-normalised coordinates), taking at
-// every level the inner child with the most room; 0 (the root) if none below it does.
-__device__ __forceinline__ int32_t wide_start_node(const RenderArgs& A, const float* p, const float* q) {
-    int32_t node = 0;
-    for (int depth = 0; depth < 64; ++depth) {
-        const uint4* np = reinterpret_cast<const uint4*>(A.hnodes4 + node);
-        const uint4 q0 = np[0], q1 = np[1], q2 = np[2], rf = np[3];
-        const uint32_t w[12] = {q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, q1.z, q1.w, q2.x, q2.y, q2.z, q2.w};
-        const int32_t ref[4] = {(int32_t)rf.x, (int32_t)rf.y, (int32_t)rf.z, (int32_t)rf.w};
-        float best = 0.0f;
-        int32_t next = -1;
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            float room = INFINITY;
-#pragma unroll
-            for (int k = 0; k < 3; ++k) {
-                const uint32_t wl = w[(6 * i + k) >> 1], wh = w[(6 * i + 3 + k) >> 1];
-                const float lo = (float)__builtin_bit_cast(_Float16, (uint16_t)(((6 * i + k) & 1) ? (wl >> 16) : (wl & 0xffffu)));
-                const float hi = (float)__builtin_bit_cast(_Float16, (uint16_t)(((6 * i + 3 + k) & 1) ? (wh >> 16) : (wh & 0xffffu)));
-                room = fminf(room, fminf(fminf(p[k] - lo, hi - p[k]), fminf(q[k] - lo, hi - q[k])));
-            }
-            const bool take = (ref[i] > 0) & (room >= best);  // (a NaN box never has room)
-            best = take ? room : best;
-            next = take ? ref[i] : next;
-        }
-        if (next < 0) break;
-        node = next;
-    }
-    return node;
-}
-
-// traverse_wide's contract (prune / leaf / on_node, unsorted children: for queries whose result does not
-// depend on the visit order), starting at 4-wide node `start`: its subtree first, then the climb — at
-// every ancestor, the children other than the one just finished (its slot + 1 rides in the parent entry,
-// A.hn4_parent), passed over when the ray's prune rejects the union box of those siblings (A.hn4_sib;
-// prune must be monotone in the box, as every query's is: a box holding another passes if that one
-// does). Every node whose box the query needs is still visited once.
-template <int CAP, typename Prune, typename Leaf, typename OnNode = NoCount>
-__device__ __forceinline__ bool traverse_wide_climb(const RenderArgs& A, const Ray& r0, int32_t start, int* stack, int stride,
-                                                    Prune prune, Leaf leaf, OnNode on_node = OnNode()) {
-    float ox = r0.ox, oy = r0.oy, oz = r0.oz;
-    node_space<true>(A, ox, oy, oz);
-    auto inv = [&](float d) {
-        d *= A.hn_scale;
-        return __frcp_rn(fabsf(d) > 1e-30f ? d : copysignf(1e-30f, d));
-    };
-    const float ix = inv(r0.dx), iy = inv(r0.dy), iz = inv(r0.dz);
-    const float oxi = ox * ix, oyi = oy * iy, ozi = oz * iz;
-    auto box_hit = [&](const uint4& b) {  // the siblings' union box (6 f16 in the first 12 B)
-        const uint32_t w[3] = {b.x, b.y, b.z};
-        float f[6];
-#pragma unroll
-        for (int k = 0; k < 6; ++k) f[k] = (float)__builtin_bit_cast(_Float16, (uint16_t)((k & 1) ? (w[k >> 1] >> 16) : (w[k >> 1] & 0xffffu)));
-        const float tx1 = fmaf(f[0], ix, -oxi), tx2 = fmaf(f[3], ix, -oxi);
-        const float ty1 = fmaf(f[1], iy, -oyi), ty2 = fmaf(f[4], iy, -oyi);
-        const float tz1 = fmaf(f[2], iz, -ozi), tz2 = fmaf(f[5], iz, -ozi);
-        const float tmin = fmaxf(fmaxf(fminf(tx1, tx2), fminf(ty1, ty2)), fminf(tz1, tz2));
-        const float tmax = fminf(fminf(fmaxf(tx1, tx2), fmaxf(ty1, ty2)), fmaxf(tz1, tz2));
-        return (tmax >= fmaxf(tmin, 0.0f)) && prune(tmin, tmax);
-    };
-    int sp = 0;
-    int32_t node = start, from = start;
-    int skip = 0;  // child slot + 1 the node step at a climbed-to ancestor leaves out
-    for (;;) {
-        on_node();
-        float key[4];
-        int32_t kr[4];
-        wide_children<Prune, false>(A, node, ix, iy, iz, oxi, oyi, ozi, prune, key, kr);
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            if (skip == i + 1) kr[i] = 0;
-            if (kr[i] < 0 && !leaf(leaf_first(kr[i]), leaf_count(kr[i]))) return true;
-        }
-        int first = -1;
-        int32_t next = 0;
-#pragma unroll
-        for (int i = 3; i >= 0; --i) {
-            first = kr[i] > 0 ? i : first;
-            next = kr[i] > 0 ? kr[i] : next;
-        }
-        if (sp + 3 > CAP) return false;
-#pragma unroll
-        for (int i = 3; i >= 0; --i)
-            if (kr[i] > 0 && i != first) stack[(sp++) * stride] = kr[i];
-        skip = 0;
-        if (first >= 0) {
-            node = next;
-        } else if (sp > 0) {
-            --sp;
-            node = stack[sp * stride];
-        } else {  // the subtree rooted at `from` is done: climb
-            for (;;) {
-                if (from == 0) return true;
-                const int32_t up = A.hn4_parent[from];
-                const bool go = box_hit(A.hn4_sib[from]);
-                from = up & 0x0fffffff;
-                if (go) {
-                    node = from;
-                    skip = up >> 28;
-                    break;
-                }
-            }
         }
     }
 }

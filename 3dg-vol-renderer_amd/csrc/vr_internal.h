@@ -125,13 +125,6 @@ constexpr int kFrameAttempts = 7;
 constexpr int32_t kFFBigCap = 1024;          // ff_fallback_kernel: Gaussians overlapping one point it can sweep
 constexpr uint32_t kFFBigThreads = 1024;     // ff_fallback_kernel: threads (scratch row stride)
 
-// Host-side polling of the staged free-flight pipeline (vr_freeflight.hip ffs_run): two pinned words
-// and their events.
-struct FFPoll {
-    uint32_t* host;
-    hipEvent_t ev[2];
-};
-
 // Kernel launch parameters (passed by value).
 struct RenderArgs {
     // camera
@@ -161,7 +154,6 @@ struct RenderArgs {
     const int32_t* prim_node4;  // the 4-wide node whose child is each record's leaf (record starts), or nullptr
     const int32_t* hn4_parent;  // parent of every HNode4 | (its slot + 1) << 28 (root: -1); nullptr: walks start at the root
     uint32_t num_nodes4;        // HNode4 count
-    const uint4* hn4_sib;       // per HNode4: f16 box of the union of its siblings (the climb's skip test)
     float hn_center[3], hn_scale;
     const SphereRecord* spheres;
     int32_t num_prims;
@@ -247,23 +239,7 @@ struct RenderArgs {
     uint32_t ff_nee_cap;     // queue capacity in rays (0: every shadow ray is traced inline)
     int32_t ff_nee_refill;   // idle lanes of a wave that trigger its refill in ff_nee_kernel
     float4* ff_tail;         // [path of the launch]: {inline radiance xyz, first queued ray | kFFTailAfter}
-    // Staged free-flight pipeline (vr_freeflight.hip ffs_* kernels): ff_pool path slots step through a
-    // hit-collection, an event-sweep and a shading kernel per iteration, queued between them; the scratch
-    // rows above are indexed by slot (ff_threads = ff_pool). ff_pool == 0: the persistent path kernel.
-    uint32_t ff_pool;
     int32_t ff_sm;           // persistent path kernel: 1 the phase-scheduled ff_path_sm_kernel, 0 ff_path_kernel
-    float4* fs_ray0;         // per slot: {origin, target optical depth of the bounce}
-    float4* fs_ray1;         // {direction, W0: start of the hit window}
-    float4* fs_tp;           // {throughput, t_prev: the sweep's segment start}
-    float4* fs_L;            // {inline radiance, t_cut: end of the collected window}
-    float4* fs_out;          // {t_scatter (-1: no scatter, -2: over capacity), albedo, -, -}
-    double* fs_acc;          // optical depth accumulated before the window (FreeFlightGaussians: a float)
-    unsigned long long* fs_rng;  // PCG32 state (stream 1)
-    uint4* fs_meta;          // {path index of the launch, first / last queued shadow ray, bounce}
-    uint4* fs_meta2;         // {flags (1: defer NEE, 2: inline radiance after the queued), window capacity, hits, -}
-    uint32_t* fs_q;          // slot queues, ff_pool entries each: collect[0], collect[1], sweep, shade
-    uint32_t* fs_cnt;        // [0], [1] collect queue lengths, [2] sweep, [3] shade, [4], [5] claim counters
-    uint32_t fs_cur;         // the collect queue this iteration consumes
     const uint32_t* gauss_order;  // record (leaf order) -> scene index
     uint32_t* rec_bits;      // RECORD_PIXEL_GAUSSIANS bitset [word][pixel] (nullptr: not recording)
     uint32_t rec_npix;       // W * H

@@ -398,7 +398,7 @@ class Device:
                "ff_window0": L.VR_OPT_FF_WINDOW0, "record_capacity": L.VR_OPT_RECORD_CAPACITY,
                "device_bvh": L.VR_OPT_DEVICE_BVH, "ff_nee_queue": L.VR_OPT_FF_NEE_QUEUE,
                "march_binned": L.VR_OPT_MARCH_BINNED, "ff_solver": L.VR_OPT_FF_SOLVER,
-               "start_subtree": L.VR_OPT_START_SUBTREE, "ff_staged": L.VR_OPT_FF_STAGED, "ff_kernel": L.VR_OPT_FF_KERNEL,
+               "start_subtree": L.VR_OPT_START_SUBTREE, "ff_kernel": L.VR_OPT_FF_KERNEL,
                "sec_tight": L.VR_OPT_SEC_TIGHT, "march_wide_min": L.VR_OPT_MARCH_WIDE_MIN}
 
     def set_option(self, name, value):

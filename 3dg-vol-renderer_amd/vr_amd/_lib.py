@@ -24,7 +24,6 @@ VR_OPT_FF_NEE_QUEUE = 6
 VR_OPT_MARCH_BINNED = 7
 VR_OPT_FF_SOLVER = 8
 VR_OPT_START_SUBTREE = 9
-VR_OPT_FF_STAGED = 10
 VR_OPT_SEC_TIGHT = 11
 VR_OPT_MARCH_WIDE_MIN = 12
 VR_OPT_FF_KERNEL = 13

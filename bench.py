@@ -408,7 +408,7 @@ def main():
     ap.add_argument("--dump-frame", default=None,
                     help="rank 0 saves the last timed frame (H x W x 3 f32 .npy; ray-march): multi-GPU equality tests")
     ap.add_argument("--opt", action="append", default=[],
-                    help="name=value device option (vr_set_option, e.g. ff_staged=0) for A/B runs")
+                    help="name=value device option (vr_set_option, e.g. ff_kernel=2) for A/B runs")
     args = ap.parse_args()
     if args.config == "main":  # tests/main.cpp renders MultiScatterGaussians
         if args.integrator == "raymarch":

@@ -380,13 +380,7 @@ typedef enum vr_option {
                                     climbs to the root (no descent from the root for rays cut near their origin);
                                     0: every walk starts at the root. Same Gaussians, same decisions; only the
                                     order of the optical-depth sum differs (float association). */
-    VR_OPT_FF_STAGED = 10,       /* free-flight integrators: 0 (default): the persistent path kernel (a whole
-                                    bounce per lane and wave iteration); 1: the staged pipeline (a pool of path
-                                    slots stepping through hit-collection, event-sweep and shading kernels,
-                                    queued between them, each with per-lane refill; slower).
-                                    Frames are identical. The staged pipeline is host-synchronous: the host
-                                    polls the path queue between iterations, so vr_render_tiles_device blocks
-                                    until the frame's iterations are issued. */
+    /* 10: retired (round 6): the staged free-flight pipeline, measured 2.3x slower than the persistent path kernel */
     VR_OPT_SEC_TIGHT = 11,       /* RayMarchingGaussians secondary rays, applied at the next upload: 1 (default):
                                     their own copy of the 4-wide tree with the exact boxes of the ellipsoids the
                                     whitened test accepts (the shared tree's boxes are padded by 5 % for the

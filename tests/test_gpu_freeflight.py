@@ -267,7 +267,7 @@ def test_first_frame_queue_sizing_equals_queue_at_its_bound():
 
 @pytest.mark.parametrize("window0", [0, 2])
 def test_multiscatter_frame_is_deterministic(window0):
-    """The same frame from three fresh contexts, bit for bit, and from the staged pipeline too, on the C2
+    """The same frame from three fresh contexts, bit for bit, on the C2
     scene with many hit windows. A window's cut once depended on whether the walk had skipped a subtree
     while the hit buffer was full, which depends on the wave's NODE/PRIM schedule (so on which paths
     shared the wave): about 100 of the C2 bench frame's 262k pixels then differed by an ulp from run to
@@ -276,7 +276,6 @@ def test_multiscatter_frame_is_deterministic(window0):
     integ = vr.MultiScatterGaussians(vr.Pinhole_Camera(CAM_POS, main_view_dir(), FOV), 4, 5)
     opts = {"ff_window0": window0} if window0 else {}
     frames = [_fresh_render(scene, integ, 160, 160, **opts)[0] for _ in range(3)]
-    frames.append(_fresh_render(scene, integ, 160, 160, ff_staged=1, **opts)[0])
     for k, f in enumerate(frames[1:], 1):
         d = np.abs(f - frames[0])
         assert np.array_equal(f, frames[0], equal_nan=True), f"frame {k}: {int((d.max(-1) > 0).sum())} pixels differ, max {np.nanmax(d):.2e}"
@@ -389,41 +388,3 @@ def test_solver_modes_change_the_frame():
     finally:
         vr.Device.get(0).set_option("ff_solver", 0)
     assert not np.array_equal(frames["analytic_newton"], frames["uniform"])
-
-
-@pytest.mark.parametrize("multi", [False, True])
-@pytest.mark.parametrize("name,W,spp", [("50_random.txt", 40, 8), ("many_gaussians.txt", 32, 8), ("god_ray.txt", 32, 4)])
-def test_staged_pipeline_equals_persistent_kernel(name, W, spp, multi, device_options):
-    """VR_OPT_FF_STAGED: the staged pipeline (path slots stepping through the hit-collection, event-sweep and
-    shading kernels) runs every path's operations in the persistent path kernel's order, so the two
-    frames are equal bit for bit (while a bounce's hits fit its first window, as here)."""
-    scene = vr.Scene.load_GMM(scene_path(name))
-    frames = {}
-    for staged in (0, 1):
-        device_options("ff_staged", staged)
-        frames[staged] = _gpu(scene, W, W, multi, spp)
-    assert np.array_equal(frames[0], frames[1])
-
-
-def test_staged_pipeline_windows_and_fallback_equal_persistent(device_options):
-    """The staged pipeline's capacity fallback (more Gaussians overlapping one point than the rows hold)
-    equals the persistent kernel's frame bit for bit. With hit windows of capacity 1 (a new collection per
-    event) both follow the oracle (test_window_capacity_does_not_change_results), but where a window ends
-    depends on how far a walk's pruning had got when its leaves were tested — the interleaving of node and
-    primitive steps among the lanes sharing a wave, which differs between the two schedules — and the
-    active Gaussians re-enter at every window start, so the frames agree up to float association."""
-    coinc, _ = _coincident_scene(200)
-    scene = vr.Scene.load_GMM(scene_path("50_random.txt"))
-    out = {}
-    for staged in (0, 1):
-        device_options("ff_staged", staged)
-        fb = _gpu(coinc, 16, 16, True, 4)
-        device_options("ff_window0", 1)
-        win = _gpu(scene, 24, 24, True, 4)
-        device_options("ff_window0", 0)
-        out[staged] = (fb, win)
-    assert np.array_equal(out[0][0], out[1][0])
-    d = np.abs(out[0][1].astype(np.float64) - out[1][1]).max()
-    same = float(np.mean(np.all(out[0][1] == out[1][1], axis=-1)))
-    print(f"capacity-1 windows: max|d| {d:.2e}, bitwise-equal pixels {same:.4f}")
-    assert d <= 1e-5 and same >= 0.5
