@@ -72,6 +72,11 @@ constexpr float kMemberAmb = VR_MEMBER_AMB;
 #endif
 constexpr float kChordBand = VR_CHORD_BAND * 1.1920928955078125e-7f;
 constexpr uint32_t kRecBoundary = 0x80000000u;  // rec_meta.w: active count | this flag
+#ifdef VR_DIAG_UNION  // diagnostic builds only: the march's counter slots report the union-walk census
+constexpr bool kDiagUnion = true;
+#else
+constexpr bool kDiagUnion = false;
+#endif
 
 // Bit of active-list slot `slot` in a ray's 64-bit hit mask. Records with more than 64 active
 // Gaussians (march_deep_kernel) find their missed members by re-intersecting the whole list instead.
@@ -334,7 +339,7 @@ __device__ __forceinline__ bool march_step(const RenderArgs& A, const Ray& ray, 
                 smu += __shfl(m, sl, 64);
                 smua += __shfl(ma, sl, 64);
                 if (!A.pure) tau_seg += __shfl(od, sl, 64);
-                if constexpr (S) {
+                if constexpr (S && !kDiagUnion) {
                     c.v[kCtrMu]++;
                     c.v[kCtrOD]++;
                     c.v[kCtrPrims]++;
@@ -355,7 +360,7 @@ __device__ __forceinline__ bool march_step(const RenderArgs& A, const Ray& ray, 
             smu += m;
             smua += m * g.albedo;
             if (!A.pure) tau_seg += optical_depth(g, q, t_k, t_k1);
-            if constexpr (S) {
+            if constexpr (S && !kDiagUnion) {
                 c.v[kCtrMu]++;
                 c.v[kCtrOD]++;
                 c.v[kCtrPrims]++;
@@ -364,7 +369,7 @@ __device__ __forceinline__ bool march_step(const RenderArgs& A, const Ray& ray, 
     }
     act.n = w;
     if (w == 0) return true;
-    if constexpr (S) c.v[kCtrSteps]++;
+    if constexpr (S && !kDiagUnion) c.v[kCtrSteps]++;
     float sigma_s = 0.0f;
     if (smu > 0.0f) {
         float a_mix = smua / smu;
@@ -452,6 +457,67 @@ __device__ __forceinline__ bool march_step(const RenderArgs& A, const Ray& ray, 
 // active list is split over the lanes (one Gaussian each), its sums and compaction then taken in
 // list order through lane broadcasts — the serial loop's operations in its order, so the result is
 // bit-identical — and lane 0 writes the records.
+#ifdef VR_DIAG_UNION
+// Diagnostic builds only (with vr_count_work): what a wave-coherent walk of the march's window queries would cost.
+// At every query call, the lanes running the query this iteration walk the 4-wide tree as one wave: a node is
+// fetched once for the wave (wave-uniform stack in LDS) and descended into if any lane's box test and prune keep
+// it (ballot). Counted per call, in the march counters' slots: kCtrSecRays += union node visits, kCtrMu += union
+// leaf visits, kCtrOD += the per-lane walk's node-fetch passes (the largest per-lane node-step count among the
+// calling lanes: what the SIMT walk's loop runs), kCtrSteps += calls; kCtrNodes keeps the per-lane node steps.
+template <typename Prune>
+__device__ void union_walk_count(const RenderArgs& A, const Ray& r0, Prune prune, Ctr& c) {
+    __shared__ int ustack[256];  // (march workgroups are one wave)
+    float ox = r0.ox, oy = r0.oy, oz = r0.oz;
+    node_space<true>(A, ox, oy, oz);
+    auto inv = [&](float d) {
+        d *= A.hn_scale;
+        return __frcp_rn(fabsf(d) > 1e-30f ? d : copysignf(1e-30f, d));
+    };
+    const float ix = inv(r0.dx), iy = inv(r0.dy), iz = inv(r0.dz);
+    const float oxi = ox * ix, oyi = oy * iy, ozi = oz * iz;
+    const uint64_t act = __ballot(1);
+    const bool first_lane = __lane_id() == (uint32_t)(__ffsll((unsigned long long)act) - 1);
+    uint32_t visits = 0, leaves = 0;
+    int sp = 0, node = 0;
+    for (;;) {
+        ++visits;
+        float key[4];
+        int32_t kr[4];
+        wide_children<Prune, false>(A, node, ix, iy, iz, oxi, oyi, ozi, prune, key, kr);
+        const int4 rf = reinterpret_cast<const int4*>(A.hnodes4 + node)[3];
+        const int32_t ref[4] = {rf.x, rf.y, rf.z, rf.w};
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const bool any = __ballot(kr[i] != 0) != 0ull;
+            if (!any) continue;
+            if (ref[i] < 0) {
+                ++leaves;
+            } else if (sp < 256) {
+                if (first_lane) ustack[sp] = ref[i];
+                ++sp;
+            }
+        }
+        __builtin_amdgcn_wave_barrier();
+        if (sp == 0) break;
+        --sp;
+        node = __builtin_amdgcn_readfirstlane(ustack[sp]);
+    }
+    if (first_lane) {
+        c.v[kCtrSecRays] += visits;
+        c.v[kCtrMu] += leaves;
+        c.v[kCtrSteps] += 1u;
+    }
+}
+// Largest per-lane value among the calling lanes (bit-sliced ballots), added once.
+__device__ __forceinline__ void union_walk_simt(uint32_t steps, Ctr& c) {
+    const uint64_t act = __ballot(1);
+    uint32_t m = 0;
+    for (int b = 15; b >= 0; --b)
+        if (__ballot(steps >= (m | (1u << b))) != 0ull) m |= 1u << b;
+    if (__lane_id() == (uint32_t)(__ffsll((unsigned long long)act) - 1)) c.v[kCtrOD] += m;
+}
+#endif
+
 // (Measured and not kept, DESIGN.md §3: window queries starting in the subtree holding the window and climbing,
 // a fast-form pre-test of the candidates, look-ahead windows over 2-4 steps, a closest-entry query merged with
 // the following entrant query, a sorting network in the entrant walk; all bit-identical, all slower at C4.)
@@ -507,7 +573,14 @@ __device__ int march(const RenderArgs& A, uint32_t p, int px, int py, int* act_b
                     }
                     return true;
                 };
+#ifdef VR_DIAG_UNION
+                if constexpr (S && W && !COOP) union_walk_count(A, ray, prune_c, c);
+                const uint32_t n0 = c.v[kCtrNodes];
+#endif
                 if (!walk(prune_c, leaf_c)) return kOverflow;
+#ifdef VR_DIAG_UNION
+                if constexpr (S && W && !COOP) union_walk_simt(c.v[kCtrNodes] - n0, c);
+#endif
                 if (best == INFINITY) break;
                 k = kfirst(ts, nts, step, best);
                 // No entry lies in (t_lo, best) and ts[k - 1] < best: the step's entrant window (t_lo, t_k] holds
@@ -525,6 +598,10 @@ __device__ int march(const RenderArgs& A, uint32_t p, int px, int py, int* act_b
             auto prune_w = [&](float tmin, float tmax) {
                 return tmax >= t_lo - kTPad * (1.0f + fabsf(t_lo)) && tmin <= t_k + kTPad * (1.0f + t_k);
             };
+#ifdef VR_DIAG_UNION
+            if constexpr (S && W && !COOP) union_walk_count(A, ray, prune_w, c);
+            const uint32_t n1 = c.v[kCtrNodes];
+#endif
             const bool ok = walk_any(
                 prune_w,
                 [&](uint32_t first, uint32_t count) {
@@ -549,6 +626,9 @@ __device__ int march(const RenderArgs& A, uint32_t p, int px, int py, int* act_b
                     }
                     return true;
                 });
+#ifdef VR_DIAG_UNION
+            if constexpr (S && W && !COOP) union_walk_simt(c.v[kCtrNodes] - n1, c);
+#endif
             if (ovf || !ok) return kOverflow;
             kq = k + 1;
             if (!march_step<S, COOP>(A, ray, p, px, py, k, t_k, act, T, prev, c, writer)) break;

@@ -28,7 +28,8 @@ ap.add_argument("--opt", action="append", default=[], help="name=value device op
 args = ap.parse_args()
 
 scene, W, H = bench.build_scene(args.config, 2025)
-W = H = args.size
+if args.size > 0:  # (0: the config's own frame size)
+    W = H = args.size
 cam = vr.Pinhole_Camera(bench.CAM_POS, bench.CAM_VIEW, bench.FOV)
 integ = vr.RayMarchingGaussians(cam, step_size=0.01, env_samples=20, t_eps=1e-6)
 dev = vr.Device.get(0)
