@@ -52,7 +52,7 @@ CAM_VIEW = np.array([0.0, 0.0, -1.0], np.float32)
 FOV = np.float32(0.25 * np.pi)
 HBM_PEAK_GBPS = 8000.0   # MI355X_MICROARCH.md: 8.0 TB/s spec
 FP32_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md: FP32 vector peak
-PMC_SUMMARY = "r05_c4_pmc_summary.json"  # rocprofv3 --pmc passes of this command (profiles/)
+PMC_SUMMARY = "r06_c4_pmc_summary.json"  # rocprofv3 --pmc passes of this command (profiles/)
 
 # Flops per executed operation of the secondary stage (an FMA counts 2, min / max / compare 1, and
 # sqrt / rcp / div / exp / erf 4, the quarter-rate transcendental model of SURVEY §8(d)):
@@ -84,7 +84,7 @@ def secondary_flops(sec):
 # a ray-Gaussian quadratic + intersect 72, an erf evaluation of the event sweep / cached entry factors /
 # distance solver 12 (fma 2 + div 4 + erf 4 + sub/mul 2), a shadow-ray optical depth 98.
 FF_FLOP_WEIGHTS = {"node4": 105, "node2": 44, "prim": 72, "erf": 12, "od": 98}
-FF_PMC_SUMMARY = "r05_ff_{cfg}_pmc_summary.json"  # rocprofv3 --pmc passes of the free-flight lines (profiles/)
+FF_PMC_SUMMARY = "r06_ff_{cfg}_pmc_summary.json"  # rocprofv3 --pmc passes of the free-flight lines (profiles/)
 
 
 def ff_roofline(work, stage_ms, cfg):
