@@ -44,8 +44,8 @@ using namespace vr;
 
 // Pinned report of a frame's counts (launch): [0] fallback queue, [1] error pixels, [2..4] rec_alloc (records,
 // overflow-pool words, capacity exceeded), [5] deep queue, [6..7] counters 2..3 (free-flight fallback paths,
-// shadow-ray queue need), [8] exact slow-path queue.
-constexpr int kReportWords = 9;
+// shadow-ray queue need), [8] exact slow-path queue, [9] band fix-up queue.
+constexpr int kReportWords = 10;
 struct vr_ctx {
     int device = 0;
     hipStream_t stream = nullptr;  // used by the synchronous vr_render
@@ -112,7 +112,7 @@ struct vr_ctx {
         void* p = nullptr;
         size_t bytes = 0;
     };
-    Buf px_first, px_T, rec_pos, rec_meta, rec_next, rec_act, tr, rec_rad, rec_alloc, rec_bloom, slowq;
+    Buf px_first, px_T, rec_pos, rec_meta, rec_next, rec_act, tr, rec_rad, rec_alloc, rec_bloom, slowq, fixq;
     Buf pcg_jump, ray_next, stack_ovf, env_order, env_base, rec_cut, rec_start;
     Buf deep;  // march_deep_kernel: pixel queue + global active lists (vr_gauss.hip)
     Buf bin_cnt, bin_off, bin_ent;  // tile bins of the binned march (VR_OPT_MARCH_BINNED)
@@ -127,6 +127,7 @@ struct vr_ctx {
     uint32_t* h_sizing = nullptr;  // pinned copy of rec_alloc for the sizing march of a context's first frame
     uint64_t rec_hint = 0, ovf_hint = 0;  // record / overflow-pool capacities (0: not known yet)
     uint64_t slow_hint = 0;               // exact slow-path queue: the most rays an earlier frame queued (+ 1/8)
+    uint64_t fix_hint = 0;                // band fix-up queue (secondary_fix_kernel): the same
     uint64_t nee_hint = 0;                // deferred-NEE queue capacity from earlier free-flight frames (0: not known)
     uint32_t last_nee_cap = 0, last_nee_bound = 0;  // the last free-flight frame's queue capacity and its bound
     // A launch found the shadow-ray queue full at its VR_OPT_FF_NEE_QUEUE bound: the frame is reported
@@ -759,6 +760,13 @@ vr_status gauss_pipeline(vr_ctx* c, RenderArgs& A, hipStream_t s, bool stats) {
     A.slowq = (uint32_t*)c->slowq.p;
     A.slowq_cap = (uint32_t)nslow;
     HIP_TRY(hipMemsetAsync(A.slowq, 0, sizeof(uint32_t), s), "hipMemsetAsync(slow queue)");
+    {  // rays with one chord in the f32 error band (secondary_fix_kernel): one per record, or what earlier frames queued
+        const uint64_t nfix = std::min<uint64_t>(std::max<uint64_t>(cap, c->fix_hint), 0x7ffffffeull / 3);
+        if ((st = grow(c->fixq, (3 * nfix + 1) * 4ull, "hipMalloc(band queue)")) != VR_OK) return st;
+        A.fixq = (uint32_t*)c->fixq.p;
+        A.fixq_cap = (uint32_t)nfix;
+        HIP_TRY(hipMemsetAsync(A.fixq, 0, sizeof(uint32_t), s), "hipMemsetAsync(band queue)");
+    }
     if ((st = grow(c->ray_next, 8, "hipMalloc(ray counter)")) != VR_OK) return st;
     A.ray_next = (unsigned long long*)c->ray_next.p;
     {  // traversal-stack overflow of the persistent kernel: kWideStackMax entries for every lane it can keep resident
@@ -910,6 +918,8 @@ vr_status collect(vr_ctx* c) {
         c->rec_hint = std::max<uint64_t>(c->rec_hint, nrec + nrec / 8);
         c->ovf_hint = std::max<uint64_t>(c->ovf_hint, nact + nact / 8);
         c->slow_hint = std::max<uint64_t>(c->slow_hint, nslow + nslow / 8);
+        const uint64_t nfix = c->h_report[9];
+        c->fix_hint = std::max<uint64_t>(c->fix_hint, nfix + nfix / 8);
         // >= 5 % of the pixels re-marched: the scene's active sets outgrow 16 slots; later frames march with
         // kActBig (same operations, so the frames are identical; kept until the next upload)
         if ((uint64_t)c->h_report[0] * 20ull >= c->report_pixels && c->report_pixels > 0) c->march_big = true;
@@ -966,6 +976,7 @@ vr_status launch(vr_ctx* c, RenderArgs& A, const vr_render_params* p, hipStream_
                 "hipMemcpyAsync(report)");
         HIP_TRY(hipMemcpyAsync(&c->h_report[5], A.deepq, sizeof(uint32_t), hipMemcpyDeviceToHost, s), "hipMemcpyAsync(report)");
         HIP_TRY(hipMemcpyAsync(&c->h_report[8], A.slowq, sizeof(uint32_t), hipMemcpyDeviceToHost, s), "hipMemcpyAsync(report)");
+        HIP_TRY(hipMemcpyAsync(&c->h_report[9], A.fixq, sizeof(uint32_t), hipMemcpyDeviceToHost, s), "hipMemcpyAsync(report)");
     }
     HIP_TRY(hipMemcpyAsync(&c->h_report[6], c->d_counters + 2, 2 * sizeof(uint32_t), hipMemcpyDeviceToHost, s),
             "hipMemcpyAsync(report)");
@@ -1084,7 +1095,7 @@ void vr_destroy(vr_ctx* c) {
     if (c->h_report) (void)hipHostFree(c->h_report);
     if (c->h_sizing) (void)hipHostFree(c->h_sizing);
     for (vr_ctx::Buf* b : {&c->px_first, &c->px_T, &c->rec_pos, &c->rec_meta, &c->rec_next, &c->rec_act, &c->tr, &c->rec_rad,
-                           &c->rec_alloc, &c->rec_bloom, &c->slowq, &c->pcg_jump, &c->ray_next,
+                           &c->rec_alloc, &c->rec_bloom, &c->slowq, &c->fixq, &c->pcg_jump, &c->ray_next,
                            &c->stack_ovf, &c->env_order, &c->env_base, &c->rec_cut, &c->rec_start, &c->deep, &c->bin_cnt, &c->bin_off, &c->bin_ent,
                            &c->ff_scratch, &c->ff_tail, &c->ff_sum, &c->ff_nee, &c->ff_fb, &c->rec_bits[0], &c->rec_bits[1],
                            &c->sfd_tmp, &c->sfd_ref, &c->sfd_loss[0], &c->sfd_loss[1], &c->sfd_out})
@@ -1725,6 +1736,7 @@ vr_status vr_get_stats(vr_ctx* c, vr_render_stats* o) {
     o->record_overflow = frame_exceeded(c) ? 1 : 0;
     o->deep_pixels = c->report_gauss ? (int64_t)std::min(c->h_report[5], kDeepQueue) : 0;
     o->slow_rays = c->report_gauss ? (int64_t)c->h_report[8] : 0;
+    o->band_rays = c->report_gauss ? (int64_t)c->h_report[9] : 0;
     return VR_OK;
 }
 

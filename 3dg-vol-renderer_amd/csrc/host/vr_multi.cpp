@@ -334,6 +334,7 @@ vr_status group_stats(vr_group* g, vr_render_stats* o) {
         o->record_overflow |= s.record_overflow;
         o->deep_pixels += s.deep_pixels;
         o->slow_rays += s.slow_rays;
+        o->band_rays += s.band_rays;
     }
     return VR_OK;
 }

@@ -72,6 +72,11 @@ constexpr float kMemberAmb = VR_MEMBER_AMB;
 #endif
 constexpr float kChordBand = VR_CHORD_BAND * 1.1920928955078125e-7f;
 constexpr uint32_t kRecBoundary = 0x80000000u;  // rec_meta.w: active count | this flag
+// An environment ray with one non-member chord in the f32 error band (kChordBand) keeps that Gaussian's id in its
+// `lim` (the last event so far, only needed for a missed member: such a ray goes to the exact slow path anyway) as
+// a NaN payload, which `t1 > lim` never overwrites: no register and no store on the traversal's path.
+__device__ __forceinline__ float band_lim(uint32_t j) { return __uint_as_float(0x7f800000u | (j + 1u)); }
+__device__ __forceinline__ uint32_t band_id(float lim) { return (__float_as_uint(lim) & 0x007fffffu) - 1u; }
 #ifdef VR_DIAG_UNION  // diagnostic builds only: the march's counter slots report the union-walk census
 constexpr bool kDiagUnion = true;
 #else
@@ -1428,6 +1433,44 @@ __device__ __forceinline__ void to_slow(const RenderArgs& A, uint32_t slot) {
     }
 }
 
+// Hands an environment ray with one chord in the f32 error band to secondary_fix_kernel: its slot, the optical
+// depth of everything else it crossed and the band Gaussian. A full queue: as to_slow.
+__device__ __forceinline__ void to_fix(const RenderArgs& A, uint32_t slot, float tau, uint32_t j) {
+    const uint32_t q = atomicAdd(A.fixq, 1u);
+    if (q < A.fixq_cap) {
+        A.fixq[1 + 3 * q] = slot;
+        A.fixq[2 + 3 * q] = __float_as_uint(tau);
+        A.fixq[3 + 3 * q] = j;
+    } else {
+        A.rec_alloc[2] = 1u;
+        A.tr[slot] = __builtin_nanf("");
+    }
+}
+
+// One queued ray of the exact slow path (result slot t, hand-out order: see tr_slot).
+template <bool S>
+__device__ void slow_ray(const RenderArgs& A, uint64_t t, int* stack, int stride, Ctr& c) {
+    const uint32_t per = rays_per_chunk(A), chunk = (uint32_t)(t / per), rem = (uint32_t)(t - (uint64_t)chunk * per);
+    uint32_t s, r;
+    ray_slot(A, chunk, rem, dev_nrec(A), s, r);
+    const float4 pos = A.rec_pos[r];
+    const uint4 meta = A.rec_meta[r];
+    ActList act{A.rec_act + meta.z, 1, (int)(meta.w & ~kRecBoundary), A.rec_bloom[r]};
+    if (s < (uint32_t)A.num_lights) {  // test_integrators.h:202-237
+        const LightRecord& lr = A.lights[s];
+        float dx = lr.px - pos.x, dy = lr.py - pos.y, dz = lr.pz - pos.z;
+        float dist = sqrtf(dot3(dx, dy, dz, dx, dy, dz));
+        normalize3(dx, dy, dz);
+        Ray sr = make_ray(pos.x, pos.y, pos.z, dx, dy, dz);
+        A.tr[t] = light_transmittance<S>(A, sr, dist, act, stack, stride, c);
+    } else {  // :242-271, Ray env_ray(pos, wi) normalises the sampled direction
+        float xi1, xi2, wx, wy, wz;
+        env_xi_at(A, A.env_order != nullptr ? A.env_base[r] : env_base_state(meta), s - (uint32_t)A.num_lights, xi1, xi2);
+        env_dir(xi1, xi2, wx, wy, wz);
+        A.tr[t] = env_transmittance<S>(A, make_ray(pos.x, pos.y, pos.z, wx, wy, wz), act, stack, stride, c);
+    }
+}
+
 // Ray complete: write its transmittance (or hand it to the exact slow path). WH: the scene's whitened
 // records (A.wrec); false: the M forms of the records (a scene with a non-positive-definite M).
 template <bool S, bool FAST, bool PURE, bool WH = !PURE>
@@ -1455,6 +1498,11 @@ __device__ __forceinline__ void sec_finish(const RenderArgs& A, SecRay& R, Ctr& 
     }
     if (!PURE && R.needs_stop) {  // the exact slow path: a light ray's stopping event, a member at the boundary,
         to_slow(A, R.slot);       // a chord in the f32 error band
+        return;
+    }
+    const bool band = !PURE && !R.light && isnan(R.lim);
+    if (band && (R.act_n >= 64 || (R.hitmask & ((1ull << R.act_n) - 1ull)) != ((1ull << R.act_n) - 1ull))) {
+        to_slow(A, R.slot);  // a band ray with a missed member (active to the last event): the whole ray exactly
         return;
     }
     if (R.act_n > 64) {  // (march_deep_kernel records) missed members: re-intersect the whole list
@@ -1501,6 +1549,7 @@ __device__ __forceinline__ void sec_finish(const RenderArgs& A, SecRay& R, Ctr& 
             to_slow(A, R.slot);
             return;
         }
+    } else if (band) {  // (no missed member: see above)
     } else {
         while (missed) {  // pre-activated, missed through rounding: active up to the last event
             int s = __ffsll((unsigned long long)missed) - 1;
@@ -1514,6 +1563,10 @@ __device__ __forceinline__ void sec_finish(const RenderArgs& A, SecRay& R, Ctr& 
                 R.tau += optical_depth_fast(g, quad_fast(g, R.ray), 0.0f, R.lim);
             }
         }
+    }
+    if (band) {  // the band Gaussian's contribution: secondary_fix_kernel
+        to_fix(A, R.slot, R.tau, band_id(R.lim));
+        return;
     }
     VR_TR_STORE(A, R.slot, expf(-R.tau));
 }
@@ -1946,8 +1999,20 @@ __global__ __launch_bounds__(BLOCK, WAVES) void secondary_ww_kernel(RenderArgs A
             auto wtest = [&](const WRec& g, uint32_t j, int ls) {
                 if constexpr (S) c.v[ls >= 0 ? kCtrMu : kCtrPrims]++;  // list members counted apart
                 const WQuad q = wquad(g, R.ray);
-                // A chord within the reference's f32 error band (kChordBand): the exact slow path decides the ray
-                if constexpr (kChordBand > 0.0f) R.needs_stop = R.needs_stop | (fmaf(-kChordBand, q.c, fabsf(9.0f - q.e2)) < 0.0f);
+                // A chord within the reference's f32 error band (kChordBand): on an environment ray, that one
+                // Gaussian's contribution is left to the reference's M form (secondary_fix_kernel; the ray's tau
+                // leaves it out, its id rides in R.lim); a member, a light ray or a second such chord sends the
+                // whole ray to the exact slow path
+                if constexpr (kChordBand > 0.0f) {
+                    if (__builtin_expect(fmaf(-kChordBand, q.c, fabsf(9.0f - q.e2)) < 0.0f, false)) {
+                        if (ls >= 0 || R.light || isnan(R.lim) || j >= 0x007fffffu) {
+                            R.needs_stop = true;  // a member, a light ray or a second band chord: the whole ray exactly
+                        } else {
+                            R.lim = band_lim(j);
+                            return;
+                        }
+                    }
+                }
                 R.cmax = (ls >= 0 && q.c > R.cmax) ? q.c : R.cmax;
                 const bool cand = ls < 0 && q.c <= R.cmax;
                 // A member whose 3-sigma surface passes within rounding of the record position (or that the ray
@@ -2059,10 +2124,37 @@ __global__ __launch_bounds__(BLOCK, WAVES) void secondary_ww_kernel(RenderArgs A
 #endif
 }
 
+// Environment rays with one chord in the reference f32 quadratic's error band (to_fix): the band Gaussian's
+// contribution as the reference computes it — its M-form crossing on the exactly normalised ray (a collapsed chord
+// contributes nothing, a phantom one its tiny depth), active from max(t0, 0) to t1 (test_integrators.h:242-271 with
+// stable tie order) — added to the optical depth of everything else the ray crossed.
+__global__ __launch_bounds__(64) void secondary_fix_kernel(RenderArgs A) {
+    const uint32_t n = min(A.fixq[0], A.fixq_cap);
+    for (uint32_t q = blockIdx.x * 64u + threadIdx.x; q < n; q += gridDim.x * 64u) {
+        const uint32_t t = A.fixq[1 + 3 * q];
+        const float tau = __uint_as_float(A.fixq[2 + 3 * q]);
+        const GRec g = load_rec(A.gauss, (int)A.fixq[3 + 3 * q]);
+        const uint32_t per = rays_per_chunk(A), chunk = t / per, rem = t - chunk * per;
+        uint32_t s, r;
+        ray_slot(A, chunk, rem, dev_nrec(A), s, r);
+        const float4 pos = A.rec_pos[r];
+        float xi1, xi2, wx, wy, wz;
+        env_xi_at(A, A.env_order != nullptr ? A.env_base[r] : env_base_state(A.rec_meta[r]), s - (uint32_t)A.num_lights, xi1, xi2);
+        env_dir(xi1, xi2, wx, wy, wz);
+        const Ray er = make_ray(pos.x, pos.y, pos.z, wx, wy, wz);
+        const Quad qd = quad(g, er);
+        float a, b;
+        const float od = intersect(qd, a, b) ? optical_depth(g, qd, a, b) : 0.0f;
+        A.tr[t] = expf(-(tau + od));
+    }
+}
+
 #ifndef VR_SLOW_RPW
 #define VR_SLOW_RPW 8  // rays per wave of the exact slow path: each ray is a long dependent chain (~250 us), so a wave
                         // of 64 lasts as long as its slowest; 64 / 16 / 12 / 8 / 6 / 4 / 2 / 1 -> 377 / 309 / 273 / 254-270 /
-                        // 262 / 276-290 / 306 / 342 us per C4 frame
+                        // 262 / 276-290 / 306 / 342 us per C4 frame (round 5). (Measured and not kept, round 6: the
+                        // persistent kernel's idle waves tracing queued rays in its drain — slow kernel 412 -> 130 us,
+                        // but the persistent kernel 76.8 -> 78.9 ms with the slow path's registers in it.)
 #endif
 #ifdef VR_DIAG_SLOW
 __device__ uint32_t g_slow_hist[2][16], g_slow_max[2], g_slow_done;
@@ -2089,26 +2181,7 @@ __global__ __launch_bounds__(BLOCK) void secondary_slow_kernel(RenderArgs A) {
 #ifdef VR_DIAG_SLOW
         const uint64_t t_beg = wall_clock64();
 #endif
-        const uint64_t t = A.slowq[1 + q];  // result slot (hand-out order, see tr_slot)
-        const uint32_t per = rays_per_chunk(A), chunk = (uint32_t)(t / per), rem = (uint32_t)(t - (uint64_t)chunk * per);
-        uint32_t s, r;
-        ray_slot(A, chunk, rem, dev_nrec(A), s, r);
-        const float4 pos = A.rec_pos[r];
-        const uint4 meta = A.rec_meta[r];
-        ActList act{A.rec_act + meta.z, 1, (int)(meta.w & ~kRecBoundary), A.rec_bloom[r]};
-        if (s < (uint32_t)A.num_lights) {  // test_integrators.h:202-237
-            const LightRecord& lr = A.lights[s];
-            float dx = lr.px - pos.x, dy = lr.py - pos.y, dz = lr.pz - pos.z;
-            float dist = sqrtf(dot3(dx, dy, dz, dx, dy, dz));
-            normalize3(dx, dy, dz);
-            Ray sr = make_ray(pos.x, pos.y, pos.z, dx, dy, dz);
-            A.tr[t] = light_transmittance<S>(A, sr, dist, act, stack, BLOCK, c);
-        } else {  // :242-271, Ray env_ray(pos, wi) normalises the sampled direction
-            float xi1, xi2, wx, wy, wz;
-            env_xi_at(A, A.env_order != nullptr ? A.env_base[r] : env_base_state(meta), s - (uint32_t)A.num_lights, xi1, xi2);
-            env_dir(xi1, xi2, wx, wy, wz);
-            A.tr[t] = env_transmittance<S>(A, make_ray(pos.x, pos.y, pos.z, wx, wy, wz), act, stack, BLOCK, c);
-        }
+        slow_ray<S>(A, A.slowq[1 + q], stack, BLOCK, c);
 #ifdef VR_DIAG_SLOW
         const uint32_t us = (uint32_t)((wall_clock64() - t_beg) / 100);  // 100 MHz constant clock
         const int kind = s < (uint32_t)A.num_lights;
@@ -2604,6 +2677,8 @@ static hipError_t secondary_launch(const RenderArgs& A, hipStream_t stream) {
 #ifndef VR_SLOW_GRID
 #define VR_SLOW_GRID 4096  // workgroups of the exact slow path (grid-stride over its queue; 32 k rays a pass at 8 per wave)
 #endif
+        hipLaunchKernelGGL(dev::secondary_fix_kernel, dim3(1024), dim3(64), 0, stream, A);
+        if ((e = hipGetLastError()) != hipSuccess) return e;
         hipLaunchKernelGGL((dev::secondary_slow_kernel<64, S>), dim3(VR_SLOW_GRID), dim3(64), 0, stream, A);
         e = hipGetLastError();
     }

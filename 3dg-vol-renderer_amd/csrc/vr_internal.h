@@ -197,6 +197,8 @@ struct RenderArgs {
     unsigned long long* rec_bloom;  // per record: 64-bit membership mask of its active list
     uint32_t* slowq;                // light rays needing the exact stopping event: [0] count, [1..] ray ids
     uint32_t slowq_cap;
+    uint32_t* fixq;                 // env rays with one chord in the f32 error band: [0] count, [1 + 3i] ray id, [2 + 3i] tau, [3 + 3i] Gaussian
+    uint32_t fixq_cap;
     unsigned long long* ray_next;   // persistent secondary kernel: next unclaimed ray id
     int32_t* stack_ovf;             // persistent secondary kernel: traversal-stack entries past its LDS stack
     uint32_t stack_ovf_lanes;       // lanes (grid x block) the overflow buffer holds

@@ -371,7 +371,7 @@ class Device:
                 "error_pixels": s.error_pixels, "stage_ms": dict(zip(self.STAGES, list(s.stage_ms))),
                 "scatter_records": s.scatter_records, "secondary_rays": s.secondary_rays,
                 "record_overflow": bool(s.record_overflow), "deep_pixels": s.deep_pixels,
-                "slow_rays": s.slow_rays}
+                "slow_rays": s.slow_rays, "band_rays": s.band_rays}
 
     def fallback_pixels(self):
         """(n, 2) int array of the (x, y) pixels of the last ray-march frame that were re-run on the

@@ -65,7 +65,8 @@ class vr_render_stats(ctypes.Structure):
     _fields_ = [("kernel_ms", ctypes.c_double), ("pixels", ctypes.c_int64), ("fallback_pixels", ctypes.c_int64),
                 ("error_pixels", ctypes.c_int64), ("stage_ms", ctypes.c_double * 4),
                 ("scatter_records", ctypes.c_int64), ("secondary_rays", ctypes.c_int64),
-                ("record_overflow", ctypes.c_int64), ("deep_pixels", ctypes.c_int64), ("slow_rays", ctypes.c_int64)]
+                ("record_overflow", ctypes.c_int64), ("deep_pixels", ctypes.c_int64), ("slow_rays", ctypes.c_int64),
+                ("band_rays", ctypes.c_int64)]
 
 
 class vr_sfd_config(ctypes.Structure):

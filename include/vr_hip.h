@@ -134,8 +134,10 @@ typedef struct vr_render_stats {
                                  again). vr_render does that itself. */
     int64_t deep_pixels;      /* pixels re-run on the global-memory active-list pass (> 64 active) */
     int64_t slow_rays;        /* RayMarchingGaussians: secondary rays traced again on the exact slow path (a light
-                                 ray's stopping event, a missed member, a member at its 3-sigma boundary, a chord
-                                 within the reference f32 quadratic's error band) */
+                                 ray's stopping event, a missed member, a member at its 3-sigma boundary, two
+                                 chords or a member's within the reference f32 quadratic's error band) */
+    int64_t band_rays;        /* RayMarchingGaussians: secondary rays with one non-member chord within that band,
+                                 whose contribution the reference's M form recomputes (secondary_fix_kernel) */
 } vr_render_stats;
 
 typedef struct vr_scene vr_scene; /* host-side scene: primitives, lights, env colour */

@@ -113,7 +113,7 @@ def test_group_stats_sum_the_ranks():
     dev = vr.Device.get(devices)
     ranks = [dev.rank_stats(r) for r in range(len(devices))]
     assert len(st["stage_ms"]) == 4
-    for key in ("pixels", "scatter_records", "secondary_rays", "fallback_pixels", "error_pixels", "deep_pixels", "slow_rays"):
+    for key in ("pixels", "scatter_records", "secondary_rays", "fallback_pixels", "error_pixels", "deep_pixels", "slow_rays", "band_rays"):
         assert st[key] == sum(r[key] for r in ranks), key
     assert st["scatter_records"] > 0
     for stage, ms in st["stage_ms"].items():

@@ -47,7 +47,7 @@ for i in range(args.frames + 1):
 out = {"lib": os.environ.get("VR_LIB_PATH", "product"), "opt": args.opt,
        "kernel_ms": float(np.mean([s["kernel_ms"] for s in stats])),
        "stage_ms": {k: round(float(np.mean([s["stage_ms"][k] for s in stats])), 3) for k in vr.Device.STAGES},
-       "mean": float(frame.mean()), "slow_rays": stats[-1]["slow_rays"], "fallback_pixels": stats[-1]["fallback_pixels"],
+       "mean": float(frame.mean()), "slow_rays": stats[-1]["slow_rays"], "band_rays": stats[-1]["band_rays"], "fallback_pixels": stats[-1]["fallback_pixels"],
        "scatter_records": stats[-1]["scatter_records"]}
 if args.counts:
     out["work"] = dev.count_work(cam, integ.params, W, H)
