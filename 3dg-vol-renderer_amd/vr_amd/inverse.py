@@ -6,7 +6,7 @@ Everything runs natively in libvr_hip.so (host/vr_inverse.cpp): the parameter ma
 loop itself (vr_sfd_optimize), whose forward renders (1 + num_stoch_samples MultiScatterGaussians
 renders with per-pixel Gaussian recording per iteration), per-pixel L1 losses and per-Gaussian
 union-of-pixels loss statistic run on the device, with the BVH of every re-uploaded scene built on
-the device. The C++ mirror (include/vr/vol_renderer.h) calls the same entry points.
+the device. The C++ mirror (include/vr/inverse_integrator.h) calls the same entry points.
 
 Deviations: the sign vectors come from a seeded PCG32 stream (vr_sfd_sign_vector)
 instead of mt19937(random_device) (:101-103, not reproducible in the reference); the eigenbasis of
