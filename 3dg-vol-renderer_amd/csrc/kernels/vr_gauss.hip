@@ -275,6 +275,225 @@ __device__ float env_transmittance(const RenderArgs& A, const Ray& er, const Act
 }
 
 // ---------------------------------------------------------------------------------------------
+// The same exact transmittances with the whole wave on one ray (the slow path, round 6). A serial walk of one
+// long ray is a chain of ~100 dependent node and record loads (~250-400 us); here the wave expands the walk one
+// tree level at a time — each lane one frontier node (its four child boxes), the hit inner children appended to
+// the next level and the hit leaves to a list in lane order (ballots: a deterministic order), then each lane
+// one listed leaf's primitives — so the chain is the tree's depth. Every Gaussian the serial walk tests is
+// tested (no prune is tighter), with the same exact M forms; only the order of the optical-depth sum differs
+// (per-lane partial sums, then a fixed butterfly). kCoopCap nodes or leaves per level at most: a wider level
+// (never seen at C4) falls back to the serial walk on lane 0.
+// ---------------------------------------------------------------------------------------------
+constexpr uint32_t kCoopCap = 256;
+__device__ __forceinline__ float wave_sum(float x) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) x += __shfl_xor(x, o, 64);
+    return x;
+}
+__device__ __forceinline__ float wave_max(float x) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) x = fmaxf(x, __shfl_xor(x, o, 64));
+    return x;
+}
+__device__ __forceinline__ float wave_min(float x) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) x = fminf(x, __shfl_xor(x, o, 64));
+    return x;
+}
+__device__ __forceinline__ uint64_t wave_or(uint64_t x) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        const uint32_t lo = __shfl_xor((uint32_t)x, o, 64), hi = __shfl_xor((uint32_t)(x >> 32), o, 64);
+        x |= ((uint64_t)hi << 32) | lo;
+    }
+    return x;
+}
+// Level-by-level walk of the 4-wide tree by the whole wave (every lane calls it with the same ray); leaf(j) runs
+// for every primitive of every hit leaf, on the lane the leaf fell to. False: a level outgrew kCoopCap.
+template <typename Prune, typename Leaf>
+__device__ bool coop_walk(const RenderArgs& A, const Ray& r0, int* buf, Prune prune, Leaf leaf) {
+    float ox = r0.ox, oy = r0.oy, oz = r0.oz;
+    node_space<true>(A, ox, oy, oz);
+    auto inv = [&](float d) {
+        d *= A.hn_scale;
+        return __frcp_rn(fabsf(d) > 1e-30f ? d : copysignf(1e-30f, d));
+    };
+    const float ix = inv(r0.dx), iy = inv(r0.dy), iz = inv(r0.dz);
+    const float oxi = ox * ix, oyi = oy * iy, ozi = oz * iz;
+    const uint32_t lane = __lane_id();
+    int* cur = buf;
+    int* nxt = buf + kCoopCap;
+    int* lv = buf + 2 * kCoopCap;
+    if (lane == 0) cur[0] = 0;
+    __builtin_amdgcn_wave_barrier();
+    uint32_t n = 1;
+    while (n > 0) {
+        uint32_t nn = 0, nl = 0;
+        for (uint32_t base = 0; base < n; base += 64u) {
+            const bool valid = base + lane < n;
+            float key[4];
+            int32_t kr[4] = {0, 0, 0, 0};
+            if (valid) wide_children<Prune, false>(A, cur[base + lane], ix, iy, iz, oxi, oyi, ozi, prune, key, kr);
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const uint64_t bi = __ballot(kr[k] > 0), bl = __ballot(kr[k] < 0);
+                const uint32_t ci = (uint32_t)__popcll(bi), cl = (uint32_t)__popcll(bl);
+                if (nn + ci > kCoopCap || nl + cl > kCoopCap) return false;
+                const uint64_t below = (1ull << lane) - 1ull;
+                if (kr[k] > 0) nxt[nn + (uint32_t)__popcll(bi & below)] = kr[k];
+                if (kr[k] < 0) lv[nl + (uint32_t)__popcll(bl & below)] = kr[k];
+                nn += ci;
+                nl += cl;
+            }
+        }
+        __builtin_amdgcn_wave_barrier();
+        for (uint32_t base = 0; base < nl; base += 64u)
+            if (base + lane < nl) {
+                const int32_t ref = lv[base + lane];
+                for (uint32_t j = leaf_first(ref); j < leaf_first(ref) + leaf_count(ref); ++j) leaf(j);
+            }
+        __builtin_amdgcn_wave_barrier();
+        int* t = cur;
+        cur = nxt;
+        nxt = t;
+        n = nn;
+    }
+    return true;
+}
+
+// light_transmittance with the wave on one ray (test_integrators.h:202-237): the three passes as there.
+template <bool S>
+__device__ float light_transmittance_coop(const RenderArgs& A, const Ray& sr, float dist, const ActList& act, int* buf,
+                                          Ctr& c, bool& ok) {
+    ok = true;
+    if (!(dist > 0.0f)) return 1.0f;
+    const GaussianRecord* __restrict__ G = A.gauss;
+    const float pad = kTPad * (1.0f + dist);
+    float tau = 0.0f;
+    bool needs_stop = false;
+    uint64_t hitmask = 0;
+    ok = coop_walk(
+        A, sr, buf, [&](float tmin, float) { return tmin <= dist + pad; },
+        [&](uint32_t j) {
+            if constexpr (S) c.v[kCtrPrims]++;
+            const GRec g = load_rec(G, (int)j);
+            const Quad q = quad(g, sr);
+            float a, b;
+            if (!intersect(q, a, b)) return;
+            const int slot = act.find((int)j);
+            float lo = a;
+            if (slot >= 0) {
+                lo = 0.0f;
+                hitmask |= slot_bit(slot);
+            }
+            if (b < dist) {
+                if constexpr (S) c.v[kCtrOD]++;
+                tau += optical_depth(g, q, lo, b);
+            } else if (lo < dist) {
+                needs_stop = true;
+            }
+        });
+    if (!ok) return 0.0f;
+    tau = wave_sum(tau);
+    hitmask = wave_or(hitmask);
+    needs_stop = __any(needs_stop);
+    if (tau >= kTauCut) return 0.0f;  // exp(-tau) == 0 exactly; later terms are >= 0
+    const uint64_t all = act.n >= 64 ? ~0ull : ((1ull << act.n) - 1ull);
+    uint64_t missed = all & ~hitmask;
+    bool deep_any = false;
+    if (act.n > 64) {  // a member is missed iff the ray does not intersect it
+        missed = 0;
+        for (int s = 0; s < act.n && !deep_any; ++s) {
+            float a, b;
+            deep_any = !intersect(quad(load_rec(G, act.get(s)), sr), a, b);
+        }
+    }
+    if (needs_stop || missed || deep_any) {
+        float tstop = INFINITY;  // first event at or beyond the light
+        ok = coop_walk(
+            A, sr, buf, [&](float, float tmax) { return tmax >= dist - pad; },
+            [&](uint32_t j) {
+                if constexpr (S) c.v[kCtrPrims]++;
+                const GRec g = load_rec(G, (int)j);
+                float a, b;
+                if (!intersect(quad(g, sr), a, b)) return;
+                if (b >= dist) tstop = fminf(tstop, (a >= dist) ? a : b);
+            });
+        if (!ok) return 0.0f;
+        tstop = wave_min(tstop);
+        if (tstop == INFINITY) tstop = dist;
+        if (needs_stop) {
+            float t3 = 0.0f;
+            ok = coop_walk(
+                A, sr, buf, [&](float tmin, float tmax) { return tmin <= dist + pad && tmax >= dist - pad; },
+                [&](uint32_t j) {
+                    if constexpr (S) c.v[kCtrPrims]++;
+                    const GRec g = load_rec(G, (int)j);
+                    const Quad q = quad(g, sr);
+                    float a, b;
+                    if (!intersect(q, a, b)) return;
+                    const float lo = act.find((int)j) >= 0 ? 0.0f : a;
+                    if (lo < dist && b >= dist) {
+                        if constexpr (S) c.v[kCtrOD]++;
+                        t3 += optical_depth(g, q, lo, tstop);
+                    }
+                });
+            if (!ok) return 0.0f;
+            tau += wave_sum(t3);
+        }
+        while (missed) {
+            const int s = __ffsll((unsigned long long)missed) - 1;
+            missed &= missed - 1;
+            const GRec g = load_rec(G, act.get(s));
+            tau += optical_depth(g, quad(g, sr), 0.0f, tstop);
+        }
+        if (deep_any)
+            for (int s = 0; s < act.n; ++s) {
+                const GRec g = load_rec(G, act.get(s));
+                const Quad q = quad(g, sr);
+                float a, b;
+                if (!intersect(q, a, b)) tau += optical_depth(g, q, 0.0f, tstop);
+            }
+    }
+    return expf(-tau);
+}
+
+// env_transmittance with the wave on one ray (test_integrators.h:242-271).
+template <bool S>
+__device__ float env_transmittance_coop(const RenderArgs& A, const Ray& er, const ActList& act, int* buf, Ctr& c, bool& ok) {
+    const GaussianRecord* __restrict__ G = A.gauss;
+    float tau = 0.0f, t_last = 0.0f;
+    uint64_t hitmask = 0;
+    ok = coop_walk(
+        A, er, buf, [&](float, float) { return true; },
+        [&](uint32_t j) {
+            if constexpr (S) c.v[kCtrPrims]++;
+            const GRec g = load_rec(G, (int)j);
+            const Quad q = quad(g, er);
+            float a, b;
+            if (!intersect(q, a, b)) return;
+            t_last = fmaxf(t_last, b);
+            const int slot = act.find((int)j);
+            if (slot >= 0) hitmask |= slot_bit(slot);
+            if constexpr (S) c.v[kCtrOD]++;
+            tau += optical_depth(g, q, slot >= 0 ? 0.0f : a, b);
+        });
+    if (!ok) return 0.0f;
+    tau = wave_sum(tau);
+    t_last = wave_max(t_last);
+    hitmask = wave_or(hitmask);
+    for (int s = 0; s < act.n; ++s) {  // members the ray misses: active to the last event
+        if (s < 64 && ((hitmask >> s) & 1ull)) continue;
+        const GRec g = load_rec(G, act.get(s));
+        const Quad q = quad(g, er);
+        float a, b;
+        if (s >= 64 && intersect(q, a, b)) continue;
+        tau += optical_depth(g, q, 0.0f, t_last);
+    }
+    return expf(-tau);
+}
+
+// ---------------------------------------------------------------------------------------------
 // Stage 1: primary march
 // ---------------------------------------------------------------------------------------------
 // Early-out weight (t_eps > 0). Stopping after step k drops
@@ -2212,6 +2431,50 @@ __global__ __launch_bounds__(BLOCK) void secondary_slow_kernel(RenderArgs A) {
             if (c.v[i]) atomicAdd(A.work + kNumCtr + i, (unsigned long long)c.v[i]);
 }
 
+// The exact slow path with the wave on one ray at a time (coop_walk; scenes with the 4-wide tree): the queue's
+// rays one per wave, so a ray's latency is the tree's depth in node and record loads instead of its whole walk.
+template <bool S>
+__global__ __launch_bounds__(64) void secondary_slow_coop_kernel(RenderArgs A) {
+    __shared__ int s_buf[3 * kCoopCap];
+    const uint32_t n = min(A.slowq[0], A.slowq_cap);
+    const uint32_t lane = __lane_id();
+    Ctr c{};
+    for (uint32_t q = blockIdx.x; q < n; q += gridDim.x) {
+        const uint64_t t = A.slowq[1 + q];
+        const uint32_t per = rays_per_chunk(A), chunk = (uint32_t)(t / per), rem = (uint32_t)(t - (uint64_t)chunk * per);
+        uint32_t s, r;
+        ray_slot(A, chunk, rem, dev_nrec(A), s, r);
+        const float4 pos = A.rec_pos[r];
+        const uint4 meta = A.rec_meta[r];
+        ActList act{A.rec_act + meta.z, 1, (int)(meta.w & ~kRecBoundary), A.rec_bloom[r]};
+        bool ok = true;
+        float tr;
+        if (s < (uint32_t)A.num_lights) {  // test_integrators.h:202-237
+            const LightRecord& lr = A.lights[s];
+            float dx = lr.px - pos.x, dy = lr.py - pos.y, dz = lr.pz - pos.z;
+            const float dist = sqrtf(dot3(dx, dy, dz, dx, dy, dz));
+            normalize3(dx, dy, dz);
+            const Ray sr = make_ray(pos.x, pos.y, pos.z, dx, dy, dz);
+            tr = light_transmittance_coop<S>(A, sr, dist, act, s_buf, c, ok);
+            __builtin_amdgcn_wave_barrier();
+            if (!ok && lane == 0) tr = light_transmittance<S>(A, sr, dist, act, s_buf, 1, c);  // a level over kCoopCap
+        } else {  // :242-271
+            float xi1, xi2, wx, wy, wz;
+            env_xi_at(A, A.env_order != nullptr ? A.env_base[r] : env_base_state(meta), s - (uint32_t)A.num_lights, xi1, xi2);
+            env_dir(xi1, xi2, wx, wy, wz);
+            const Ray er = make_ray(pos.x, pos.y, pos.z, wx, wy, wz);
+            tr = env_transmittance_coop<S>(A, er, act, s_buf, c, ok);
+            __builtin_amdgcn_wave_barrier();
+            if (!ok && lane == 0) tr = env_transmittance<S>(A, er, act, s_buf, 1, c);
+        }
+        if (lane == 0) A.tr[t] = tr;
+        __builtin_amdgcn_wave_barrier();
+    }
+    if constexpr (S)
+        for (int i = 0; i < kNumCtr; ++i)
+            if (c.v[i]) atomicAdd(A.work + kNumCtr + i, (unsigned long long)c.v[i]);
+}
+
 #ifdef VR_DIAG_LEVELS
 __global__ __launch_bounds__(256) void depth_kernel(const int32_t* __restrict__ parent, uint32_t n) {
     const uint32_t i = blockIdx.x * 256u + threadIdx.x;
@@ -2679,7 +2942,16 @@ static hipError_t secondary_launch(const RenderArgs& A, hipStream_t stream) {
 #endif
         hipLaunchKernelGGL(dev::secondary_fix_kernel, dim3(1024), dim3(64), 0, stream, A);
         if ((e = hipGetLastError()) != hipSuccess) return e;
-        hipLaunchKernelGGL((dev::secondary_slow_kernel<64, S>), dim3(VR_SLOW_GRID), dim3(64), 0, stream, A);
+#ifndef VR_SLOW_COOP
+#define VR_SLOW_COOP 1  // 1: the wave-cooperative exact slow path on scenes with the 4-wide tree (A/B)
+#endif
+#ifndef VR_SLOW_COOP_GRID
+#define VR_SLOW_COOP_GRID 8192  // one-wave workgroups of the cooperative slow path (one queued ray at a time each)
+#endif
+        if (VR_SLOW_COOP && A.hnodes4 != nullptr)
+            hipLaunchKernelGGL(dev::secondary_slow_coop_kernel<S>, dim3(VR_SLOW_COOP_GRID), dim3(64), 0, stream, A);
+        else
+            hipLaunchKernelGGL((dev::secondary_slow_kernel<64, S>), dim3(VR_SLOW_GRID), dim3(64), 0, stream, A);
         e = hipGetLastError();
     }
     return e;
