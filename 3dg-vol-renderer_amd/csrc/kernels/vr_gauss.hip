@@ -77,6 +77,13 @@ constexpr uint32_t kRecBoundary = 0x80000000u;  // rec_meta.w: active count | th
 // a NaN payload, which `t1 > lim` never overwrites: no register and no store on the traversal's path.
 __device__ __forceinline__ float band_lim(uint32_t j) { return __uint_as_float(0x7f800000u | (j + 1u)); }
 __device__ __forceinline__ uint32_t band_id(float lim) { return (__float_as_uint(lim) & 0x007fffffu) - 1u; }
+#ifndef VR_MARCH_DEEP
+// Private-memory (scratch) stack entries of the primary march's 4-wide walks past its LDS stack; a walk past both goes
+// to the fallback pass. Round 6, C4 (same frame hash): LDS 24 + 0 -> 14 + 10 moved the quarter-tile workgroup from
+// 10 to 7.5 KB of LDS, 4 -> 5 waves/SIMD, march 13.95 -> 12.92 ms (12 + 12: 13.02, 10 + 14: 13.2, 16 + 8: 13.7).
+#define VR_MARCH_DEEP 10
+#endif
+
 #ifdef VR_DIAG_UNION  // diagnostic builds only: the march's counter slots report the union-walk census
 constexpr bool kDiagUnion = true;
 #else
@@ -745,7 +752,7 @@ __device__ __forceinline__ void union_walk_simt(uint32_t steps, Ctr& c) {
 // (Measured and not kept, DESIGN.md §3: window queries starting in the subtree holding the window and climbing,
 // a fast-form pre-test of the candidates, look-ahead windows over 2-4 steps, a closest-entry query merged with
 // the following entrant query, a sorting network in the entrant walk; all bit-identical, all slower at C4.)
-template <int ACT, bool S, bool H, bool W = false, int CAP = kStackSize, bool COOP = false>
+template <int ACT, bool S, bool H, bool W = false, int CAP = kStackSize, bool COOP = false, int DEEP = 0>
 __device__ int march(const RenderArgs& A, uint32_t p, int px, int py, int* act_base, int* stack, int stride, Ctr& c,
                      int act_stride = -1) {
     const bool writer = !COOP || __lane_id() == 0u;  // COOP: lane 0 writes the pixel's records
@@ -760,7 +767,8 @@ __device__ int march(const RenderArgs& A, uint32_t p, int px, int py, int* act_b
     ActList act{act_base, act_stride < 0 ? stride : act_stride, 0, 0};
     auto walk = [&](auto prune, auto leaf) -> bool {
         if constexpr (W) {
-            return traverse_wide<CAP>(A, ray, stack, stride, prune, leaf, NodeCount<S>{&c});
+            return traverse_wide<CAP, decltype(prune), decltype(leaf), NodeCount<S>, true, DEEP>(A, ray, stack, stride, prune, leaf,
+                                                                                                NodeCount<S>{&c});
         } else {
             traverse<H>(A, ray, stack, stride, prune, leaf, NodeCount<S>{&c});
             return true;
@@ -769,8 +777,8 @@ __device__ int march(const RenderArgs& A, uint32_t p, int px, int py, int* act_b
     // the entrants query collects every entry of (t_lo, t_k] whatever the visit order: no sorting network
     auto walk_any = [&](auto prune, auto leaf) -> bool {
         if constexpr (W) {
-            return traverse_wide<CAP, decltype(prune), decltype(leaf), NodeCount<S>, false>(A, ray, stack, stride, prune, leaf,
-                                                                                             NodeCount<S>{&c});
+            return traverse_wide<CAP, decltype(prune), decltype(leaf), NodeCount<S>, false, DEEP>(A, ray, stack, stride, prune, leaf,
+                                                                                                    NodeCount<S>{&c});
         } else {
             return walk(prune, leaf);
         }
@@ -893,7 +901,7 @@ __global__ __launch_bounds__(BLOCK) void march_kernel(RenderArgs A) {
     Ctr c{};
     int st = kOK;
     if (x < (int)A.width && y < (int)A.height) {
-        st = march<ACT, S, H, W, STACK>(A, p, x, y, s_act + threadIdx.x, s_stack + threadIdx.x, BLOCK, c);
+        st = march<ACT, S, H, W, STACK, false, W ? VR_MARCH_DEEP : 0>(A, p, x, y, s_act + threadIdx.x, s_stack + threadIdx.x, BLOCK, c);
     } else {
         A.px_first[p] = kNoRecord;
         A.px_T[p] = 0.0f;
@@ -2069,6 +2077,12 @@ constexpr int kPrimUnroll = VR_WW_PRIM_UNROLL, kNodeUnroll = VR_WW_NODE_UNROLL;
 // S = true is the instrumented build (vr_count_work): the same schedule, counting its own work.
 // WH: the whitened records (A.wrec); false (PureRayMarching, or a scene with a non-positive-definite M):
 // the records' M forms with the membership lookup of the record's active list.
+#ifdef VR_DIAG_DRAIN  // diagnostic builds only: the persistent kernel's tail (100 MHz clock ticks, printed by the last wave)
+// [0] ray latencies, [1] latencies of the rays handed out once the claim counter was exhausted (log2 us buckets);
+// wave exits after the exhaustion in 50-us buckets
+__device__ unsigned long long g_dr_t0, g_dr_done, g_dr_end;
+__device__ uint32_t g_dr_hist[2][20], g_dr_max[2], g_dr_exit[64], g_dr_waves;
+#endif
 template <int BLOCK, int STACK, bool S, bool PURE, int WAVES, int QCAP, bool H, bool W, bool WH = !PURE>
 __global__ __launch_bounds__(BLOCK, WAVES) void secondary_ww_kernel(RenderArgs A) {
     __shared__ int s_stack[(STACK + kQueueLds<QCAP>) * BLOCK];
@@ -2123,6 +2137,15 @@ __global__ __launch_bounds__(BLOCK, WAVES) void secondary_ww_kernel(RenderArgs A
 #else
     auto rf_lap = [](int, bool) {};
 #endif
+#ifdef VR_DIAG_DRAIN
+    uint64_t dr_ray0 = 0;
+    bool dr_late = false, dr_seen = false;
+    __shared__ uint32_t s_dr_hist[2][20], s_dr_max[2];  // (workgroup-local: global atomics per ray slow the frame ~90x)
+    if (threadIdx.x < 40u) (&s_dr_hist[0][0])[threadIdx.x] = 0u;
+    if (threadIdx.x < 2u) s_dr_max[threadIdx.x] = 0u;
+    __syncthreads();
+    if (lane == 0u) atomicCAS(&g_dr_t0, 0ull, (unsigned long long)wall_clock64());
+#endif
     for (;;) {
         const uint64_t idle = __ballot(!live);
         if (__popcll(idle) >= kRefillMin) {  // refill once enough lanes are idle (amortises sec_init)
@@ -2145,6 +2168,10 @@ __global__ __launch_bounds__(BLOCK, WAVES) void secondary_ww_kernel(RenderArgs A
                     pool_end = ((part + 1u) * per) >> split;
                 }
                 counter_done = cnext + 1u >= nunits;
+#ifdef VR_DIAG_DRAIN
+                if (cnext + 1u >= nunits && !dr_seen && lane == 0u) atomicCAS(&g_dr_done, 0ull, (unsigned long long)wall_clock64());
+                dr_seen = dr_seen || cnext + 1u >= nunits;
+#endif
             }
             rf_lap(1, true);
             const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(idle >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)idle, 0u));
@@ -2152,6 +2179,10 @@ __global__ __launch_bounds__(BLOCK, WAVES) void secondary_ww_kernel(RenderArgs A
                 t = pool + rank;
                 if constexpr (S) c.v[kCtrSecRays]++;
                 live = sec_init(A, nrec, chunk, t, R, H);  // false: padding id, or complete already (Tr written)
+#ifdef VR_DIAG_DRAIN
+                dr_ray0 = wall_clock64();
+                dr_late = counter_done;
+#endif
                 sp = 0;
                 node = -1;
                 Q.n = 0;
@@ -2330,8 +2361,51 @@ __global__ __launch_bounds__(BLOCK, WAVES) void secondary_ww_kernel(RenderArgs A
         if (live && (cut_reached<PURE>(R) || (node == -1 && !Q.has_prim()))) {
             fin = true;  // written at the next refill (the lane idles until then anyway)
             live = false;
+#ifdef VR_DIAG_DRAIN
+            const uint32_t us = (uint32_t)((wall_clock64() - dr_ray0) / 100u);
+            atomicAdd(&s_dr_hist[0][min(31 - __clz(us | 1), 19)], 1u);
+            atomicMax(&s_dr_max[0], us);
+            if (dr_late) {
+                atomicAdd(&s_dr_hist[1][min(31 - __clz(us | 1), 19)], 1u);
+                atomicMax(&s_dr_max[1], us);
+            }
+#endif
         }
     }
+#ifdef VR_DIAG_DRAIN
+    {
+        const unsigned long long now = wall_clock64(), done = atomicAdd(&g_dr_done, 0ull);
+        if (lane == 0u && done != 0ull && now > done) atomicAdd(&g_dr_exit[min((uint32_t)((now - done) / 5000u), 63u)], 1u);
+    }
+    __syncthreads();
+    if (threadIdx.x < 40u) {
+        const uint32_t v = (&s_dr_hist[0][0])[threadIdx.x];
+        if (v) atomicAdd(&g_dr_hist[0][0] + threadIdx.x, v);
+    }
+    if (threadIdx.x < 2u) atomicMax(&g_dr_max[threadIdx.x], s_dr_max[threadIdx.x]);
+    if (lane == 0u) {
+        const unsigned long long now = wall_clock64();
+        atomicMax(&g_dr_end, now);
+        __threadfence();
+        if (atomicAdd(&g_dr_waves, 1u) == waves - 1u) {
+            const unsigned long long t0 = atomicExch(&g_dr_t0, 0ull), end = atomicExch(&g_dr_end, 0ull);
+            const unsigned long long dn = atomicExch(&g_dr_done, 0ull);
+            printf("drain: waves %u units %u kernel %.1f us, claims exhausted at %.1f us, drain %.1f us; max ray %u us, max late ray %u us\n",
+                   waves, nunits, (end - t0) / 100.0, (dn - t0) / 100.0, (end - dn) / 100.0, atomicExch(&g_dr_max[0], 0u),
+                   atomicExch(&g_dr_max[1], 0u));
+            for (int k = 0; k < 2; ++k)
+                for (int b = 0; b < 20; ++b) {
+                    const uint32_t v = atomicExch(&g_dr_hist[k][b], 0u);
+                    if (v) printf("  %s rays us<%u: %u\n", k ? "late" : "all", 2u << b, v);
+                }
+            for (int b = 0; b < 64; ++b) {
+                const uint32_t v = atomicExch(&g_dr_exit[b], 0u);
+                if (v) printf("  wave exits %u-%u us after exhaustion: %u\n", 50u * b, 50u * b + 50u, v);
+            }
+            atomicExch(&g_dr_waves, 0u);
+        }
+    }
+#endif
 #ifdef VR_DIAG_REFILL
     c.v[kCtrNodes] = rf_cyc[0];
     c.v[kCtrPrims] = rf_cyc[1];
@@ -2824,7 +2898,7 @@ __global__ __launch_bounds__(256) void accumulate_kernel(RenderArgs A) {
 #define VR_MARCH_ACT 16  // active-list LDS slots per lane of the primary march (A/B)
 #endif
 #ifndef VR_MARCH_STACK4
-#define VR_MARCH_STACK4 24  // LDS stack entries per lane of the primary march's 4-wide walks (A/B; overflow: fallback)
+#define VR_MARCH_STACK4 14  // LDS stack entries per lane of the primary march's 4-wide walks (A/B; then VR_MARCH_DEEP)
 #endif
 #ifndef VR_MARCH_ACT_BIG
 #define VR_MARCH_ACT_BIG 32  // the primary march's slots once a scene's frames overflow 16 on >= 5 % of their pixels

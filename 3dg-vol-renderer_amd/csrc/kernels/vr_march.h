@@ -532,9 +532,12 @@ __device__ __forceinline__ void wide_children(const RenderArgs& A, int node, flo
 // if the LDS stack (cap entries) could overflow — the caller then re-runs the work on the pair tree.
 // SORT = false: children in the node's order (a query whose result does not depend on the visit order,
 // e.g. a window query that collects every entry of an interval).
-template <int CAP, typename Prune, typename Leaf, typename OnNode = NoCount, bool SORT = true>
+// DEEP > 0: entries past the CAP LDS entries go to DEEP more in the lane's private (scratch) memory before the walk
+// gives up (the LDS stack then sizes the kernel's occupancy, not the deepest walk).
+template <int CAP, typename Prune, typename Leaf, typename OnNode = NoCount, bool SORT = true, int DEEP = 0>
 __device__ __forceinline__ bool traverse_wide(const RenderArgs& A, const Ray& r0, int* stack, int stride, Prune prune,
                                               Leaf leaf, OnNode on_node = OnNode()) {
+    [[maybe_unused]] volatile int deep[DEEP > 0 ? DEEP : 1];
     float ox = r0.ox, oy = r0.oy, oz = r0.oz;
     node_space<true>(A, ox, oy, oz);
     // |d| clamped away from 0 (axis-parallel rays, e.g. an orthographic camera looking along an
@@ -562,16 +565,28 @@ __device__ __forceinline__ bool traverse_wide(const RenderArgs& A, const Ray& r0
             first = kr[i] > 0 ? i : first;
             next = kr[i] > 0 ? kr[i] : next;
         }
-        if (sp + 3 > CAP) return false;
+        if (sp + 3 > CAP + DEEP) return false;
+        // (DEEP: the LDS-only form while no lane of the wave can reach past CAP)
+        if (DEEP == 0 || __builtin_expect(__ballot(sp > CAP - 3) == 0ull, 1)) {
 #pragma unroll
-        for (int i = 3; i >= 0; --i)
-            if (kr[i] > 0 && i != first) stack[(sp++) * stride] = kr[i];
+            for (int i = 3; i >= 0; --i)
+                if (kr[i] > 0 && i != first) stack[(sp++) * stride] = kr[i];
+        } else {
+#pragma unroll
+            for (int i = 3; i >= 0; --i)
+                if (kr[i] > 0 && i != first) {
+                    if (sp < CAP) stack[sp * stride] = kr[i];
+                    else deep[sp - CAP] = kr[i];
+                    ++sp;
+                }
+        }
         if (first >= 0) {
             node = next;
         } else {
             if (sp == 0) return true;
             --sp;
-            node = stack[sp * stride];
+            if (DEEP == 0 || __builtin_expect(__ballot(sp >= CAP) == 0ull, 1)) node = stack[sp * stride];
+            else node = sp < CAP ? stack[sp * stride] : deep[sp - CAP];
         }
     }
 }
