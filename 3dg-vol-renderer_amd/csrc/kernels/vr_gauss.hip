@@ -2103,7 +2103,12 @@ __global__ __launch_bounds__(BLOCK, WAVES) void secondary_ww_kernel(RenderArgs A
     // Claim units: a chunk's rays in hand-out order, cut into 2^split equal parts when the launch has
     // few chunks per resident wave (a frame share of a multi-GPU split): shorter last units, a shorter
     // tail of the persistent launch (8-way C4 share: 22.7 -> 21.7 ms). Whole chunks otherwise (record
-    // locality).
+    // locality). (Measured and not kept, round 6: a guided tail — the launch's last 1/2/4 units per wave handed
+    // out in 1/8 or 1/16 chunks — 8-way share prediction 7.12 -> 7.19/7.15/7.13, 1/16: 6.93; the tail after
+    // the counter runs out is the in-flight rays' latency, not the unstarted rays left in a wave's pool. Nor is
+    // that latency a few long walks: handing rays past 150/300/600/1200 node steps to the wave-per-ray slow path
+    // re-routed 17 k/15/0/0 rays per C4 frame and cost 1.8 ms in spills. A ray waits on its wave's NODE/PRIM
+    // schedule: ~100-250 us typical, up to ~2 ms, over ~30 node steps; VR_DIAG_DRAIN.)
     const uint32_t waves = gridDim.x * (BLOCK / 64u), cpw = nchunks / max(waves, 1u);
 #ifndef VR_WW_SPLIT_CPW
 #define VR_WW_SPLIT_CPW 32  // chunks per resident wave below which claim units get shorter (A/B)

@@ -633,6 +633,7 @@ def main():
                        "integrator": "RayMarchingGaussians", "step_size": 0.01, "env_samples": args.env_samples,
                        "t_eps": args.t_eps, "lights": len(LIGHTS), "parallelism": f"tiles{world}",
                        "setup_s": t_setup, "fallback_pixels": per_step[-1]["fallback_pixels"],
+                       "slow_rays": per_step[-1].get("slow_rays"), "band_rays": per_step[-1].get("band_rays"),
                        "render_call": call},
             "roofline": roof,
             "cpu_baseline": cpu,

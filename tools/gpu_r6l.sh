@@ -1,0 +1,14 @@
+#!/bin/bash
+# Long secondary walks to the wave-per-ray exact slow path (VR_WW_LONG node steps): frame hash + slow-ray count,
+# C4 bench per build, 8-way share balance per build.
+cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
+O=gpurun_out/r6l; mkdir -p $O
+T="cur long150 long300 long600 long1200"
+lib() { if [ "$1" = cur ]; then echo $PWD/3dg-vol-renderer_amd/libvr_hip.so; else echo $PWD/_ab/$1/libvr_hip.so; fi; }
+for t in $T; do echo "$t $(VR_LIB_PATH=$(lib $t) timeout -k 10 120 python3 tools/frame_hash.py 2>/dev/null | tail -1)"; done
+bash tools/ab_run.sh $T && python3 tools/ab_summary.py $T || exit 1
+for t in $T; do python3 -c "import json;d=json.loads(open('gpurun_out/ab/$t.log').read().strip().splitlines()[-1]);print('$t', {k:v for k,v in d['config'].items() if 'slow' in k or 'band' in k})"; done
+for t in $T; do
+  VR_LIB_PATH=$(lib $t) timeout -k 10 300 python3 -u tools/share_balance.py --ranks 8 > $O/share_$t.json 2> $O/share_$t.log || { tail -5 $O/share_$t.log; exit 1; }
+  echo "$t $(grep share_balance $O/share_$t.log | tail -1)"
+done
