@@ -2057,7 +2057,8 @@ __device__ __forceinline__ void list_advance(LeafQueue& Q, int& node, int start)
 #define VR_WW_NODE_STEPS 6
 #endif
 #ifndef VR_WW_PRIM_STEPS
-#define VR_WW_PRIM_STEPS 4  // A/B round 4 (tight tree, C4 secondary): 3: 77.1, 4: 77.1-77.3, 5: 77.6-78.0, 7: 85.7 ms
+#define VR_WW_PRIM_STEPS 3  // A/B round 4 (tight tree, C4 secondary): 3: 77.1, 4: 77.1-77.3, 5: 77.6-78.0, 7: 85.7 ms;
+                            // round 6 (with PRIM bias 85, tools/gpu_r6n.sh): 3 + 85 %: 78.0 vs 4 + 70 %: 78.4-78.5 ms
 #endif
 #ifndef VR_WW_PRIM_UNROLL
 #define VR_WW_PRIM_UNROLL 5  // unroll of the PRIM iteration's step loop (A/B: code size vs. scheduling)
@@ -2067,7 +2068,8 @@ __device__ __forceinline__ void list_advance(LeafQueue& Q, int& node, int start)
 #endif
 constexpr int kRefillMin = VR_WW_REFILL, kNodeSteps = VR_WW_NODE_STEPS, kPrimSteps = VR_WW_PRIM_STEPS;
 #ifndef VR_WW_PRIM_BIAS
-#define VR_WW_PRIM_BIAS 70  // a PRIM iteration needs this many % of the lanes a NODE iteration could use (A/B)
+#define VR_WW_PRIM_BIAS 85  // a PRIM iteration needs this many % of the lanes a NODE iteration could use (A/B, round 6:
+                            // 60 / 70 / 85 / 100 % -> 79.1 / 78.5 / 78.0-78.3 / 78.7 ms at 4 PRIM steps)
 #endif
 constexpr int kPrimBias = VR_WW_PRIM_BIAS;
 constexpr int kPrimUnroll = VR_WW_PRIM_UNROLL, kNodeUnroll = VR_WW_NODE_UNROLL;
