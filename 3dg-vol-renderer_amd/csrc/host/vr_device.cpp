@@ -28,7 +28,7 @@ hipError_t gauss_record_cut(const RenderArgs& A, float budget, hipStream_t strea
 hipError_t gauss_whiten(const GaussianRecord* rec, WRecord* out, uint32_t n, uint32_t* bad, hipStream_t stream);
 hipError_t gauss_bin(const RenderArgs& A, bool emit, hipStream_t stream);
 hipError_t gauss_parents(const HNode4* nodes, uint32_t n, int32_t* parent, int32_t* prim_node, hipStream_t stream);
-hipError_t gauss_refit_secondary(const HNode4* src, HNode4* dst, uint32_t n, const GaussianRecord* rec, const int32_t* parent,
+hipError_t gauss_refit_secondary(const HNode4* src, HNode4* dst, HNode4* dst_t, uint32_t n, const GaussianRecord* rec, const int32_t* parent,
                                  uint8_t* depth, float* nbox, uint32_t* maxd, const float hc[3], float hs, float diag,
                                  hipStream_t stream);
 hipError_t gauss_bin_scan(const uint32_t* cnt, uint32_t* off, uint32_t n, void* tmp, size_t& tmp_bytes, hipStream_t stream);
@@ -430,13 +430,15 @@ vr_status upload_secondary_tree(vr_ctx* c) {
     uint8_t* depth = nullptr;
     float* nbox = nullptr;
     uint32_t* maxd = nullptr;
-    hipError_t e = hipMalloc(&c->d_hnodes4s, n * sizeof(HNode4));
+    // n nodes as refit (HNode4), then (VR_SEC_SOA) the same n nodes with their boxes laid out per axis for the
+    // secondary kernel's node step (soa_nodes_kernel)
+    hipError_t e = hipMalloc(&c->d_hnodes4s, (VR_SEC_SOA ? 2 : 1) * n * sizeof(HNode4));
     if (e == hipSuccess) e = hipMalloc(&depth, n);
     if (e == hipSuccess) e = hipMalloc(&nbox, n * 6 * sizeof(float));
     if (e == hipSuccess) e = hipMalloc(&maxd, sizeof(uint32_t));
     if (e == hipSuccess)
-        e = gauss_refit_secondary(c->d_hnodes4, c->d_hnodes4s, (uint32_t)n, c->d_gauss, c->d_parent4, depth, nbox, maxd,
-                                  c->hn_center, c->hn_scale, (float)std::sqrt(d2), c->stream);
+        e = gauss_refit_secondary(c->d_hnodes4, c->d_hnodes4s, VR_SEC_SOA ? c->d_hnodes4s + n : nullptr, (uint32_t)n, c->d_gauss,
+                                  c->d_parent4, depth, nbox, maxd, c->hn_center, c->hn_scale, (float)std::sqrt(d2), c->stream);
     if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
     for (void* p : {(void*)depth, (void*)nbox, (void*)maxd})
         if (p) (void)hipFree(p);
@@ -565,6 +567,7 @@ vr_status fill_args(vr_ctx* c, const vr_camera* cam, const vr_render_params* p, 
     A.hnodes = c->d_hnodes;
     A.hnodes4 = c->d_hnodes4;
     A.hnodes4s = c->d_hnodes4s ? c->d_hnodes4s : c->d_hnodes4;
+    A.hnodes4t = (VR_SEC_SOA && c->d_hnodes4s) ? c->d_hnodes4s + c->num_nodes4 : nullptr;
     A.hn4_parent = c->d_parent4;
     A.prim_node4 = c->d_prim_node4;
     A.num_nodes4 = (uint32_t)c->num_nodes4;

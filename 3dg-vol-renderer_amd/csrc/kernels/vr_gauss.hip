@@ -1883,7 +1883,7 @@ __device__ __forceinline__ uint32_t ovf_slot(const RenderArgs& A, int sp) {
 // (a min-reduction over the inner children's entry distances), the other inner children are pushed
 // and the leaf children queued in the node's child order. Empty slots carry NaN boxes, so the slab
 // test alone rejects them. Ring queues only (QCAP = 1 + 2^k).
-template <int BLOCK, bool S, int QCAP, int STACK>
+template <int BLOCK, bool S, int QCAP, int STACK, bool SOA = false>
 __device__ __forceinline__ void sec_node4v(const RenderArgs& A, SecRay& R, LdsInt* stack, int& sp, int& node, LeafQueue& Q,
                                            Ctr& c) {
     static_assert(kQueueRing<QCAP>, "sec_node4v: ring leaf queue");
@@ -1895,10 +1895,32 @@ __device__ __forceinline__ void sec_node4v(const RenderArgs& A, SecRay& R, LdsIn
 #ifdef VR_DIAG_LEVELS
     R.lv[min((int)g_diag_depth[node & kNodeIndexMask] >> 1, 7)]++;
 #endif
-    const uint4* np = reinterpret_cast<const uint4*>(A.hnodes4s + (node & kNodeIndexMask));
+    const uint4* np = reinterpret_cast<const uint4*>((SOA ? A.hnodes4t : A.hnodes4s) + (node & kNodeIndexMask));
     const uint4 q0 = np[0], q1 = np[1], q2 = np[2], rf = np[3];
     const uint32_t w[12] = {q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, q1.z, q1.w, q2.x, q2.y, q2.z, q2.w};
     const int32_t ref[4] = {(int32_t)rf.x, (int32_t)rf.y, (int32_t)rf.z, (int32_t)rf.w};
+    // SOA (soa_nodes_kernel's layout): per axis, the ray's near bound word pair and far bound word pair, picked once
+    // for the four children by the sign of its direction: for 1/d > 0 the near slab is the min (fma is monotone in
+    // the bound), so the slab distances are the min/max of the AoS test bit for bit, without the per-child min/max
+    float smin[4], smax[4];  // SOA: the children's slab entry / exit, accumulated axis by axis
+    if constexpr (SOA) {
+        const float inv[3] = {R.ix, R.iy, R.iz}, oi[3] = {R.oxi, R.oyi, R.ozi};
+#pragma unroll
+        for (int ax = 0; ax < 3; ++ax) {
+            const bool neg = inv[ax] < 0.0f;
+            const uint32_t n01 = neg ? w[4 * ax + 2] : w[4 * ax], n23 = neg ? w[4 * ax + 3] : w[4 * ax + 1];
+            const uint32_t f01 = neg ? w[4 * ax] : w[4 * ax + 2], f23 = neg ? w[4 * ax + 1] : w[4 * ax + 3];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const uint32_t nwd = i < 2 ? n01 : n23, fwd = i < 2 ? f01 : f23;
+                const float nb = (float)__builtin_bit_cast(_Float16, (uint16_t)((i & 1) ? (nwd >> 16) : (nwd & 0xffffu)));
+                const float fb = (float)__builtin_bit_cast(_Float16, (uint16_t)((i & 1) ? (fwd >> 16) : (fwd & 0xffffu)));
+                const float tn = fmaf(nb, inv[ax], -oi[ax]), tf = fmaf(fb, inv[ax], -oi[ax]);
+                smin[i] = ax == 0 ? tn : fmaxf(smin[i], tn);
+                smax[i] = ax == 0 ? tf : fminf(smax[i], tf);
+            }
+        }
+    }
     LdsInt* ext = stack + STACK * BLOCK;
     float best = INFINITY;
     int32_t next = 0;  // the nearest inner child
@@ -1909,17 +1931,23 @@ __device__ __forceinline__ void sec_node4v(const RenderArgs& A, SecRay& R, LdsIn
     int cur = head + Q.n;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-        float f[6];
+        float tmin, tmax;
+        if constexpr (SOA) {
+            tmin = smin[i];
+            tmax = smax[i];
+        } else {
+            float f[6];
 #pragma unroll
-        for (int k = 0; k < 6; ++k) {
-            const uint32_t word = w[(6 * i + k) >> 1];
-            f[k] = (float)__builtin_bit_cast(_Float16, (uint16_t)(((6 * i + k) & 1) ? (word >> 16) : (word & 0xffffu)));
+            for (int k = 0; k < 6; ++k) {
+                const uint32_t word = w[(6 * i + k) >> 1];
+                f[k] = (float)__builtin_bit_cast(_Float16, (uint16_t)(((6 * i + k) & 1) ? (word >> 16) : (word & 0xffffu)));
+            }
+            const float tx1 = fmaf(f[0], R.ix, -R.oxi), tx2 = fmaf(f[3], R.ix, -R.oxi);
+            const float ty1 = fmaf(f[1], R.iy, -R.oyi), ty2 = fmaf(f[4], R.iy, -R.oyi);
+            const float tz1 = fmaf(f[2], R.iz, -R.ozi), tz2 = fmaf(f[5], R.iz, -R.ozi);
+            tmin = fmaxf(fmaxf(fminf(tx1, tx2), fminf(ty1, ty2)), fminf(tz1, tz2));
+            tmax = fminf(fminf(fmaxf(tx1, tx2), fmaxf(ty1, ty2)), fmaxf(tz1, tz2));
         }
-        const float tx1 = fmaf(f[0], R.ix, -R.oxi), tx2 = fmaf(f[3], R.ix, -R.oxi);
-        const float ty1 = fmaf(f[1], R.iy, -R.oyi), ty2 = fmaf(f[4], R.iy, -R.oyi);
-        const float tz1 = fmaf(f[2], R.iz, -R.ozi), tz2 = fmaf(f[5], R.iz, -R.ozi);
-        const float tmin = fmaxf(fmaxf(fminf(tx1, tx2), fminf(ty1, ty2)), fminf(tz1, tz2));
-        const float tmax = fminf(fminf(fmaxf(tx1, tx2), fmaxf(ty1, ty2)), fmaxf(tz1, tz2));
         // [max(tmin, 0), min(tmax, plim)] not empty; a NaN box (empty slot) fails the first compare; the
         // subtree the ray has just finished (child slot skip - 1, right after a climb) is skipped
         const bool hit = (tmin <= fminf(tmax, R.plim)) & (tmax >= 0.0f) & (skip != i + 1);
@@ -2085,7 +2113,7 @@ constexpr int kPrimUnroll = VR_WW_PRIM_UNROLL, kNodeUnroll = VR_WW_NODE_UNROLL;
 __device__ unsigned long long g_dr_t0, g_dr_done, g_dr_end;
 __device__ uint32_t g_dr_hist[2][20], g_dr_max[2], g_dr_exit[64], g_dr_waves;
 #endif
-template <int BLOCK, int STACK, bool S, bool PURE, int WAVES, int QCAP, bool H, bool W, bool WH = !PURE>
+template <int BLOCK, int STACK, bool S, bool PURE, int WAVES, int QCAP, bool H, bool W, bool WH = !PURE, bool SOA = false>
 __global__ __launch_bounds__(BLOCK, WAVES) void secondary_ww_kernel(RenderArgs A) {
     __shared__ int s_stack[(STACK + kQueueLds<QCAP>) * BLOCK];
     LdsInt* stack = (LdsInt*)(s_stack + threadIdx.x);  // LDS-typed: stack/queue accesses are ds_* ops, never flat
@@ -2358,7 +2386,7 @@ __global__ __launch_bounds__(BLOCK, WAVES) void secondary_ww_kernel(RenderArgs A
                 if constexpr (S) c.v[kCtrSteps] += (__ballot(go) != 0ull && lane == 0u) ? 1u : 0u;
 #endif
                 if (go) {
-                    if constexpr (W) sec_node4v<BLOCK, S, QCAP, STACK>(A, R, stack, sp, node, Q, c);
+                    if constexpr (W) sec_node4v<BLOCK, S, QCAP, STACK, SOA>(A, R, stack, sp, node, Q, c);
                     else sec_node<BLOCK, S, QCAP, STACK, H>(A, R, stack, sp, node, Q, c);
                 }
                 go = go && node >= 0 && Q.n <= QCAP - kRoom;
@@ -2686,6 +2714,31 @@ __global__ __launch_bounds__(256) void refit_kernel(const HNode4* __restrict__ s
 // child is that Gaussian's leaf is a leaf-level node near the record (the Gaussian holds the position),
 // found with two loads instead of a descent from the root (record_start_kernel 0.63 -> ~0.1 ms at C4); the
 // descent remains for a record without one.
+// The secondary rays' per-axis node copy (VR_SEC_SOA): node i's words 4a..4a+3 hold axis a's box bounds as f16
+// pairs {min of children 0, 1}, {min of 2, 3}, {max of 0, 1}, {max of 2, 3}; words 12-15 the child refs. A ray
+// picks its near and far bound of an axis once per node (the sign of its direction), for all four children at
+// once, instead of a min and a max per child and axis (sec_node4v<SOA>).
+__global__ __launch_bounds__(256) void soa_nodes_kernel(const HNode4* __restrict__ src, HNode4* __restrict__ dst, uint32_t n) {
+    const uint32_t i = blockIdx.x * 256u + threadIdx.x;
+    if (i >= n) return;
+    const HNode4 a = src[i];
+    uint32_t w[16];
+#pragma unroll
+    for (int ax = 0; ax < 3; ++ax) {
+        w[4 * ax + 0] = (uint32_t)a.h[0][ax] | ((uint32_t)a.h[1][ax] << 16);
+        w[4 * ax + 1] = (uint32_t)a.h[2][ax] | ((uint32_t)a.h[3][ax] << 16);
+        w[4 * ax + 2] = (uint32_t)a.h[0][3 + ax] | ((uint32_t)a.h[1][3 + ax] << 16);
+        w[4 * ax + 3] = (uint32_t)a.h[2][3 + ax] | ((uint32_t)a.h[3][3 + ax] << 16);
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) w[12 + k] = (uint32_t)a.c[k];
+    uint4* o = reinterpret_cast<uint4*>(dst + i);
+    o[0] = make_uint4(w[0], w[1], w[2], w[3]);
+    o[1] = make_uint4(w[4], w[5], w[6], w[7]);
+    o[2] = make_uint4(w[8], w[9], w[10], w[11]);
+    o[3] = make_uint4(w[12], w[13], w[14], w[15]);
+}
+
 __global__ __launch_bounds__(256) void prim_node_kernel(const HNode4* __restrict__ nodes, uint32_t n, int32_t* __restrict__ map) {
     const uint32_t i = blockIdx.x * 256u + threadIdx.x;
     if (i >= n) return;
@@ -2972,7 +3025,7 @@ hipError_t gauss_march(const RenderArgs& A, hipStream_t stream, bool stats) {
 // One launch of the persistent kernel: one resident grid (every CU filled to the kernel's occupancy).
 // LDS words per lane: 14 traversal-stack entries (deeper ones overflow to global memory) + the
 // 8-entry LDS ring of the 9-entry leaf queue = 22 (7 blocks of 256 lanes per CU).
-template <bool S, bool PURE, bool H, bool W, bool WH = !PURE>
+template <bool S, bool PURE, bool H, bool W, bool WH = !PURE, bool SOA = false>
 static hipError_t ww_launch(const RenderArgs& A, hipStream_t stream) {
 #ifndef VR_WW_STACK
 #define VR_WW_STACK 14  // LDS traversal-stack entries per lane (deeper ones spill to the global overflow)
@@ -2985,7 +3038,7 @@ static hipError_t ww_launch(const RenderArgs& A, hipStream_t stream) {
 #endif
     constexpr int kStack = VR_WW_STACK, kQueue = VR_WW_QCAP;
     constexpr int kWaves = PURE ? 5 : WH ? VR_WW_WAVES : 6;  // PureRayMarching's marched depth does not fit 80 VGPRs without spills
-    const void* fn = (const void*)dev::secondary_ww_kernel<kBlockSecondary, kStack, S, PURE, kWaves, kQueue, H, W, WH>;
+    const void* fn = (const void*)dev::secondary_ww_kernel<kBlockSecondary, kStack, S, PURE, kWaves, kQueue, H, W, WH, SOA>;
     int dv = 0, cus = 0, per_cu = 0;
     if (hipGetDevice(&dv) != hipSuccess) return hipErrorUnknown;
     if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dv) != hipSuccess) return hipErrorUnknown;
@@ -2998,7 +3051,7 @@ static hipError_t ww_launch(const RenderArgs& A, hipStream_t stream) {
     if (e != hipSuccess) return e;
     RenderArgs B = A;  // the tight tree only under the whitened test (the M forms: the shared tree's padded boxes)
     if (PURE || !WH) B.hnodes4s = A.hnodes4;
-    hipLaunchKernelGGL((dev::secondary_ww_kernel<kBlockSecondary, kStack, S, PURE, kWaves, kQueue, H, W, WH>), dim3((unsigned)grid),
+    hipLaunchKernelGGL((dev::secondary_ww_kernel<kBlockSecondary, kStack, S, PURE, kWaves, kQueue, H, W, WH, SOA>), dim3((unsigned)grid),
                        dim3(kBlockSecondary), 0, stream, B);
     return hipGetLastError();
 }
@@ -3010,7 +3063,9 @@ static hipError_t secondary_launch(const RenderArgs& A, hipStream_t stream) {
         if (A.hnodes != nullptr && A.hnodes4 != nullptr) e = ww_launch<S, PURE, true, true, false>(A, stream);
         else if (A.hnodes != nullptr) e = ww_launch<S, PURE, true, false, false>(A, stream);
         else e = ww_launch<S, PURE, false, false, false>(A, stream);
-    } else if (A.hnodes != nullptr && A.hnodes4 != nullptr)  // 4-wide half-precision tree
+    } else if (!PURE && A.hnodes != nullptr && A.hnodes4 != nullptr && A.hnodes4t != nullptr)  // the tight tree, per axis
+        e = ww_launch<S, PURE, true, true, true, true>(A, stream);
+    else if (A.hnodes != nullptr && A.hnodes4 != nullptr)  // 4-wide half-precision tree
         e = ww_launch<S, PURE, true, true>(A, stream);
     else if (A.hnodes != nullptr)
         e = ww_launch<S, PURE, true, false>(A, stream);
@@ -3075,9 +3130,9 @@ hipError_t gauss_parents(const HNode4* nodes, uint32_t n, int32_t* parent, int32
 
 // The secondary rays' tree (refit_kernel): nodes 0..n-1 of `src` with tight boxes into `dst`. Scratch:
 // depth (n B), nbox (24 n B), maxd (one word, device) and host_maxd (pinned or pageable host word).
-hipError_t gauss_refit_secondary(const HNode4* src, HNode4* dst, uint32_t n, const GaussianRecord* rec, const int32_t* parent,
-                                 uint8_t* depth, float* nbox, uint32_t* maxd, const float hc[3], float hs, float diag,
-                                 hipStream_t stream) {
+hipError_t gauss_refit_secondary(const HNode4* src, HNode4* dst, HNode4* dst_t, uint32_t n, const GaussianRecord* rec,
+                                 const int32_t* parent, uint8_t* depth, float* nbox, uint32_t* maxd, const float hc[3], float hs,
+                                 float diag, hipStream_t stream) {
     if (n == 0) return hipSuccess;
     hipError_t e = hipMemsetAsync(maxd, 0, sizeof(uint32_t), stream);
     if (e != hipSuccess) return e;
@@ -3091,6 +3146,10 @@ hipError_t gauss_refit_secondary(const HNode4* src, HNode4* dst, uint32_t n, con
     for (int level = (int)md; level >= 0; --level) {
         hipLaunchKernelGGL(dev::refit_kernel, dim3((n + 255) / 256), dim3(256), 0, stream, src, dst, rec, depth, (uint32_t)level, n,
                            nbox, c, hs, diag);
+        if ((e = hipGetLastError()) != hipSuccess) return e;
+    }
+    if (dst_t != nullptr) {
+        hipLaunchKernelGGL(dev::soa_nodes_kernel, dim3((n + 255) / 256), dim3(256), 0, stream, dst, dst_t, n);
         if ((e = hipGetLastError()) != hipSuccess) return e;
     }
     return hipSuccess;

@@ -66,6 +66,10 @@ struct HNode4 {
 };
 static_assert(sizeof(HNode4) == 64, "4-wide half node must be 64 B");
 
+#ifndef VR_SEC_SOA
+#define VR_SEC_SOA 1  // the secondary rays' node step reads a per-axis copy of their tree (sign-selected slabs; A/B)
+#endif
+
 #ifndef VR_LEAF_MAX
 #define VR_LEAF_MAX 2  // A/B (round 3, every line): 2 beats 3 by 0.8-2.8 % (C4 +1.7 %), 1 and 4 lose
 #endif
@@ -151,6 +155,7 @@ struct RenderArgs {
     const HNode* hnodes;      // nullptr: the scene is not suited to half-precision boxes (see vr_device.cpp)
     const HNode4* hnodes4;    // 4-wide collapse of the same tree (secondary rays); nullptr with hnodes
     const HNode4* hnodes4s;   // the secondary rays' copy with tight boxes (gauss_refit_secondary), else hnodes4
+    const HNode4* hnodes4t;   // hnodes4s's nodes with the boxes laid out per axis (soa_nodes_kernel), or nullptr
     const int32_t* prim_node4;  // the 4-wide node whose child is each record's leaf (record starts), or nullptr
     const int32_t* hn4_parent;  // parent of every HNode4 | (its slot + 1) << 28 (root: -1); nullptr: walks start at the root
     uint32_t num_nodes4;        // HNode4 count
