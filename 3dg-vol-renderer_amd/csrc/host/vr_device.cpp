@@ -28,6 +28,7 @@ hipError_t gauss_record_cut(const RenderArgs& A, float budget, hipStream_t strea
 hipError_t gauss_whiten(const GaussianRecord* rec, WRecord* out, uint32_t n, uint32_t* bad, hipStream_t stream);
 hipError_t gauss_bin(const RenderArgs& A, bool emit, hipStream_t stream);
 hipError_t gauss_parents(const HNode4* nodes, uint32_t n, int32_t* parent, int32_t* prim_node, hipStream_t stream);
+hipError_t gauss_soa_nodes(const HNode4* src, HNode4* dst, uint32_t n, hipStream_t stream);
 hipError_t gauss_refit_secondary(const HNode4* src, HNode4* dst, HNode4* dst_t, uint32_t n, const GaussianRecord* rec, const int32_t* parent,
                                  uint8_t* depth, float* nbox, uint32_t* maxd, const float hc[3], float hs, float diag,
                                  hipStream_t stream);
@@ -60,6 +61,7 @@ struct vr_ctx {
     HNode* d_hnodes = nullptr;
     HNode4* d_hnodes4 = nullptr;
     HNode4* d_hnodes4s = nullptr;  // the secondary rays' copy with tight boxes (VR_OPT_SEC_TIGHT)
+    HNode4* d_hnodes4w = nullptr;  // d_hnodes4 laid out per axis (the 4-wide walks' node tests, wide_children)
     int32_t* d_parent4 = nullptr;  // parent of every HNode4 (the secondary rays' climb out of their start subtree)
     int32_t* d_prim_node4 = nullptr;  // the HNode4 whose child is each record's leaf (record starts)
     size_t num_nodes4 = 0;
@@ -185,6 +187,8 @@ void free_scene(vr_ctx* c) {
     c->d_hnodes4 = nullptr;
     if (c->d_hnodes4s) (void)hipFree(c->d_hnodes4s);
     c->d_hnodes4s = nullptr;
+    if (c->d_hnodes4w) (void)hipFree(c->d_hnodes4w);
+    c->d_hnodes4w = nullptr;
     if (c->d_parent4) (void)hipFree(c->d_parent4);
     c->d_parent4 = nullptr;
     if (c->d_prim_node4) (void)hipFree(c->d_prim_node4);
@@ -234,6 +238,8 @@ vr_status upload_half_nodes(vr_ctx* c, const std::vector<BVHNode>& nodes) {
     c->d_hnodes4 = nullptr;
     if (c->d_hnodes4s) (void)hipFree(c->d_hnodes4s);
     c->d_hnodes4s = nullptr;
+    if (c->d_hnodes4w) (void)hipFree(c->d_hnodes4w);
+    c->d_hnodes4w = nullptr;
     if (!c->opt_half_nodes) return VR_OK;
     double half = 0.0;
     for (int k = 0; k < 3; ++k) {
@@ -459,7 +465,12 @@ vr_status upload_parents(vr_ctx* c) {
     c->d_parent4 = nullptr;
     if (c->d_prim_node4) (void)hipFree(c->d_prim_node4);
     c->d_prim_node4 = nullptr;
+    if (c->d_hnodes4w) (void)hipFree(c->d_hnodes4w);
+    c->d_hnodes4w = nullptr;
     if (!c->d_hnodes4 || c->num_nodes4 == 0) return VR_OK;
+    // every 4-wide walk's node test reads the per-axis copy (wide_children): it exists whenever d_hnodes4 does
+    HIP_TRY(hipMalloc(&c->d_hnodes4w, c->num_nodes4 * sizeof(HNode4)), "hipMalloc(per-axis wide nodes)");
+    HIP_TRY(gauss_soa_nodes(c->d_hnodes4, c->d_hnodes4w, (uint32_t)c->num_nodes4, c->stream), "per-axis wide nodes");
     HIP_TRY(hipMalloc(&c->d_parent4, c->num_nodes4 * sizeof(int32_t)), "hipMalloc(wide-node parents)");
     if (c->num_prims > 0)
         HIP_TRY(hipMalloc(&c->d_prim_node4, (size_t)c->num_prims * sizeof(int32_t)), "hipMalloc(record leaf nodes)");
@@ -568,6 +579,7 @@ vr_status fill_args(vr_ctx* c, const vr_camera* cam, const vr_render_params* p, 
     A.hnodes4 = c->d_hnodes4;
     A.hnodes4s = c->d_hnodes4s ? c->d_hnodes4s : c->d_hnodes4;
     A.hnodes4t = (VR_SEC_SOA && c->d_hnodes4s) ? c->d_hnodes4s + c->num_nodes4 : nullptr;
+    A.hnodes4w = c->d_hnodes4w;
     A.hn4_parent = c->d_parent4;
     A.prim_node4 = c->d_prim_node4;
     A.num_nodes4 = (uint32_t)c->num_nodes4;

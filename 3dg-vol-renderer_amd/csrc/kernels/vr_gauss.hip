@@ -3155,6 +3155,12 @@ hipError_t gauss_refit_secondary(const HNode4* src, HNode4* dst, HNode4* dst_t, 
     return hipSuccess;
 }
 
+hipError_t gauss_soa_nodes(const HNode4* src, HNode4* dst, uint32_t n, hipStream_t stream) {
+    if (n == 0) return hipSuccess;
+    hipLaunchKernelGGL(dev::soa_nodes_kernel, dim3((n + 255) / 256), dim3(256), 0, stream, src, dst, n);
+    return hipGetLastError();
+}
+
 hipError_t gauss_whiten(const GaussianRecord* rec, WRecord* out, uint32_t n, uint32_t* bad, hipStream_t stream) {
     hipLaunchKernelGGL(dev::whiten_kernel, dim3((n + 255) / 256), dim3(256), 0, stream, rec, out, n, bad);
     return hipGetLastError();

@@ -493,26 +493,39 @@ __device__ __forceinline__ void cswap(float& ka, int32_t& ra, float& kb, int32_t
 
 // Slab tests of the four children of 4-wide half node `node` (HNode4) for a ray already in the
 // nodes' normalised coordinates, sorted near to far; misses (and empty slots) get key +inf, ref 0.
+// The node comes from the per-axis copy (A.hnodes4w, soa_nodes_kernel: per axis the f16 word pairs {min of children
+// 0, 1}, {min 2, 3}, {max 0, 1}, {max 2, 3}; then the refs): the ray takes its near and far word pair of each axis
+// once for the four children by the sign of 1/d — for 1/d > 0 the fma is monotone in the bound, so the near
+// bound's slab distance is the min of the two — the same tmin / tmax bit for bit as a min and a max per child.
 template <typename Hit, bool SORT = true>
 __device__ __forceinline__ void wide_children(const RenderArgs& A, int node, float ix, float iy, float iz, float oxi,
                                               float oyi, float ozi, Hit hit, float* key, int32_t* kr) {
-    const uint4* np = reinterpret_cast<const uint4*>(A.hnodes4 + node);
+    const uint4* np = reinterpret_cast<const uint4*>(A.hnodes4w + node);
     const uint4 q0 = np[0], q1 = np[1], q2 = np[2], rf = np[3];
     const uint32_t w[12] = {q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, q1.z, q1.w, q2.x, q2.y, q2.z, q2.w};
     const int32_t ref[4] = {(int32_t)rf.x, (int32_t)rf.y, (int32_t)rf.z, (int32_t)rf.w};
+    float smin[4], smax[4];
+    {
+        const float inv[3] = {ix, iy, iz}, oi[3] = {oxi, oyi, ozi};
+#pragma unroll
+        for (int ax = 0; ax < 3; ++ax) {
+            const bool neg = inv[ax] < 0.0f;
+            const uint32_t n01 = neg ? w[4 * ax + 2] : w[4 * ax], n23 = neg ? w[4 * ax + 3] : w[4 * ax + 1];
+            const uint32_t f01 = neg ? w[4 * ax] : w[4 * ax + 2], f23 = neg ? w[4 * ax + 1] : w[4 * ax + 3];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const uint32_t nwd = i < 2 ? n01 : n23, fwd = i < 2 ? f01 : f23;
+                const float nb = (float)__builtin_bit_cast(_Float16, (uint16_t)((i & 1) ? (nwd >> 16) : (nwd & 0xffffu)));
+                const float fb = (float)__builtin_bit_cast(_Float16, (uint16_t)((i & 1) ? (fwd >> 16) : (fwd & 0xffffu)));
+                const float tn = fmaf(nb, inv[ax], -oi[ax]), tf = fmaf(fb, inv[ax], -oi[ax]);
+                smin[i] = ax == 0 ? tn : fmaxf(smin[i], tn);
+                smax[i] = ax == 0 ? tf : fminf(smax[i], tf);
+            }
+        }
+    }
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-        float f[6];
-#pragma unroll
-        for (int k = 0; k < 6; ++k) {
-            const uint32_t word = w[(6 * i + k) >> 1];
-            f[k] = (float)__builtin_bit_cast(_Float16, (uint16_t)(((6 * i + k) & 1) ? (word >> 16) : (word & 0xffffu)));
-        }
-        const float tx1 = fmaf(f[0], ix, -oxi), tx2 = fmaf(f[3], ix, -oxi);
-        const float ty1 = fmaf(f[1], iy, -oyi), ty2 = fmaf(f[4], iy, -oyi);
-        const float tz1 = fmaf(f[2], iz, -ozi), tz2 = fmaf(f[5], iz, -ozi);
-        const float tmin = fmaxf(fmaxf(fminf(tx1, tx2), fminf(ty1, ty2)), fminf(tz1, tz2));
-        const float tmax = fminf(fminf(fmaxf(tx1, tx2), fmaxf(ty1, ty2)), fmaxf(tz1, tz2));
+        const float tmin = smin[i], tmax = smax[i];
         const bool h = (ref[i] != 0) && (tmax >= fmaxf(tmin, 0.0f)) && hit(tmin, tmax);
         key[i] = h ? tmin : INFINITY;
         kr[i] = h ? ref[i] : 0;

@@ -156,6 +156,7 @@ struct RenderArgs {
     const HNode4* hnodes4;    // 4-wide collapse of the same tree (secondary rays); nullptr with hnodes
     const HNode4* hnodes4s;   // the secondary rays' copy with tight boxes (gauss_refit_secondary), else hnodes4
     const HNode4* hnodes4t;   // hnodes4s's nodes with the boxes laid out per axis (soa_nodes_kernel), or nullptr
+    const HNode4* hnodes4w;   // hnodes4's nodes laid out per axis (soa_nodes_kernel; read by wide_children), with hnodes4
     const int32_t* prim_node4;  // the 4-wide node whose child is each record's leaf (record starts), or nullptr
     const int32_t* hn4_parent;  // parent of every HNode4 | (its slot + 1) << 28 (root: -1); nullptr: walks start at the root
     uint32_t num_nodes4;        // HNode4 count
