@@ -379,9 +379,13 @@ __device__ __forceinline__ float transmittance_up_to(const RenderArgs& A, const 
 // may lag the node steps by a few primitives (it then prunes less, never more). Returns false if the
 // stack could overflow (the caller redoes the walk on the pair tree).
 #ifndef VR_COLLECT_STEPS
-#define VR_COLLECT_STEPS 4  // node steps / primitives per lane per wave iteration of the collection walk
+#define VR_COLLECT_STEPS 6  // node steps / primitives per lane per wave iteration of the collection walk (round 6 A/B,
+                            // 4 / 6 / 8: C4 multi-scatter 81.8 / 82.9 / 81.9, C5 260.8 / 263.0 / - Mpaths/s)
 #endif
-constexpr int kCollectQueue = 8, kCollectSteps = VR_COLLECT_STEPS;
+#ifndef VR_FFSM_COLLECT_STEPS
+#define VR_FFSM_COLLECT_STEPS 8  // the same in the phase-scheduled kernel's COLLECT phase (C2: 4 / 6 / 8 -> 33.5 / 33.6 / 34.1)
+#endif
+constexpr int kCollectQueue = 8, kCollectSteps = VR_COLLECT_STEPS, kSmCollectSteps = VR_FFSM_COLLECT_STEPS;
 template <typename Prune, typename Prim, typename Cnt>
 __device__ __forceinline__ bool collect_walk(const RenderArgs& A, const Ray& r0, int* stack, int* ring, Prune prune,
                                              Prim prim, Cnt* cnt) {
@@ -1232,7 +1236,7 @@ __global__ void __launch_bounds__(kFFBlock, VR_FFSM_WAVES) ff_path_sm_kernel(Ren
             const int np = __popcll(__ballot(has_prim)), nn = __popcll(__ballot(can_node));
             if (nn == 0 || (np > 0 && np >= nn)) {  // PRIM iteration
                 bool go = has_prim;
-                for (int k = 0; k < kCollectSteps; ++k) {
+                for (int k = 0; k < kSmCollectSteps; ++k) {
                     if (go) {
                         if (j == end) {
                             const int32_t ref = ring[qh * kFFBlock];
@@ -1259,7 +1263,7 @@ __global__ void __launch_bounds__(kFFBlock, VR_FFSM_WAVES) ff_path_sm_kernel(Ren
                 const float ix = inv(P.ray.dx), iy = inv(P.ray.dy), iz = inv(P.ray.dz);
                 const float oxi = ox * ix, oyi = oy * iy, ozi = oz * iz;
                 bool go = can_node;
-                for (int k = 0; k < kCollectSteps; ++k) {
+                for (int k = 0; k < kSmCollectSteps; ++k) {
                     if (go) {
                         S.C.add(kFFNode4);
                         float key[4];
