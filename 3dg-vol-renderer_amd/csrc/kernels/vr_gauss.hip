@@ -3051,6 +3051,7 @@ static hipError_t ww_launch(const RenderArgs& A, hipStream_t stream) {
     if (e != hipSuccess) return e;
     RenderArgs B = A;  // the tight tree only under the whitened test (the M forms: the shared tree's padded boxes)
     if (PURE || !WH) B.hnodes4s = A.hnodes4;
+    if (SOA && B.hnodes4s == A.hnodes4) B.hnodes4t = A.hnodes4w;  // the per-axis copy of the tree walked
     hipLaunchKernelGGL((dev::secondary_ww_kernel<kBlockSecondary, kStack, S, PURE, kWaves, kQueue, H, W, WH, SOA>), dim3((unsigned)grid),
                        dim3(kBlockSecondary), 0, stream, B);
     return hipGetLastError();
@@ -3059,14 +3060,13 @@ static hipError_t ww_launch(const RenderArgs& A, hipStream_t stream) {
 template <bool S, bool PURE>
 static hipError_t secondary_launch(const RenderArgs& A, hipStream_t stream) {
     hipError_t e;
+    // (4-wide trees: the node step reads the per-axis copy of the tree the variant walks, VR_SEC_SOA)
     if (!PURE && A.wrec == nullptr) {  // a record without a Cholesky factor: the M forms (rare scenes)
-        if (A.hnodes != nullptr && A.hnodes4 != nullptr) e = ww_launch<S, PURE, true, true, false>(A, stream);
+        if (A.hnodes != nullptr && A.hnodes4 != nullptr) e = ww_launch<S, PURE, true, true, false, VR_SEC_SOA != 0>(A, stream);
         else if (A.hnodes != nullptr) e = ww_launch<S, PURE, true, false, false>(A, stream);
         else e = ww_launch<S, PURE, false, false, false>(A, stream);
-    } else if (!PURE && A.hnodes != nullptr && A.hnodes4 != nullptr && A.hnodes4t != nullptr)  // the tight tree, per axis
-        e = ww_launch<S, PURE, true, true, true, true>(A, stream);
-    else if (A.hnodes != nullptr && A.hnodes4 != nullptr)  // 4-wide half-precision tree
-        e = ww_launch<S, PURE, true, true>(A, stream);
+    } else if (A.hnodes != nullptr && A.hnodes4 != nullptr)  // 4-wide half-precision tree
+        e = ww_launch<S, PURE, true, true, !PURE, VR_SEC_SOA != 0>(A, stream);
     else if (A.hnodes != nullptr)
         e = ww_launch<S, PURE, true, false>(A, stream);
     else  // f32 child-pair tree (scenes whose leaf boxes are too small for f16 boxes)
